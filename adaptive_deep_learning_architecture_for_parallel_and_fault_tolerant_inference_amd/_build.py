@@ -1,0 +1,125 @@
+"""In-tree native build (no setuptools / JIT cache).
+
+* ``_C``        gfx950 HIP kernels + pybind11 bindings, built with hipcc
+                (``--offload-arch=gfx950``), linked against the HIP runtime
+                that torch already loaded (same SONAME libamdhip64.so.7).
+* ``_runtime``  host C++17 runtime (framing transport, LZ4 frame codec,
+                zfp-style reversible codec, membership store), built with g++.
+
+Objects go to ``build/``; the two ``.so`` files are written next to this
+file so they travel to the GPU box with the repo snapshot.  Rebuilds are
+incremental on source/header mtimes.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+from typing import List
+
+PKG_DIR = Path(__file__).resolve().parent
+ROOT = PKG_DIR.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes() -> List[str]:
+    import pybind11
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _newer(target: Path, deps: List[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def kernel_lib_path() -> Path:
+    return PKG_DIR / f"_C{EXT}"
+
+
+def runtime_lib_path() -> Path:
+    return PKG_DIR / f"_runtime{EXT}"
+
+
+def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
+    src_dir = CSRC / "kernels"
+    headers = list(src_dir.glob("*.h"))
+    srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp"))
+    out_dir = BUILD / "kernels"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    inc = _py_includes() + [f"-I{src_dir}"]
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1",
+              "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-result"] + inc
+
+    def compile_one(src: Path) -> Path:
+        obj = out_dir / (src.name + ".o")
+        if _newer(obj, [src] + headers):
+            cmd = common + ["-c", str(src), "-o", str(obj)]
+            if src.suffix == ".cpp":
+                cmd = common + ["-x", "hip", "-c", str(src), "-o", str(obj)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            _run(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    lib = kernel_lib_path()
+    if _newer(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib)] + [str(o) for o in objs]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        _run(cmd)
+    return lib
+
+
+def build_runtime(verbose: bool = False, jobs: int = 8) -> Path:
+    src_dir = CSRC / "runtime"
+    headers = list(src_dir.glob("*.h"))
+    srcs = sorted(src_dir.glob("*.cpp"))
+    out_dir = BUILD / "runtime"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    flags = ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-pthread",
+             f"-I{src_dir}"] + _py_includes()
+
+    def compile_one(src: Path) -> Path:
+        obj = out_dir / (src.name + ".o")
+        if _newer(obj, [src] + headers):
+            cmd = flags + ["-c", str(src), "-o", str(obj)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            _run(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    lib = runtime_lib_path()
+    if objs and _newer(lib, objs):
+        cmd = ["g++", "-shared", "-fPIC", "-pthread", "-o", str(lib)] + [str(o) for o in objs]
+        _run(cmd)
+    return lib
+
+
+def build_all(verbose: bool = False) -> None:
+    build_runtime(verbose)
+    build_kernels(verbose)
+
+
+if __name__ == "__main__":
+    build_all(verbose="-v" in sys.argv)
+    print("built", kernel_lib_path(), runtime_lib_path())

@@ -1,0 +1,280 @@
+"""Named-layer graph IR.
+
+The reference cuts a Keras functional graph at named layers
+(`src/dag_util.py:3-62`, `src/dispatcher.py:39-53`).  We do not depend on
+Keras: models are described by this small IR whose layer names, layer order
+and per-layer weight lists are byte-identical to the Keras
+`applications.resnet` graphs, so `part_at` lists and Keras `get_weights()`
+lists port over 1:1.
+
+Shapes are per-image NHWC (``(H, W, C)``) or ``(C,)``; the batch dimension is
+implicit.  Layers are stored in Keras creation order, which is a valid
+topological order.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+# op kinds understood by the runtime
+OPS = (
+    "input",      # graph input, attrs: shape
+    "zeropad",    # attrs: pad=((t,b),(l,r))
+    "conv",       # attrs: filters, kernel=(kh,kw), stride, padding('valid'|'same'), use_bias
+    "bn",         # attrs: epsilon
+    "relu",
+    "add",
+    "maxpool",    # attrs: pool, stride, padding
+    "gap",        # global average pool
+    "dense",      # attrs: units, activation(None|'softmax'), use_bias
+    "softmax",
+)
+
+
+@dataclass
+class Layer:
+    name: str
+    op: str
+    inputs: List[str]
+    attrs: Dict = field(default_factory=dict)
+    out_shape: Tuple[int, ...] = ()
+
+    # ---- weights (Keras get_weights() order) ----
+    def weight_shapes(self, in_shapes: Sequence[Tuple[int, ...]]) -> List[Tuple[str, Tuple[int, ...]]]:
+        """Return [(weight_name, shape)] in Keras order.
+
+        conv: kernel HWIO + bias; bn: gamma, beta, moving_mean, moving_variance;
+        dense: kernel (in, out) + bias.
+        """
+        if self.op == "conv":
+            kh, kw = self.attrs["kernel"]
+            cin = in_shapes[0][-1]
+            out = [(f"{self.name}/kernel", (kh, kw, cin, self.attrs["filters"]))]
+            if self.attrs.get("use_bias", True):
+                out.append((f"{self.name}/bias", (self.attrs["filters"],)))
+            return out
+        if self.op == "bn":
+            c = in_shapes[0][-1]
+            return [(f"{self.name}/{n}", (c,)) for n in ("gamma", "beta", "moving_mean", "moving_variance")]
+        if self.op == "dense":
+            cin = in_shapes[0][-1]
+            out = [(f"{self.name}/kernel", (cin, self.attrs["units"]))]
+            if self.attrs.get("use_bias", True):
+                out.append((f"{self.name}/bias", (self.attrs["units"],)))
+            return out
+        return []
+
+    def macs(self, in_shapes: Sequence[Tuple[int, ...]]) -> int:
+        """Multiply-accumulates per image."""
+        if self.op == "conv":
+            kh, kw = self.attrs["kernel"]
+            oh, ow, co = self.out_shape
+            return oh * ow * co * kh * kw * in_shapes[0][-1]
+        if self.op == "dense":
+            return in_shapes[0][-1] * self.attrs["units"]
+        return 0
+
+    def to_json(self) -> Dict:
+        return {"name": self.name, "op": self.op, "inputs": list(self.inputs),
+                "attrs": _jsonable(self.attrs), "out_shape": list(self.out_shape)}
+
+    @staticmethod
+    def from_json(d: Dict) -> "Layer":
+        attrs = dict(d.get("attrs", {}))
+        for k in ("kernel", "pad"):
+            if k in attrs and isinstance(attrs[k], list):
+                attrs[k] = _tuplify(attrs[k])
+        return Layer(d["name"], d["op"], list(d["inputs"]), attrs, tuple(d.get("out_shape", ())))
+
+
+def _tuplify(x):
+    if isinstance(x, list):
+        return tuple(_tuplify(v) for v in x)
+    return x
+
+
+def _jsonable(attrs: Dict) -> Dict:
+    def conv(v):
+        if isinstance(v, tuple):
+            return [conv(x) for x in v]
+        return v
+    return {k: conv(v) for k, v in attrs.items()}
+
+
+class Graph:
+    """An ordered DAG of named layers (one output tensor per layer)."""
+
+    def __init__(self, name: str = "model"):
+        self.name = name
+        self.layers: Dict[str, Layer] = {}
+        self.order: List[str] = []
+        self.input_names: List[str] = []
+        self.output_names: List[str] = []
+        self._consumers: Optional[Dict[str, List[str]]] = None
+
+    # ---------------------------------------------------------------- build
+    def add(self, layer: Layer) -> str:
+        if layer.name in self.layers:
+            raise ValueError(f"duplicate layer name {layer.name!r}")
+        for i in layer.inputs:
+            if i not in self.layers:
+                raise ValueError(f"layer {layer.name!r} consumes unknown tensor {i!r}")
+        layer.out_shape = tuple(layer.out_shape) or self._infer_shape(layer)
+        self.layers[layer.name] = layer
+        self.order.append(layer.name)
+        if layer.op == "input":
+            self.input_names.append(layer.name)
+        self._consumers = None
+        return layer.name
+
+    def _infer_shape(self, layer: Layer) -> Tuple[int, ...]:
+        ins = [self.layers[i].out_shape for i in layer.inputs]
+        a = layer.attrs
+        if layer.op == "input":
+            return tuple(a["shape"])
+        if layer.op == "zeropad":
+            (t, b), (l, r) = a["pad"]
+            h, w, c = ins[0]
+            return (h + t + b, w + l + r, c)
+        if layer.op == "conv":
+            h, w, _ = ins[0]
+            kh, kw = a["kernel"]
+            s = a.get("stride", 1)
+            if a.get("padding", "valid") == "same":
+                return (-(-h // s), -(-w // s), a["filters"])
+            return ((h - kh) // s + 1, (w - kw) // s + 1, a["filters"])
+        if layer.op in ("bn", "relu", "softmax"):
+            return ins[0]
+        if layer.op == "add":
+            if any(s != ins[0] for s in ins):
+                raise ValueError(f"add {layer.name}: mismatched shapes {ins}")
+            return ins[0]
+        if layer.op == "maxpool":
+            h, w, c = ins[0]
+            p, s = a["pool"], a["stride"]
+            if a.get("padding", "valid") == "same":
+                return (-(-h // s), -(-w // s), c)
+            return ((h - p) // s + 1, (w - p) // s + 1, c)
+        if layer.op == "gap":
+            return (ins[0][-1],)
+        if layer.op == "dense":
+            return (a["units"],)
+        raise ValueError(f"unknown op {layer.op}")
+
+    # -------------------------------------------------------------- queries
+    def __getitem__(self, name: str) -> Layer:
+        return self.layers[name]
+
+    def get_layer(self, name: str) -> Layer:
+        if name not in self.layers:
+            raise KeyError(f"no layer named {name!r} in {self.name}")
+        return self.layers[name]
+
+    def __len__(self) -> int:
+        return len(self.order)
+
+    def index(self, name: str) -> int:
+        return self.order.index(name)
+
+    @property
+    def output(self) -> str:
+        return self.output_names[0] if self.output_names else self.order[-1]
+
+    @property
+    def input(self) -> str:
+        return self.input_names[0]
+
+    def consumers(self) -> Dict[str, List[str]]:
+        if self._consumers is None:
+            c: Dict[str, List[str]] = {n: [] for n in self.order}
+            for n in self.order:
+                for i in self.layers[n].inputs:
+                    c[i].append(n)
+            self._consumers = c
+        return self._consumers
+
+    def in_shapes(self, name: str) -> List[Tuple[int, ...]]:
+        return [self.layers[i].out_shape for i in self.layers[name].inputs]
+
+    def weight_specs(self, names: Optional[Iterable[str]] = None) -> List[Tuple[str, Tuple[int, ...]]]:
+        names = self.order if names is None else list(names)
+        out = []
+        for n in names:
+            out.extend(self.layers[n].weight_shapes(self.in_shapes(n)))
+        return out
+
+    def count_params(self) -> int:
+        total = 0
+        for _, shp in self.weight_specs():
+            p = 1
+            for d in shp:
+                p *= d
+            total += p
+        return total
+
+    def layer_macs(self, name: str) -> int:
+        return self.layers[name].macs(self.in_shapes(name))
+
+    def total_macs(self) -> int:
+        return sum(self.layer_macs(n) for n in self.order)
+
+    def ancestors(self, name: str, inclusive: bool = True) -> set:
+        """All layers that `name` transitively depends on."""
+        seen = set()
+        stack = [name]
+        while stack:
+            n = stack.pop()
+            if n in seen:
+                continue
+            seen.add(n)
+            stack.extend(self.layers[n].inputs)
+        if not inclusive:
+            seen.discard(name)
+        return seen
+
+    def tensor_bytes(self, name: str, dtype_bytes: int = 2) -> int:
+        p = 1
+        for d in self.layers[name].out_shape:
+            p *= d
+        return p * dtype_bytes
+
+    # ------------------------------------------------------- serialization
+    def to_json(self) -> str:
+        return json.dumps({
+            "format": "adapt-graph-v1",
+            "name": self.name,
+            "layers": [self.layers[n].to_json() for n in self.order],
+            "inputs": self.input_names,
+            "outputs": self.output_names,
+        })
+
+    @staticmethod
+    def from_json(s: str) -> "Graph":
+        d = json.loads(s)
+        if d.get("format") != "adapt-graph-v1":
+            raise ValueError("not an adapt-graph-v1 document")
+        g = Graph(d["name"])
+        for ld in d["layers"]:
+            layer = Layer.from_json(ld)
+            # sub-graph inputs may reference tensors produced elsewhere; they
+            # are declared as 'input' layers by the slicer, so add() succeeds.
+            g.layers[layer.name] = layer
+            g.order.append(layer.name)
+        g.input_names = list(d["inputs"])
+        g.output_names = list(d["outputs"])
+        return g
+
+    def summary(self) -> str:
+        lines = [f"Model: {self.name}", f"{'Layer':40s} {'Op':8s} {'Output':>18s} {'Params':>10s}"]
+        for n in self.order:
+            L = self.layers[n]
+            p = 0
+            for _, shp in L.weight_shapes(self.in_shapes(n)):
+                q = 1
+                for d in shp:
+                    q *= d
+                p += q
+            lines.append(f"{n:40s} {L.op:8s} {str(L.out_shape):>18s} {p:>10d}")
+        lines.append(f"Total params: {self.count_params():,}")
+        return "\n".join(lines)

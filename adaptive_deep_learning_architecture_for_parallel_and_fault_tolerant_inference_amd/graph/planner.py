@@ -1,0 +1,162 @@
+"""Cost model and balanced pipeline partition planner.
+
+The reference takes `part_at` from the user verbatim (`test/test.py:15-18`)
+and binds slice *i* to worker *i* (`src/dispatcher.py:55-63`), or, in the
+gen-2 design, to any live worker per hop (`src/dispatcher.py:176-201`).  On
+repartition after a worker joins/leaves we must choose cuts
+ourselves, so this module provides:
+
+* a per-layer cost model (MFMA-rate compute + HBM traffic, both per image),
+  optionally replaced by measured per-layer times from the runtime;
+* `plan_cuts(g, k)`: the min-max-stage DP over *articulation* cut points
+  (layers whose ancestor set is exactly the topological prefix, e.g.
+  ``pool1_pool`` and every ``*_out``), adding each boundary's transfer time on
+  one xGMI link.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .ir import Graph
+
+# MI355X ballpark figures (MI355X_MICROARCH.md): dense bf16 MFMA ~2.5 PF,
+# achievable HBM ~6.3 TB/s, one xGMI link ~150 GB/s.
+@dataclass
+class HwModel:
+    mfma_flops: float = 2.5e15 * 0.45     # sustained fraction for implicit-GEMM conv
+    hbm_bw: float = 6.0e12
+    link_bw: float = 150e9
+    launch_s: float = 1.5e-6              # kernel boundary inside a hipGraph
+    act_bytes: int = 2                    # bf16 activations
+
+
+def layer_costs(g: Graph, batch: int = 32, hw: Optional[HwModel] = None) -> Dict[str, float]:
+    """Estimated seconds per layer for a batch (roofline max of compute / memory)."""
+    hw = hw or HwModel()
+    out = {}
+    for n in g.order:
+        L = g.layers[n]
+        if L.op in ("input",):
+            out[n] = 0.0
+            continue
+        macs = g.layer_macs(n) * batch
+        byts = sum(g.tensor_bytes(i, hw.act_bytes) for i in L.inputs) * batch + g.tensor_bytes(n, hw.act_bytes) * batch
+        if L.op in ("bn", "relu", "zeropad"):
+            # fused into the producing conv / pool at runtime
+            out[n] = 0.0
+            continue
+        if L.op == "add":
+            byts = g.tensor_bytes(n, hw.act_bytes) * batch   # residual read inside the conv epilogue
+            out[n] = byts / hw.hbm_bw
+            continue
+        t = max(2.0 * macs / hw.mfma_flops, byts / hw.hbm_bw) + hw.launch_s
+        out[n] = t
+    return out
+
+
+def articulation_points(g: Graph) -> List[str]:
+    """Layers `c` such that ancestors(c) == topological prefix up to c (single-tensor cuts
+    whose stage cost is a contiguous prefix-sum range)."""
+    res = []
+    seen = set()
+    # running check: a layer is an articulation point iff no layer after it
+    # consumes a layer before-or-at it other than itself.
+    order = g.order
+    idx = {n: i for i, n in enumerate(order)}
+    # last_use[i] = max index of any consumer of layer i
+    cons = g.consumers()
+    last_use = [max((idx[c] for c in cons[n]), default=i) for i, n in enumerate(order)]
+    running_max = -1
+    for i, n in enumerate(order):
+        # all layers < i must have their last use <= i... except layer i itself
+        if i > 0 and running_max <= i and g.layers[n].op != "input" and n != g.output:
+            res.append(n)
+        running_max = max(running_max, last_use[i])
+        seen.add(n)
+    # verify (cheap for <=600 layers)
+    verified = []
+    for n in res:
+        anc = g.ancestors(n)
+        if anc == set(order[: idx[n] + 1]):
+            verified.append(n)
+    return verified
+
+
+def default_candidates(g: Graph) -> List[str]:
+    """Articulation points at fusion-group ends (post-activation tensors): cutting
+    there never splits a conv+BN+add+ReLU epilogue across stages."""
+    return [n for n in articulation_points(g)
+            if g.layers[n].op in ("relu", "maxpool") and (n.endswith("_out") or n.endswith("_pool"))]
+
+
+def plan_cuts(g: Graph, stages: int, batch: int = 32, hw: Optional[HwModel] = None,
+              costs: Optional[Dict[str, float]] = None,
+              candidates: Optional[Sequence[str]] = None) -> Tuple[List[str], List[float]]:
+    """Min-max DP: returns (part_at, per-stage estimated seconds)."""
+    if stages < 1:
+        raise ValueError("stages must be >= 1")
+    hw = hw or HwModel()
+    costs = costs or layer_costs(g, batch, hw)
+    if stages == 1:
+        return [], [sum(costs.values())]
+    cands = list(candidates) if candidates is not None else default_candidates(g)
+    order = g.order
+    idx = {n: i for i, n in enumerate(order)}
+    cands = sorted(set(cands), key=lambda n: idx[n])
+    if len(cands) < stages - 1:
+        raise ValueError(f"only {len(cands)} cut candidates for {stages} stages")
+    prefix = [0.0]
+    for n in order:
+        prefix.append(prefix[-1] + costs.get(n, 0.0))
+    total = prefix[-1]
+    # positions: 0 = start, cands..., end
+    pos = [-1] + [idx[c] for c in cands] + [len(order) - 1]
+    comm = [0.0] + [g.tensor_bytes(c, hw.act_bytes) * batch / hw.link_bw for c in cands] + [0.0]
+
+    def seg(a: int, b: int) -> float:   # stage from after pos[a] to pos[b] inclusive
+        t = prefix[pos[b] + 1] - prefix[pos[a] + 1]
+        # receive / compute / send run on separate HIP streams over a stream of
+        # micro-batches, so a stage's steady-state period is the max of the three.
+        return max(t, comm[a], comm[b])
+
+    P = len(pos)
+    INF = float("inf")
+    # dp[k][j]: best max cost covering up to pos[j] with k stages
+    dp = [[INF] * P for _ in range(stages + 1)]
+    arg = [[-1] * P for _ in range(stages + 1)]
+    dp[0][0] = 0.0
+    for k in range(1, stages + 1):
+        for j in range(1, P):
+            best, barg = INF, -1
+            for i in range(0, j):
+                if dp[k - 1][i] == INF:
+                    continue
+                v = max(dp[k - 1][i], seg(i, j))
+                if v < best:
+                    best, barg = v, i
+            dp[k][j] = best
+            arg[k][j] = barg
+    # reconstruct
+    j = P - 1
+    cuts = []
+    k = stages
+    per = []
+    while k > 0:
+        i = arg[k][j]
+        per.append(seg(i, j))
+        if i > 0:
+            cuts.append(cands[i - 1])
+        j = i
+        k -= 1
+    cuts.reverse()
+    per.reverse()
+    if len(cuts) != stages - 1:
+        raise RuntimeError("planner failed to place all cuts")
+    return cuts, per
+
+
+def balance_ratio(per_stage: Sequence[float]) -> float:
+    """max stage / ideal (1.0 = perfect)."""
+    tot = sum(per_stage)
+    return max(per_stage) / (tot / len(per_stage)) if tot > 0 else 1.0

@@ -1,0 +1,154 @@
+"""Fused implicit-GEMM convolution (csrc/kernels/conv_igemm.hip).
+
+Replaces what the reference gets from TF/cuDNN inside `model.predict`
+(`src/node.py:177`): Conv2D + BatchNormalization [+ Add] [+ ReLU] of the
+Keras ResNet graph run as ONE MFMA launch with BN folded into the weights.
+
+Host side here: BN folding, weight packing to ``[Npad][Kpad]`` bf16 with
+``k = (kh, kw, ci)``, tile-config choice, and the shape checks that keep a
+launch inside its buffers (done before every launch).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._lib import kernels, ptr, stream_handle
+
+BK = 64
+# tile configs (must match ADAPT_CONV_CFGS in conv_igemm.hip)
+CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (32, 64)}
+_CFG_EFF = {0: 1.0, 4: 0.97, 1: 0.86, 2: 0.86, 3: 0.66, 5: 0.42}
+NUM_CUS = 256
+
+
+def fold_bn(kernel_hwio: np.ndarray, bias: Optional[np.ndarray], bn: Optional[dict], eps: float = 1.001e-5):
+    """Fold inference BN into conv weights: returns (kernel_hwio, bias) fp32."""
+    k = kernel_hwio.astype(np.float64)
+    cout = k.shape[-1]
+    b = np.zeros(cout) if bias is None else bias.astype(np.float64)
+    if bn is not None:
+        s = bn["gamma"].astype(np.float64) / np.sqrt(bn["moving_variance"].astype(np.float64) + eps)
+        k = k * s
+        b = (b - bn["moving_mean"]) * s + bn["beta"]
+    return k.astype(np.float32), b.astype(np.float32)
+
+
+@dataclass
+class PackedConv:
+    """Device-resident packed weights for one (possibly BN-folded) conv."""
+    w: torch.Tensor          # [Npad][Kpad] bf16
+    bias: torch.Tensor       # [N] fp32
+    kh: int
+    kw: int
+    cin: int                 # (padded) input channels the kernel consumes
+    cout: int
+    stride: int
+    pad_t: int
+    pad_l: int
+    pad_b: int
+    pad_r: int
+
+    @property
+    def K(self) -> int:
+        return self.kh * self.kw * self.cin
+
+    @property
+    def Kpad(self) -> int:
+        return self.w.shape[1]
+
+    def out_hw(self, h: int, w: int):
+        oh = (h + self.pad_t + self.pad_b - self.kh) // self.stride + 1
+        ow = (w + self.pad_l + self.pad_r - self.kw) // self.stride + 1
+        return oh, ow
+
+
+def pack_conv(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, device, cin_pad: Optional[int] = None,
+              row_align: int = 256) -> PackedConv:
+    kh, kw, cin, cout = kernel_hwio.shape
+    cp = cin_pad or cin
+    if cp % 8:
+        raise ValueError(f"conv input channels must be a multiple of 8 (got {cp}); pad the input")
+    k = np.zeros((kh, kw, cp, cout), np.float32)
+    k[:, :, :cin, :] = kernel_hwio
+    K = kh * kw * cp
+    Kpad = int(math.ceil(K / BK) * BK)
+    Npad = int(math.ceil(cout / row_align) * row_align)
+    wt = np.zeros((Npad, Kpad), np.float32)
+    wt[:cout, :K] = k.transpose(3, 0, 1, 2).reshape(cout, K)       # [cout][kh][kw][ci]
+    (pt, pb), (pl, pr) = pads
+    return PackedConv(
+        w=torch.from_numpy(wt).to(device=device, dtype=torch.bfloat16).contiguous(),
+        bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),
+        kh=kh, kw=kw, cin=cp, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
+
+
+def choose_cfg(M: int, N: int, Kpad: int, occupancy: int = 2):
+    """Heuristic (cfg, ksplit): minimise waves-of-blocks x per-block work / efficiency."""
+    best = None
+    ktiles = Kpad // BK
+    for cfg, (bm, bn) in CFG_TILES.items():
+        if N % 8:
+            continue
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        for ks in (1, 2, 4, 8):
+            if ks > 1 and (ktiles // ks < 4):
+                continue
+            blocks = tiles * ks
+            waves = math.ceil(blocks / (NUM_CUS * occupancy))
+            work = bm * bn * (Kpad / ks)
+            t = waves * work / _CFG_EFF[cfg]
+            if ks > 1:
+                t += M * N * 4 * (ks + 1) / 2e3   # slab write + reduce traffic (arbitrary units)
+                t *= 1.05
+            # small-grid penalty: fewer blocks than CUs leaves the chip idle
+            if blocks < NUM_CUS:
+                t *= 1.0 + 0.15 * (NUM_CUS - blocks) / NUM_CUS
+            cand = (t, cfg, ks)
+            if best is None or cand < best:
+                best = cand
+    return best[1], best[2]
+
+
+def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                 relu: bool = False, cfg: Optional[int] = None, ksplit: int = 1,
+                 workspace: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """x: [B,H,W,Cin] bf16 NHWC; out: [B,OH,OW,Cout] bf16 (or fp32 [M][Cout] for GEMM use)."""
+    if x.dim() == 2:
+        B, H, W, C = x.shape[0], 1, 1, x.shape[1]
+    else:
+        B, H, W, C = x.shape
+    if C != pc.cin:
+        raise ValueError(f"conv expects {pc.cin} input channels, got {C}")
+    if x.dtype != torch.bfloat16 or not x.is_contiguous():
+        raise ValueError("conv input must be contiguous bf16 NHWC")
+    OH, OW = pc.out_hw(H, W)
+    M = B * OH * OW
+    N = pc.cout
+    out_f32 = out.dtype == torch.float32
+    if out.numel() != M * N or not out.is_contiguous():
+        raise ValueError(f"conv output buffer has {out.numel()} elements, need {M * N}")
+    if residual is not None and (residual.numel() != M * N or residual.dtype != torch.bfloat16):
+        raise ValueError("residual must be bf16 with the output's shape")
+    if cfg is None:
+        cfg, ksplit = choose_cfg(M, N, pc.Kpad)
+    bm, bn = CFG_TILES[cfg]
+    if pc.w.shape[0] < math.ceil(N / bn) * bn:
+        raise ValueError("packed weights not padded to the tile's N")
+    ws_ptr = 0
+    if ksplit > 1:
+        need = ksplit * M * N
+        if workspace is None:
+            workspace = torch.empty(need, dtype=torch.float32, device=x.device)
+        if workspace.numel() < need or workspace.dtype != torch.float32:
+            raise ValueError(f"split-K {ksplit} needs an fp32 workspace of {need} elements")
+        ws_ptr = ptr(workspace)
+    kernels().conv_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr,
+                           B, H, W, C, OH, OW, N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l,
+                           pc.K, pc.Kpad, N, int(relu), int(ksplit), int(cfg), bool(out_f32),
+                           stream_handle(stream))
+    return out

@@ -1,0 +1,129 @@
+"""Wrappers for the memory-bound NHWC kernels (csrc/kernels/eltwise.hip).
+
+Each wrapper validates dtype / contiguity / element counts on the host before
+launching; all kernels require the channel count to be a multiple of 8
+(16-byte vectors).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._lib import kernels, ptr, stream_handle
+
+
+def _chk(t: torch.Tensor, dtype=torch.bfloat16, name="tensor"):
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a device tensor")
+
+
+def input_pack(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    """fp32 NHWC [B,H,W,C] -> bf16 NHWC [B,H,W,Cp] zero-padded channels."""
+    _chk(x, torch.float32, "x")
+    _chk(out, torch.bfloat16, "out")
+    B, H, W, C = x.shape
+    Cp = out.shape[-1]
+    if out.shape[:3] != x.shape[:3] or Cp % 8 or Cp < C:
+        raise ValueError(f"input_pack: bad shapes {tuple(x.shape)} -> {tuple(out.shape)}")
+    kernels().input_pack(ptr(x), ptr(out), B * H * W, C, Cp, stream_handle(stream))
+    return out
+
+
+def bn_act(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, out: torch.Tensor, relu: bool = False,
+           stream=None) -> torch.Tensor:
+    _chk(x, name="x"); _chk(out, name="out")
+    _chk(scale, torch.float32, "scale"); _chk(shift, torch.float32, "shift")
+    C = x.shape[-1]
+    if C % 8 or scale.numel() != C or shift.numel() != C or out.numel() != x.numel():
+        raise ValueError("bn_act: bad shapes")
+    kernels().bn_act(ptr(x), ptr(out), ptr(scale), ptr(shift), x.numel(), C, int(relu), stream_handle(stream))
+    return out
+
+
+def add_act(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, relu: bool = False, stream=None) -> torch.Tensor:
+    _chk(a, name="a"); _chk(b, name="b"); _chk(out, name="out")
+    if a.numel() != b.numel() or a.numel() != out.numel() or a.numel() % 8:
+        raise ValueError("add_act: bad shapes")
+    kernels().add_act(ptr(a), ptr(b), ptr(out), a.numel(), int(relu), stream_handle(stream))
+    return out
+
+
+def relu(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    _chk(x, name="x"); _chk(out, name="out")
+    if x.numel() != out.numel() or x.numel() % 8:
+        raise ValueError("relu: bad shapes")
+    kernels().relu(ptr(x), ptr(out), x.numel(), stream_handle(stream))
+    return out
+
+
+def maxpool(x: torch.Tensor, out: torch.Tensor, k: int, s: int, pad_t: int = 0, pad_l: int = 0,
+            pad_zero: bool = True, stream=None) -> torch.Tensor:
+    _chk(x, name="x"); _chk(out, name="out")
+    B, H, W, C = x.shape
+    Bo, OH, OW, Co = out.shape
+    if Bo != B or Co != C or C % 8:
+        raise ValueError("maxpool: bad shapes")
+    # every output window must start inside the padded extent
+    if (OH - 1) * s - pad_t + k > H + pad_t + 2 * k or (OW - 1) * s - pad_l + k > W + pad_l + 2 * k:
+        raise ValueError("maxpool: output larger than padded input")
+    kernels().maxpool(ptr(x), ptr(out), B, H, W, C, OH, OW, k, s, pad_t, pad_l, int(pad_zero), stream_handle(stream))
+    return out
+
+
+def gap(x: torch.Tensor, out: Optional[torch.Tensor] = None, out32: Optional[torch.Tensor] = None,
+        stream=None) -> torch.Tensor:
+    _chk(x, name="x")
+    B, H, W, C = x.shape
+    if C % 8:
+        raise ValueError("gap: C % 8 != 0")
+    if out is not None:
+        _chk(out, name="out")
+        if out.numel() != B * C:
+            raise ValueError("gap: bad out")
+    if out32 is not None:
+        _chk(out32, torch.float32, "out32")
+        if out32.numel() != B * C:
+            raise ValueError("gap: bad out32")
+    kernels().gap(ptr(x), ptr(out), ptr(out32), B, H * W, C, stream_handle(stream))
+    return out if out is not None else out32
+
+
+def softmax_rows(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    rows, n = x.shape
+    if out.shape != x.shape:
+        raise ValueError("softmax: bad out")
+    kernels().softmax_rows(ptr(x), ptr(out), rows, n, n, stream_handle(stream))
+    return out
+
+
+def cast_bf16_f32(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    _chk(x, name="x"); _chk(out, torch.float32, "out")
+    if x.numel() != out.numel():
+        raise ValueError("cast: size mismatch")
+    kernels().cast_bf16_f32(ptr(x), ptr(out), x.numel(), stream_handle(stream))
+    return out
+
+
+def cast_f32_bf16(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    _chk(x, torch.float32, "x"); _chk(out, name="out")
+    if x.numel() != out.numel():
+        raise ValueError("cast: size mismatch")
+    kernels().cast_f32_bf16(ptr(x), ptr(out), x.numel(), stream_handle(stream))
+    return out
+
+
+def pad(x: torch.Tensor, out: torch.Tensor, pad_t: int, pad_l: int, stream=None) -> torch.Tensor:
+    """Materialised zero padding (NHWC)."""
+    _chk(x, name="x"); _chk(out, name="out")
+    B, H, W, C = x.shape
+    Bo, OH, OW, Co = out.shape
+    if Bo != B or Co != C or C % 8 or OH < H + pad_t or OW < W + pad_l:
+        raise ValueError("pad: bad shapes")
+    kernels().pad(ptr(x), ptr(out), B, H, W, C, OH, OW, pad_t, pad_l, stream_handle(stream))
+    return out

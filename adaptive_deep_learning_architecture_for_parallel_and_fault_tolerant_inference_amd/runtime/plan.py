@@ -1,0 +1,178 @@
+"""Launch-plan compiler: graph (slice) -> fused kernel steps.
+
+The reference re-creates each slice as a Keras model on the worker
+(`src/node.py:40-45,77-78`) and calls `model.predict` per request
+(`src/node.py:177`), i.e. one TF op per Keras layer.  Here a slice is
+compiled once into a short list of fused steps that map 1:1 onto our HIP
+kernels:
+
+* ``conv``     Conv2D [+BN folded] [+Add residual] [+ReLU]; a preceding
+               ZeroPadding2D is folded into the conv's address math
+* ``maxpool``  [ZeroPadding2D +] MaxPooling2D
+* ``bn``       standalone BN [+ReLU] (only when a cut exposes the raw conv output)
+* ``add``      standalone Add [+ReLU]
+* ``relu``, ``pad`` (materialised ZeroPadding2D), ``gap``,
+* ``dense``    Dense (+softmax) as a GEMM on the conv kernel + row softmax
+* ``pack``     fp32 image -> bf16 NHWC padded to 8 channels (stem input)
+
+Fusion never hides a tensor that the slice must emit or that another layer
+consumes, so any cut (including the multi-tensor frontier of BASELINE
+config 2) is executable.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Set
+
+from ..graph.ir import Graph
+
+
+@dataclass
+class Step:
+    kind: str
+    out: str                       # tensor name produced (name of the last covered layer)
+    ins: List[str]                 # tensor names consumed (physical names)
+    covers: List[str]              # graph layers executed by this step
+    p: Dict = field(default_factory=dict)
+
+
+def _phys(name: str, packed: Set[str]) -> str:
+    return name + "#packed" if name in packed else name
+
+
+def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
+    outputs = list(outputs or g.output_names)
+    outset = set(outputs)
+    cons = g.consumers()
+    done: Set[str] = set()
+    produced: Set[str] = set()
+    steps: List[Step] = []
+    packed: Set[str] = set()
+    pad_fold: Dict[str, tuple] = {}     # consumer layer -> (source tensor, pad)
+
+    def single(n: str) -> Optional[str]:
+        """The unique consumer of n, if n may be fused into it."""
+        if n in outset:
+            return None
+        c = cons.get(n, [])
+        return c[0] if len(c) == 1 else None
+
+    for n in g.order:
+        L = g.layers[n]
+        if L.op != "input":
+            continue
+        produced.add(n)
+        done.add(n)
+        c = L.out_shape[-1] if L.out_shape else 0
+        if len(L.out_shape) == 3 and c % 8 and L.attrs.get("stands_for", "input") == "input":
+            packed.add(n)
+            steps.append(Step("pack", n + "#packed", [n], [], {"cin": c, "cpad": ((c + 7) // 8) * 8}))
+
+    for n in g.order:
+        if n in done:
+            continue
+        L = g.layers[n]
+        a = L.attrs
+        if L.op == "zeropad":
+            c = single(n)
+            if c is not None and g.layers[c].op in ("conv", "maxpool") and g.layers[c].attrs.get("padding", "valid") == "valid":
+                pad_fold[c] = (L.inputs[0], a["pad"])
+                done.add(n)
+                continue
+            steps.append(Step("pad", n, [_phys(L.inputs[0], packed)], [n], {"pad": a["pad"]}))
+        elif L.op == "conv":
+            src = L.inputs[0]
+            pads = ((0, 0), (0, 0))
+            cover = [n]
+            if n in pad_fold:
+                src, pads = pad_fold[n]
+                cover = [g.layers[n].inputs[0], n]
+            if a.get("padding", "valid") == "same":
+                kh, kw = a["kernel"]
+                pads = (((kh - 1) // 2, kh - 1 - (kh - 1) // 2), ((kw - 1) // 2, kw - 1 - (kw - 1) // 2))
+                if a.get("stride", 1) != 1:
+                    raise NotImplementedError("'same' padding with stride > 1")
+            bn = None
+            relu = False
+            res = None
+            out = n
+            c1 = single(n)
+            if c1 is not None and g.layers[c1].op == "bn":
+                bn = c1
+                cover.append(c1)
+                out = c1
+                c2 = single(c1)
+                if c2 is not None and g.layers[c2].op == "relu":
+                    relu = True
+                    cover.append(c2)
+                    out = c2
+                elif c2 is not None and g.layers[c2].op == "add" and len(g.layers[c2].inputs) == 2:
+                    other = [i for i in g.layers[c2].inputs if i != c1]
+                    if len(other) == 1 and other[0] in produced:
+                        res = other[0]
+                        cover.append(c2)
+                        out = c2
+                        c3 = single(c2)
+                        if c3 is not None and g.layers[c3].op == "relu":
+                            relu = True
+                            cover.append(c3)
+                            out = c3
+            steps.append(Step("conv", out, [_phys(src, packed)] + ([res] if res else []), cover,
+                              {"conv": n, "bn": bn, "relu": relu, "residual": res, "pads": pads,
+                               "stride": a.get("stride", 1), "kernel": tuple(a["kernel"]),
+                               "filters": a["filters"], "packed_input": src in packed}))
+            done.update(cover)
+        elif L.op == "maxpool":
+            src = L.inputs[0]
+            pads = ((0, 0), (0, 0))
+            cover = [n]
+            if n in pad_fold:
+                src, pads = pad_fold[n]
+                cover = [L.inputs[0], n]
+            steps.append(Step("maxpool", n, [_phys(src, packed)], cover,
+                              {"pool": a["pool"], "stride": a["stride"], "pads": pads}))
+            done.update(cover)
+        elif L.op == "bn":
+            cover = [n]
+            relu = False
+            out = n
+            c = single(n)
+            if c is not None and g.layers[c].op == "relu":
+                relu = True
+                cover.append(c)
+                out = c
+            steps.append(Step("bn", out, [L.inputs[0]], cover, {"bn": n, "relu": relu}))
+            done.update(cover)
+        elif L.op == "add":
+            cover = [n]
+            relu = False
+            out = n
+            c = single(n)
+            if c is not None and g.layers[c].op == "relu":
+                relu = True
+                cover.append(c)
+                out = c
+            if len(L.inputs) != 2:
+                raise NotImplementedError("add with != 2 inputs")
+            steps.append(Step("add", out, list(L.inputs), cover, {"relu": relu}))
+            done.update(cover)
+        elif L.op == "relu":
+            steps.append(Step("relu", n, [L.inputs[0]], [n]))
+            done.add(n)
+        elif L.op == "gap":
+            steps.append(Step("gap", n, [L.inputs[0]], [n]))
+            done.add(n)
+        elif L.op == "dense":
+            steps.append(Step("dense", n, [L.inputs[0]], [n],
+                              {"units": a["units"], "softmax": a.get("activation") == "softmax"}))
+            done.add(n)
+        elif L.op == "softmax":
+            steps.append(Step("softmax", n, [L.inputs[0]], [n]))
+            done.add(n)
+        else:
+            raise NotImplementedError(f"op {L.op}")
+        produced.add(steps[-1].out)
+    missing = [o for o in outputs if o not in produced]
+    if missing:
+        raise RuntimeError(f"plan does not produce outputs {missing}")
+    return steps

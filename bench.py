@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 inference images/sec (whole node), bs=32 per
+pipeline micro-batch, synthetic 224x224x3 input, random-init weights
+(BASELINE.json: "images/sec (whole node) ResNet-50 bs=32 at 1/2/4/8 MI355X").
+
+Single GPU:    python bench.py --steps 50 --warmup 10
+N GPUs:        python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+                   --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+Parallelism (``--mode``):
+  dp    every GPU runs the whole model on its own bs=32 batch (replicas)
+  pp    the model is cut into N stages (balanced planner or --part-at), one per
+        GPU; bs=32 micro-batches stream through RCCL send/recv over xGMI
+  ppdp  R replicas of a k-stage pipeline (R*k = N), --stages k
+A step = one bs=32 batch per pipeline replica slot: dp processes 32*N images
+per step, pp keeps N micro-batches in flight and completes N per step, so
+per-GPU work is fixed as N grows (weak scaling) in every mode.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+PKG = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--mode", default="dp", choices=["dp", "pp", "ppdp"])
+    ap.add_argument("--stages", type=int, default=0, help="stages per pipeline for ppdp")
+    ap.add_argument("--part-at", default="", help="comma-separated cut layers (pp)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--tune", action="store_true", help="autotune conv tiles before timing")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+BASELINE_IMG_S = None   # the reference publishes no absolute number
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from importlib import import_module
+    resnet = import_module(f"{PKG}.models.resnet")
+    runner = import_module(f"{PKG}.parallel.runner")
+
+    g = resnet.build_resnet(args.model)
+    weights = resnet.init_weights(g, seed=args.seed)
+    part_at = [s for s in args.part_at.split(",") if s]
+    job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
+                           stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune)
+    # synthetic input, resident on device (data="synthetic")
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    job.set_synthetic_input(torch.randn((args.batch, 224, 224, 3), generator=gen, device=dev))
+
+    for _ in range(args.warmup):
+        job.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        job.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    images = job.images_per_step * args.steps
+    value = images / elapsed
+    if rank == 0:
+        rec = {
+            "metric": "images/sec (whole node) ResNet-50 bs=32",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / BASELINE_IMG_S, 4) if BASELINE_IMG_S else None),
+            "dtype": "bf16",
+            "data": "synthetic 224x224x3 NHWC fp32 input, random-init weights (seeded)",
+            "config": {"model": args.model, "global_batch": job.global_batch, "seq_len": None,
+                       "image": [224, 224, 3], "parallelism": job.parallelism, "part_at": job.part_at,
+                       "micro_batch": args.batch, "hipgraph": not args.no_graph},
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+// pybind11 bindings for the gfx950 kernels.  Tensors cross the boundary as
+// raw device pointers (uintptr_t) plus the HIP stream handle of the caller's
+// current torch stream, so launches are captured by hipGraphs the runtime
+// records (runtime/executor.py).  Shape checks happen on the host in
+// ops/*.py before any launch.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.h"
+
+
+
+namespace py = pybind11;
+using u64 = uintptr_t;
+
+static void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+template <typename T>
+static T* P(u64 v) { return reinterpret_cast<T*>(v); }
+static hipStream_t S(u64 v) { return reinterpret_cast<hipStream_t>(v); }
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "ADAPT MI355X (gfx950) HIP kernels";
+  m.def("conv_num_cfgs", &adapt::conv_num_cfgs);
+  m.def("conv_cfg_tile", [](int cfg) {
+    int bm, bn;
+    adapt::conv_cfg_tile(cfg, &bm, &bn);
+    return py::make_tuple(bm, bn);
+  });
+  m.def(
+      "conv_forward",
+      [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, int B, int H, int W, int Cin, int OH, int OW, int N,
+         int KH, int KW, int stride, int pad_t, int pad_l, int K, int Kpad, int ldo, int relu, int ksplit, int cfg,
+         bool out_f32, u64 stream) {
+        adapt::ConvParams p;
+        p.x = P<const bf16>(x);
+        p.w = P<const bf16>(w);
+        p.bias = P<const float>(bias);
+        p.res = P<const bf16>(res);
+        p.out = P<void>(out);
+        p.ws = P<float>(ws);
+        p.B = B; p.H = H; p.W = W; p.Cin = Cin;
+        p.OH = OH; p.OW = OW; p.N = N;
+        p.KH = KH; p.KW = KW; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
+        p.M = B * OH * OW; p.K = K; p.Kpad = Kpad; p.ldo = ldo;
+        p.relu = relu; p.ksplit = ksplit < 1 ? 1 : ksplit;
+        py::gil_scoped_release nogil;
+        check(adapt::conv_forward(p, cfg, S(stream), out_f32), "conv_forward");
+      });
+  m.def("input_pack", [](u64 x, u64 y, size_t pixels, int C, int Cp, u64 s) {
+    check(adapt::input_pack(P<const float>(x), P<bf16>(y), pixels, C, Cp, S(s)), "input_pack");
+  });
+  m.def("bn_act", [](u64 x, u64 y, u64 scale, u64 shift, size_t elems, int C, int relu, u64 s) {
+    check(adapt::bn_act(P<const bf16>(x), P<bf16>(y), P<const float>(scale), P<const float>(shift), elems, C, relu,
+                        S(s)), "bn_act");
+  });
+  m.def("add_act", [](u64 a, u64 b, u64 y, size_t elems, int relu, u64 s) {
+    check(adapt::add_act(P<const bf16>(a), P<const bf16>(b), P<bf16>(y), elems, relu, S(s)), "add_act");
+  });
+  m.def("relu", [](u64 x, u64 y, size_t elems, u64 s) {
+    check(adapt::relu(P<const bf16>(x), P<bf16>(y), elems, S(s)), "relu");
+  });
+  m.def("maxpool", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int K, int Sd, int pad_t, int pad_l,
+                      int pad_zero, u64 s) {
+    check(adapt::maxpool(P<const bf16>(x), P<bf16>(y), B, H, W, C, OH, OW, K, Sd, pad_t, pad_l, pad_zero, S(s)),
+          "maxpool");
+  });
+  m.def("gap", [](u64 x, u64 y, u64 y32, int B, int HW, int C, u64 s) {
+    check(adapt::gap(P<const bf16>(x), P<bf16>(y), P<float>(y32), B, HW, C, S(s)), "gap");
+  });
+  m.def("softmax_rows", [](u64 x, u64 y, int rows, int N, int ldx, u64 s) {
+    check(adapt::softmax_rows(P<const float>(x), P<float>(y), rows, N, ldx, S(s)), "softmax_rows");
+  });
+  m.def("pad", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int pt, int pl, u64 s) {
+    check(adapt::pad(P<const bf16>(x), P<bf16>(y), B, H, W, C, OH, OW, pt, pl, S(s)), "pad");
+  });
+  m.def("cast_bf16_f32", [](u64 x, u64 y, size_t n, u64 s) {
+    check(adapt::cast_bf16_f32(P<const bf16>(x), P<float>(y), n, S(s)), "cast_bf16_f32");
+  });
+  m.def("cast_f32_bf16", [](u64 x, u64 y, size_t n, u64 s) {
+    check(adapt::cast_f32_bf16(P<const float>(x), P<bf16>(y), n, S(s)), "cast_f32_bf16");
+  });
+}

@@ -1,0 +1,36 @@
+// Host-visible declarations of the ADAPT gfx950 kernels.
+#pragma once
+#include "common.h"
+
+namespace adapt {
+struct ConvParams {
+  const bf16* x;
+  const bf16* w;
+  const float* bias;
+  const bf16* res;
+  void* out;
+  float* ws;
+  int B, H, W, Cin;
+  int OH, OW, N;
+  int KH, KW, stride, pad_t, pad_l;
+  int M, K, Kpad, ldo;
+  int relu;
+  int ksplit;
+};
+hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
+int conv_num_cfgs();
+void conv_cfg_tile(int cfg, int* bm, int* bn);
+hipError_t input_pack(const float* x, bf16* y, size_t pixels, int C, int Cp, hipStream_t s);
+hipError_t bn_act(const bf16* x, bf16* y, const float* scale, const float* shift, size_t elems, int C, int relu,
+                  hipStream_t s);
+hipError_t add_act(const bf16* a, const bf16* b, bf16* y, size_t elems, int relu, hipStream_t s);
+hipError_t relu(const bf16* x, bf16* y, size_t elems, hipStream_t s);
+hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
+                   int pad_l, int pad_zero, hipStream_t s);
+hipError_t gap(const bf16* x, bf16* y, float* y32, int B, int HW, int C, hipStream_t s);
+hipError_t softmax_rows(const float* x, float* y, int rows, int N, int ldx, hipStream_t s);
+hipError_t cast_bf16_f32(const bf16* x, float* y, size_t n, hipStream_t s);
+hipError_t pad(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
+               hipStream_t s);
+hipError_t cast_f32_bf16(const float* x, bf16* y, size_t n, hipStream_t s);
+}  // namespace adapt

@@ -1,0 +1,132 @@
+"""Numerics of every gfx950 kernel against a plain PyTorch fp32 reference
+(SURVEY §4 item 2).  Runs only on the MI355X box (`-m gpu`)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+PKG = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import importlib
+    conv = importlib.import_module(f"{PKG}.ops.conv")
+    E = importlib.import_module(f"{PKG}.ops.eltwise")
+    lib = importlib.import_module(f"{PKG}.ops._lib")
+    lib.kernels()   # must load the in-tree HIP library
+    return conv, E
+
+
+def _ref_conv(x_nhwc, k_hwio, bias, stride, pads, residual=None, relu=False):
+    x = x_nhwc.float().permute(0, 3, 1, 2)
+    (pt, pb), (pl, pr) = pads
+    x = F.pad(x, (pl, pr, pt, pb))
+    w = k_hwio.float().permute(3, 2, 0, 1)
+    y = F.conv2d(x, w, bias.float(), stride=stride).permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y
+
+
+CONV_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad
+    (2, 56, 56, 64, 64, 1, 1, 0),
+    (2, 56, 56, 64, 256, 1, 1, 0),
+    (2, 56, 56, 64, 64, 3, 1, 1),
+    (2, 56, 56, 256, 128, 1, 2, 0),
+    (2, 28, 28, 128, 128, 3, 1, 1),
+    (4, 7, 7, 512, 512, 3, 1, 1),
+    (2, 14, 14, 1024, 2048, 1, 2, 0),
+    (2, 224, 224, 8, 64, 7, 2, 3),     # stem (input padded to 8 channels)
+    (3, 9, 11, 24, 40, 3, 2, 1),       # odd sizes, M/N tails
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5])
+def test_conv_vs_torch(ops, case, cfg):
+    conv, _ = ops
+    B, H, W, Cin, Cout, k, s, p = case
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(B, H, W, Cin, device=dev).to(torch.bfloat16)
+    kern = (torch.randn(k, k, Cin, Cout) / math.sqrt(k * k * Cin)).numpy()
+    bias = (torch.randn(Cout) * 0.1).numpy()
+    pc = conv.pack_conv(kern, bias, s, ((p, p), (p, p)), dev)
+    OH, OW = pc.out_hw(H, W)
+    res = torch.randn(B, OH, OW, Cout, device=dev).to(torch.bfloat16)
+    out = torch.empty(B, OH, OW, Cout, device=dev, dtype=torch.bfloat16)
+    ks = 1
+    ws = None
+    if cfg is not None and pc.Kpad // 64 >= 4:
+        ks = 2
+        ws = torch.empty(ks * B * OH * OW * Cout, device=dev, dtype=torch.float32)
+    conv.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws)
+    torch.cuda.synchronize()
+    wq = torch.from_numpy(kern).to(dev).to(torch.bfloat16).float()      # kernel sees bf16 weights
+    ref = _ref_conv(x, wq, torch.from_numpy(bias).to(dev), s, ((p, p), (p, p)), res, True)
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
+
+
+def test_conv_f32_out_dense(ops):
+    conv, _ = ops
+    dev = "cuda"
+    B, K, N = 32, 2048, 1000
+    x = torch.randn(B, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, N) / math.sqrt(K)).numpy()
+    b = torch.randn(N).numpy()
+    pc = conv.pack_conv(w.reshape(1, 1, K, N), b, 1, ((0, 0), (0, 0)), dev)
+    out = torch.empty(B, N, device=dev, dtype=torch.float32)
+    conv.conv_forward(x, pc, out)
+    ref = x.float() @ torch.from_numpy(w).to(dev).to(torch.bfloat16).float() + torch.from_numpy(b).to(dev)
+    assert torch.allclose(out, ref, atol=2e-2, rtol=2e-2)
+
+
+def test_eltwise(ops):
+    _, E = ops
+    dev = "cuda"
+    torch.manual_seed(1)
+    x = torch.randn(2, 9, 10, 64, device=dev).to(torch.bfloat16)
+    y = torch.randn(2, 9, 10, 64, device=dev).to(torch.bfloat16)
+    out = torch.empty_like(x)
+    E.relu(x, out)
+    assert torch.equal(out, torch.relu(x))
+    E.add_act(x, y, out, relu=True)
+    assert torch.allclose(out.float(), torch.relu(x.float() + y.float()), atol=1e-2, rtol=1e-2)
+    sc = torch.rand(64, device=dev) + 0.5
+    sh = torch.randn(64, device=dev)
+    E.bn_act(x, sc, sh, out, relu=False)
+    assert torch.allclose(out.float(), x.float() * sc + sh, atol=2e-2, rtol=1e-2)
+    # maxpool with Keras zero-pad semantics
+    xp = torch.randn(2, 112, 112, 64, device=dev).to(torch.bfloat16)
+    mp = torch.empty(2, 56, 56, 64, device=dev, dtype=torch.bfloat16)
+    E.maxpool(xp, mp, 3, 2, 1, 1, True)
+    ref = F.max_pool2d(F.pad(xp.float().permute(0, 3, 1, 2), (1, 1, 1, 1)), 3, 2).permute(0, 2, 3, 1)
+    assert torch.equal(mp.float(), ref)
+    # gap
+    g = torch.empty(2, 64, device=dev, dtype=torch.bfloat16)
+    g32 = torch.empty(2, 64, device=dev, dtype=torch.float32)
+    E.gap(xp, g, g32)
+    assert torch.allclose(g32, xp.float().mean(dim=(1, 2)), atol=1e-3, rtol=1e-3)
+    # softmax
+    lg = torch.randn(4, 1000, device=dev) * 5
+    pr = torch.empty_like(lg)
+    E.softmax_rows(lg, pr)
+    assert torch.allclose(pr, torch.softmax(lg, -1), atol=1e-5, rtol=1e-4)
+    # input pack + pad
+    img = torch.randn(2, 5, 6, 3, device=dev)
+    pk = torch.empty(2, 5, 6, 8, device=dev, dtype=torch.bfloat16)
+    E.input_pack(img, pk)
+    assert torch.equal(pk[..., :3], img.to(torch.bfloat16)) and pk[..., 3:].abs().sum().item() == 0
+    pd = torch.empty(2, 11, 12, 64, device=dev, dtype=torch.bfloat16)
+    E.pad(x, pd, 1, 1)
+    assert torch.equal(pd, F.pad(x, (0, 0, 1, 1, 1, 1)))
