@@ -1,0 +1,109 @@
+"""Array codecs for the wire (weights, activations, inputs, results).
+
+Reference: every array crossing a socket is ``lz4.frame.compress(
+zfpy.compress_numpy(arr))`` (`src/dispatcher.py:92-98`, `src/node.py:122-125`),
+unconditionally.  We keep that codec as ``"zfp+lz4"`` (native, see
+csrc/runtime) and add policies, because over xGMI compression only pays when
+codec throughput beats the link:
+
+* ``"zfp+lz4"``  reference behaviour (float32/float64 arrays)
+* ``"lz4"``      LZ4 frame over the raw bytes (any dtype, incl. bf16)
+* ``"none"``     raw bytes
+
+Every encoded message is self-describing::
+
+    u8 codec | u8 dtype | u8 ndim | u8 flags | u64 shape[ndim] | payload
+
+so the receiver never needs out-of-band metadata.  A codec that would expand
+the data falls back to ``none`` for that message.
+"""
+from __future__ import annotations
+
+import struct
+from typing import Tuple
+
+import numpy as np
+
+from ..native import runtime
+
+CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3}
+_CODEC_NAMES = {v: k for k, v in CODECS.items()}
+# dtype codes (bf16 travels as raw 16-bit words)
+DTYPES = {0: np.float32, 1: np.float64, 2: np.float16, 3: np.uint16, 4: np.int32, 5: np.int64, 6: np.uint8,
+          7: np.int8, 8: np.bool_}
+BF16 = 9          # flag value: payload is bfloat16 (numpy has no bf16; carried as uint16)
+_DT_CODE = {np.dtype(v): k for k, v in DTYPES.items()}
+
+
+def _header(codec: int, dtype_code: int, shape: Tuple[int, ...]) -> bytes:
+    return struct.pack(f"<BBBB{len(shape)}Q", codec, dtype_code, len(shape), 0, *shape)
+
+
+def _parse(buf: bytes):
+    codec, dt, nd, _flags = struct.unpack_from("<BBBB", buf, 0)
+    shape = struct.unpack_from(f"<{nd}Q", buf, 4)
+    return codec, dt, tuple(shape), 4 + 8 * nd
+
+
+def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads: int = 4) -> bytes:
+    """Encode an ndarray.  `bf16=True` marks a uint16 array as bfloat16 payload."""
+    arr = np.ascontiguousarray(arr)
+    rt = runtime()
+    dt_code = BF16 if bf16 else _DT_CODE.get(arr.dtype)
+    if dt_code is None:
+        raise TypeError(f"unsupported dtype {arr.dtype}")
+    c = CODECS[codec]
+    if c in (2, 3) and arr.dtype not in (np.float32, np.float64):
+        c = 1                               # zfp is float32/float64 only
+    if c in (2, 3) and (arr.ndim > 4 or arr.ndim == 0):
+        arr_z = arr.reshape(-1) if arr.ndim == 0 else arr.reshape((-1,) + arr.shape[-3:])
+    else:
+        arr_z = arr
+    raw = arr.view(np.uint8).reshape(-1) if arr.size else np.zeros(0, np.uint8)
+    if c == 0:
+        payload = raw.tobytes()
+    elif c == 1:
+        payload = rt.lz4_compress(raw)
+    elif c == 2:
+        payload = rt.lz4_compress(rt.zfp_compress(arr_z, threads))
+    else:
+        payload = rt.zfp_compress(arr_z, threads)
+    if c != 0 and len(payload) >= raw.nbytes:
+        c, payload = 0, raw.tobytes()
+    return _header(c, dt_code, arr.shape) + payload
+
+
+def decode(buf, threads: int = 4) -> np.ndarray:
+    """Inverse of `encode`.  bfloat16 payloads come back as uint16 arrays
+    (use `is_bf16` to tell); everything else with its own dtype."""
+    buf = bytes(buf) if not isinstance(buf, (bytes, bytearray, memoryview)) else buf
+    codec, dt, shape, off = _parse(buf)
+    rt = runtime()
+    body = memoryview(buf)[off:]
+    np_dt = np.uint16 if dt == BF16 else DTYPES[dt]
+    if codec == 0:
+        return np.frombuffer(bytes(body), dtype=np_dt).reshape(shape).copy()
+    if codec == 1:
+        return np.frombuffer(rt.lz4_decompress(body), dtype=np_dt).reshape(shape).copy()
+    if codec == 2:
+        return rt.zfp_decompress(rt.lz4_decompress(body), threads).reshape(shape)
+    if codec == 3:
+        return rt.zfp_decompress(body, threads).reshape(shape)
+    raise ValueError(f"unknown codec id {codec}")
+
+
+def is_bf16(buf) -> bool:
+    return _parse(buf)[1] == BF16
+
+
+def codec_of(buf) -> str:
+    return _CODEC_NAMES[_parse(buf)[0]]
+
+
+# reference-named helpers (`_comp` / `_decomp`, src/dispatcher.py:92-98)
+def comp(arr: np.ndarray) -> bytes:
+    return encode(arr, "zfp+lz4")
+
+
+def decomp(byts) -> np.ndarray:
+    return decode(byts)

@@ -1,0 +1,95 @@
+"""`Model`: a graph + its weights, with the slice of the Keras Model API the
+reference uses (`get_layer`, `layers`, `input`/`output`, `get_weights`,
+`set_weights`, `to_json`, `summary`, `predict`, `count_params`;
+`src/dispatcher.py:43-48,235-243`, `test/test.py:13-14`)."""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..graph.ir import Graph, Layer
+
+
+class Model:
+    def __init__(self, graph: Graph, weights: Dict[str, np.ndarray], name: Optional[str] = None):
+        self.graph = graph
+        self.weights = weights
+        self.name = name or graph.name
+        self._executors = {}
+
+    # ------------------------------------------------ Keras-like surface
+    @property
+    def layers(self) -> List[Layer]:
+        return [self.graph.layers[n] for n in self.graph.order]
+
+    def get_layer(self, name: str) -> Layer:
+        return self.graph.get_layer(name)
+
+    @property
+    def input(self) -> str:
+        return self.graph.input
+
+    @property
+    def output(self) -> str:
+        return self.graph.output
+
+    def get_weights(self) -> List[np.ndarray]:
+        return [self.weights[n] for n, _ in self.graph.weight_specs()]
+
+    def set_weights(self, arrays: List[np.ndarray]) -> None:
+        from .resnet import set_weights
+        self.weights = set_weights(self.graph, arrays)
+        self._executors.clear()
+
+    def to_json(self) -> str:
+        return self.graph.to_json()
+
+    def summary(self, print_fn=print) -> str:
+        s = self.graph.summary()
+        if print_fn:
+            print_fn(s)
+        return s
+
+    def count_params(self) -> int:
+        return self.graph.count_params()
+
+    # ------------------------------------------------------------ compute
+    def predict(self, x: np.ndarray, device: Optional[str] = None, batch: Optional[int] = None) -> np.ndarray:
+        """Single-device inference (`test/local_infer.py:22`): our HIP runtime on
+        a GPU, the fp32 oracle on CPU.  Inputs are NHWC float32 images."""
+        import torch
+        x = np.asarray(x, np.float32)
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device == "cpu":
+            from ..ops.reference import ReferenceExecutor
+            ex = self._executors.get("cpu")
+            if ex is None:
+                ex = self._executors["cpu"] = ReferenceExecutor(self.graph, self.weights)
+            return ex(torch.from_numpy(x)).numpy()
+        from ..runtime.executor import SliceExecutor
+        b = batch or x.shape[0]
+        key = (device, b)
+        ex = self._executors.get(key)
+        if ex is None:
+            ex = self._executors[key] = SliceExecutor(self.graph, self.weights, b, device=device)
+        outs = []
+        for i in range(0, x.shape[0], b):
+            chunk = x[i:i + b]
+            n = chunk.shape[0]
+            if n < b:
+                chunk = np.concatenate([chunk, np.zeros((b - n,) + chunk.shape[1:], np.float32)])
+            y = ex(torch.from_numpy(chunk).to(device))
+            outs.append(y[:n].float().cpu().numpy())
+        return np.concatenate(outs)
+
+    def __call__(self, x, **kw):
+        return self.predict(x, **kw)
+
+
+def resnet(depth: str = "resnet50", seed: int = 0, weights: Optional[Dict[str, np.ndarray]] = None, **kw) -> Model:
+    """`ResNet50(weights=...)` analogue: random-init (seeded) or given weights."""
+    from .resnet import build_resnet, init_weights
+    g = build_resnet(depth, **kw)
+    return Model(g, weights if weights is not None else init_weights(g, seed))

@@ -23,6 +23,8 @@ STACKS = {
     "resnet50": (3, 4, 6, 3),
     "resnet101": (3, 4, 23, 3),
     "resnet152": (3, 8, 36, 3),
+    "resnet_tiny": (1, 1, 1, 1),     # same layer naming/structure; for fast CPU tests
+    "resnet_mini": (2, 2, 2, 2),
 }
 
 

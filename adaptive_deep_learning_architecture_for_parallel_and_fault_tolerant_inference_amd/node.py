@@ -1,0 +1,404 @@
+"""Worker node: one process per MI355X (public API of `src/node.py`).
+
+Reference worker (`src/node.py:24-211`): a config server receives the Keras
+JSON + index + weights and ACKs (`:65-98`), a data server reads activations
+(`:137-161`), a client loop runs ``model.predict`` and forwards the result
+(`:163-179`); the process registers nowhere although the dispatcher waits on
+etcd for it.  Here:
+
+* **membership**: a leased ``/workers/{id}`` record (host, ports, device,
+  state, epoch) with a keepalive heartbeat; death => lease expiry => the
+  dispatcher repartitions;
+* **config server** (``config_port``, 6001): framed JSON command, then for
+  ``configure`` the slice (manifest + ASCII index + weights, the reference
+  order) and an ACK ``0x06`` (NAK ``0x15`` + reason frame on failure);
+* **data plane** per *epoch*: ``StageRuntime`` receives micro-batches from its
+  upstream (dispatcher for stage 0, previous stage otherwise), runs the slice
+  (our HIP runtime on the GPU, the fp32 oracle on CPU) and forwards to its
+  downstream (next stage, or the dispatcher's result port for the last
+  stage).  Receive, compute and send run on three threads with bounded
+  queues so transfers overlap compute.  A new ``configure`` aborts the old
+  epoch's links (sockets closed => blocked peers unblock) and starts the new
+  one — this is how survivors re-form a pipeline after a failure;
+* **links**: TCP framed messages (any host, CPU or GPU; codec per link), or
+  RCCL point-to-point over xGMI between GPU stages (parallel/rccl_link.py).
+
+CLI:  python -m <pkg>.node --dispatcher 127.0.0.1 --membership-port 2379 \
+          --data-port 6000 --config-port 6001 --device cuda:0
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import queue
+import socket
+import threading
+import time
+import traceback
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from .graph.manifest import ACK, NAK, SliceManifest, arrays_to_dict, recv_slice
+from .node_state import NodeState, StateEnum, socket_recv, socket_send
+from .transport.messages import Message, connect, listen, recv_message, send_message
+
+DATA_PORT = 6000     # receive input data      (src/node.py:20)
+CONFIG_PORT = 6001   # receive model config    (src/node.py:21)
+RESULT_PORT = 6003   # send results            (src/node.py:22)
+CTRL_CHUNK = 1 << 16
+
+
+def get_local_ip() -> str:
+    """UDP-connect trick with 127.0.0.1 fallback (`src/node.py:197-208`)."""
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        s.connect(("1.1.1.1", 1))
+        ip = s.getsockname()[0]
+    except OSError:
+        ip = "127.0.0.1"
+    finally:
+        s.close()
+    return ip
+
+
+class StageRuntime:
+    """One epoch's data plane on this node."""
+
+    def __init__(self, node: "Node", cfg: Dict, manifest: SliceManifest, weights: Dict[str, np.ndarray]):
+        from .runtime.stage import StageCompute
+        self.node = node
+        self.cfg = cfg
+        self.epoch = int(cfg["epoch"])
+        self.stage = int(cfg["stage"])
+        self.codec = cfg.get("codec", "lz4")
+        self.manifest = manifest
+        g = manifest.graph()
+        self.compute = StageCompute(g, weights, int(cfg["batch"]), node.device,
+                                    graph_capture=cfg.get("graph", True))
+        self.inq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
+        self.outq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
+        self.stop = threading.Event()
+        self.upstream: Optional[socket.socket] = None
+        self.downstream: Optional[socket.socket] = None
+        self.processed = 0
+        self.threads = []
+        self.error: Optional[str] = None
+
+    # downstream = next stage's data port, or the dispatcher result port
+    def _connect_downstream(self) -> socket.socket:
+        nxt = self.cfg.get("next")
+        hello = json.dumps({"epoch": self.epoch, "from_stage": self.stage,
+                            "replica": self.cfg.get("replica", 0)}).encode()
+        host, port = (nxt["host"], nxt["port"]) if nxt else tuple(self.cfg["result_addr"])
+        deadline = time.time() + float(self.cfg.get("connect_timeout", 10.0))
+        while True:
+            try:
+                return connect(host, int(port), hello=hello)
+            except OSError:
+                if time.time() > deadline or self.stop.is_set():
+                    raise
+                time.sleep(0.05)
+
+    def attach_upstream(self, sock: socket.socket) -> None:
+        self.upstream = sock
+        t = threading.Thread(target=self._recv_loop, daemon=True, name=f"stage{self.stage}-recv-e{self.epoch}")
+        t.start()
+        self.threads.append(t)
+
+    def start(self) -> None:
+        for fn, nm in ((self._compute_loop, "compute"), (self._send_loop, "send")):
+            t = threading.Thread(target=fn, daemon=True, name=f"stage{self.stage}-{nm}-e{self.epoch}")
+            t.start()
+            self.threads.append(t)
+
+    def _fail(self, where: str, e: BaseException) -> None:
+        if not self.stop.is_set():
+            self.error = f"{where}: {type(e).__name__}: {e}"
+        self.abort()
+
+    def _recv_loop(self) -> None:
+        try:
+            while not self.stop.is_set():
+                m = recv_message(self.upstream, self.node.state.chunk_size)
+                if m is None:
+                    break
+                if m.epoch != self.epoch:
+                    continue                     # stale micro-batch from an older epoch
+                while not self.stop.is_set():
+                    try:
+                        self.inq.put(m, timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+        except Exception as e:  # noqa: BLE001 - any transport error ends the epoch
+            self._fail("recv", e)
+
+    def _compute_loop(self) -> None:
+        try:
+            while not self.stop.is_set():
+                try:
+                    m = self.inq.get(timeout=0.1)
+                except queue.Empty:
+                    continue
+                self.node.state.state = StateEnum.BUSY
+                outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
+                self.processed += 1
+                out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
+                while not self.stop.is_set():
+                    try:
+                        self.outq.put(out, timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+        except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            self._fail("compute", e)
+
+    def _send_loop(self) -> None:
+        try:
+            self.downstream = self._connect_downstream()
+            while not self.stop.is_set():
+                try:
+                    m = self.outq.get(timeout=0.1)
+                except queue.Empty:
+                    continue
+                send_message(self.downstream, m, self.codec, self.node.state.chunk_size)
+        except Exception as e:  # noqa: BLE001
+            self._fail("send", e)
+
+    def abort(self) -> None:
+        self.stop.set()
+        for s in (self.upstream, self.downstream):
+            if s is not None:
+                try:
+                    s.shutdown(socket.SHUT_RDWR)
+                except OSError:
+                    pass
+                try:
+                    s.close()
+                except OSError:
+                    pass
+
+
+class Node:
+    def __init__(self, dispatcher_ip: str = "127.0.0.1", membership_port: int = 2379, data_port: int = DATA_PORT,
+                 config_port: int = CONFIG_PORT, device: Optional[str] = None, node_id: Optional[str] = None,
+                 chunk_size: int = 512 * 1000, host: str = "0.0.0.0", advertise_host: Optional[str] = None,
+                 heartbeat_ttl: float = 1.0, register: bool = True) -> None:
+        self.weights_ready_event = threading.Event()        # reference attribute (src/node.py:27)
+        if device is None:
+            import torch
+            device = "cuda:0" if torch.cuda.is_available() else "cpu"
+        self.device = device
+        self.host = host
+        self.advertise_host = advertise_host or ("127.0.0.1" if dispatcher_ip in ("127.0.0.1", "localhost")
+                                                 else get_local_ip())
+        self.data_sock = listen(host, data_port)
+        self.config_sock = listen(host, config_port)
+        self.data_port = self.data_sock.getsockname()[1]
+        self.config_port = self.config_sock.getsockname()[1]
+        self.node_id = node_id or f"{self.advertise_host}:{self.config_port}"
+        self.state = NodeState(chunk_size, dispatcher_ip, membership_port, node_id=self.node_id)
+        self.dispatcher_ip = dispatcher_ip
+        self.membership_port = membership_port
+        self.heartbeat_ttl = heartbeat_ttl
+        self.register = register
+        self.registration = None
+        self.runtime: Optional[StageRuntime] = None
+        self._rt_lock = threading.Lock()
+        self._pending_upstream: Dict[int, list] = {}
+        self._slice_cache: Dict[str, Tuple[SliceManifest, Dict[str, np.ndarray]]] = {}
+        self._stop = threading.Event()
+        self.threads = []
+
+    # ---------------------------------------------------------- lifecycle
+    def record(self) -> Dict:
+        rec = {"id": self.node_id, "host": self.advertise_host, "data_port": self.data_port,
+               "config_port": self.config_port, "device": self.device, "pid": os.getpid(),
+               "state": self.state.state.name, "epoch": self.state.epoch}
+        try:
+            import torch
+            if self.device.startswith("cuda"):
+                rec["gpu"] = torch.cuda.get_device_name(torch.device(self.device))
+        except Exception:  # noqa: BLE001 - telemetry is best effort
+            pass
+        return rec
+
+    def run(self, block: bool = True) -> None:
+        for fn, nm in ((self._config_server, "config"), (self._data_server, "data")):
+            t = threading.Thread(target=fn, daemon=True, name=f"node-{nm}")
+            t.start()
+            self.threads.append(t)
+        if self.register:
+            from .membership.client import MembershipClient, Registration
+            deadline = time.time() + 30
+            while True:
+                try:
+                    client = MembershipClient(self.dispatcher_ip, self.membership_port)
+                    self.registration = Registration(client, self.node_id, self.record(), ttl=self.heartbeat_ttl)
+                    break
+                except (OSError, ConnectionError):
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.2)
+        if block:
+            try:
+                while not self._stop.wait(1.0):
+                    pass
+            except KeyboardInterrupt:
+                pass
+            finally:
+                self.stop()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self.registration is not None:
+            self.registration.close(revoke=True)
+        with self._rt_lock:
+            if self.runtime is not None:
+                self.runtime.abort()
+        for s in (self.data_sock, self.config_sock):
+            try:
+                s.close()
+            except OSError:
+                pass
+
+    def _publish(self, **kw) -> None:
+        if self.registration is not None:
+            try:
+                self.registration.put(**kw)
+            except (OSError, ConnectionError, RuntimeError):
+                pass
+
+    # ------------------------------------------------------- config plane
+    def _config_server(self) -> None:
+        while not self._stop.is_set():
+            try:
+                conn, _ = self.config_sock.accept()
+            except OSError:
+                break
+            threading.Thread(target=self._handle_config, args=(conn,), daemon=True).start()
+
+    def _handle_config(self, conn: socket.socket) -> None:
+        try:
+            raw = socket_recv(conn, CTRL_CHUNK)
+            if not raw:
+                return
+            cmd = json.loads(raw)
+            op = cmd.get("cmd")
+            if op == "configure":
+                if cmd.get("cached"):
+                    key = cmd["cache_key"]
+                    if key not in self._slice_cache:
+                        conn.sendall(NAK)
+                        socket_send(b"slice not cached", conn, CTRL_CHUNK)
+                        return
+                    m, w = self._slice_cache[key]
+                else:
+                    m, arrays = recv_slice(conn, self.state.chunk_size)
+                    w = arrays_to_dict(m, arrays)
+                    if cmd.get("cache_key"):
+                        self._slice_cache[cmd["cache_key"]] = (m, w)
+                self.state.weights = w
+                self.weights_ready_event.set()
+                self._start_epoch(cmd, m, w)
+                conn.sendall(ACK)
+            elif op == "stop_epoch":
+                with self._rt_lock:
+                    if self.runtime is not None:
+                        self.runtime.abort()
+                        self.runtime = None
+                self.state.state = StateEnum.IDLE
+                self._publish(state="IDLE")
+                conn.sendall(ACK)
+            elif op == "status":
+                rt = self.runtime
+                st = {"epoch": self.state.epoch, "state": self.state.state.name,
+                      "processed": rt.processed if rt else 0, "error": rt.error if rt else None}
+                conn.sendall(ACK)
+                socket_send(json.dumps(st).encode(), conn, CTRL_CHUNK)
+            elif op == "shutdown":
+                conn.sendall(ACK)
+                threading.Thread(target=self.stop, daemon=True).start()
+            else:
+                conn.sendall(NAK)
+                socket_send(f"unknown cmd {op}".encode(), conn, CTRL_CHUNK)
+        except Exception as e:  # noqa: BLE001 - report failure to the dispatcher
+            traceback.print_exc()
+            self.state.state = StateEnum.PARSE_ERROR
+            try:
+                conn.sendall(NAK)
+                socket_send(f"{type(e).__name__}: {e}".encode(), conn, CTRL_CHUNK)
+            except OSError:
+                pass
+        finally:
+            try:
+                conn.close()
+            except OSError:
+                pass
+
+    def _start_epoch(self, cfg: Dict, m: SliceManifest, w: Dict[str, np.ndarray]) -> None:
+        with self._rt_lock:
+            old = self.runtime
+            if old is not None:
+                old.abort()
+            rt = StageRuntime(self, cfg, m, w)
+            self.runtime = rt
+            self.state.epoch = rt.epoch
+            self.state.partition_index = m.part_index
+            self.state.model = rt.compute
+            self.state.next_node = (cfg.get("next") or {}).get("host", "dispatcher")
+            rt.start()
+            for s in self._pending_upstream.pop(rt.epoch, []):
+                rt.attach_upstream(s)
+            for e in [e for e in self._pending_upstream if e < rt.epoch]:
+                for s in self._pending_upstream.pop(e):
+                    s.close()
+        self.state.state = StateEnum.BUSY
+        self._publish(state="BUSY", epoch=rt.epoch, partition=m.part_index)
+
+    # --------------------------------------------------------- data plane
+    def _data_server(self) -> None:
+        while not self._stop.is_set():
+            try:
+                conn, _ = self.data_sock.accept()
+            except OSError:
+                break
+            conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            try:
+                hello = json.loads(socket_recv(conn, CTRL_CHUNK) or b"{}")
+            except (RuntimeError, ValueError, OSError):
+                conn.close()
+                continue
+            ep = int(hello.get("epoch", -1))
+            with self._rt_lock:
+                rt = self.runtime
+                if rt is not None and rt.epoch == ep:
+                    rt.attach_upstream(conn)
+                elif rt is None or ep > rt.epoch:
+                    self._pending_upstream.setdefault(ep, []).append(conn)   # config not here yet
+                else:
+                    conn.close()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="ADAPT worker node (one per GPU)")
+    ap.add_argument("--dispatcher", default="127.0.0.1", help="dispatcher / membership host")
+    ap.add_argument("--membership-port", type=int, default=2379)
+    ap.add_argument("--data-port", type=int, default=DATA_PORT)
+    ap.add_argument("--config-port", type=int, default=CONFIG_PORT)
+    ap.add_argument("--device", default=None, help="cuda:N or cpu (default: cuda:0 if present)")
+    ap.add_argument("--id", default=None)
+    ap.add_argument("--ttl", type=float, default=1.0, help="membership lease TTL (s)")
+    ap.add_argument("--chunk-size", type=int, default=512 * 1000)
+    a = ap.parse_args(argv)
+    node = Node(a.dispatcher, a.membership_port, a.data_port, a.config_port, a.device, a.id, a.chunk_size,
+                heartbeat_ttl=a.ttl)
+    print(f"node {node.node_id} device={node.device} data={node.data_port} config={node.config_port}", flush=True)
+    node.run(block=True)
+
+
+if __name__ == "__main__":
+    main()

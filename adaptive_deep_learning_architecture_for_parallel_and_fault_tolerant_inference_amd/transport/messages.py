@@ -1,0 +1,83 @@
+"""Data-plane messages on TCP links (dispatcher <-> stage 0 / last stage, and
+stage <-> stage in TCP ("RCCL-less") mode).
+
+Reference: a request on :6000 is ``u32be partition_index`` + one frame of
+``lz4(zfp(x))`` followed by SHUT_WR on a fresh connection per message
+(`src/dispatcher.py:204-220`); results come back on :6003 as bare frames with
+no request id (`src/dispatcher.py:121-151`).  We keep persistent connections
+and make every message self-identifying so replays after a failure can be
+de-duplicated:
+
+    frame 0 : header  = "ADPT" | u32 partition | u64 req_id | u32 epoch | u32 count | u32 ntensors   (BE)
+    frame 1..ntensors : codec-encoded tensors (codec/__init__.py), frontier order
+
+`count` is the number of valid images (a partial micro-batch is zero-padded
+by the receiver).
+"""
+from __future__ import annotations
+
+import socket
+import struct
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from .. import codec as C
+from ..node_state import socket_recv, socket_send
+
+MAGIC = b"ADPT"
+HDR = struct.Struct(">4sIQIII")
+
+
+@dataclass
+class Message:
+    partition: int
+    req_id: int
+    epoch: int
+    count: int
+    tensors: List[np.ndarray] = field(default_factory=list)
+    bf16: List[bool] = field(default_factory=list)     # tensor carries bfloat16 bits (uint16 view)
+
+
+def send_message(sock: socket.socket, m: Message, codec: str = "lz4", chunk_size: int = 512000,
+                 timeout_ms: int = -1) -> None:
+    socket_send(HDR.pack(MAGIC, m.partition, m.req_id, m.epoch, m.count, len(m.tensors)), sock, chunk_size,
+                timeout_ms)
+    flags = m.bf16 or [False] * len(m.tensors)
+    for t, b in zip(m.tensors, flags):
+        socket_send(C.encode(t, codec, bf16=b), sock, chunk_size, timeout_ms)
+
+
+def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int = -1) -> Optional[Message]:
+    h = socket_recv(sock, chunk_size, timeout_ms)
+    if not h:
+        return None
+    magic, part, rid, epoch, count, nt = HDR.unpack(h)
+    if magic != MAGIC:
+        raise ValueError("bad data-plane message magic")
+    ts, bf = [], []
+    for _ in range(nt):
+        buf = socket_recv(sock, chunk_size, timeout_ms)
+        if not buf:
+            raise ConnectionError("closed inside a message")
+        bf.append(C.is_bf16(buf))
+        ts.append(C.decode(buf))
+    return Message(part, rid, epoch, count, ts, bf)
+
+
+def connect(host: str, port: int, timeout: float = 5.0, hello: Optional[bytes] = None) -> socket.socket:
+    s = socket.create_connection((host, port), timeout=timeout)
+    s.settimeout(None)
+    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    if hello is not None:
+        socket_send(hello, s, 1 << 16)
+    return s
+
+
+def listen(host: str = "0.0.0.0", port: int = 0, backlog: int = 64) -> socket.socket:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    s.bind((host, port))
+    s.listen(backlog)
+    return s

@@ -1,0 +1,159 @@
+// pybind11 module `_runtime`: framing transport + LZ4 frame + reversible zfp.
+// Every call releases the GIL around its native work so the dispatcher's and
+// workers' I/O threads run concurrently (the reference's threads serialize on
+// the GIL inside pure-Python chunk loops, `src/node_state.py:70-89`).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+
+#include "runtime.h"
+
+namespace py = pybind11;
+using namespace adapt_rt;
+
+static py::bytes to_bytes(const std::vector<uint8_t>& v) {
+  return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+}
+
+static std::pair<const uint8_t*, size_t> view(const py::buffer& b, py::buffer_info& info) {
+  info = b.request();
+  return {static_cast<const uint8_t*>(info.ptr), (size_t)(info.size * info.itemsize)};
+}
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "ADAPT host runtime: framing transport, LZ4 frame codec, reversible zfp-style codec";
+
+  // ------------------------------------------------------------- framing
+  m.def("send_frame", [](int fd, py::buffer data, size_t chunk, int timeout_ms) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    py::gil_scoped_release nogil;
+    send_frame(fd, v.first, v.second, chunk, timeout_ms);
+  }, py::arg("fd"), py::arg("data"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
+  m.def("send_all", [](int fd, py::buffer data, size_t chunk, int timeout_ms) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    py::gil_scoped_release nogil;
+    send_all(fd, v.first, v.second, chunk, timeout_ms);
+  }, py::arg("fd"), py::arg("data"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
+  m.def("recv_frame", [](int fd, size_t chunk, int timeout_ms, size_t max_len) -> py::object {
+    std::vector<uint8_t> out;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = recv_frame(fd, out, chunk, timeout_ms, max_len);
+    }
+    if (!ok) return py::none();
+    return to_bytes(out);
+  }, py::arg("fd"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1, py::arg("max_len") = 0);
+  m.def("recv_exact", [](int fd, size_t n, int timeout_ms) -> py::object {
+    std::vector<uint8_t> out(n);
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = recv_exact(fd, out.data(), n, n ? n : 1, timeout_ms, true);
+    }
+    if (!ok) return py::none();
+    return to_bytes(out);
+  }, py::arg("fd"), py::arg("n"), py::arg("timeout_ms") = -1);
+  m.def("recv_frame_into", [](int fd, py::buffer dst, size_t chunk, int timeout_ms) -> py::object {
+    // receive a frame directly into a writable buffer (e.g. pinned host memory)
+    py::buffer_info info = dst.request(true);
+    size_t cap = (size_t)(info.size * info.itemsize);
+    uint8_t hdr[8];
+    uint64_t n = 0;
+    {
+      py::gil_scoped_release nogil;
+      if (!recv_exact(fd, hdr, 8, 8, timeout_ms, true)) return py::none();
+      for (int i = 0; i < 8; ++i) n = (n << 8) | hdr[i];
+      if (n > cap) throw std::runtime_error("frame larger than destination buffer");
+      if (n) recv_exact(fd, static_cast<uint8_t*>(info.ptr), (size_t)n, chunk, timeout_ms, false);
+    }
+    return py::int_(n);
+  }, py::arg("fd"), py::arg("dst"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
+
+  // ---------------------------------------------------------------- LZ4
+  m.def("xxh32", [](py::buffer data, uint32_t seed) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    return xxh32(v.first, v.second, seed);
+  }, py::arg("data"), py::arg("seed") = 0);
+  m.def("lz4_compress", [](py::buffer data, int accel) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    std::vector<uint8_t> out;
+    {
+      py::gil_scoped_release nogil;
+      out = lz4_frame_compress(v.first, v.second, accel);
+    }
+    return to_bytes(out);
+  }, py::arg("data"), py::arg("accel") = 1);
+  m.def("lz4_decompress", [](py::buffer data) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    std::vector<uint8_t> out;
+    {
+      py::gil_scoped_release nogil;
+      out = lz4_frame_decompress(v.first, v.second);
+    }
+    return to_bytes(out);
+  });
+  m.def("lz4_block_compress", [](py::buffer data, int accel) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    std::vector<uint8_t> out(lz4_block_bound(v.second));
+    size_t n;
+    {
+      py::gil_scoped_release nogil;
+      n = lz4_block_compress(v.first, v.second, out.data(), out.size(), accel);
+    }
+    out.resize(n);
+    return to_bytes(out);
+  }, py::arg("data"), py::arg("accel") = 1);
+  m.def("lz4_block_decompress", [](py::buffer data, size_t max_out) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    std::vector<uint8_t> out(max_out);
+    size_t n;
+    {
+      py::gil_scoped_release nogil;
+      n = lz4_block_decompress(v.first, v.second, out.data(), out.size());
+    }
+    out.resize(n);
+    return to_bytes(out);
+  });
+
+  // ---------------------------------------------------------------- zfp
+  m.def("zfp_compress", [](py::array arr, int threads) {
+    py::buffer_info info = arr.request();
+    int code;
+    if (info.format == py::format_descriptor<float>::format() && info.itemsize == 4) code = 0;
+    else if (info.format == py::format_descriptor<double>::format() && info.itemsize == 8) code = 1;
+    else throw std::runtime_error("zfp_compress: float32 or float64 arrays only");
+    if (!(arr.flags() & py::array::c_style)) throw std::runtime_error("zfp_compress: array must be C-contiguous");
+    std::vector<size_t> shape;
+    for (auto s : info.shape) shape.push_back((size_t)s);
+    if (shape.empty()) shape.push_back(1);
+    std::vector<uint8_t> out;
+    {
+      py::gil_scoped_release nogil;
+      out = zfp_compress(info.ptr, code, shape, threads);
+    }
+    return to_bytes(out);
+  }, py::arg("arr"), py::arg("threads") = 4);
+  m.def("zfp_decompress", [](py::buffer data, int threads) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    ZfpHeader h = zfp_header(v.first, v.second);
+    std::vector<ssize_t> shape(h.shape.begin(), h.shape.end());
+    py::array out = h.dtype == 0 ? py::array(py::dtype::of<float>(), shape) : py::array(py::dtype::of<double>(), shape);
+    void* dst = out.mutable_data();
+    {
+      py::gil_scoped_release nogil;
+      zfp_decompress(v.first, v.second, dst, threads);
+    }
+    return out;
+  }, py::arg("data"), py::arg("threads") = 4);
+}
