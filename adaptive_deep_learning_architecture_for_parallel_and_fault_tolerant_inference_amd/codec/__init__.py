@@ -47,7 +47,9 @@ def _parse(buf: bytes):
 
 def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads: int = 4) -> bytes:
     """Encode an ndarray.  `bf16=True` marks a uint16 array as bfloat16 payload."""
-    arr = np.ascontiguousarray(arr)
+    arr = np.asarray(arr)
+    if not arr.flags.c_contiguous:
+        arr = arr.copy(order="C")            # (np.ascontiguousarray would promote 0-d to 1-d)
     rt = runtime()
     dt_code = BF16 if bf16 else _DT_CODE.get(arr.dtype)
     if dt_code is None:
@@ -59,7 +61,7 @@ def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads:
         arr_z = arr.reshape(-1) if arr.ndim == 0 else arr.reshape((-1,) + arr.shape[-3:])
     else:
         arr_z = arr
-    raw = arr.view(np.uint8).reshape(-1) if arr.size else np.zeros(0, np.uint8)
+    raw = arr.reshape(-1).view(np.uint8) if arr.size else np.zeros(0, np.uint8)
     if c == 0:
         payload = raw.tobytes()
     elif c == 1:

@@ -123,6 +123,7 @@ class DEFER:
         self._order_buf: Dict[int, np.ndarray] = {}
         self._next_emit = 0
         self._output: Optional[queue.Queue] = None
+        self._result_conns: set = set()
 
     # ------------------------------------------------------------ helpers
     @staticmethod
@@ -243,7 +244,7 @@ class DEFER:
         with self._reconf_lock:
             t0 = time.time()
             live = self._get_available_workers()
-            if len(live) < self.min_workers or not live:
+            if not live:
                 self._log(f"no workers available ({len(live)})")
                 return False
             g = self._model.graph
@@ -344,6 +345,7 @@ class DEFER:
                 break
             conn.settimeout(None)
             conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            self._result_conns.add(conn)
             threading.Thread(target=self._result_conn, args=(conn, output_stream), daemon=True).start()
 
     def _result_conn(self, conn: socket.socket, output_stream: "queue.Queue") -> None:
@@ -359,6 +361,7 @@ class DEFER:
         except (OSError, RuntimeError, ValueError):
             pass
         finally:
+            self._result_conns.discard(conn)
             conn.close()
 
     def _complete(self, m: Message, output_stream: "queue.Queue") -> None:
@@ -488,10 +491,15 @@ class DEFER:
                 except OSError:
                     pass
         self._shutdown_event.set()
-        try:
-            self.result_sock.close()
-        except OSError:
-            pass
+        for c in [self.result_sock] + list(self._result_conns):
+            try:
+                c.shutdown(socket.SHUT_RDWR)
+            except OSError:
+                pass
+            try:
+                c.close()
+            except OSError:
+                pass
         p = self.pipeline
         if p is not None and p.stage0 is not None:
             try:

@@ -1,0 +1,115 @@
+"""Graph IR, ResNet builders, slicer, planner and plan compiler (CPU)."""
+import pytest
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph.ir import Graph
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph.planner import (
+    articulation_points, balance_ratio, default_candidates, plan_cuts)
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph.slicer import (
+    is_single_tensor_cut, partition, subgraph, validate_slices)
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.plan import compile_plan
+
+
+@pytest.fixture(scope="module")
+def r50():
+    return build_resnet("resnet50")
+
+
+def test_resnet_param_counts_match_keras():
+    # Keras applications totals
+    assert build_resnet("resnet50").count_params() == 25_636_712
+    assert build_resnet("resnet152").count_params() == 60_419_944
+
+
+def test_resnet50_structure(r50):
+    assert len(r50) == 177
+    assert len(r50.weight_specs()) == 320          # get_weights() list length
+    assert abs(r50.total_macs() / 1e9 - 3.858) < 0.01
+    assert r50.order[:7] == ["input_1", "conv1_pad", "conv1_conv", "conv1_bn", "conv1_relu", "pool1_pad", "pool1_pool"]
+    assert r50["conv3_block1_0_conv"].attrs["stride"] == 2 and r50["conv3_block1_1_conv"].attrs["stride"] == 2
+    assert r50["conv5_block3_out"].out_shape == (7, 7, 2048)
+    assert r50["predictions"].out_shape == (1000,)
+    # shortcut conv exists only in block 1 of each stage
+    assert "conv2_block2_0_conv" not in r50.layers and "conv4_block1_0_conv" in r50.layers
+
+
+def test_graph_json_roundtrip(r50):
+    g2 = Graph.from_json(r50.to_json())
+    assert g2.order == r50.order
+    assert g2["conv2_block1_2_conv"].attrs["kernel"] == (3, 3)
+    assert g2.count_params() == r50.count_params()
+
+
+def test_single_tensor_cut_matches_reference_semantics(r50):
+    s = partition(r50, ["conv4_block1_out"])
+    validate_slices(r50, s)
+    assert s[0].outputs == ["conv4_block1_out"] and s[1].inputs == ["conv4_block1_out"]
+    assert s[0].layers[-1] == "conv4_block1_out"
+    assert s[0].name == "part1" and s[1].name == "part2"
+    assert len(s[0].layers) + len(s[1].layers) == len(r50)
+
+
+def test_multi_tensor_frontier_config2(r50):
+    # BASELINE config 2: part_at=['conv3_block1_1_conv'] is not a single-tensor cut
+    s = partition(r50, ["conv3_block1_1_conv"])
+    validate_slices(r50, s)
+    assert s[0].outputs == ["conv2_block3_out", "conv3_block1_1_conv"]
+    assert not is_single_tensor_cut(r50, "conv3_block1_1_conv")
+    assert is_single_tensor_cut(r50, "conv3_block1_out")
+    assert "conv3_block1_0_conv" in s[1].layers
+
+
+def test_relay_through_middle_stage(r50):
+    # a tensor produced in part 1 and consumed in part 3 must be relayed by part 2
+    s = partition(r50, ["conv3_block1_1_conv", "conv3_block1_2_conv"])
+    validate_slices(r50, s)
+    assert "conv2_block3_out" in s[1].relay
+
+
+def test_bad_cuts(r50):
+    with pytest.raises(KeyError):
+        partition(r50, ["nope"])
+    with pytest.raises(ValueError):
+        partition(r50, ["conv4_block1_out", "conv3_block1_out"])   # out of order
+
+
+def test_subgraph_inputs(r50):
+    s = partition(r50, ["conv3_block1_1_conv"])
+    sg = subgraph(r50, s[1])
+    assert sg.input_names == ["conv2_block3_out", "conv3_block1_1_conv"]
+    assert sg["conv3_block1_1_conv"].op == "input"
+    assert sg.output_names == ["predictions"]
+
+
+def test_planner_balanced(r50):
+    cuts, per = plan_cuts(r50, 4)
+    assert len(cuts) == 3 and balance_ratio(per) < 1.4
+    assert all(c in default_candidates(r50) for c in cuts)
+    cuts8, per8 = plan_cuts(r50, 8)
+    assert len(cuts8) == 7
+    assert plan_cuts(r50, 1)[0] == []
+    r152 = build_resnet("resnet152")
+    c, p = plan_cuts(r152, 4)
+    assert balance_ratio(p) < 1.15
+    assert "conv4_block1_out" in articulation_points(r50)
+    assert "conv3_block1_1_conv" not in articulation_points(r50)
+
+
+def test_plan_fuses_resnet(r50):
+    steps = compile_plan(r50)
+    kinds = [s.kind for s in steps]
+    assert kinds.count("conv") == 53 and kinds.count("bn") == 0 and kinds.count("add") == 0
+    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds[-2:] == ["gap", "dense"]
+    c1 = steps[1]
+    assert c1.p["pads"] == ((3, 3), (3, 3)) and c1.p["relu"] and c1.out == "conv1_relu"
+    res = [s for s in steps if s.kind == "conv" and s.p["residual"]]
+    assert len(res) == 16 and all(s.out.endswith("_out") for s in res)
+
+
+def test_plan_unfused_at_cut(r50):
+    s = partition(r50, ["conv3_block1_1_conv"])
+    st2 = compile_plan(subgraph(r50, s[1]))
+    bn = [s for s in st2 if s.kind == "bn"]
+    assert len(bn) == 1 and bn[0].p["relu"] and bn[0].out == "conv3_block1_1_relu"   # BN + ReLU standalone
+    st1 = compile_plan(subgraph(r50, s[0]))
+    assert st1[-1].kind == "conv" and st1[-1].out == "conv3_block1_1_conv" and not st1[-1].p["bn"]
