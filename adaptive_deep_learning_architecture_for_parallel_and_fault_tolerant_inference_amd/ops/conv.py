@@ -21,8 +21,18 @@ from ._lib import kernels, ptr, stream_handle
 
 BK = 64
 # tile configs (must match ADAPT_CONV_CFGS in conv_igemm.hip)
-CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (32, 64)}
+CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (32, 64),
+             # v2: LDS-DMA multi-stage ring (conv_glds.hip)
+             6: (128, 128), 7: (128, 128), 8: (128, 64), 9: (64, 128), 10: (64, 64), 11: (256, 64), 12: (64, 256)}
+V1_CFGS = (0, 1, 2, 3, 4, 5)
 _CFG_EFF = {0: 1.0, 4: 0.97, 1: 0.86, 2: 0.86, 3: 0.66, 5: 0.42}
+
+
+def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
+    """v2 configs split k -> (tap, ci) with shifts: non-1x1 convs need a power-of-two Cin."""
+    if cfg in V1_CFGS:
+        return True
+    return pure or (pc.cin & (pc.cin - 1)) == 0
 NUM_CUS = 256
 
 
@@ -91,7 +101,8 @@ def choose_cfg(M: int, N: int, Kpad: int, occupancy: int = 2):
     """Heuristic (cfg, ksplit): minimise waves-of-blocks x per-block work / efficiency."""
     best = None
     ktiles = Kpad // BK
-    for cfg, (bm, bn) in CFG_TILES.items():
+    for cfg in V1_CFGS:
+        bm, bn = CFG_TILES[cfg]
         if N % 8:
             continue
         tiles = math.ceil(M / bm) * math.ceil(N / bn)
@@ -139,6 +150,9 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
     bm, bn = CFG_TILES[cfg]
     if pc.w.shape[0] < math.ceil(N / bn) * bn:
         raise ValueError("packed weights not padded to the tile's N")
+    pure = pc.kh == 1 and pc.kw == 1 and pc.stride == 1 and pc.pad_t == 0 and pc.pad_l == 0 and OH == H and OW == W
+    if not cfg_supported(cfg, pc, pure):
+        raise ValueError(f"tile config {cfg} needs a power-of-two input channel count (got {pc.cin})")
     ws_ptr = 0
     if ksplit > 1:
         need = ksplit * M * N

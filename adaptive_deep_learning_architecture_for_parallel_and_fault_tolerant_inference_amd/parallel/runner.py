@@ -25,21 +25,51 @@ from .pipeline import StageLink, stage_ranks
 
 
 class DPJob:
-    def __init__(self, g, weights, world: int, rank: int, device, batch: int, graph: bool = True, tune: bool = False):
-        self.ex = SliceExecutor(g, weights, batch, device=device, tune=tune)
+    """Whole-model replica per GPU.  With ``streams > 1`` the GPU keeps that many
+    independent bs=`batch` micro-batches in flight on separate HIP streams (the
+    reference's concurrent in-flight requests, `concurrency_sem`,
+    `src/dispatcher.py:151,183`): each stream replays its own hipGraph over its
+    own activation buffers while sharing the resident weights, so the small
+    per-layer GEMMs of different micro-batches fill CUs the other leaves idle."""
+
+    def __init__(self, g, weights, world: int, rank: int, device, batch: int, graph: bool = True, tune: bool = False,
+                 streams: int = 1):
+        self.device = torch.device(device)
+        self.exs = [SliceExecutor(g, weights, batch, device=device, tune=tune and i == 0) for i in range(streams)]
+        for ex in self.exs[1:]:           # share packed weights with the first executor
+            ex.packed = self.exs[0].packed
+            ex.cfg = dict(self.exs[0].cfg)
+            ex._ensure_ws()               # private split-K workspace per stream
+        self.ex = self.exs[0]
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(streams)] if streams > 1 else [None]
         if graph:
-            self.ex.capture()
-        self.images_per_step = batch * world
-        self.global_batch = batch * world
-        self.parallelism = f"dp{world}"
+            for ex, s in zip(self.exs, self.streams):
+                if s is None:
+                    ex.capture()
+                else:
+                    with torch.cuda.stream(s):
+                        ex.capture()
+        self.images_per_step = batch * world * streams
+        self.global_batch = batch * world * streams
+        self.parallelism = f"dp{world}" + (f"x{streams}streams" if streams > 1 else "")
         self.part_at: List[str] = []
         self.input_name = g.input
 
     def set_synthetic_input(self, x: torch.Tensor) -> None:
-        self.ex.input_buf(self.input_name).copy_(x)
+        for ex in self.exs:
+            ex.input_buf(self.input_name).copy_(x)
 
     def step(self) -> None:
-        self.ex.forward(0)
+        if len(self.exs) == 1:
+            self.ex.forward(0)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for ex, s in zip(self.exs, self.streams):
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                ex.forward(0)
+        for s in self.streams:
+            cur.wait_stream(s)
 
     def outputs(self):
         return {o: self.ex.output_buf(o) for o in self.ex.outputs}
@@ -49,7 +79,8 @@ class PipelineJob:
     """One stage of a (replicated) pipeline; step() = `stages` micro-batch ticks."""
 
     def __init__(self, g, weights, world: int, rank: int, device, batch: int, stages: int,
-                 part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False, nsets: int = 2):
+                 part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False, nsets: int = 2,
+                 host_staged: bool = False):
         if world % stages:
             raise ValueError(f"world {world} not divisible by stages {stages}")
         self.stages = stages
@@ -73,7 +104,8 @@ class PipelineJob:
         self.prev, self.next = rk["prev"], rk["next"]
         in_bufs = [[self.ex.input_buf(n, j) for n in sl.inputs] for j in range(nsets)]
         out_bufs = [[self.ex.output_buf(n, j) for n in sl.outputs] for j in range(nsets)]
-        self.link = StageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next)
+        self.link = StageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next,
+                              host_staged=host_staged)
         self.images_per_step = batch * world          # stages ticks x replicas x batch / stages-per-image
         self.global_batch = batch * world
         self.parallelism = f"pp{stages}" if self.replicas == 1 else f"pp{stages}xdp{self.replicas}"
@@ -84,9 +116,14 @@ class PipelineJob:
             for j in range(self.ex.num_sets):
                 self.ex.input_buf(self.slice.inputs[0], j).copy_(x)
 
+    def set_total_steps(self, n: int) -> None:
+        """Number of step() calls that will follow (lets the link avoid posting
+        receives for micro-batches that never come)."""
+        self._total_ticks = n * self.stages
+
     def step(self) -> None:
         if not self._primed:
-            self.link.prime()
+            self.link.prime(getattr(self, "_total_ticks", None))
             self._primed = True
         for _ in range(self.stages):
             self.link.step()
@@ -96,15 +133,18 @@ class PipelineJob:
 
 
 def build_job(g, weights, mode: str, world: int, rank: int, device, batch: int = 32, stages: int = 0,
-              part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False):
+              part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False,
+              host_staged: bool = False, streams: int = 1):
     if mode == "dp" or world == 1 and not part_at:
-        return DPJob(g, weights, world, rank, device, batch, graph=graph, tune=tune)
+        return DPJob(g, weights, world, rank, device, batch, graph=graph, tune=tune, streams=streams)
     if mode == "pp":
         k = len(part_at) + 1 if part_at else world
         if k != world:
             raise ValueError(f"pp mode: {k} stages for {world} ranks")
-        return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune)
+        return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune,
+                           host_staged=host_staged)
     if mode == "ppdp":
         k = stages or (len(part_at) + 1 if part_at else 2)
-        return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune)
+        return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune,
+                           host_staged=host_staged)
     raise ValueError(f"unknown mode {mode}")

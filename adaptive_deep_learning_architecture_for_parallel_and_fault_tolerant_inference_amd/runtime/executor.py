@@ -269,15 +269,22 @@ class SliceExecutor:
                         continue
                     ws = torch.empty(ks * M * N, dtype=torch.float32, device=self.device) if ks > 1 else None
                     try:
-                        for _ in range(2):
-                            conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws)
+                        conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws)
+                        torch.cuda.synchronize(self.device)
+                        # time device work only: `reps` launches captured in one hipGraph
+                        gg = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(gg):
+                            for _ in range(reps):
+                                conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws)
+                        gg.replay()
                         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s.record()
-                        for _ in range(reps):
-                            conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws)
+                        for _ in range(3):
+                            gg.replay()
                         e.record()
                         e.synchronize()
-                        t = s.elapsed_time(e) / reps
+                        t = s.elapsed_time(e) / (3 * reps)
+                        del gg
                     except (RuntimeError, ValueError):
                         continue
                     if best is None or t < best[0]:

@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--tune", action="store_true", help="autotune conv tiles before timing")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="independent bs=--batch micro-batches in flight per GPU (dp mode)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo = host-staged rehearsal (several ranks per GPU)")
     return ap.parse_args()
 
 
@@ -54,10 +58,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev_idx = local % max(1, ndev)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    backend = args.backend
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from importlib import import_module
     resnet = import_module(f"{PKG}.models.resnet")
@@ -67,11 +77,14 @@ def main():
     weights = resnet.init_weights(g, seed=args.seed)
     part_at = [s for s in args.part_at.split(",") if s]
     job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
-                           stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune)
+                           stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune,
+                           host_staged=(backend != "nccl"), streams=args.streams)
     # synthetic input, resident on device (data="synthetic")
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     job.set_synthetic_input(torch.randn((args.batch, 224, 224, 3), generator=gen, device=dev))
 
+    if hasattr(job, "set_total_steps"):
+        job.set_total_steps(args.warmup + args.steps)
     for _ in range(args.warmup):
         job.step()
     torch.cuda.synchronize(dev)
@@ -86,8 +99,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    if hasattr(job, "finish"):
+        job.finish()
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = t.to(dev) if backend == "nccl" else t
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     images = job.images_per_step * args.steps

@@ -1,0 +1,286 @@
+// Implicit-GEMM convolution, v2: LDS-DMA (global_load_lds) multi-stage ring.
+//
+// Same contract as conv_igemm.hip (out = act(X*W^T + bias (+res)), BN folded
+// on the host) but the A/B tiles move HBM -> LDS with
+// `__builtin_amdgcn_global_load_lds` (16 B per lane, no VGPR round trip):
+//
+// * STAGES-deep ring of [BM|BN][64] bf16 tiles; STAGES-1 tiles stay in flight
+//   across the K loop (counted `s_waitcnt vmcnt(N)`, raw `s_barrier`, never a
+//   vmcnt(0) drain inside the loop: cdna_hip_programming.md §5 "Pipelining
+//   across barriers").
+// * The LDS image is lane-linear per wave instruction (1 KiB = 8 rows x 128 B);
+//   the XOR chunk swizzle that makes the MFMA fragment reads conflict-free is
+//   applied to the per-lane GLOBAL source address and again on the ds_read
+//   (rule 21: linear dest + inverse-swizzled source + swizzled read).
+// * Implicit im2col: each lane's source address is a (pixel, tap, channel)
+//   gather; padding pixels, k >= K and m >= M read a 16-byte zero page, so the
+//   DMA never needs a mask.
+// * Fused epilogue identical to v1 (LDS fp32 tile -> 16-byte row segments).
+#include "kernels.h"
+
+namespace adapt {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+namespace {
+constexpr int BK2 = 64;
+constexpr int NT2 = 256;
+
+__device__ __forceinline__ int swz2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+}  // namespace
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, bool OUT_F32>
+__global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_INS = BM / 32, B_INS = BN / 32;   // glds instructions per wave per tile
+  constexpr int LPW = A_INS + B_INS;
+  constexpr int TILE_A = BM * 128, STAGE_BYTES = (BM + BN) * 128;
+  constexpr int EPI_LD = BN + 4;
+  constexpr int EPI_BYTES = BM * EPI_LD * 4;
+  constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+  static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int tilesM = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = tile / tilesN, tn = tile % tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int ktiles_total = p.Kpad / BK2;
+  const int kt_per = (ktiles_total + p.ksplit - 1) / p.ksplit;
+  const int kt0 = blockIdx.y * kt_per;
+  const int kt1 = min(ktiles_total, kt0 + kt_per);
+  const int nk = kt1 > kt0 ? kt1 - kt0 : 0;
+
+  // ---- per-lane source bookkeeping (rows fixed over the K loop)
+  const int lrow = lane >> 3;      // row within the 8-row piece
+  const int pchunk = lane & 7;     // physical LDS chunk this lane writes
+  int a_base[A_INS], a_ih0[A_INS], a_iw0[A_INS], a_c[A_INS];
+  const int ohw = p.OH * p.OW;
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i) {
+    const int r = (wave * A_INS + i) * 8 + lrow;        // tile row
+    const int m = m0 + r;
+    a_c[i] = pchunk ^ ((r >> 1) & 7);                   // logical chunk this lane fetches
+    if (PURE) {
+      a_base[i] = m < p.M ? m * p.Cin : -1;
+      a_ih0[i] = a_iw0[i] = 0;
+    } else if (m < p.M) {
+      const int img = m / ohw;
+      const int rr = m - img * ohw;
+      const int oh = rr / p.OW;
+      const int ow = rr - oh * p.OW;
+      a_base[i] = img * p.H * p.W * p.Cin;
+      a_ih0[i] = oh * p.stride - p.pad_t;
+      a_iw0[i] = ow * p.stride - p.pad_l;
+    } else {
+      a_base[i] = -1;
+      a_ih0[i] = a_iw0[i] = 0;
+    }
+  }
+  const bf16* b_src[B_INS];
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int r = (wave * B_INS + i) * 8 + lrow;
+    b_src[i] = p.w + (size_t)(n0 + r) * p.Kpad + (pchunk ^ ((r >> 1) & 7)) * 8;
+  }
+  // integer helpers for k -> (tap, ci); Cin is a power of two (host-checked)
+  const int cin_shift = __builtin_ctz(p.Cin);
+  const int kw_magic = (65536 + p.KW - 1) / p.KW;
+
+  auto issue = [&](int kt, int slot) {
+    char* sa = smem + slot * STAGE_BYTES;
+    char* sb = sa + TILE_A;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const int k = kt * BK2 + a_c[i] * 8;
+      const bf16* src = zero;
+      if (a_base[i] >= 0 && k < p.K) {
+        if (PURE) {
+          src = p.x + a_base[i] + k;
+        } else {
+          const int tap = k >> cin_shift;
+          const int ci = k & (p.Cin - 1);
+          const int kh = (tap * kw_magic) >> 16;
+          const int kw = tap - kh * p.KW;
+          const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+          if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+            src = p.x + a_base[i] + (ih * p.W + iw) * p.Cin + ci;
+        }
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sa + (wave * A_INS + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (size_t)kt * BK2),
+                                       (lds_void*)(sb + (wave * B_INS + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(kt0 + s, s);
+
+  for (int t = 0; t < nk; ++t) {
+    // tile t must have landed; later tiles may stay in flight
+    const int ahead = nk - 1 - t;      // tiles issued after t (capped at STAGES-2)
+    if (STAGES >= 4 && ahead >= 2) wait_vm<(STAGES >= 4 ? 2 * LPW : 0)>();
+    else if (STAGES >= 3 && ahead >= 1) wait_vm<(STAGES >= 3 ? LPW : 0)>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    const char* sa = smem + (t % STAGES) * STAGE_BYTES;
+    const char* sb = sa + TILE_A;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vm<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ---- epilogue (as conv_igemm.hip)
+  float* epi = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * TN + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) epi[(wm * TM + i * 16 + fq * 4 + r) * EPI_LD + col] = acc[i][j][r];
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  constexpr int NCH = BM * CPR;
+  if (p.ksplit > 1) {
+    float* slab = p.ws + (size_t)blockIdx.y * p.M * p.N;
+    for (int c = tid; c < NCH; c += NT2) {
+      const int row = c / CPR, cc = c % CPR;
+      const int m = m0 + row, n = n0 + cc * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float* e = epi + row * EPI_LD + cc * 8;
+      *(f32x4*)(slab + (size_t)m * p.N + n) = *(const f32x4*)e;
+      *(f32x4*)(slab + (size_t)m * p.N + n + 4) = *(const f32x4*)(e + 4);
+    }
+    return;
+  }
+  for (int c = tid; c < NCH; c += NT2) {
+    const int row = c / CPR, cc = c % CPR;
+    const int m = m0 + row, n = n0 + cc * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const float* e = epi + row * EPI_LD + cc * 8;
+    f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    if (p.bias) {
+      f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+      v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+      v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+    }
+    if (p.res) {
+      V8 r;
+      r.u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += bf2f(r.e[t]);
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    }
+    if (OUT_F32) {
+      float* o = (float*)p.out + (size_t)m * p.ldo + n;
+      *(f32x4*)o = (f32x4){v[0], v[1], v[2], v[3]};
+      *(f32x4*)(o + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+    } else {
+      V8 o;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
+      *(u32x4*)((bf16*)p.out + (size_t)m * p.ldo + n) = o.u;
+    }
+  }
+}
+
+// 16-byte aligned zero page that out-of-range lanes fetch from
+__device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
+
+// v2 tile configs: id -> BM, BN, WM, WN, STAGES (ids continue after the v1 configs)
+#define ADAPT_GLDS_CFGS(X)   \
+  X(6, 128, 128, 2, 2, 3)    \
+  X(7, 128, 128, 2, 2, 2)    \
+  X(8, 128, 64, 2, 2, 4)     \
+  X(9, 64, 128, 2, 2, 4)     \
+  X(10, 64, 64, 2, 2, 4)     \
+  X(11, 256, 64, 4, 1, 3)    \
+  X(12, 64, 256, 1, 4, 3)
+
+int conv_glds_num_cfgs() { return 7; }
+
+bool conv_glds_cfg_tile(int cfg, int* bm, int* bn) {
+  switch (cfg) {
+#define X(id, BM_, BN_, WM_, WN_, S_) case id: *bm = BM_; *bn = BN_; return true;
+    ADAPT_GLDS_CFGS(X)
+#undef X
+  }
+  return false;
+}
+
+template <int BM, int BN, int WM, int WN, int S>
+static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, bool out_f32) {
+  static bf16* zero = nullptr;
+  if (!zero) {
+    hipError_t e = hipGetSymbolAddress((void**)&zero, HIP_SYMBOL(g_zero_page));
+    if (e != hipSuccess) return e;
+  }
+  const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
+  dim3 grid(tilesM * tilesN, p.ksplit), block(NT2);
+  if (pure) {
+    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, true, true>), grid, block, 0, s, p, zero);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, true, false>), grid, block, 0, s, p, zero);
+  } else {
+    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, false, true>), grid, block, 0, s, p, zero);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, false, false>), grid, block, 0, s, p, zero);
+  }
+  return hipGetLastError();
+}
+
+hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pure, bool out_f32) {
+  switch (cfg) {
+#define X(id, BM_, BN_, WM_, WN_, S_) case id: return launch_glds<BM_, BN_, WM_, WN_, S_>(p, s, pure, out_f32);
+    ADAPT_GLDS_CFGS(X)
+#undef X
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace adapt

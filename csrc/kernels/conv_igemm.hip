@@ -291,7 +291,7 @@ void conv_cfg_tile(int cfg, int* bm, int* bn) {
     ADAPT_CONV_CFGS(X)
 #undef X
   }
-  *bm = *bn = 0;
+  if (!conv_glds_cfg_tile(cfg, bm, bn)) *bm = *bn = 0;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -317,7 +317,10 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
 #define X(id, BM_, BN_, WM_, WN_) case id: e = launch_cfg<BM_, BN_, WM_, WN_>(p, s, pure, out_f32); break;
     ADAPT_CONV_CFGS(X)
 #undef X
-    default: return hipErrorInvalidValue;
+    default:
+      // v2 (LDS-DMA ring) configs; needs a power-of-two Cin for the k -> (tap, ci) split
+      if (!pure && (p.Cin & (p.Cin - 1))) return hipErrorInvalidValue;
+      e = conv_glds_launch(p, cfg, s, pure, out_f32);
   }
   if (e != hipSuccess || p.ksplit <= 1) return e;
   const size_t chunks = (size_t)p.M * (p.N / 8);

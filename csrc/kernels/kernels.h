@@ -18,6 +18,8 @@ struct ConvParams {
   int ksplit;
 };
 hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
+hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pure, bool out_f32);
+bool conv_glds_cfg_tile(int cfg, int* bm, int* bn);
 int conv_num_cfgs();
 void conv_cfg_tile(int cfg, int* bm, int* bn);
 hipError_t input_pack(const float* x, bf16* y, size_t pixels, int C, int Cp, hipStream_t s);

@@ -50,7 +50,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_conv_vs_torch(ops, case, cfg):
     conv, _ = ops
     B, H, W, Cin, Cout, k, s, p = case
@@ -66,8 +66,13 @@ def test_conv_vs_torch(ops, case, cfg):
     ks = 1
     ws = None
     if cfg is not None and pc.Kpad // 64 >= 4:
-        ks = 2
+        ks = 2 if cfg % 2 == 0 else 3
         ws = torch.empty(ks * B * OH * OW * Cout, device=dev, dtype=torch.float32)
+    pure = k == 1 and s == 1 and p == 0
+    if cfg is not None and not conv.cfg_supported(cfg, pc, pure):
+        with pytest.raises(ValueError):
+            conv.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws)
+        return
     conv.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws)
     torch.cuda.synchronize()
     wq = torch.from_numpy(kern).to(dev).to(torch.bfloat16).float()      # kernel sees bf16 weights
