@@ -75,7 +75,19 @@ class DEFER:
                  membership_port: int = 2379, result_port: int = RESULT_PORT, chunk_size: int = 512 * 1000,
                  batch: int = 1, codec: str = "lz4", weight_codec: str = "zfp+lz4", max_inflight: int = 8,
                  task_timeout: float = 30.0, worker_wait: float = 5.0, elastic: bool = False,
-                 ordered: bool = False, device_graph: bool = True, min_workers: int = 1) -> None:
+                 ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
+                 transport: str = "tcp") -> None:
+        """transport: stage-to-stage links — "tcp" (framed, codec; any host),
+        "rccl" (RCCL p2p over xGMI between GPU workers), "gloo" (CPU workers)."""
+        if transport not in ("tcp", "rccl", "gloo"):
+            raise ValueError(f"unknown transport {transport!r}")
+        self.transport = transport
+        self._store_server = None
+        self._store_port = 0
+        if transport != "tcp":
+            from .parallel.epoch_group import make_store_server
+            self._store_server = make_store_server()       # rendezvous for per-epoch communicators
+            self._store_port = self._store_server.port
         self.computeNodes = list(computeNodes or [])
         self.dispatchIP = self.get_local_ip()
         self.chunk_size = chunk_size
@@ -276,15 +288,37 @@ class DEFER:
                     nxt = {"host": recs[st + 1]["host"], "port": int(recs[st + 1]["data_port"])}
                 cfg = {"cmd": "configure", "epoch": epoch, "stage": st, "stages": k, "batch": self.batch,
                        "next": nxt, "result_addr": [self._result_host(rec), self.result_port],
-                       "codec": self.codec, "graph": self.device_graph}
+                       "codec": self.codec, "graph": self.device_graph, "transport": self.transport}
+                if self.transport != "tcp":
+                    cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
+                                         "store_host": self._result_host(rec), "store_port": self._store_port,
+                                         "timeout": 30}
                 if self._acquire_and_configure_worker(st + 1, members[st], cfg) is None:
                     self._log(f"worker {members[st]} vanished during configuration")
                     return False
+            # live workers left out of this epoch drop their old data plane
+            for wid in live[k:]:
+                self._send_ctrl(wid, {"cmd": "stop_epoch"})
             hello = json.dumps({"epoch": epoch, "from_stage": -1}).encode()
             s0 = connect(recs[0]["host"], int(recs[0]["data_port"]), hello=hello)
             self.pipeline = Pipeline(epoch, cuts, members, recs, s0)
             self._log(f"epoch {epoch}: {k} stages on {members} cuts={cuts} ({(time.time() - t0) * 1e3:.0f} ms)")
             return True
+
+    def _send_ctrl(self, wid: str, cmd: dict) -> bool:
+        with self.worker_lock:
+            rec = self.workers.get(wid)
+        if rec is None:
+            return False
+        try:
+            s = socket.create_connection((rec["host"], int(rec["config_port"])), timeout=2)
+            try:
+                socket_send(json.dumps(cmd).encode(), s, CTRL_CHUNK)
+                return s.recv(1) == ACK
+            finally:
+                s.close()
+        except OSError:
+            return False
 
     def _result_host(self, rec: dict) -> str:
         return "127.0.0.1" if rec.get("host") in ("127.0.0.1", "localhost") else self.dispatchIP

@@ -33,6 +33,7 @@ import json
 import os
 import queue
 import socket
+import sys
 import threading
 import time
 import traceback
@@ -344,7 +345,11 @@ class Node:
             old = self.runtime
             if old is not None:
                 old.abort()
-            rt = StageRuntime(self, cfg, m, w)
+            if cfg.get("transport", "tcp") == "tcp":
+                rt = StageRuntime(self, cfg, m, w)
+            else:                                   # RCCL (xGMI) / gloo stage-to-stage links
+                from .parallel.stage_runtime import CollectiveStageRuntime
+                rt = CollectiveStageRuntime(self, cfg, m, w)
             self.runtime = rt
             self.state.epoch = rt.epoch
             self.state.partition_index = m.part_index
@@ -398,6 +403,12 @@ def main(argv=None):
                 heartbeat_ttl=a.ttl)
     print(f"node {node.node_id} device={node.device} data={node.data_port} config={node.config_port}", flush=True)
     node.run(block=True)
+    # Communicator threads of aborted epochs may still sit in backend waits on
+    # peers that will never answer; leave without running interpreter
+    # finalization over them.
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 if __name__ == "__main__":

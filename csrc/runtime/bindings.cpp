@@ -13,6 +13,22 @@
 namespace py = pybind11;
 using namespace adapt_rt;
 
+// GIL release whose destructor may propagate the forced unwind that CPython
+// 3.10 uses to retire a daemon thread returning from native code during
+// interpreter finalization (pybind11's gil_scoped_release destructor is
+// noexcept, which turns that unwind into std::terminate).
+struct NoGil {
+  PyThreadState* st;
+  NoGil() : st(PyEval_SaveThread()) {}
+  NoGil(const NoGil&) = delete;
+  NoGil& operator=(const NoGil&) = delete;
+  ~NoGil() noexcept(false) {
+    PyThreadState* s = st;
+    st = nullptr;
+    if (s) PyEval_RestoreThread(s);
+  }
+};
+
 static py::bytes to_bytes(const std::vector<uint8_t>& v) {
   return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
 }
@@ -29,20 +45,20 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("send_frame", [](int fd, py::buffer data, size_t chunk, int timeout_ms) {
     py::buffer_info info;
     auto v = view(data, info);
-    py::gil_scoped_release nogil;
+    NoGil nogil;
     send_frame(fd, v.first, v.second, chunk, timeout_ms);
   }, py::arg("fd"), py::arg("data"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
   m.def("send_all", [](int fd, py::buffer data, size_t chunk, int timeout_ms) {
     py::buffer_info info;
     auto v = view(data, info);
-    py::gil_scoped_release nogil;
+    NoGil nogil;
     send_all(fd, v.first, v.second, chunk, timeout_ms);
   }, py::arg("fd"), py::arg("data"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
   m.def("recv_frame", [](int fd, size_t chunk, int timeout_ms, size_t max_len) -> py::object {
     std::vector<uint8_t> out;
     bool ok;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       ok = recv_frame(fd, out, chunk, timeout_ms, max_len);
     }
     if (!ok) return py::none();
@@ -52,7 +68,7 @@ PYBIND11_MODULE(_runtime, m) {
     std::vector<uint8_t> out(n);
     bool ok;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       ok = recv_exact(fd, out.data(), n, n ? n : 1, timeout_ms, true);
     }
     if (!ok) return py::none();
@@ -65,7 +81,7 @@ PYBIND11_MODULE(_runtime, m) {
     uint8_t hdr[8];
     uint64_t n = 0;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       if (!recv_exact(fd, hdr, 8, 8, timeout_ms, true)) return py::none();
       for (int i = 0; i < 8; ++i) n = (n << 8) | hdr[i];
       if (n > cap) throw std::runtime_error("frame larger than destination buffer");
@@ -85,7 +101,7 @@ PYBIND11_MODULE(_runtime, m) {
     auto v = view(data, info);
     std::vector<uint8_t> out;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       out = lz4_frame_compress(v.first, v.second, accel);
     }
     return to_bytes(out);
@@ -95,7 +111,7 @@ PYBIND11_MODULE(_runtime, m) {
     auto v = view(data, info);
     std::vector<uint8_t> out;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       out = lz4_frame_decompress(v.first, v.second);
     }
     return to_bytes(out);
@@ -106,7 +122,7 @@ PYBIND11_MODULE(_runtime, m) {
     std::vector<uint8_t> out(lz4_block_bound(v.second));
     size_t n;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       n = lz4_block_compress(v.first, v.second, out.data(), out.size(), accel);
     }
     out.resize(n);
@@ -118,7 +134,7 @@ PYBIND11_MODULE(_runtime, m) {
     std::vector<uint8_t> out(max_out);
     size_t n;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       n = lz4_block_decompress(v.first, v.second, out.data(), out.size());
     }
     out.resize(n);
@@ -138,7 +154,7 @@ PYBIND11_MODULE(_runtime, m) {
     if (shape.empty()) shape.push_back(1);
     std::vector<uint8_t> out;
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       out = zfp_compress(info.ptr, code, shape, threads);
     }
     return to_bytes(out);
@@ -151,7 +167,7 @@ PYBIND11_MODULE(_runtime, m) {
     py::array out = h.dtype == 0 ? py::array(py::dtype::of<float>(), shape) : py::array(py::dtype::of<double>(), shape);
     void* dst = out.mutable_data();
     {
-      py::gil_scoped_release nogil;
+      NoGil nogil;
       zfp_decompress(v.first, v.second, dst, threads);
     }
     return out;

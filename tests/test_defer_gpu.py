@@ -1,0 +1,41 @@
+"""DEFER dispatcher + GPU Node on the MI355X: both data-plane transports
+(TCP framed links; RCCL epoch communicator) serve ResNet-50 through our HIP
+runtime and match the fp32 oracle."""
+import queue
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.dispatcher import DEFER
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.model import resnet
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.node import Node
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("transport", ["tcp", "rccl"])
+def test_defer_gpu_node(transport):
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
+              transport=transport)
+    d.membership_server.start()
+    node = Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id="gpu0",
+                heartbeat_ttl=1.0)
+    node.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, [], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(0)
+        xs = [rng.standard_normal((4, 224, 224, 3)).astype(np.float32) for _ in range(3)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=120) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert got.shape == (12, 1000)
+        assert np.abs(got - want).sum(-1).max() < 0.1
+        assert type(node.runtime).__name__ == ("StageRuntime" if transport == "tcp" else "CollectiveStageRuntime")
+    finally:
+        d.shutdown(stop_workers=True)
+        node.stop()

@@ -65,9 +65,13 @@ def _spawn_worker(port, wid):
 
 
 @pytest.mark.slow
-def test_fault_injection_sigkill_repartition_replay(tiny):
+@pytest.mark.parametrize("transport", ["tcp", "gloo"])
+def test_fault_injection_sigkill_repartition_replay(tiny, transport):
+    """TCP links, and collective links (the RCCL code path, here on gloo/CPU):
+    kill the middle stage mid-stream; survivors are re-formed into a new epoch
+    with re-planned cuts and every request is answered exactly once."""
     d = DEFER(membership_port=0, result_port=0, worker_wait=60, max_inflight=4, task_timeout=20, min_workers=3,
-              weight_codec="lz4")
+              weight_codec="lz4", transport=transport)
     d.membership_server.start()
     procs = [_spawn_worker(d.membership_port, f"p{i}") for i in range(3)]
     try:
