@@ -26,7 +26,7 @@ import numpy as np
 
 from ..native import runtime
 
-CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3}
+CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3, "zvc": 4}
 _CODEC_NAMES = {v: k for k, v in CODECS.items()}
 # dtype codes (bf16 travels as raw 16-bit words)
 DTYPES = {0: np.float32, 1: np.float64, 2: np.float16, 3: np.uint16, 4: np.int32, 5: np.int64, 6: np.uint8,
@@ -57,6 +57,8 @@ def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads:
     c = CODECS[codec]
     if c in (2, 3) and arr.dtype not in (np.float32, np.float64):
         c = 1                               # zfp is float32/float64 only
+    if c == 4 and arr.dtype.itemsize not in (2, 4):
+        c = 1                               # zvc works on 2- or 4-byte elements
     if c in (2, 3) and (arr.ndim > 4 or arr.ndim == 0):
         arr_z = arr.reshape(-1) if arr.ndim == 0 else arr.reshape((-1,) + arr.shape[-3:])
     else:
@@ -68,8 +70,10 @@ def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads:
         payload = rt.lz4_compress(raw)
     elif c == 2:
         payload = rt.lz4_compress(rt.zfp_compress(arr_z, threads))
-    else:
+    elif c == 3:
         payload = rt.zfp_compress(arr_z, threads)
+    else:
+        payload = rt.zvc_compress(raw, arr.dtype.itemsize)
     if c != 0 and len(payload) >= raw.nbytes:
         c, payload = 0, raw.tobytes()
     return _header(c, dt_code, arr.shape) + payload
@@ -91,6 +95,8 @@ def decode(buf, threads: int = 4) -> np.ndarray:
         return rt.zfp_decompress(rt.lz4_decompress(body), threads).reshape(shape)
     if codec == 3:
         return rt.zfp_decompress(body, threads).reshape(shape)
+    if codec == 4:
+        return np.frombuffer(rt.zvc_decompress(body), dtype=np_dt).reshape(shape).copy()
     raise ValueError(f"unknown codec id {codec}")
 
 

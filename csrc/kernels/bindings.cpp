@@ -51,6 +51,33 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         check(adapt::conv_forward(p, cfg, S(stream), out_f32), "conv_forward");
       });
+  m.def("zvc_seg", &adapt::zvc_seg);
+  m.def("zvc_scratch_bytes", &adapt::zvc_scratch_bytes);
+  m.def("zvc_max_stream", &adapt::zvc_max_stream);
+  m.def("zvc_gpu_compress", [](u64 in, size_t n, int esz, u64 scratch, u64 sizes, u64 offs, u64 out, u64 total,
+                               u64 s) {
+    check(adapt::zvc_gpu_compress(P<const void>(in), n, esz, P<uint8_t>(scratch), P<uint32_t>(sizes),
+                                  P<uint32_t>(offs), P<uint8_t>(out), P<uint64_t>(total), S(s)),
+          "zvc_gpu_compress");
+  });
+  m.def("zvc_gpu_decompress", [](u64 stream, u64 offs, int nseg, size_t n, int esz, u64 out, u64 s) {
+    check(adapt::zvc_gpu_decompress(P<const uint8_t>(stream), P<const uint32_t>(offs), nseg, n, esz, P<void>(out),
+                                    S(s)),
+          "zvc_gpu_decompress");
+  });
+  m.def("lz4_gpu_chunk", &adapt::lz4_gpu_chunk);
+  m.def("lz4_gpu_scratch_bytes", &adapt::lz4_gpu_scratch_bytes);
+  m.def("lz4_gpu_max_frame", &adapt::lz4_gpu_max_frame);
+  m.def("lz4_gpu_compress", [](u64 in, size_t n, u64 scratch, u64 sizes, u64 offs, u64 out, u64 total, u64 s) {
+    check(adapt::lz4_gpu_compress(P<const uint8_t>(in), n, P<uint8_t>(scratch), P<uint32_t>(sizes),
+                                  P<uint32_t>(offs), P<uint8_t>(out), P<uint64_t>(total), S(s)),
+          "lz4_gpu_compress");
+  });
+  m.def("lz4_gpu_decompress", [](u64 frame, u64 offs, u64 sizes, int nchunks, u64 out, size_t n, u64 err, u64 s) {
+    check(adapt::lz4_gpu_decompress(P<const uint8_t>(frame), P<const uint32_t>(offs), P<const uint32_t>(sizes),
+                                    nchunks, P<uint8_t>(out), n, P<int>(err), S(s)),
+          "lz4_gpu_decompress");
+  });
   m.def("input_pack", [](u64 x, u64 y, size_t pixels, int C, int Cp, u64 s) {
     check(adapt::input_pack(P<const float>(x), P<bf16>(y), pixels, C, Cp, S(s)), "input_pack");
   });

@@ -18,6 +18,20 @@ struct ConvParams {
   int ksplit;
 };
 hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
+int zvc_seg();
+size_t zvc_scratch_bytes(size_t n, int esz);
+size_t zvc_max_stream(size_t n, int esz);
+hipError_t zvc_gpu_compress(const void* in, size_t n, int esz, uint8_t* scratch, uint32_t* sizes, uint32_t* offs,
+                            uint8_t* out, uint64_t* total, hipStream_t s);
+hipError_t zvc_gpu_decompress(const uint8_t* stream, const uint32_t* offs, int nseg, size_t n, int esz, void* out,
+                              hipStream_t s);
+int lz4_gpu_chunk();
+size_t lz4_gpu_scratch_bytes(size_t n);
+size_t lz4_gpu_max_frame(size_t n);
+hipError_t lz4_gpu_compress(const uint8_t* in, size_t n, uint8_t* scratch, uint32_t* sizes, uint32_t* offs,
+                            uint8_t* out, uint64_t* total, hipStream_t s);
+hipError_t lz4_gpu_decompress(const uint8_t* frame, const uint32_t* offs, const uint32_t* sizes, int nchunks,
+                              uint8_t* out, size_t n, int* err, hipStream_t s);
 hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pure, bool out_f32);
 bool conv_glds_cfg_tile(int cfg, int* bm, int* bn);
 int conv_num_cfgs();

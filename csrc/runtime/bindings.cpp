@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
 #include <stdexcept>
 
 #include "runtime.h"
@@ -116,6 +117,17 @@ PYBIND11_MODULE(_runtime, m) {
     }
     return to_bytes(out);
   });
+  m.def("lz4_frame_blocks", [](py::buffer data) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    Lz4FrameBlocks b = lz4_frame_blocks(v.first, v.second);
+    py::array_t<uint32_t> offs(b.offsets.size()), words(b.words.size());
+    if (!b.offsets.empty()) {
+      std::memcpy(offs.mutable_data(), b.offsets.data(), b.offsets.size() * 4);
+      std::memcpy(words.mutable_data(), b.words.data(), b.words.size() * 4);
+    }
+    return py::make_tuple(b.content_size, b.block_max, b.independent, offs, words);
+  });
   m.def("lz4_block_compress", [](py::buffer data, int accel) {
     py::buffer_info info;
     auto v = view(data, info);
@@ -138,6 +150,38 @@ PYBIND11_MODULE(_runtime, m) {
       n = lz4_block_decompress(v.first, v.second, out.data(), out.size());
     }
     out.resize(n);
+    return to_bytes(out);
+  });
+
+  // ---------------------------------------------------------------- zvc
+  m.def("zvc_compress", [](py::buffer data, int esz) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    if (v.second % esz) throw std::runtime_error("zvc_compress: byte length not a multiple of the element size");
+    std::vector<uint8_t> out;
+    {
+      NoGil nogil;
+      out = zvc_compress(v.first, v.second / esz, esz);
+    }
+    return to_bytes(out);
+  }, py::arg("data"), py::arg("esz") = 2);
+  m.def("zvc_info", [](py::buffer data) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    ZvcHeader h = zvc_header(v.first, v.second);
+    py::array_t<uint32_t> offs(h.offsets.size());
+    if (!h.offsets.empty()) std::memcpy(offs.mutable_data(), h.offsets.data(), h.offsets.size() * 4);
+    return py::make_tuple(h.n, h.esz, h.nseg, offs);
+  });
+  m.def("zvc_decompress", [](py::buffer data) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    ZvcHeader h = zvc_header(v.first, v.second);
+    std::vector<uint8_t> out(h.n * h.esz);
+    {
+      NoGil nogil;
+      zvc_decompress(v.first, v.second, out.data());
+    }
     return to_bytes(out);
   });
 

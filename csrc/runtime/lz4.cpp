@@ -212,6 +212,32 @@ std::vector<uint8_t> lz4_frame_compress(const uint8_t* src, size_t n, int accel)
   return out;
 }
 
+Lz4FrameBlocks lz4_frame_blocks(const uint8_t* src, size_t n) {
+  Lz4FrameBlocks r;
+  if (n < 7 || rd32(src) != LZ4F_MAGIC) throw std::runtime_error("lz4f: bad magic");
+  uint8_t flg = src[4], bd = src[5];
+  bool bchk = flg & (1u << 4), has_cs = flg & (1u << 3), dict = flg & 1u;
+  size_t hlen = 2 + (has_cs ? 8 : 0) + (dict ? 4 : 0);
+  if (n < 4 + hlen + 1) throw std::runtime_error("lz4f: truncated header");
+  r.independent = flg & (1u << 5);
+  r.block_max = (size_t)1 << (8 + 2 * ((bd >> 4) & 7));
+  r.content_size = 0;
+  if (has_cs) std::memcpy(&r.content_size, src + 6, 8);
+  size_t pos = 4 + hlen + 1;
+  for (;;) {
+    if (n - pos < 4) throw std::runtime_error("lz4f: truncated block size");
+    uint32_t bs = rd32(src + pos);
+    pos += 4;
+    if (bs == 0) break;
+    size_t len = bs & 0x7FFFFFFFU;
+    if (n - pos < len) throw std::runtime_error("lz4f: truncated block");
+    r.offsets.push_back((uint32_t)pos);
+    r.words.push_back(bs);
+    pos += len + (bchk ? 4 : 0);
+  }
+  return r;
+}
+
 std::vector<uint8_t> lz4_frame_decompress(const uint8_t* src, size_t n) {
   std::vector<uint8_t> out;
   size_t pos = 0;

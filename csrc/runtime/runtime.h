@@ -14,6 +14,25 @@ size_t lz4_block_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap
 size_t lz4_block_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap);
 std::vector<uint8_t> lz4_frame_compress(const uint8_t* src, size_t n, int accel);
 std::vector<uint8_t> lz4_frame_decompress(const uint8_t* src, size_t n);
+struct Lz4FrameBlocks {
+  uint64_t content_size;
+  size_t block_max;
+  bool independent;
+  std::vector<uint32_t> offsets;   // payload offset of each block within the frame
+  std::vector<uint32_t> words;     // block size words (high bit = stored raw)
+};
+Lz4FrameBlocks lz4_frame_blocks(const uint8_t* src, size_t n);
+
+// ---- zero-value compression stream "AZVC" (zvc.cpp; GPU twin: kernels/zvc_gpu.hip)
+struct ZvcHeader {
+  uint64_t n;
+  int esz;
+  uint32_t nseg;
+  std::vector<uint32_t> offsets;   // segment offsets relative to the payload start
+};
+std::vector<uint8_t> zvc_compress(const uint8_t* in, size_t n, int esz);
+ZvcHeader zvc_header(const uint8_t* p, size_t len);
+void zvc_decompress(const uint8_t* p, size_t len, uint8_t* out);
 
 // ---- reversible zfp-style codec (zfp_rev.cpp)
 struct ZfpHeader {

@@ -135,3 +135,51 @@ def test_eltwise(ops):
     pd = torch.empty(2, 11, 12, 64, device=dev, dtype=torch.bfloat16)
     E.pad(x, pd, 1, 1)
     assert torch.equal(pd, F.pad(x, (0, 0, 1, 1, 1, 1)))
+
+
+@pytest.mark.parametrize("n_elems", [1, 7, 513, 100_000, 3_211_264])
+def test_gpu_lz4_roundtrip_and_host_interop(ops, n_elems):
+    import importlib
+    gl = importlib.import_module(f"{PKG}.codec.gpu_lz4")
+    rt = importlib.import_module(f"{PKG}.native").runtime()
+    torch.manual_seed(n_elems)
+    # post-ReLU bf16 activations: ~half zeros, the case the side-stream codec targets
+    x = torch.relu(torch.randn(n_elems, device="cuda")).to(torch.bfloat16)
+    codec = gl.GpuLZ4(x.numel() * 2 + 4096)
+    codec.compress(x)
+    frame = codec.frame_bytes()
+    host = rt.lz4_decompress(frame)                       # standard LZ4 frame
+    assert host == x.view(torch.uint8).cpu().numpy().tobytes()
+    y = torch.empty_like(x)
+    codec.decompress(frame, y)
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int16), x.view(torch.int16))
+    if n_elems >= 100_000:
+        assert len(frame) <= x.numel() * 2 + 16 + 4 * (x.numel() * 2 // 1024 + 1)   # never worse than stored
+    # a host-produced frame (4 MiB blocks) takes the host path
+    z = torch.empty_like(x)
+    codec.decompress(rt.lz4_compress(x.view(torch.uint8).cpu().numpy()), z)
+    assert torch.equal(z.view(torch.int16), x.view(torch.int16))
+
+
+@pytest.mark.parametrize("n_elems,dtype", [(1, torch.bfloat16), (4097, torch.bfloat16), (3_211_264, torch.bfloat16),
+                                           (100_003, torch.float32)])
+def test_gpu_zvc_matches_host_codec(ops, n_elems, dtype):
+    import importlib
+    gz = importlib.import_module(f"{PKG}.codec.gpu_zvc")
+    rt = importlib.import_module(f"{PKG}.native").runtime()
+    torch.manual_seed(n_elems)
+    x = torch.relu(torch.randn(n_elems, device="cuda")).to(dtype)
+    esz = x.element_size()
+    codec = gz.GpuZVC(n_elems, esz)
+    codec.compress(x)
+    s = codec.stream_bytes()
+    raw = x.view(torch.uint8).cpu().numpy()
+    assert s == rt.zvc_compress(raw, esz)                 # byte-identical to the host encoder
+    assert rt.zvc_decompress(s) == raw.tobytes()
+    y = torch.empty_like(x)
+    codec.decompress(s, y)
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.uint8), x.view(torch.uint8))
+    if n_elems > 4096:
+        assert len(s) < 0.65 * x.numel() * esz            # ~half zeros removed

@@ -66,7 +66,21 @@ def test_zfp_compresses_smooth_data(rt):
     assert len(rt.zfp_compress(x)) < x.nbytes * 0.8
 
 
-@pytest.mark.parametrize("codec", ["none", "lz4", "zfp+lz4", "zfp"])
+def test_zvc_host_codec(rt):
+    rng = np.random.default_rng(4)
+    for n, esz in ((1, 2), (63, 2), (4096, 2), (10_001, 2), (5000, 4)):
+        a = rng.integers(0, 65535 if esz == 2 else 2**31, n).astype(np.uint16 if esz == 2 else np.uint32)
+        a[rng.random(n) < 0.5] = 0
+        s = rt.zvc_compress(a.view(np.uint8), esz)
+        assert s[:4] == b"AZVC"
+        assert np.array_equal(np.frombuffer(rt.zvc_decompress(s), a.dtype), a)
+        if n >= 4096:
+            assert len(s) < 0.7 * a.nbytes
+    with pytest.raises(RuntimeError):
+        rt.zvc_decompress(b"AZVC" + bytes(10))
+
+
+@pytest.mark.parametrize("codec", ["none", "lz4", "zfp+lz4", "zfp", "zvc"])
 def test_codec_container(codec):
     rng = np.random.default_rng(2)
     for a in (rng.standard_normal((2, 3, 4, 5, 6)).astype(np.float32), np.zeros((3, 4), np.float64),

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Activation-compression measurements on real ResNet-50 bs=32 frontier
+tensors: GPU LZ4 (side stream) vs host LZ4 vs host zfp+lz4 (the reference's
+codec), compression ratio and throughput, and how much a side-stream encode
+slows the overlapped next forward.
+
+    python tools/codec_bench.py [--batch 32] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd import codec as C  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.gpu_lz4 import GpuLZ4  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.gpu_zvc import GpuZVC  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet, init_weights  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.native import runtime  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import SliceExecutor  # noqa: E402
+
+CUTS = ["pool1_pool", "conv2_block3_out", "conv3_block4_out", "conv4_block6_out", "conv5_block3_out"]
+
+
+def gpu_time(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    g = build_resnet("resnet50")
+    w = init_weights(g, 0)
+    ex = SliceExecutor(g, w, a.batch, outputs=CUTS + [g.output])
+    x = torch.randn(a.batch, 224, 224, 3, device="cuda")
+    outs = ex.run({g.input: x})
+    torch.cuda.synchronize()
+    rt = runtime()
+    rows = []
+    full = SliceExecutor(g, w, a.batch)
+    full.capture()
+    t_fwd = gpu_time(lambda: full.forward(0), reps=20)
+    for name in CUTS:
+        t = outs[name].contiguous()
+        nbytes = t.numel() * 2
+        codec = GpuLZ4(nbytes)
+        codec.compress(t)
+        frame = codec.frame_bytes()
+        t_gpu = gpu_time(lambda: (codec.compress(t), codec.done.synchronize()), reps=10)
+        host = t.view(torch.int16).cpu().numpy().view(np.uint16)
+        t0 = time.perf_counter()
+        hf = rt.lz4_compress(host)
+        t_host = time.perf_counter() - t0
+        f32 = t.float().cpu().numpy()
+        t0 = time.perf_counter()
+        zf = C.encode(f32, "zfp+lz4")
+        t_zfp = time.perf_counter() - t0
+        zc = GpuZVC(t.numel(), 2)
+        zc.compress(t)
+        zs = zc.stream_bytes()
+        t_zvc = gpu_time(lambda: (zc.compress(t), zc.done.synchronize()), reps=20)
+        out_t = torch.empty_like(t)
+        t_zvc_dec = gpu_time(lambda: zc.decompress(zs, out_t), reps=5)
+        # overlap: forward on the compute stream while the side stream encodes
+        def both():
+            zc.compress(t)
+            full.forward(0)
+        t_both = gpu_time(both, reps=10)
+        rows.append({"tensor": name, "shape": list(t.shape), "mbytes": nbytes / 1e6,
+                     "gpu_zvc_ratio": nbytes / len(zs), "gpu_zvc_GBps": nbytes / t_zvc / 1e9,
+                     "gpu_zvc_dec_GBps_incl_h2d": nbytes / t_zvc_dec / 1e9,
+                     "gpu_lz4_ratio": nbytes / len(frame), "gpu_lz4_GBps": nbytes / t_gpu / 1e9,
+                     "host_lz4_ratio": nbytes / len(hf), "host_lz4_GBps": nbytes / t_host / 1e9,
+                     "zfp_lz4_ratio_vs_bf16": nbytes / len(zf), "zfp_lz4_GBps": f32.nbytes / t_zfp / 1e9,
+                     "fwd_ms": t_fwd * 1e3, "fwd_plus_side_encode_ms": t_both * 1e3})
+    for r in rows:
+        print(f"{r['tensor']:18s} {r['mbytes']:7.1f} MB | GPU zvc x{r['gpu_zvc_ratio']:.2f} {r['gpu_zvc_GBps']:7.1f} GB/s"
+              f" | GPU lz4 x{r['gpu_lz4_ratio']:.2f} {r['gpu_lz4_GBps']:7.1f} GB/s"
+              f" | host lz4 x{r['host_lz4_ratio']:.2f} {r['host_lz4_GBps']:5.2f} GB/s"
+              f" | zfp+lz4 x{r['zfp_lz4_ratio_vs_bf16']:.2f} {r['zfp_lz4_GBps']:5.2f} GB/s"
+              f" | fwd {r['fwd_ms']:.3f} ms, fwd||encode {r['fwd_plus_side_encode_ms']:.3f} ms")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
