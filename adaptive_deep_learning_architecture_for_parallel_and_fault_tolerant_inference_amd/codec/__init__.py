@@ -79,6 +79,19 @@ def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads:
     return _header(c, dt_code, arr.shape) + payload
 
 
+def wrap(payload: bytes, codec: str, dtype, shape, bf16: bool = False) -> bytes:
+    """Container around a payload that was already encoded elsewhere (e.g. by the
+    GPU codecs on a side stream); `decode` reads it like any other message."""
+    dt_code = BF16 if bf16 else _DT_CODE[np.dtype(dtype)]
+    return _header(CODECS[codec], dt_code, tuple(int(s) for s in shape)) + payload
+
+
+def payload_of(buf):
+    """(codec name, dtype code, shape, payload memoryview) of an encoded message."""
+    codec, dt, shape, off = _parse(buf)
+    return _CODEC_NAMES[codec], dt, shape, memoryview(buf)[off:]
+
+
 def decode(buf, threads: int = 4) -> np.ndarray:
     """Inverse of `encode`.  bfloat16 payloads come back as uint16 arrays
     (use `is_bf16` to tell); everything else with its own dtype."""

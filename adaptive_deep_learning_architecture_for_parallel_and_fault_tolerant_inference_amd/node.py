@@ -76,8 +76,13 @@ class StageRuntime:
         self.codec = cfg.get("codec", "lz4")
         self.manifest = manifest
         g = manifest.graph()
+        # GPU stages with a GPU codec compress frontier tensors on a side HIP stream
+        # while the next micro-batch computes (two buffer sets ping-pong)
+        self.gpu_codec = self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")
         self.compute = StageCompute(g, weights, int(cfg["batch"]), node.device,
-                                    graph_capture=cfg.get("graph", True))
+                                    graph_capture=cfg.get("graph", True), num_sets=2 if self.gpu_codec else 1)
+        if self.gpu_codec:
+            self._init_gpu_codec()
         self.inq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
         self.outq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
         self.stop = threading.Event()
@@ -136,6 +141,72 @@ class StageRuntime:
         except Exception as e:  # noqa: BLE001 - any transport error ends the epoch
             self._fail("recv", e)
 
+    # ------------------------------------------------ GPU side-stream codec
+    def _init_gpu_codec(self) -> None:
+        from .codec.gpu_lz4 import GpuLZ4
+        from .codec.gpu_zvc import GpuZVC
+        ex = self.compute.ex
+        self.codecs = []
+        for j in range(2):
+            per = []
+            for o in self.compute.outputs:
+                t = ex.output_buf(o, j)
+                if self.codec == "zvc" and t.element_size() in (2, 4):
+                    per.append(GpuZVC(t.numel(), t.element_size(), self.compute.device))
+                else:
+                    per.append(GpuLZ4(t.numel() * t.element_size(), self.compute.device))
+            self.codecs.append(per)
+        self._set_free = [None, None]     # codec-done events guarding each output set
+        self._tick = 0
+
+    def _compute_gpu(self, m: Message) -> Message:
+        import torch
+        from .runtime.stage import to_torch
+        j = self._tick % 2
+        self._tick += 1
+        ex = self.compute.ex
+        for ev in self._set_free[j] or []:
+            ev.synchronize()                  # the encoders reading set j are done
+        for name, a, b in zip(self.compute.inputs, m.tensors, m.bf16):
+            dst = ex.input_buf(name, j)
+            t = to_torch(a, b, dst.device)
+            if t.dtype != dst.dtype:
+                t = t.to(dst.dtype)
+            if t.shape[-1] != dst.shape[-1]:
+                t = torch.nn.functional.pad(t, (0, dst.shape[-1] - t.shape[-1]))
+            if t.shape[0] < dst.shape[0]:
+                dst.zero_()
+            dst[: t.shape[0]].copy_(t)
+        outs = ex.forward(j)
+        ev = torch.cuda.Event()
+        ev.record()
+        dones = []
+        for o, codec in zip(self.compute.outputs, self.codecs[j]):
+            dones.append(codec.compress(outs[o], after=ev))
+        self._set_free[j] = [torch.cuda.Event() for _ in dones]
+        for e, c in zip(self._set_free[j], self.codecs[j]):
+            e.record(c.stream)
+        shapes = [tuple(outs[o].shape) for o in self.compute.outputs]
+        dtypes = [outs[o].dtype for o in self.compute.outputs]
+        return Message(self.stage + 2, m.req_id, m.epoch, m.count, [("gpu", j, k) for k in range(len(shapes))],
+                       [d == torch.bfloat16 for d in dtypes]), shapes, dtypes
+
+    def _finish_gpu_message(self, item) -> Message:
+        import numpy as np
+        import torch
+        from . import codec as C
+        m, shapes, dtypes = item
+        bufs = []
+        for (_, j, k), shp, dt in zip(m.tensors, shapes, dtypes):
+            c = self.codecs[j][k]
+            payload = c.stream_bytes() if hasattr(c, "stream_bytes") else c.frame_bytes()
+            name = "zvc" if hasattr(c, "stream_bytes") else "lz4"
+            np_dt = np.uint16 if dt == torch.bfloat16 else np.float32
+            # the receiver only needs the first `count` images: a partial batch is
+            # still sent whole (padding rows are zeros, cheap under either codec)
+            bufs.append(C.wrap(payload, name, np_dt, shp, bf16=(dt == torch.bfloat16)))
+        return Message(m.partition, m.req_id, m.epoch, m.count, bufs, m.bf16)
+
     def _compute_loop(self) -> None:
         try:
             while not self.stop.is_set():
@@ -144,9 +215,12 @@ class StageRuntime:
                 except queue.Empty:
                     continue
                 self.node.state.state = StateEnum.BUSY
-                outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
+                if self.gpu_codec:
+                    out = self._compute_gpu(m)
+                else:
+                    outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
+                    out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
                 self.processed += 1
-                out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
                 while not self.stop.is_set():
                     try:
                         self.outq.put(out, timeout=0.1)
@@ -165,6 +239,8 @@ class StageRuntime:
                     m = self.outq.get(timeout=0.1)
                 except queue.Empty:
                     continue
+                if isinstance(m, tuple):                   # GPU-encoded frontier (side stream)
+                    m = self._finish_gpu_message(m)
                 send_message(self.downstream, m, self.codec, self.node.state.chunk_size)
         except Exception as e:  # noqa: BLE001
             self._fail("send", e)

@@ -46,7 +46,9 @@ def send_message(sock: socket.socket, m: Message, codec: str = "lz4", chunk_size
                 timeout_ms)
     flags = m.bf16 or [False] * len(m.tensors)
     for t, b in zip(m.tensors, flags):
-        socket_send(C.encode(t, codec, bf16=b), sock, chunk_size, timeout_ms)
+        # bytes = a container already encoded elsewhere (GPU side-stream codec)
+        buf = t if isinstance(t, (bytes, bytearray)) else C.encode(t, codec, bf16=b)
+        socket_send(buf, sock, chunk_size, timeout_ms)
 
 
 def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int = -1) -> Optional[Message]:

@@ -39,3 +39,33 @@ def test_defer_gpu_node(transport):
     finally:
         d.shutdown(stop_workers=True)
         node.stop()
+
+
+@pytest.mark.parametrize("codec", ["zvc", "lz4"])
+def test_defer_two_gpu_stages_side_stream_codec(codec):
+    """Two stage processes' worth of Nodes (sharing the one GPU of the test box)
+    over TCP links, frontier compressed by the GPU codec on a side stream; the
+    multi-tensor cut of BASELINE config 2."""
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
+              codec=codec, min_workers=2)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"g{i}",
+                  heartbeat_ttl=1.0) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["conv3_block1_1_conv"], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(1)
+        xs = [rng.standard_normal((4, 224, 224, 3)).astype(np.float32) for _ in range(4)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=120) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert np.abs(got - want).sum(-1).max() < 0.1
+        assert all(n.runtime.gpu_codec for n in nodes)
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
