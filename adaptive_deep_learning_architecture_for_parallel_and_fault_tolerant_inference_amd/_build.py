@@ -91,7 +91,7 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
 def build_runtime(verbose: bool = False, jobs: int = 8) -> Path:
     src_dir = CSRC / "runtime"
     headers = list(src_dir.glob("*.h"))
-    srcs = sorted(src_dir.glob("*.cpp"))
+    srcs = sorted(s for s in src_dir.glob("*.cpp") if s.name != "selftest.cpp")
     out_dir = BUILD / "runtime"
     out_dir.mkdir(parents=True, exist_ok=True)
     flags = ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-pthread",

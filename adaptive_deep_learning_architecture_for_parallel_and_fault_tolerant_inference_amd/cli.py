@@ -1,0 +1,182 @@
+"""Command line: ``python -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd <cmd>``
+
+The reference has no CLI: `bash src/start_etcd.sh`, `python -m src.node`
+(edit the source for the dispatcher IP) and `python test/test.py` (edit the
+worker list / cut list in the source) (`README.md:36-56`).  Subcommands:
+
+  membership   run the membership service (etcd stand-in, port 2379)
+  node         run a worker (one per GPU)
+  serve        dispatcher + synthetic request stream, prints throughput
+               (`test/test.py`); --spawn N starts N local workers
+  local-infer  single-device throughput (`test/local_infer.py`)
+  plan         balanced cut planner: cuts, per-stage cost, frontier bytes
+  summary      model summary (layers, shapes, params)
+
+All take --config FILE (YAML) plus ADAPT_* environment overrides (utils/config.py).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import queue
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+
+from .utils.config import AdaptConfig
+
+PKG = __package__
+
+
+def _common(ap):
+    ap.add_argument("--config", default=None, help="YAML config file")
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--part-at", default=None, help="comma-separated cut layers or auto:K")
+
+
+def _cfg(a, **extra) -> AdaptConfig:
+    ov = {"model": a.model, "batch": a.batch, "part_at": a.part_at}
+    ov.update(extra)
+    return AdaptConfig.load(a.config, overrides=ov)
+
+
+def _model(cfg: AdaptConfig):
+    from .graph.manifest import load_keras_weight_list, load_model
+    from .models.model import Model, resnet
+    m = resnet(cfg.model, seed=cfg.seed, input_shape=tuple(cfg.image), classes=cfg.classes)
+    if cfg.weights:
+        if cfg.weights.endswith(".npz"):
+            m.weights = load_keras_weight_list(m.graph, cfg.weights)
+        else:
+            g, w = load_model(cfg.weights)
+            m = Model(g, w)
+    return m
+
+
+def cmd_membership(argv):
+    from .membership.server import main
+    main(argv)
+
+
+def cmd_node(argv):
+    from .node import main
+    main(argv)
+
+
+def cmd_serve(argv):
+    ap = argparse.ArgumentParser(prog="serve")
+    _common(ap)
+    ap.add_argument("--requests", type=int, default=100)
+    ap.add_argument("--spawn", type=int, default=0, help="start N local workers")
+    ap.add_argument("--device", default=None, help="device for spawned workers (cpu, cuda, cuda:i)")
+    ap.add_argument("--transport", default=None)
+    ap.add_argument("--codec", default=None)
+    a = ap.parse_args(argv)
+    cfg = _cfg(a, transport=a.transport, codec=a.codec)
+    from .dispatcher import DEFER
+    m = _model(cfg)
+    cuts = cfg.cuts(m.graph)
+    d = DEFER(membership_port=cfg.membership_port, result_port=cfg.result_port, chunk_size=cfg.chunk_size,
+              batch=cfg.batch, codec=cfg.codec, weight_codec=cfg.weight_codec, max_inflight=cfg.max_inflight,
+              task_timeout=cfg.task_timeout, worker_wait=max(cfg.worker_wait, 60 if a.spawn else 0),
+              elastic=cfg.elastic, ordered=cfg.ordered, transport=cfg.transport, min_workers=max(1, a.spawn))
+    d.membership_server.start()
+    procs = []
+    for i in range(a.spawn):
+        dev = a.device or "cpu"
+        if dev == "cuda":
+            dev = f"cuda:{i}"
+        procs.append(subprocess.Popen([sys.executable, "-m", f"{PKG}.node", "--membership-port",
+                                       str(d.membership_port), "--data-port", "0", "--config-port", "0",
+                                       "--device", dev, "--id", f"local{i}", "--ttl", str(cfg.lease_ttl)],
+                                      start_new_session=True))
+    inq, outq = queue.Queue(cfg.max_inflight * 2), queue.Queue()
+    x = np.random.default_rng(cfg.seed).standard_normal((cfg.batch,) + tuple(cfg.image)).astype(np.float32)
+    t = threading.Thread(target=d.run_defer, args=(m, cuts, inq, outq), daemon=True)
+    start = time.time()
+    t.start()
+
+    def feed():
+        for _ in range(a.requests):
+            inq.put(x)
+
+    threading.Thread(target=feed, daemon=True).start()
+    try:
+        for i in range(a.requests):
+            outq.get(timeout=600)
+        run = time.time() - start
+        print(f"{a.requests} results in {run:.3f} seconds")
+        print(f"Throughput: {a.requests * cfg.batch / run:.2f} img/s ({a.requests / run:.2f} req/s)")
+        for ts, ev in d.events:
+            print(f"  [{ts - start:8.3f}s] {ev}")
+    finally:
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+
+
+def cmd_local_infer(argv):
+    ap = argparse.ArgumentParser(prog="local-infer")
+    _common(ap)
+    ap.add_argument("--requests", type=int, default=10)
+    ap.add_argument("--device", default=None)
+    a = ap.parse_args(argv)
+    cfg = _cfg(a)
+    m = _model(cfg)
+    x = np.random.default_rng(cfg.seed).standard_normal((cfg.batch,) + tuple(cfg.image)).astype(np.float32)
+    m.predict(x, device=a.device)          # build / capture
+    start = time.time()
+    for _ in range(a.requests):
+        res = m.predict(x, device=a.device)
+    run = time.time() - start
+    print(res.shape)
+    print(f"{a.requests} results in {run:.4f} seconds")
+    print(f"Throughput: {a.requests / run:.2f} req/s ({a.requests * cfg.batch / run:.1f} img/s at batch {cfg.batch})")
+
+
+def cmd_plan(argv):
+    ap = argparse.ArgumentParser(prog="plan")
+    _common(ap)
+    ap.add_argument("--stages", type=int, default=2)
+    a = ap.parse_args(argv)
+    cfg = _cfg(a)
+    from .graph.planner import balance_ratio, plan_cuts
+    from .graph.slicer import frontier_bytes, partition
+    m = _model(cfg)
+    cuts = cfg.cuts(m.graph) if cfg.part_at else plan_cuts(m.graph, a.stages, batch=max(cfg.batch, 1))[0]
+    _, per = plan_cuts(m.graph, len(cuts) + 1, batch=max(cfg.batch, 1), candidates=cuts) if cuts else ([], [0])
+    print(f"part_at = {cuts}   (max stage / ideal = {balance_ratio(per):.3f})")
+    for s, t in zip(partition(m.graph, cuts), per):
+        fb = frontier_bytes(m.graph, s.outputs) * max(cfg.batch, 1)
+        print(f"  {s.name}: {len(s.layers):3d} layers, est {t * 1e3:7.3f} ms, sends {s.outputs} ({fb / 1e6:.1f} MB bf16)")
+
+
+def cmd_summary(argv):
+    ap = argparse.ArgumentParser(prog="summary")
+    _common(ap)
+    a = ap.parse_args(argv)
+    _model(_cfg(a)).summary()
+
+
+COMMANDS = {"membership": cmd_membership, "node": cmd_node, "serve": cmd_serve, "local-infer": cmd_local_infer,
+            "plan": cmd_plan, "summary": cmd_summary}
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in COMMANDS:
+        print(__doc__)
+        sys.exit(0 if not argv else 2)
+    COMMANDS[argv[0]](argv[1:])
+
+
+if __name__ == "__main__":
+    main()

@@ -53,6 +53,7 @@ from .membership.store import KVStore
 from .models.model import Model
 from .node_state import socket_recv, socket_send
 from .transport.messages import Message, connect, listen, recv_message, send_message
+from .utils.telemetry import METRICS, TRACER
 
 DATA_PORT = 6000     # send input data                 (src/dispatcher.py:15)
 CONFIG_PORT = 6001   # send model config + weights     (src/dispatcher.py:16)
@@ -210,6 +211,11 @@ class DEFER:
         if self.computeNodes:
             allowed = set(self.computeNodes)
             ws = {k: v for k, v in ws.items() if k in allowed or v.get("host") in allowed or "0.0.0.0" in allowed}
+        # workers that failed to load a slice (StateEnum.PARSE_ERROR) are not offered again
+        ws = {k: v for k, v in ws.items() if v.get("state") != "PARSE_ERROR"}
+        # deterministic order (host, device) keeps stage placement - and each worker's
+        # cached slices - stable across epochs; consecutive GPUs of a host become
+        # consecutive stages (neighbouring xGMI peers)
         return sorted(ws, key=lambda k: (ws[k].get("host", ""), ws[k].get("device", ""), k))
 
     # ---------------------------------------------------------- configure
@@ -402,7 +408,11 @@ class DEFER:
         with self.inflight_lock:
             task = self.inflight_tasks.pop(m.req_id, None)
         if task is None:
+            METRICS.inc("results_duplicate_dropped")
             return                                   # duplicate from a replay: drop
+        METRICS.observe("request_latency_ms", (time.time() - task["start_time"]) * 1e3)
+        METRICS.inc("results")
+        TRACER.event("complete", req=m.req_id, epoch=m.epoch, count=m.count)
         pred = m.tensors[0]
         if m.bf16 and m.bf16[0]:
             pred = (pred.astype(np.uint32) << 16).view(np.float32)

@@ -320,6 +320,9 @@ class Node:
                     if time.time() > deadline:
                         raise
                     time.sleep(0.2)
+            t = threading.Thread(target=self._telemetry_loop, daemon=True, name="node-telemetry")
+            t.start()
+            self.threads.append(t)
         if block:
             try:
                 while not self._stop.wait(1.0):
@@ -328,6 +331,24 @@ class Node:
                 pass
             finally:
                 self.stop()
+
+    def _telemetry_loop(self, period: float = 2.0) -> None:
+        """Publish load + amdsmi readings into the membership record (the
+        reference imports psutil / pynvml for this but never uses them,
+        `src/node.py:10`, `src/node_state.py:6`)."""
+        from .utils.telemetry import gpu_telemetry
+        idx = int(self.device.split(":")[1]) if self.device.startswith("cuda:") else None
+        while not self._stop.wait(period):
+            rt = self.runtime
+            rec = {"processed": rt.processed if rt else 0, "error": rt.error if rt else None}
+            if idx is not None:
+                rec.update(gpu_telemetry(idx))
+            try:
+                import psutil
+                rec["cpu_percent"] = psutil.cpu_percent(interval=None)
+            except Exception:  # noqa: BLE001
+                pass
+            self._publish(**rec)
 
     def stop(self) -> None:
         self._stop.set()
