@@ -29,10 +29,10 @@ _CFG_EFF = {0: 1.0, 4: 0.97, 1: 0.86, 2: 0.86, 3: 0.66, 5: 0.42}
 
 
 def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
-    """v2 configs split k -> (tap, ci) with shifts: non-1x1 convs need a power-of-two Cin."""
+    """v2 configs walk K tap-major in 64-channel slices: they need Cin % 64 == 0."""
     if cfg in V1_CFGS:
         return True
-    return pure or (pc.cin & (pc.cin - 1)) == 0
+    return pc.cin % 64 == 0
 NUM_CUS = 256
 
 

@@ -65,29 +65,40 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
   const int nk = kt1 > kt0 ? kt1 - kt0 : 0;
 
   // ---- per-lane source bookkeeping (rows fixed over the K loop)
+  //
+  // Tap-major K walk: when Cin % 64 == 0 (every ResNet conv except the stem) a
+  // 64-wide K tile never straddles a filter tap, so the loop visits taps
+  // (kh, kw) in order and the 64-channel slices of each tap.  Each lane keeps
+  // one 64-bit source pointer per A row for the *centre* pixel; a tap moves it
+  // by a wave-uniform (kh*W + kw)*Cin element offset and the per-row bounds
+  // test runs once per tap, so the steady-state cost per glds is a pointer add
+  // and a select (the per-tile integer division of v1 is gone).
   const int lrow = lane >> 3;      // row within the 8-row piece
   const int pchunk = lane & 7;     // physical LDS chunk this lane writes
-  int a_base[A_INS], a_ih0[A_INS], a_iw0[A_INS], a_c[A_INS];
+  const bf16* a_ptr[A_INS];        // element (pixel row0 tap origin, channel chunk) or null
+  int a_ih0[A_INS], a_iw0[A_INS];
   const int ohw = p.OH * p.OW;
 #pragma unroll
   for (int i = 0; i < A_INS; ++i) {
     const int r = (wave * A_INS + i) * 8 + lrow;        // tile row
     const int m = m0 + r;
-    a_c[i] = pchunk ^ ((r >> 1) & 7);                   // logical chunk this lane fetches
-    if (PURE) {
-      a_base[i] = m < p.M ? m * p.Cin : -1;
-      a_ih0[i] = a_iw0[i] = 0;
-    } else if (m < p.M) {
-      const int img = m / ohw;
-      const int rr = m - img * ohw;
-      const int oh = rr / p.OW;
-      const int ow = rr - oh * p.OW;
-      a_base[i] = img * p.H * p.W * p.Cin;
-      a_ih0[i] = oh * p.stride - p.pad_t;
-      a_iw0[i] = ow * p.stride - p.pad_l;
-    } else {
-      a_base[i] = -1;
-      a_ih0[i] = a_iw0[i] = 0;
+    const int c = pchunk ^ ((r >> 1) & 7);              // logical chunk this lane fetches
+    a_ih0[i] = a_iw0[i] = 0;
+    a_ptr[i] = nullptr;
+    if (m < p.M) {
+      if (PURE) {
+        a_ptr[i] = p.x + (size_t)m * p.Cin + c * 8;
+      } else {
+        const int img = m / ohw;
+        const int rr = m - img * ohw;
+        const int oh = rr / p.OW;
+        const int ow = rr - oh * p.OW;
+        a_ih0[i] = oh * p.stride - p.pad_t;
+        a_iw0[i] = ow * p.stride - p.pad_l;
+        // origin of the receptive field (may point outside the image; only
+        // dereferenced after the per-tap bounds test)
+        a_ptr[i] = p.x + ((size_t)img * p.H * p.W + (ptrdiff_t)a_ih0[i] * p.W + a_iw0[i]) * p.Cin + c * 8;
+      }
     }
   }
   const bf16* b_src[B_INS];
@@ -96,36 +107,55 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
     const int r = (wave * B_INS + i) * 8 + lrow;
     b_src[i] = p.w + (size_t)(n0 + r) * p.Kpad + (pchunk ^ ((r >> 1) & 7)) * 8;
   }
-  // integer helpers for k -> (tap, ci); Cin is a power of two (host-checked)
-  const int cin_shift = __builtin_ctz(p.Cin);
-  const int kw_magic = (65536 + p.KW - 1) / p.KW;
-
-  auto issue = [&](int kt, int slot) {
-    char* sa = smem + slot * STAGE_BYTES;
-    char* sb = sa + TILE_A;
+  // issue cursor (wave-uniform): tap (kh, kw) and channel slice cc of the next tile to fetch
+  const int cpt = p.Cin >> 6;          // 64-channel slices per tap (>= 1 on this path)
+  int ck = kt0;                        // next K tile to issue
+  int c_kh = 0, c_kw = 0, c_cc = 0;
+  if (!PURE) {
+    const int tap = ck / cpt;
+    c_cc = ck - tap * cpt;
+    c_kh = tap / p.KW;
+    c_kw = tap - c_kh * p.KW;
+  }
+  unsigned a_ok = 0;                   // per-row validity bits for the current tap
+  ptrdiff_t tap_off = 0;
+  auto tap_update = [&]() {
+    tap_off = ((ptrdiff_t)c_kh * p.W + c_kw) * p.Cin;
+    a_ok = 0;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
-      const int k = kt * BK2 + a_c[i] * 8;
-      const bf16* src = zero;
-      if (a_base[i] >= 0 && k < p.K) {
-        if (PURE) {
-          src = p.x + a_base[i] + k;
-        } else {
-          const int tap = k >> cin_shift;
-          const int ci = k & (p.Cin - 1);
-          const int kh = (tap * kw_magic) >> 16;
-          const int kw = tap - kh * p.KW;
-          const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
-          if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-            src = p.x + a_base[i] + (ih * p.W + iw) * p.Cin + ci;
-        }
-      }
+      const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+      if (a_ptr[i] != nullptr && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) a_ok |= 1u << i;
+    }
+  };
+  if (!PURE) tap_update();
+
+  auto issue = [&](int slot) {
+    char* sa = smem + slot * STAGE_BYTES;
+    char* sb = sa + TILE_A;
+    const int kt = ck;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const bf16* src;
+      if (PURE) src = a_ptr[i] != nullptr ? a_ptr[i] + (size_t)kt * BK2 : zero;
+      else src = ((a_ok >> i) & 1u) ? a_ptr[i] + tap_off + c_cc * BK2 : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sa + (wave * A_INS + i) * 1024), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (size_t)kt * BK2),
                                        (lds_void*)(sb + (wave * B_INS + i) * 1024), 16, 0, 0);
+    }
+    ++ck;
+    if (!PURE) {
+      if (++c_cc == cpt) {
+        c_cc = 0;
+        if (++c_kw == p.KW) {
+          c_kw = 0;
+          ++c_kh;
+        }
+        tap_update();
+      }
     }
   };
 
@@ -138,7 +168,7 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(kt0 + s, s);
+    if (s < nk) issue(s);
 
   for (int t = 0; t < nk; ++t) {
     // tile t must have landed; later tiles may stay in flight
@@ -149,7 +179,7 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    if (t + STAGES - 1 < nk) issue((t + STAGES - 1) % STAGES);
     const char* sa = smem + (t % STAGES) * STAGE_BYTES;
     const char* sb = sa + TILE_A;
 #pragma unroll

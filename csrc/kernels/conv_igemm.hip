@@ -318,8 +318,8 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
     ADAPT_CONV_CFGS(X)
 #undef X
     default:
-      // v2 (LDS-DMA ring) configs; needs a power-of-two Cin for the k -> (tap, ci) split
-      if (!pure && (p.Cin & (p.Cin - 1))) return hipErrorInvalidValue;
+      // v2 (LDS-DMA ring) configs walk K tap-major in 64-channel slices
+      if (p.Cin % 64) return hipErrorInvalidValue;
       e = conv_glds_launch(p, cfg, s, pure, out_f32);
   }
   if (e != hipSuccess || p.ksplit <= 1) return e;
