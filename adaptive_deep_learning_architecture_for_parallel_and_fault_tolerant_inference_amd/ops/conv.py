@@ -23,7 +23,10 @@ BK = 64
 # tile configs (must match ADAPT_CONV_CFGS in conv_igemm.hip)
 CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (32, 64),
              # v2: LDS-DMA multi-stage ring (conv_glds.hip)
-             6: (128, 128), 7: (128, 128), 8: (128, 64), 9: (64, 128), 10: (64, 64), 11: (256, 64), 12: (64, 256)}
+             6: (128, 128), 7: (128, 128), 8: (128, 64), 9: (64, 128), 10: (64, 64), 11: (256, 64), 12: (64, 256),
+             13: (128, 128), 14: (128, 128), 15: (64, 128), 16: (64, 64), 17: (128, 64), 18: (64, 128),
+             19: (256, 64), 20: (128, 128), 21: (64, 64), 22: (128, 128), 23: (64, 128), 24: (64, 64),
+             25: (128, 64), 26: (256, 64), 27: (64, 256), 28: (128, 256), 29: (256, 128)}
 V1_CFGS = (0, 1, 2, 3, 4, 5)
 _CFG_EFF = {0: 1.0, 4: 0.97, 1: 0.86, 2: 0.86, 3: 0.66, 5: 0.42}
 

@@ -24,27 +24,37 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 namespace {
 constexpr int BK2 = 64;
-constexpr int NT2 = 256;
 
 __device__ __forceinline__ int swz2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+
+// wait until at most min(ahead, K) tiles (LPW glds each) are still in flight
+template <int LPW, int K> __device__ __forceinline__ void wait_tiles(int ahead) {
+  if constexpr (K == 0) {
+    wait_vm<0>();
+  } else {
+    if (ahead >= K) wait_vm<K * LPW>();
+    else wait_tiles<LPW, K - 1>(ahead);
+  }
+}
 }  // namespace
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, bool OUT_F32>
-__global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
+template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
+  constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_INS = BM / 32, B_INS = BN / 32;   // glds instructions per wave per tile
+  constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);   // glds instructions per wave per tile
   constexpr int LPW = A_INS + B_INS;
   constexpr int TILE_A = BM * 128, STAGE_BYTES = (BM + BN) * 128;
   constexpr int EPI_LD = BN + 4;
   constexpr int EPI_BYTES = BM * EPI_LD * 4;
   constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+  static_assert((NW == 4 || NW == 8) && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "waves / tile split");
+  static_assert(STAGES >= 2 && LDS_BYTES <= 160 * 1024, "stages");
   static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -130,32 +140,35 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
   };
   if (!PURE) tap_update();
 
+  // Branch-free issue of the next K tile into ring slot `slot` (one basic
+  // block, so the interleaved schedule below can place its pieces between
+  // MFMAs).  Tiles past this block's K range fetch the zero page: the ring
+  // is always STAGES-1 tiles ahead and the wait count is a constant.
   auto issue = [&](int slot) {
     char* sa = smem + slot * STAGE_BYTES;
     char* sb = sa + TILE_A;
     const int kt = ck;
+    const bool live = kt < kt1;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
       const bf16* src;
-      if (PURE) src = a_ptr[i] != nullptr ? a_ptr[i] + (size_t)kt * BK2 : zero;
-      else src = ((a_ok >> i) & 1u) ? a_ptr[i] + tap_off + c_cc * BK2 : zero;
+      if (PURE) src = (live && a_ptr[i] != nullptr) ? a_ptr[i] + (size_t)kt * BK2 : zero;
+      else src = (live && ((a_ok >> i) & 1u)) ? a_ptr[i] + tap_off + c_cc * BK2 : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sa + (wave * A_INS + i) * 1024), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (size_t)kt * BK2),
-                                       (lds_void*)(sb + (wave * B_INS + i) * 1024), 16, 0, 0);
+      const bf16* src = live ? b_src[i] + (size_t)kt * BK2 : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (wave * B_INS + i) * 1024), 16, 0, 0);
     }
     ++ck;
     if (!PURE) {
-      if (++c_cc == cpt) {
-        c_cc = 0;
-        if (++c_kw == p.KW) {
-          c_kw = 0;
-          ++c_kh;
-        }
-        tap_update();
-      }
+      const bool roll_c = ++c_cc == cpt;
+      const bool roll_w = roll_c && c_kw + 1 == p.KW;
+      c_cc = roll_c ? 0 : c_cc;
+      c_kw = roll_w ? 0 : (roll_c ? c_kw + 1 : c_kw);
+      c_kh += roll_w ? 1 : 0;
+      tap_update();
     }
   };
 
@@ -167,33 +180,47 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
 
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s);
+  for (int s = 0; s < STAGES - 1; ++s) issue(s);
 
+  constexpr int MT = 2 * FM * FN;          // MFMAs per wave per K tile
   for (int t = 0; t < nk; ++t) {
-    // tile t must have landed; later tiles may stay in flight
-    const int ahead = nk - 1 - t;      // tiles issued after t (capped at STAGES-2)
-    if (STAGES >= 4 && ahead >= 2) wait_vm<(STAGES >= 4 ? 2 * LPW : 0)>();
-    else if (STAGES >= 3 && ahead >= 1) wait_vm<(STAGES >= 3 ? LPW : 0)>();
-    else wait_vm<0>();
+    // tile t must have landed; the STAGES-2 tiles issued after it stay in flight
+    wait_vm<(STAGES - 2) * LPW>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue((t + STAGES - 1) % STAGES);
+    const int nslot = (t + STAGES - 1) % STAGES;
+    if constexpr (!ILV) issue(nslot);
     const char* sa = smem + (t % STAGES) * STAGE_BYTES;
     const char* sb = sa + TILE_A;
+    bf16x8 af[2][FM], bfr[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, ks * 4 + fq));
+      for (int i = 0; i < FM; ++i) af[ks][i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, ks * 4 + fq));
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, ks * 4 + fq));
+      for (int j = 0; j < FN; ++j) bfr[ks][j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, ks * 4 + fq));
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+    if constexpr (ILV) {
+      // LDS-DMA pieces for tile t+STAGES-1 spread between this tile's MFMAs
+      // (one wave per SIMD: a piece costs ~100 issue cycles that otherwise
+      // serialise in front of the MFMA block)
+      issue(nslot);
+      constexpr int MPP = MT / LPW > 0 ? MT / LPW : 1;
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 * (FM + FN), 0);   // ds_read
+#pragma unroll
+      for (int q = 0; q < LPW; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MPP, 0);          // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);            // VMEM (LDS-DMA piece)
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, MT, 0);             // the rest
     }
   }
   wait_vm<0>();
@@ -216,7 +243,7 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
   constexpr int NCH = BM * CPR;
   if (p.ksplit > 1) {
     float* slab = p.ws + (size_t)blockIdx.y * p.M * p.N;
-    for (int c = tid; c < NCH; c += NT2) {
+    for (int c = tid; c < NCH; c += NT) {
       const int row = c / CPR, cc = c % CPR;
       const int m = m0 + row, n = n0 + cc * 8;
       if (m >= p.M || n >= p.N) continue;
@@ -226,7 +253,7 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
     }
     return;
   }
-  for (int c = tid; c < NCH; c += NT2) {
+  for (int c = tid; c < NCH; c += NT) {
     const int row = c / CPR, cc = c % CPR;
     const int m = m0 + row, n = n0 + cc * 8;
     if (m >= p.M || n >= p.N) continue;
@@ -264,28 +291,46 @@ __global__ __launch_bounds__(NT2, 1) void conv_glds_kernel(ConvParams p, const b
 // 16-byte aligned zero page that out-of-range lanes fetch from
 __device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
 
-// v2 tile configs: id -> BM, BN, WM, WN, STAGES (ids continue after the v1 configs)
-#define ADAPT_GLDS_CFGS(X)   \
-  X(6, 128, 128, 2, 2, 3)    \
-  X(7, 128, 128, 2, 2, 2)    \
-  X(8, 128, 64, 2, 2, 4)     \
-  X(9, 64, 128, 2, 2, 4)     \
-  X(10, 64, 64, 2, 2, 4)     \
-  X(11, 256, 64, 4, 1, 3)    \
-  X(12, 64, 256, 1, 4, 3)
+// v2 tile configs: id -> BM, BN, WM, WN (WM*WN = 4 or 8 waves), STAGES, interleaved issue
+// (ids continue after the v1 configs)
+#define ADAPT_GLDS_CFGS(X)          \
+  X(6, 128, 128, 2, 2, 3, false)    \
+  X(7, 128, 128, 2, 2, 2, false)    \
+  X(8, 128, 64, 2, 2, 4, false)     \
+  X(9, 64, 128, 2, 2, 4, false)     \
+  X(10, 64, 64, 2, 2, 4, false)     \
+  X(11, 256, 64, 4, 1, 3, false)    \
+  X(12, 64, 256, 1, 4, 3, false)    \
+  X(13, 128, 128, 2, 2, 3, true)    \
+  X(14, 128, 128, 4, 2, 3, false)   \
+  X(15, 64, 128, 2, 4, 4, false)    \
+  X(16, 64, 64, 2, 2, 4, true)      \
+  X(17, 128, 64, 4, 2, 4, false)    \
+  X(18, 64, 128, 2, 2, 4, true)     \
+  X(19, 256, 64, 4, 2, 3, false)    \
+  X(20, 128, 128, 4, 2, 3, true)    \
+  X(21, 64, 64, 2, 4, 4, false)     \
+  X(22, 128, 128, 4, 2, 4, true)    \
+  X(23, 64, 128, 2, 4, 4, true)     \
+  X(24, 64, 64, 2, 4, 4, true)      \
+  X(25, 128, 64, 4, 2, 4, true)     \
+  X(26, 256, 64, 4, 2, 3, true)     \
+  X(27, 64, 256, 2, 4, 3, true)     \
+  X(28, 128, 256, 4, 2, 3, true)    \
+  X(29, 256, 128, 4, 2, 3, true)
 
-int conv_glds_num_cfgs() { return 7; }
+int conv_glds_num_cfgs() { return 24; }
 
 bool conv_glds_cfg_tile(int cfg, int* bm, int* bn) {
   switch (cfg) {
-#define X(id, BM_, BN_, WM_, WN_, S_) case id: *bm = BM_; *bn = BN_; return true;
+#define X(id, BM_, BN_, WM_, WN_, S_, I_) case id: *bm = BM_; *bn = BN_; return true;
     ADAPT_GLDS_CFGS(X)
 #undef X
   }
   return false;
 }
 
-template <int BM, int BN, int WM, int WN, int S>
+template <int BM, int BN, int WM, int WN, int S, bool ILV>
 static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, bool out_f32) {
   static bf16* zero = nullptr;
   if (!zero) {
@@ -293,20 +338,20 @@ static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, boo
     if (e != hipSuccess) return e;
   }
   const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
-  dim3 grid(tilesM * tilesN, p.ksplit), block(NT2);
+  dim3 grid(tilesM * tilesN, p.ksplit), block(WM * WN * 64);
   if (pure) {
-    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, true, true>), grid, block, 0, s, p, zero);
-    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, true, false>), grid, block, 0, s, p, zero);
+    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, true>), grid, block, 0, s, p, zero);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, false>), grid, block, 0, s, p, zero);
   } else {
-    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, false, true>), grid, block, 0, s, p, zero);
-    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, false, false>), grid, block, 0, s, p, zero);
+    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, false, true>), grid, block, 0, s, p, zero);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, false, false>), grid, block, 0, s, p, zero);
   }
   return hipGetLastError();
 }
 
 hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pure, bool out_f32) {
   switch (cfg) {
-#define X(id, BM_, BN_, WM_, WN_, S_) case id: return launch_glds<BM_, BN_, WM_, WN_, S_>(p, s, pure, out_f32);
+#define X(id, BM_, BN_, WM_, WN_, S_, I_) case id: return launch_glds<BM_, BN_, WM_, WN_, S_, I_>(p, s, pure, out_f32);
     ADAPT_GLDS_CFGS(X)
 #undef X
   }
