@@ -169,3 +169,58 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
                            pc.K, pc.Kpad, N, int(relu), int(ksplit), int(cfg), bool(out_f32),
                            stream_handle(stream))
     return out
+
+
+# ------------------------------------------------------------------ stem
+STEM_K = 224          # 7 filter rows x (8 kw x 4 channels), csrc/kernels/stem.hip ST_K
+
+
+@dataclass
+class PackedStem:
+    """conv1 (7x7/s2, 64 filters, BN folded) packed as [64][kh*32 + kw*4 + c] bf16."""
+    w: torch.Tensor
+    bias: torch.Tensor
+    cin: int
+    pad_t: int
+    pad_l: int
+    pad_b: int
+    pad_r: int
+
+    def out_hw(self, h: int, w: int):
+        return (h + self.pad_t + self.pad_b - 7) // 2 + 1, (w + self.pad_l + self.pad_r - 7) // 2 + 1
+
+
+def pack_stem(kernel_hwio: np.ndarray, bias: np.ndarray, pads, device) -> PackedStem:
+    kh, kw, cin, cout = kernel_hwio.shape
+    if (kh, kw, cout) != (7, 7, 64) or cin > 4:
+        raise ValueError(f"stem kernel must be 7x7x(<=4)x64, got {kernel_hwio.shape}")
+    wt = np.zeros((64, 7, 8, 4), np.float32)                 # [cout][kh][kw(8)][c(4)]
+    wt[:, :, :7, :cin] = kernel_hwio.transpose(3, 0, 1, 2)
+    (pt, pb), (pl, pr) = pads
+    return PackedStem(w=torch.from_numpy(wt.reshape(64, STEM_K)).to(device=device, dtype=torch.bfloat16).contiguous(),
+                      bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),
+                      cin=cin, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
+
+
+def stem_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool: bool = True, pool_pad: int = 1,
+                 stream=None) -> torch.Tensor:
+    """x: [B,H,W,C<=4] fp32 NHWC -> relu(conv7x7/s2(x)) [-> maxpool 3x3/s2 pad pool_pad], bf16 NHWC 64 ch."""
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 4:
+        raise ValueError("stem input must be contiguous fp32 NHWC")
+    B, H, W, C = x.shape
+    if C != ps.cin:
+        raise ValueError(f"stem expects {ps.cin} channels, got {C}")
+    OH, OW = ps.out_hw(H, W)
+    if OW > 112:
+        raise ValueError(f"stem kernel handles conv rows up to 112 pixels (got {OW})")
+    PH = PW = 0
+    if pool:
+        PH, PW = (OH + 2 * pool_pad - 3) // 2 + 1, (OW + 2 * pool_pad - 3) // 2 + 1
+        need = B * PH * PW * 64
+    else:
+        need = B * OH * OW * 64
+    if out.numel() != need or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError(f"stem output buffer must be contiguous bf16 with {need} elements")
+    kernels().stem_forward(ptr(x), ptr(ps.w), ptr(ps.bias), ptr(out), B, H, W, C, OH, OW, ps.pad_t, ps.pad_l,
+                           int(pool), PH, PW, pool_pad, stream_handle(stream))
+    return out

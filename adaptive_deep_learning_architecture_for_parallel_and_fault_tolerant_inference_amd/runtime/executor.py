@@ -125,6 +125,16 @@ class SliceExecutor:
                 kf, bf = conv_ops.fold_bn(k, b, bn, eps)
                 cin_pad = ((k.shape[2] + 7) // 8) * 8
                 self.packed[i] = conv_ops.pack_conv(kf, bf, p["stride"], p["pads"], dev, cin_pad=cin_pad)
+            elif st.kind == "stem":
+                p = st.p
+                k = weights[f"{p['conv']}/kernel"]
+                bn = None
+                eps = 1e-3
+                if p["bn"]:
+                    bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
+                    eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
+                kf, bf = conv_ops.fold_bn(k, weights.get(f"{p['conv']}/bias"), bn, eps)
+                self.packed[i] = conv_ops.pack_stem(kf, bf, p["pads"], dev)
             elif st.kind == "dense":
                 name = st.out
                 k = weights[f"{name}/kernel"]                     # (in, out)
@@ -305,6 +315,9 @@ class SliceExecutor:
             k = st.kind
             if k == "pack":
                 E.input_pack(b[st.ins[0]], b[st.out], stream=stream)
+            elif k == "stem":
+                conv_ops.stem_forward(b[st.ins[0]], self.packed[i], b[st.out], pool=st.p["pool"],
+                                      pool_pad=st.p["pool_pad"], stream=stream)
             elif k == "conv":
                 cfg, ks = self.cfg[i]
                 res = b[st.ins[1]] if len(st.ins) > 1 else None

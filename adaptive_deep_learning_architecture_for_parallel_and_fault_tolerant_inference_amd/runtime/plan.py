@@ -14,6 +14,9 @@ kernels:
 * ``relu``, ``pad`` (materialised ZeroPadding2D), ``gap``,
 * ``dense``    Dense (+softmax) as a GEMM on the conv kernel + row softmax
 * ``pack``     fp32 image -> bf16 NHWC padded to 8 channels (stem input)
+* ``stem``     fp32 image -> conv1 7x7/s2 (+BN, ReLU) [-> pool1 3x3/s2] in one
+               launch (csrc/kernels/stem.hip); replaces pack+conv[+maxpool]
+               when the cut allows it
 
 Fusion never hides a tensor that the slice must emit or that another layer
 consumes, so any cut (including the multi-tensor frontier of BASELINE
@@ -21,6 +24,7 @@ config 2) is executable.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set
 
@@ -175,4 +179,46 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
     missing = [o for o in outputs if o not in produced]
     if missing:
         raise RuntimeError(f"plan does not produce outputs {missing}")
+    if os.environ.get("ADAPT_NO_STEM", "0") != "1":
+        steps = _fuse_stem(g, steps, outset)
+    return steps
+
+
+STEM_MAX_OW = 112     # csrc/kernels/stem.hip ST_OWMAX
+
+
+def _fuse_stem(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
+    """pack -> conv(7x7/s2, 64 filters, BN+ReLU) [-> maxpool 3x3/s2 pad 1]  ==>  one ``stem`` step."""
+    def users(t: str) -> List[int]:
+        return [j for j, s in enumerate(steps) if t in s.ins]
+
+    for i, st in enumerate(steps):
+        if st.kind != "pack" or st.p["cin"] > 4:
+            continue
+        u = users(st.out)
+        if len(u) != 1 or steps[u[0]].kind != "conv":
+            continue
+        cv = steps[u[0]]
+        p = cv.p
+        oh, ow = g.layers[p["conv"]].out_shape[:2]
+        if (p["kernel"] != (7, 7) or p["stride"] != 2 or p["filters"] != 64 or not p["relu"] or p["residual"]
+                or ow > STEM_MAX_OW):
+            continue
+        drop = {i, u[0]}
+        covers = list(cv.covers)
+        out = cv.out
+        pool = None
+        mu = users(cv.out)
+        if cv.out not in outset and len(mu) == 1 and steps[mu[0]].kind == "maxpool":
+            mp = steps[mu[0]]
+            if mp.p["pool"] in (3, (3, 3)) and mp.p["stride"] in (2, (2, 2)) and mp.p["pads"] == ((1, 1), (1, 1)):
+                pool = mp.p["pads"][0][0]
+                covers += mp.covers
+                out = mp.out
+                drop.add(mu[0])
+        stem = Step("stem", out, [st.ins[0]], covers,
+                    {"conv": p["conv"], "bn": p["bn"], "pads": p["pads"], "pool": pool is not None,
+                     "pool_pad": pool or 0, "filters": 64})
+        first = min(drop)
+        return [stem if j == first else s for j, s in enumerate(steps) if j == first or j not in drop]
     return steps

@@ -78,6 +78,12 @@ PYBIND11_MODULE(_C, m) {
                                     nchunks, P<uint8_t>(out), n, P<int>(err), S(s)),
           "lz4_gpu_decompress");
   });
+  m.def("stem_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW, int pad_t,
+                           int pad_l, int pool, int PH, int PW, int pool_pad, u64 s) {
+    check(adapt::stem_forward(P<const float>(x), P<const bf16>(w), P<const float>(bias), P<bf16>(out), B, H, W, C,
+                              OH, OW, pad_t, pad_l, pool, PH, PW, pool_pad, S(s)),
+          "stem_forward");
+  });
   m.def("input_pack", [](u64 x, u64 y, size_t pixels, int C, int Cp, u64 s) {
     check(adapt::input_pack(P<const float>(x), P<bf16>(y), pixels, C, Cp, S(s)), "input_pack");
   });

@@ -1,0 +1,193 @@
+// ResNet stem: fp32 image -> [7x7/s2 conv + folded BN + ReLU] -> [3x3/s2 max-pool]
+// in ONE launch (SURVEY §2.4 rows conv1_pad/conv1_conv/conv1_bn/conv1_relu/
+// pool1_pad/pool1_pool; the reference runs these as six Keras layers inside
+// `model.predict`, src/node.py:177).
+//
+// Why a dedicated kernel: the generic implicit-GEMM path needs Cin % 8, so the
+// 3-channel image is first packed to 8 channels (K = 7*7*8 = 392 -> 448, 3x the
+// real K = 147) and the 51 MB conv1 output makes a round trip through HBM for
+// the max-pool.  Here:
+//
+// * the block stages the fp32 input rows it needs into LDS as bf16 with the
+//   channel dim padded to 4, so one filter row (kw = 0..7 x 4 ch) is 64
+//   contiguous bytes and K = 7 rows x 32 = 224 (one 16x16x32 MFMA k-step per
+//   filter row, the kw = 7 / c = 3 slots carry zero weights);
+// * A fragments are single 16-byte ds_read_b128 (stride 2 -> 2 pixel columns
+//   = 16 B between neighbouring output pixels: conflict-free);
+// * the 64-output-channel weight panel (7 x 4 fragments) lives in VGPRs for the
+//   whole block;
+// * conv outputs (bias + ReLU, rounded to bf16 exactly like the unfused path)
+//   stay in LDS and the block emits the max-pooled rows directly.  One pool
+//   row needs conv rows 2p-1..2p+1: the row shared with the neighbouring
+//   block is recomputed (cheap: the stem is memory-bound).
+#include "kernels.h"
+
+namespace adapt {
+namespace {
+
+constexpr int ST_NT = 256;              // 4 waves
+constexpr int ST_OWMAX = 112;           // widest conv row a block stages (224-px input)
+constexpr int ST_PWC = 2 * ST_OWMAX + 8;  // patch columns (kw up to 7 past 2*ow)
+constexpr int ST_CROWS_POOL = 3, ST_CROWS_CONV = 2;
+constexpr int ST_PROWS = 2 * (ST_CROWS_POOL - 1) + 7;   // 11 input rows
+constexpr int ST_K = 224;               // 7 filter rows x (8 kw x 4 ch)
+static_assert(ST_PWC <= ST_NT, "one thread per patch column");
+
+struct __attribute__((aligned(8))) bf16x4s {
+  bf16 v[4];
+};
+
+}  // namespace
+
+template <bool POOL>
+__global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
+                                                        const float* __restrict__ bias, bf16* __restrict__ out,
+                                                        int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
+                                                        int PH, int PW, int pool_pad) {
+  __shared__ __attribute__((aligned(16))) bf16 patch[ST_PROWS * ST_PWC * 4];          // 20.4 KB
+  __shared__ __attribute__((aligned(16))) bf16 stage[ST_CROWS_POOL * ST_OWMAX * 64];  // 43 KB
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // 1-D grid, XCD-aware: the row blocks of one image (which share 7 of their 11
+  // input rows with their neighbours) run on the same XCD and hit its L2
+  constexpr int CROWS = POOL ? ST_CROWS_POOL : ST_CROWS_CONV;
+  const int rows_per_img = POOL ? PH : (OH + CROWS - 1) / CROWS;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = logical / rows_per_img;
+  const int t = logical - img * rows_per_img;
+  constexpr int PROWS = 2 * (CROWS - 1) + 7;
+  const int r0 = POOL ? 2 * t - pool_pad : CROWS * t;    // first conv row of this block
+  const int ih0 = 2 * r0 - pad_t;                          // input row of patch row 0
+  const int tpr = (OW + 15) >> 4;                          // 16-pixel m-tiles per conv row
+  const int pwc = 2 * tpr * 16 + 8;                        // patch columns in use
+
+  // ---- weight panel -> VGPRs (7 k-steps x 4 n-tiles of 16 columns)
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 bw[7][4];
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bw[s][n] = *(const bf16x8*)(w + (size_t)(n * 16 + fr) * ST_K + s * 32 + fq * 8);
+
+  // ---- stage input rows: fp32 NHWC (C <= 4) -> bf16 [row][col][4], zero outside the image.
+  // Thread j owns patch column j for every row (no index division); all of its
+  // loads are issued before the first conversion so the round trips overlap.
+  const float* xi = x + (size_t)img * H * W * C;
+  {
+    const int j = tid, iw = j - pad_l;
+    const bool colok = j < pwc && (unsigned)iw < (unsigned)W;
+    float pv[PROWS][4];
+#pragma unroll
+    for (int i = 0; i < PROWS; ++i) {
+      const int ih = ih0 + i;
+      const bool ok = colok && (unsigned)ih < (unsigned)H;
+      const float* px = xi + (ok ? ((size_t)ih * W + iw) * C : 0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pv[i][c] = (ok && c < C) ? px[c] : 0.f;
+    }
+    if (j < pwc) {
+#pragma unroll
+      for (int i = 0; i < PROWS; ++i) {
+        bf16x4s v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v.v[c] = f2bf(pv[i][c]);
+        *(bf16x4s*)(patch + (i * ST_PWC + j) * 4) = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- conv: each wave takes m-tiles round-robin; one tile = 16 pixels x 64 channels.
+  // The MFMA computes the transposed tile (weights as the A operand) so each
+  // lane ends up with 4 consecutive channels of one pixel: one 8-byte LDS
+  // store per 16-channel group instead of four 2-byte ones.
+  float b4[4][4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b4[n][r] = bias[n * 16 + 4 * fq + r];
+  const int ntiles = CROWS * tpr;
+  for (int mt = wave; mt < ntiles; mt += ST_NT / 64) {
+    const int rr = mt / tpr, c0 = (mt - rr * tpr) * 16;
+    f32x4 acc[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int ow = c0 + fr;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      // k = s*32 + 8*fq + e  ->  filter row s, kw = 2*fq + e/4, c = e%4
+      const bf16x8 a = *(const bf16x8*)(patch + ((2 * rr + s) * ST_PWC + 2 * ow + 2 * fq) * 4);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][n], a, acc[n], 0, 0, 0);
+    }
+    // C^T fragment: channel = 16*n + 4*fq + r, pixel = c0 + fr
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      bf16x4s v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v.v[r] = f2bf(fmaxf(acc[n][r] + b4[n][r], 0.f));
+      *(bf16x4s*)(stage + (rr * ST_OWMAX + ow) * 64 + n * 16 + 4 * fq) = v;
+    }
+  }
+  __syncthreads();
+
+  if (!POOL) {
+    // conv rows -> global, 16 B per lane
+    for (int idx = tid; idx < CROWS * OW * 8; idx += ST_NT) {
+      const int ch8 = idx & 7, pix = idx >> 3;
+      const int rr = pix / OW, ow = pix - rr * OW;
+      const int oh = r0 + rr;
+      if (oh >= OH) continue;
+      *(u32x4*)(out + (((size_t)img * OH + oh) * OW + ow) * 64 + ch8 * 8) =
+          *(const u32x4*)(stage + (rr * ST_OWMAX + ow) * 64 + ch8 * 8);
+    }
+    return;
+  }
+  // ---- 3x3/s2 max-pool of the staged conv rows: pool row t.  Post-ReLU values
+  // are >= 0, so the zero padding of pool1_pad is the 0 the max starts from.
+  for (int idx = tid; idx < PW * 8; idx += ST_NT) {
+    const int ch8 = idx & 7, pw = idx >> 3;
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = 0.f;
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+      const int oh = r0 + dr;
+      if ((unsigned)oh >= (unsigned)OH) continue;
+#pragma unroll
+      for (int dc = 0; dc < 3; ++dc) {
+        const int ow = 2 * pw - pool_pad + dc;
+        if ((unsigned)ow >= (unsigned)OW) continue;
+        V8 v;
+        v.u = *(const u32x4*)(stage + (dr * ST_OWMAX + ow) * 64 + ch8 * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], bf2f(v.e[e]));
+      }
+    }
+    V8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.e[e] = f2bf(m[e]);
+    *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = o.u;
+  }
+}
+
+hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
+                        int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
+                        hipStream_t s) {
+  if (C < 1 || C > 4 || OW < 1 || OW > ST_OWMAX || OH < 1 || B < 1) return hipErrorInvalidValue;
+  if (pool) {
+    if (PH < 1 || PW < 1 || PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1)
+      return hipErrorInvalidValue;
+    dim3 grid(PH * B);
+    hipLaunchKernelGGL(stem_kernel<true>, grid, dim3(ST_NT), 0, s, x, w, bias, out, H, W, C, OH, OW, pad_t, pad_l,
+                       PH, PW, pool_pad);
+  } else {
+    dim3 grid((OH + ST_CROWS_CONV - 1) / ST_CROWS_CONV * B);
+    hipLaunchKernelGGL(stem_kernel<false>, grid, dim3(ST_NT), 0, s, x, w, bias, out, H, W, C, OH, OW, pad_t, pad_l,
+                       0, 0, 0);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace adapt

@@ -98,12 +98,28 @@ def test_planner_balanced(r50):
 def test_plan_fuses_resnet(r50):
     steps = compile_plan(r50)
     kinds = [s.kind for s in steps]
-    assert kinds.count("conv") == 53 and kinds.count("bn") == 0 and kinds.count("add") == 0
-    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds[-2:] == ["gap", "dense"]
-    c1 = steps[1]
-    assert c1.p["pads"] == ((3, 3), (3, 3)) and c1.p["relu"] and c1.out == "conv1_relu"
+    assert kinds.count("bn") == 0 and kinds.count("add") == 0
+    assert kinds.count("conv") == 52 and kinds[0] == "stem" and kinds[-2:] == ["gap", "dense"]
+    st = steps[0]
+    assert st.p["pads"] == ((3, 3), (3, 3)) and st.p["pool"] and st.out == "pool1_pool" and st.ins == ["input_1"]
+    assert st.covers == ["conv1_pad", "conv1_conv", "conv1_bn", "conv1_relu", "pool1_pad", "pool1_pool"]
     res = [s for s in steps if s.kind == "conv" and s.p["residual"]]
     assert len(res) == 16 and all(s.out.endswith("_out") for s in res)
+
+
+def test_plan_stem_respects_cuts(r50, monkeypatch):
+    # cut right after conv1_relu: the stem keeps the conv (fused pack) but not the pool
+    s = partition(r50, ["conv1_relu"])
+    st1 = compile_plan(subgraph(r50, s[0]))
+    assert [x.kind for x in st1] == ["stem"] and not st1[0].p["pool"] and st1[0].out == "conv1_relu"
+    st2 = compile_plan(subgraph(r50, s[1]))
+    assert st2[0].kind == "maxpool"
+    # cut inside the stem (raw conv output exposed): no stem kernel, generic path
+    s = partition(r50, ["conv1_conv"])
+    assert [x.kind for x in compile_plan(subgraph(r50, s[0]))] == ["pack", "conv"]
+    monkeypatch.setenv("ADAPT_NO_STEM", "1")
+    kinds = [x.kind for x in compile_plan(r50)]
+    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds.count("conv") == 53
 
 
 def test_plan_unfused_at_cut(r50):

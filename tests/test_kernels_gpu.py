@@ -1,5 +1,6 @@
 """Numerics of every gfx950 kernel against a plain PyTorch fp32 reference
 (SURVEY §4 item 2).  Runs only on the MI355X box (`-m gpu`)."""
+import importlib
 import math
 
 import numpy as np
@@ -49,8 +50,11 @@ CONV_CASES = [
 ]
 
 
+ALL_CFGS = sorted(importlib.import_module(f"{PKG}.ops.conv").CFG_TILES)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("cfg", [None] + ALL_CFGS)
 def test_conv_vs_torch(ops, case, cfg):
     conv, _ = ops
     B, H, W, Cin, Cout, k, s, p = case
@@ -77,6 +81,37 @@ def test_conv_vs_torch(ops, case, cfg):
     torch.cuda.synchronize()
     wq = torch.from_numpy(kern).to(dev).to(torch.bfloat16).float()      # kernel sees bf16 weights
     ref = _ref_conv(x, wq, torch.from_numpy(bias).to(dev), s, ((p, p), (p, p)), res, True)
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("B,H,W,pool", [(4, 224, 224, True), (3, 224, 224, False), (2, 64, 48, True),
+                                         (2, 37, 29, True), (1, 21, 30, False)])
+def test_stem_vs_torch(ops, B, H, W, pool):
+    """Fused fp32-image -> conv1(7x7/s2)+BN+ReLU [-> 3x3/s2 max-pool] vs F.conv2d/F.max_pool2d."""
+    conv, _ = ops
+    dev = "cuda"
+    torch.manual_seed(1)
+    x = torch.randn(B, H, W, 3, device=dev) * 40.0          # caffe-preprocessed pixel scale
+    kern = (torch.randn(7, 7, 3, 64) / math.sqrt(147) / 40.0).numpy()
+    bias = (torch.randn(64) * 0.1).numpy()
+    ps = conv.pack_stem(kern, bias, ((3, 3), (3, 3)), dev)
+    OH, OW = ps.out_hw(H, W)
+    if pool:
+        PH, PW = (OH - 1) // 2 + 1, (OW - 1) // 2 + 1
+        out = torch.empty(B, PH, PW, 64, device=dev, dtype=torch.bfloat16)
+    else:
+        out = torch.empty(B, OH, OW, 64, device=dev, dtype=torch.bfloat16)
+    conv.stem_forward(x, ps, out, pool=pool)
+    torch.cuda.synchronize()
+    xq = x.to(torch.bfloat16).float()                       # kernel stages the image as bf16
+    wq = torch.from_numpy(kern).to(dev).to(torch.bfloat16).float()
+    ref = _ref_conv(xq, wq, torch.from_numpy(bias).to(dev), 2, ((3, 3), (3, 3)), None, True)
+    if pool:
+        r = F.pad(ref.permute(0, 3, 1, 2), (1, 1, 1, 1))    # ZeroPadding2D(1) then MaxPool2D(3, 2)
+        ref = F.max_pool2d(r, 3, 2).permute(0, 2, 3, 1)
+    assert out.shape == ref.shape
     err = (out.float() - ref).abs().max().item()
     scale = ref.abs().max().item() + 1e-6
     assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
