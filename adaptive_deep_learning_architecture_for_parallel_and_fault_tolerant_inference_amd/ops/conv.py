@@ -128,10 +128,31 @@ def choose_cfg(M: int, N: int, Kpad: int, occupancy: int = 2):
     return best[1], best[2]
 
 
+def sk_plan(M: int, N: int, Kpad: int, cfg: int, mult: int = 1):
+    """Stream-K launch shape: (tiles, grid, iters per block, fp32 workspace elements)."""
+    bm, bn = CFG_TILES[cfg]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    g, it = kernels().conv_sk_plan(tiles, Kpad // BK, mult)
+    return tiles, g, it, g * 2 * bm * bn
+
+
+def workspace_elems(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int:
+    """fp32 workspace a launch needs: split-K slabs or stream-K partial slots."""
+    if ksplit > 1:
+        return ksplit * M * N
+    if ksplit < 0:
+        return sk_plan(M, N, Kpad, cfg, -ksplit)[3]
+    return 0
+
+
 def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: Optional[torch.Tensor] = None,
                  relu: bool = False, cfg: Optional[int] = None, ksplit: int = 1,
-                 workspace: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    """x: [B,H,W,Cin] bf16 NHWC; out: [B,OH,OW,Cout] bf16 (or fp32 [M][Cout] for GEMM use)."""
+                 workspace: Optional[torch.Tensor] = None, stream=None,
+                 counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x: [B,H,W,Cin] bf16 NHWC; out: [B,OH,OW,Cout] bf16 (or fp32 [M][Cout] for GEMM use).
+
+    ksplit > 1: split-K (fp32 slabs + reduce launch); ksplit < 0: stream-K over
+    -ksplit x 256 blocks (v2 configs; needs `counters`, int32 zeros, one per tile)."""
     if x.dim() == 2:
         B, H, W, C = x.shape[0], 1, 1, x.shape[1]
     else:
@@ -156,15 +177,25 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
     pure = pc.kh == 1 and pc.kw == 1 and pc.stride == 1 and pc.pad_t == 0 and pc.pad_l == 0 and OH == H and OW == W
     if not cfg_supported(cfg, pc, pure):
         raise ValueError(f"tile config {cfg} needs a power-of-two input channel count (got {pc.cin})")
-    ws_ptr = 0
-    if ksplit > 1:
-        need = ksplit * M * N
+    if ksplit == 0 or (ksplit < 0 and cfg in V1_CFGS):
+        raise ValueError(f"ksplit {ksplit} not supported by tile config {cfg}")
+    ws_ptr = ctr_ptr = 0
+    sk_iters = 0
+    need = workspace_elems(M, N, pc.Kpad, cfg, ksplit)
+    if need:
         if workspace is None:
             workspace = torch.empty(need, dtype=torch.float32, device=x.device)
         if workspace.numel() < need or workspace.dtype != torch.float32:
-            raise ValueError(f"split-K {ksplit} needs an fp32 workspace of {need} elements")
+            raise ValueError(f"ksplit {ksplit} needs an fp32 workspace of {need} elements")
         ws_ptr = ptr(workspace)
-    kernels().conv_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr,
+    if ksplit < 0:
+        tiles, _, sk_iters, _ = sk_plan(M, N, pc.Kpad, cfg, -ksplit)
+        if counters is None:
+            counters = torch.zeros(tiles, dtype=torch.int32, device=x.device)
+        if counters.numel() < tiles or counters.dtype != torch.int32:
+            raise ValueError(f"stream-K needs {tiles} int32 tile counters")
+        ctr_ptr = ptr(counters)
+    kernels().conv_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, ctr_ptr, sk_iters,
                            B, H, W, C, OH, OW, N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l,
                            pc.K, pc.Kpad, N, int(relu), int(ksplit), int(cfg), bool(out_f32),
                            stream_handle(stream))

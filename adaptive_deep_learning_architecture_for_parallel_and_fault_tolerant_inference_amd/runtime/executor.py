@@ -198,6 +198,7 @@ class SliceExecutor:
             if st.kind == "dense" and st.p["softmax"]:
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
         self._ws: Optional[torch.Tensor] = None
+        self._ctr: Optional[torch.Tensor] = None
 
     def bufs(self, set_idx: int = 0):
         return ChainMap(self.sets[set_idx], self.internal)
@@ -231,13 +232,18 @@ class SliceExecutor:
         return B, H, W, C, OH, OW, pc
 
     def _ensure_ws(self) -> None:
-        need = 0
+        need = ctr = 0
         for i, (cfg, ks) in self.cfg.items():
-            if ks > 1:
+            if ks != 1:
                 B, H, W, C, OH, OW, pc = self._conv_geom(i)
-                need = max(need, ks * B * OH * OW * pc.cout)
+                need = max(need, conv_ops.workspace_elems(B * OH * OW, pc.cout, pc.Kpad, cfg, ks))
+                if ks < 0:
+                    ctr = max(ctr, conv_ops.sk_plan(B * OH * OW, pc.cout, pc.Kpad, cfg, -ks)[0])
         if need and (self._ws is None or self._ws.numel() < need):
             self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        if ctr and (self._ctr is None or self._ctr.numel() < ctr):
+            # stream-K arrival counters: zero once, every launch leaves them zero
+            self._ctr = torch.zeros(ctr, dtype=torch.int32, device=self.device)
 
     def _select_configs(self, tune: bool) -> None:
         table = load_tuning()
@@ -274,18 +280,25 @@ class SliceExecutor:
             best = None
             ktiles = pc.Kpad // conv_ops.BK
             for cfg in conv_ops.CFG_TILES:
-                for ks in (1, 2, 3, 4, 6, 8):
+                for ks in (1, 2, 3, 4, 6, 8, -1, -2):
                     if ks > 1 and ktiles // ks < 2:
                         continue
-                    ws = torch.empty(ks * M * N, dtype=torch.float32, device=self.device) if ks > 1 else None
+                    if ks < 0 and cfg in conv_ops.V1_CFGS:
+                        continue
                     try:
-                        conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws)
+                        need = conv_ops.workspace_elems(M, N, pc.Kpad, cfg, ks)
+                        ws = torch.empty(need, dtype=torch.float32, device=self.device) if need else None
+                        ctr = None
+                        if ks < 0:
+                            ctr = torch.zeros(conv_ops.sk_plan(M, N, pc.Kpad, cfg, -ks)[0], dtype=torch.int32,
+                                              device=self.device)
+                        conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr)
                         torch.cuda.synchronize(self.device)
                         # time device work only: `reps` launches captured in one hipGraph
                         gg = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(gg):
                             for _ in range(reps):
-                                conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws)
+                                conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr)
                         gg.replay()
                         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s.record()
@@ -322,7 +335,7 @@ class SliceExecutor:
                 cfg, ks = self.cfg[i]
                 res = b[st.ins[1]] if len(st.ins) > 1 else None
                 conv_ops.conv_forward(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
-                                      cfg=cfg, ksplit=ks, workspace=self._ws, stream=stream)
+                                      cfg=cfg, ksplit=ks, workspace=self._ws, stream=stream, counters=self._ctr)
             elif k == "maxpool":
                 (pt, _), (pl, _) = st.p["pads"]
                 E.maxpool(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, True, stream=stream)
@@ -342,7 +355,8 @@ class SliceExecutor:
                 cfg, ks = self.cfg[i]
                 x = b[st.ins[0]].reshape(self.batch, -1)
                 dst = self._logits[i] if st.p["softmax"] else b[st.out]
-                conv_ops.conv_forward(x, self.packed[i], dst, cfg=cfg, ksplit=ks, workspace=self._ws, stream=stream)
+                conv_ops.conv_forward(x, self.packed[i], dst, cfg=cfg, ksplit=ks, workspace=self._ws, stream=stream,
+                                      counters=self._ctr)
                 if st.p["softmax"]:
                     E.softmax_rows(dst, b[st.out], stream=stream)
             elif k == "softmax":

@@ -26,6 +26,11 @@ static hipStream_t S(u64 v) { return reinterpret_cast<hipStream_t>(v); }
 PYBIND11_MODULE(_C, m) {
   m.doc() = "ADAPT MI355X (gfx950) HIP kernels";
   m.def("conv_num_cfgs", &adapt::conv_num_cfgs);
+  m.def("conv_sk_plan", [](int tiles, int kt, int mult) {
+    int g, it;
+    adapt::conv_sk_plan(tiles, kt, mult, &g, &it);
+    return py::make_tuple(g, it);
+  });
   m.def("conv_cfg_tile", [](int cfg) {
     int bm, bn;
     adapt::conv_cfg_tile(cfg, &bm, &bn);
@@ -33,9 +38,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def(
       "conv_forward",
-      [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, int B, int H, int W, int Cin, int OH, int OW, int N,
-         int KH, int KW, int stride, int pad_t, int pad_l, int K, int Kpad, int ldo, int relu, int ksplit, int cfg,
-         bool out_f32, u64 stream) {
+      [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, u64 counters, int sk_iters, int B, int H, int W,
+         int Cin, int OH, int OW, int N, int KH, int KW, int stride, int pad_t, int pad_l, int K, int Kpad, int ldo,
+         int relu, int ksplit, int cfg, bool out_f32, u64 stream) {
         adapt::ConvParams p;
         p.x = P<const bf16>(x);
         p.w = P<const bf16>(w);
@@ -43,6 +48,8 @@ PYBIND11_MODULE(_C, m) {
         p.res = P<const bf16>(res);
         p.out = P<void>(out);
         p.ws = P<float>(ws);
+        p.counters = P<int>(counters);
+        p.sk_iters = sk_iters;
         p.B = B; p.H = H; p.W = W; p.Cin = Cin;
         p.OH = OH; p.OW = OW; p.N = N;
         p.KH = KH; p.KW = KW; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;

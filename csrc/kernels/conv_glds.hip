@@ -42,36 +42,55 @@ template <int LPW, int K> __device__ __forceinline__ void wait_tiles(int ahead) 
 }
 }  // namespace
 
+// Stream-K bookkeeping of one (tile, K-range) segment.  slot < 0: the segment
+// covers the whole K range (normal epilogue).
+struct SkSeg {
+  int slot;      // this segment's fp32 partial slot in p.ws
+  int nseg;      // segments (= consecutive blocks) covering the tile
+  int seg;       // this segment's index among them (summation order)
+  int g_first;   // first block covering the tile
+};
+
+__device__ __forceinline__ int sk_slot(int g, int tile, int kt, int iters) {
+  // a block's first segment uses slot 2g, its last (when it started in an earlier tile) 2g+1
+  return 2 * g + ((long long)g * iters >= (long long)tile * kt ? 0 : 1);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+constexpr int CPOL_SC1 = 16;   // gfx950 cache policy: sc1 (bypass L1, write-through L2)
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+struct GldsShape {
+  static constexpr int NW = WM * WN, NT = NW * 64;
+  static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int EPI_BYTES = BM * (BN + 4) * 4;
+  static constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
+};
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32>
-__global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
-  constexpr int NW = WM * WN, NT = NW * 64;
+__device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __restrict__ zero, char* smem,
+                                          int tile, int kt0, int kt1, int split_idx, const SkSeg& sk) {
+  using S = GldsShape<BM, BN, WM, WN, STAGES>;
+  constexpr int NW = S::NW, NT = S::NT;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);   // glds instructions per wave per tile
   constexpr int LPW = A_INS + B_INS;
-  constexpr int TILE_A = BM * 128, STAGE_BYTES = (BM + BN) * 128;
+  constexpr int TILE_A = BM * 128, STAGE_BYTES = S::STAGE_BYTES;
   constexpr int EPI_LD = BN + 4;
-  constexpr int EPI_BYTES = BM * EPI_LD * 4;
-  constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
   static_assert((NW == 4 || NW == 8) && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "waves / tile split");
-  static_assert(STAGES >= 2 && LDS_BYTES <= 160 * 1024, "stages");
+  static_assert(STAGES >= 2 && S::LDS_BYTES + 16 <= 160 * 1024, "stages");
   static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
 
   const int tilesN = (p.N + BN - 1) / BN;
-  const int tilesM = (p.M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, tilesM * tilesN);
   const int tm = tile / tilesN, tn = tile % tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
-
-  const int ktiles_total = p.Kpad / BK2;
-  const int kt_per = (ktiles_total + p.ksplit - 1) / p.ksplit;
-  const int kt0 = blockIdx.y * kt_per;
-  const int kt1 = min(ktiles_total, kt0 + kt_per);
   const int nk = kt1 > kt0 ? kt1 - kt0 : 0;
 
   // ---- per-lane source bookkeeping (rows fixed over the K loop)
@@ -242,7 +261,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p
   constexpr int CPR = BN / 8;
   constexpr int NCH = BM * CPR;
   if (p.ksplit > 1) {
-    float* slab = p.ws + (size_t)blockIdx.y * p.M * p.N;
+    float* slab = p.ws + (size_t)split_idx * p.M * p.N;
     for (int c = tid; c < NCH; c += NT) {
       const int row = c / CPR, cc = c % CPR;
       const int m = m0 + row, n = n0 + cc * 8;
@@ -253,13 +272,63 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p
     }
     return;
   }
+  const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);
+  if (sk.slot >= 0) {
+    // Stream-K partial tile: publish it with 16-B sc1 stores, then one lane
+    // counts the arrival; the last of the tile's segments combines all partials
+    // in segment order (deterministic) and runs the epilogue.  Nobody waits
+    // on anybody, so co-residency of the grid is never required.
+    // (MI355X_MICROARCH.md "inter-workgroup visibility", hand-off row 1.)
+    const int base = sk.slot * BM * BN;
+    for (int c = tid; c < NCH; c += NT) {
+      const int row = c / CPR, cc = c % CPR;
+      const float* e = epi + row * EPI_LD + cc * 8;
+      const int off = (base + row * BN + cc * 8) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)e, wsr, off, 0, CPOL_SC1);
+      __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(e + 4), wsr, off + 16, 0, CPOL_SC1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)(smem + S::LDS_BYTES);
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == sk.nseg - 1;
+      if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+  }
+  const int ktt = p.Kpad / BK2;
   for (int c = tid; c < NCH; c += NT) {
     const int row = c / CPR, cc = c % CPR;
     const int m = m0 + row, n = n0 + cc * 8;
     if (m >= p.M || n >= p.N) continue;
     const float* e = epi + row * EPI_LD + cc * 8;
-    f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    float v[8];
+    if (sk.slot < 0) {
+      f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
+      v[0] = v0[0]; v[1] = v0[1]; v[2] = v0[2]; v[3] = v0[3];
+      v[4] = v1[0]; v[5] = v1[1]; v[6] = v1[2]; v[7] = v1[3];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = 0.f;
+      for (int sg = 0; sg < sk.nseg; ++sg) {
+        f32x4 v0, v1;
+        if (sg == sk.seg) {
+          v0 = *(const f32x4*)e;
+          v1 = *(const f32x4*)(e + 4);
+        } else {
+          const int off = (sk_slot(sk.g_first + sg, tile, ktt, p.sk_iters) * BM * BN + row * BN + cc * 8) * 4;
+          u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(wsr, off, 0, CPOL_SC1);
+          u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(wsr, off + 16, 0, CPOL_SC1);
+          v0 = __builtin_bit_cast(f32x4, r0);
+          v1 = __builtin_bit_cast(f32x4, r1);
+        }
+        v[0] += v0[0]; v[1] += v0[1]; v[2] += v0[2]; v[3] += v0[3];
+        v[4] += v1[0]; v[5] += v1[1]; v[6] += v1[2]; v[7] += v1[3];
+      }
+    }
     if (p.bias) {
       f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
       v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
@@ -285,6 +354,44 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p
       for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
       *(u32x4*)((bf16*)p.out + (size_t)m * p.ldo + n) = o.u;
     }
+  }
+}
+
+// One launch = (a) data-parallel tiles x split-K slices (p.ksplit >= 1), or
+// (b) stream-K (p.ksplit < 0): the tiles x K-tiles iteration space is cut into
+// equal contiguous ranges of p.sk_iters, one per block, so ~200-tile problems
+// keep every CU busy instead of leaving a quarter of the chip idle.
+template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
+  using S = GldsShape<BM, BN, WM, WN, STAGES>;
+  __shared__ __attribute__((aligned(16))) char smem[S::LDS_BYTES + 16];
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int kt = p.Kpad / BK2;
+  if (p.ksplit >= 1) {
+    const int tile = xcd_remap(blockIdx.x, tiles);
+    const int kt_per = (kt + p.ksplit - 1) / p.ksplit;
+    const int kt0 = blockIdx.y * kt_per;
+    const int kt1 = min(kt, kt0 + kt_per);
+    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32>(p, zero, smem, tile, kt0, kt1, blockIdx.y,
+                                                          SkSeg{-1, 1, 0, 0});
+    return;
+  }
+  const int g = blockIdx.x, iters = p.sk_iters;
+  const int total = tiles * kt;
+  int it = g * iters;
+  const int it_end = min(total, it + iters);
+  while (it < it_end) {
+    const int tile = it / kt;
+    const int kbeg = it - tile * kt;
+    const int kend = min(kt, kbeg + (it_end - it));
+    SkSeg sk{-1, 1, 0, 0};
+    if (kbeg != 0 || kend != kt) {
+      const int g_first = (tile * kt) / iters, g_last = ((tile + 1) * kt - 1) / iters;
+      sk = SkSeg{sk_slot(g, tile, kt, iters), g_last - g_first + 1, g - g_first, g_first};
+    }
+    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32>(p, zero, smem, tile, kbeg, kend, 0, sk);
+    it += kend - kbeg;
+    __syncthreads();   // the next segment's DMA reuses the epilogue's LDS
   }
 }
 
@@ -321,6 +428,17 @@ __device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
 
 int conv_glds_num_cfgs() { return 24; }
 
+// stream-K grid: `mult` x 256 blocks (one per CU), each taking ceil(total / G)
+// consecutive (tile, K-tile) iterations
+void conv_sk_plan(int tiles, int kt, int mult, int* grid, int* iters) {
+  const long long total = (long long)tiles * kt;
+  long long G = 256LL * (mult > 0 ? mult : 1);
+  if (G > total) G = total;
+  const long long it = (total + G - 1) / G;
+  *iters = (int)it;
+  *grid = (int)((total + it - 1) / it);
+}
+
 bool conv_glds_cfg_tile(int cfg, int* bm, int* bn) {
   switch (cfg) {
 #define X(id, BM_, BN_, WM_, WN_, S_, I_) case id: *bm = BM_; *bn = BN_; return true;
@@ -339,6 +457,12 @@ static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, boo
   }
   const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
   dim3 grid(tilesM * tilesN, p.ksplit), block(WM * WN * 64);
+  if (p.ksplit < 0) {
+    int g, iters;
+    conv_sk_plan(tilesM * tilesN, p.Kpad / BK2, -p.ksplit, &g, &iters);
+    if (!p.counters || !p.ws || iters != p.sk_iters) return hipErrorInvalidValue;
+    grid = dim3(g, 1);
+  }
   if (pure) {
     if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, true>), grid, block, 0, s, p, zero);
     else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, false>), grid, block, 0, s, p, zero);

@@ -313,6 +313,7 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
   const bool pure = (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.pad_t == 0 && p.pad_l == 0 &&
                      p.H == p.OH && p.W == p.OW);
   hipError_t e = hipErrorInvalidValue;
+  if (p.ksplit == 0 || (p.ksplit < 0 && cfg < conv_num_cfgs())) return hipErrorInvalidValue;   // stream-K: v2 only
   switch (cfg) {
 #define X(id, BM_, BN_, WM_, WN_) case id: e = launch_cfg<BM_, BN_, WM_, WN_>(p, s, pure, out_f32); break;
     ADAPT_CONV_CFGS(X)

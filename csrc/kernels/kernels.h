@@ -15,8 +15,11 @@ struct ConvParams {
   int KH, KW, stride, pad_t, pad_l;
   int M, K, Kpad, ldo;
   int relu;
-  int ksplit;
+  int ksplit;       // >= 1: split-K slices (fp32 slabs in ws + reduce); < 0: stream-K over -ksplit x 256 blocks
+  int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
+  int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_sk_plan)
 };
+void conv_sk_plan(int tiles, int kt, int mult, int* grid, int* iters);
 hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
 int zvc_seg();
 size_t zvc_scratch_bytes(size_t n, int esz);

@@ -37,6 +37,13 @@ struct __attribute__((aligned(8))) bf16x4s {
   bf16 v[4];
 };
 
+// staged conv output: [pixel][64 ch] bf16 = 8 chunks of 16 B per pixel, chunk
+// index XOR-swizzled by (pixel >> 1) so the C^T fragment stores (16 pixels x
+// one chunk) spread over all 64 banks
+__device__ __forceinline__ int stage_off(int row, int pix, int chunk) {
+  return ((row * ST_OWMAX + pix) * 8 + (chunk ^ ((pix >> 1) & 7))) * 8;   // in bf16 elements
+}
+
 }  // namespace
 
 template <bool POOL>
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
       bf16x4s v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) v.v[r] = f2bf(fmaxf(acc[n][r] + b4[n][r], 0.f));
-      *(bf16x4s*)(stage + (rr * ST_OWMAX + ow) * 64 + n * 16 + 4 * fq) = v;
+      *(bf16x4s*)(stage + stage_off(rr, ow, 2 * n + (fq >> 1)) + 4 * (fq & 1)) = v;
     }
   }
   __syncthreads();
@@ -140,7 +147,7 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
       const int oh = r0 + rr;
       if (oh >= OH) continue;
       *(u32x4*)(out + (((size_t)img * OH + oh) * OW + ow) * 64 + ch8 * 8) =
-          *(const u32x4*)(stage + (rr * ST_OWMAX + ow) * 64 + ch8 * 8);
+          *(const u32x4*)(stage + stage_off(rr, ow, ch8));
     }
     return;
   }
@@ -160,7 +167,7 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
         const int ow = 2 * pw - pool_pad + dc;
         if ((unsigned)ow >= (unsigned)OW) continue;
         V8 v;
-        v.u = *(const u32x4*)(stage + (dr * ST_OWMAX + ow) * 64 + ch8 * 8);
+        v.u = *(const u32x4*)(stage + stage_off(dr, ow, ch8));
 #pragma unroll
         for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], bf2f(v.e[e]));
       }

@@ -117,6 +117,45 @@ def test_stem_vs_torch(ops, B, H, W, pool):
     assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
 
 
+V2_CFGS = [c for c in ALL_CFGS if c >= 6]
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] % 64 == 0])
+@pytest.mark.parametrize("cfg", V2_CFGS)
+@pytest.mark.parametrize("mult", [1, 2])
+def test_conv_stream_k(ops, case, cfg, mult):
+    """Stream-K (ksplit < 0): partial tiles published by one block and combined by
+    the last arriver must match torch, be bitwise reproducible and leave the
+    tile counters at zero."""
+    conv, _ = ops
+    B, H, W, Cin, Cout, k, s, p = case
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(B, H, W, Cin, device=dev).to(torch.bfloat16)
+    kern = (torch.randn(k, k, Cin, Cout) / math.sqrt(k * k * Cin)).numpy()
+    bias = (torch.randn(Cout) * 0.1).numpy()
+    pc = conv.pack_conv(kern, bias, s, ((p, p), (p, p)), dev)
+    OH, OW = pc.out_hw(H, W)
+    M = B * OH * OW
+    res = torch.randn(B, OH, OW, Cout, device=dev).to(torch.bfloat16)
+    out = torch.empty(B, OH, OW, Cout, device=dev, dtype=torch.bfloat16)
+    tiles, grid, iters, need = conv.sk_plan(M, Cout, pc.Kpad, cfg, mult)
+    ws = torch.empty(need, device=dev, dtype=torch.float32)
+    ctr = torch.zeros(tiles, device=dev, dtype=torch.int32)
+    conv.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=-mult, workspace=ws, counters=ctr)
+    torch.cuda.synchronize()
+    assert int(ctr.abs().sum()) == 0
+    out2 = torch.empty_like(out)
+    conv.conv_forward(x, pc, out2, residual=res, relu=True, cfg=cfg, ksplit=-mult, workspace=ws, counters=ctr)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    wq = torch.from_numpy(kern).to(dev).to(torch.bfloat16).float()
+    ref = _ref_conv(x, wq, torch.from_numpy(bias).to(dev), s, ((p, p), (p, p)), res, True)
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale}) grid {grid} iters {iters}"
+
+
 def test_conv_f32_out_dense(ops):
     conv, _ = ops
     dev = "cuda"

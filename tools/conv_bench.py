@@ -28,7 +28,7 @@ R50 = [  # B, H, W, Cin, Cout, k, stride, pad, residual
 ]
 
 
-def bench(shape, only=None, reps=20):
+def bench(shape, only=None, reps=20, ks_list=(1, 2, 3, 4, 6, 8, -1, -2)):
     B, H, W, Cin, Cout, k, s, p, has_res = shape
     dev = "cuda"
     x = torch.randn(B, H, W, Cin, device=dev).to(torch.bfloat16)
@@ -45,17 +45,22 @@ def bench(shape, only=None, reps=20):
     for cfg in (only or C.CFG_TILES):
         if not C.cfg_supported(cfg, pc, pure):
             continue
-        for ks in (1, 2, 3, 4, 6, 8):
+        for ks in ks_list:
             if ks > 1 and pc.Kpad // 64 // ks < 2:
                 continue
-            ws = torch.empty(ks * M * N, device=dev, dtype=torch.float32) if ks > 1 else None
+            if ks < 0 and cfg in C.V1_CFGS:
+                continue
+            need = C.workspace_elems(M, N, pc.Kpad, cfg, ks)
+            ws = torch.empty(need, device=dev, dtype=torch.float32) if need else None
+            ctr = torch.zeros(C.sk_plan(M, N, pc.Kpad, cfg, -ks)[0], device=dev, dtype=torch.int32) if ks < 0 else None
             try:
-                C.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws)
+                C.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for _ in range(reps):
-                        C.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws)
+                        C.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws,
+                                       counters=ctr)
                 g.replay()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -68,7 +73,7 @@ def bench(shape, only=None, reps=20):
                 print("skip", cfg, ks, e)
                 continue
             bm, bn = C.CFG_TILES[cfg]
-            blocks = math.ceil(M / bm) * math.ceil(N / bn) * ks
+            blocks = C.sk_plan(M, N, pc.Kpad, cfg, -ks)[1] if ks < 0 else math.ceil(M / bm) * math.ceil(N / bn) * ks
             rows.append((t, cfg, ks, blocks))
     rows.sort()
     print(f"\n== B{B} {H}x{W}x{Cin} -> {Cout} k{k} s{s}  M={M} N={N} K={pc.K}  "
@@ -83,11 +88,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", action="append", default=[])
     ap.add_argument("--only", default="")
+    ap.add_argument("--ks", default="1,2,3,4,6,8,-1,-2")
     a = ap.parse_args()
     only = [int(c) for c in a.only.split(",") if c] or None
     shapes = [tuple(int(v) for v in s.split(",")) + ((0,) if len(s.split(",")) == 8 else ()) for s in a.shape] or R50
     for sh in shapes:
-        bench(sh, only)
+        bench(sh, only, ks_list=[int(k) for k in a.ks.split(",")])
 
 
 if __name__ == "__main__":
