@@ -47,6 +47,14 @@ def _parse(buf: bytes):
 
 def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads: int = 4) -> bytes:
     """Encode an ndarray.  `bf16=True` marks a uint16 array as bfloat16 payload."""
+    hdr, payload = encode_parts(arr, codec, bf16, threads)
+    return hdr + bytes(payload)
+
+
+def encode_parts(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads: int = 4):
+    """(header bytes, payload buffer) of `encode`, without concatenating them:
+    for ``none`` the payload is a zero-copy view of `arr`, and the framing layer
+    sends both parts as one frame (`send_frame_parts`)."""
     arr = np.asarray(arr)
     if not arr.flags.c_contiguous:
         arr = arr.copy(order="C")            # (np.ascontiguousarray would promote 0-d to 1-d)
@@ -65,7 +73,7 @@ def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads:
         arr_z = arr
     raw = arr.reshape(-1).view(np.uint8) if arr.size else np.zeros(0, np.uint8)
     if c == 0:
-        payload = raw.tobytes()
+        payload = memoryview(raw)
     elif c == 1:
         payload = rt.lz4_compress(raw)
     elif c == 2:
@@ -75,8 +83,8 @@ def encode(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, threads:
     else:
         payload = rt.zvc_compress(raw, arr.dtype.itemsize)
     if c != 0 and len(payload) >= raw.nbytes:
-        c, payload = 0, raw.tobytes()
-    return _header(c, dt_code, arr.shape) + payload
+        c, payload = 0, memoryview(raw)
+    return _header(c, dt_code, arr.shape), payload
 
 
 def wrap(payload: bytes, codec: str, dtype, shape, bf16: bool = False) -> bytes:
@@ -92,24 +100,30 @@ def payload_of(buf):
     return _CODEC_NAMES[codec], dt, shape, memoryview(buf)[off:]
 
 
-def decode(buf, threads: int = 4) -> np.ndarray:
+def decode(buf, threads: int = 4, copy: bool = True) -> np.ndarray:
     """Inverse of `encode`.  bfloat16 payloads come back as uint16 arrays
-    (use `is_bf16` to tell); everything else with its own dtype."""
+    (use `is_bf16` to tell); everything else with its own dtype.  With
+    ``copy=False`` raw / LZ4 / ZVC payloads come back as read-only views of the
+    received (or decompressed) buffer instead of fresh copies."""
     buf = bytes(buf) if not isinstance(buf, (bytes, bytearray, memoryview)) else buf
     codec, dt, shape, off = _parse(buf)
     rt = runtime()
     body = memoryview(buf)[off:]
     np_dt = np.uint16 if dt == BF16 else DTYPES[dt]
+
+    def _fin(a):
+        a = a.reshape(shape)
+        return a.copy() if copy else a
     if codec == 0:
-        return np.frombuffer(bytes(body), dtype=np_dt).reshape(shape).copy()
+        return _fin(np.frombuffer(body, dtype=np_dt))
     if codec == 1:
-        return np.frombuffer(rt.lz4_decompress(body), dtype=np_dt).reshape(shape).copy()
+        return _fin(np.frombuffer(rt.lz4_decompress(body), dtype=np_dt))
     if codec == 2:
         return rt.zfp_decompress(rt.lz4_decompress(body), threads).reshape(shape)
     if codec == 3:
         return rt.zfp_decompress(body, threads).reshape(shape)
     if codec == 4:
-        return np.frombuffer(rt.zvc_decompress(body), dtype=np_dt).reshape(shape).copy()
+        return _fin(np.frombuffer(rt.zvc_decompress(body), dtype=np_dt))
     raise ValueError(f"unknown codec id {codec}")
 
 

@@ -39,6 +39,10 @@ class GpuLZ4:
         self.stream = torch.cuda.Stream(device=self.device)
         self.done = torch.cuda.Event()
         self._n = 0
+        self._host: Optional[torch.Tensor] = None     # persistent pinned D2H buffer (frame_view)
+        self._stage: Optional[torch.Tensor] = None    # persistent pinned H2D staging (decompress)
+        self._dframe: Optional[torch.Tensor] = None
+        self._h2d_done: Optional[torch.cuda.Event] = None
 
     def compress(self, t: torch.Tensor, after: Optional[torch.cuda.Event] = None) -> torch.cuda.Event:
         """Enqueue compression of `t` (any dtype, contiguous) on the side stream."""
@@ -62,15 +66,35 @@ class GpuLZ4:
         self._n = n
         return self.done
 
-    def frame_bytes(self) -> bytes:
-        """Wait for the last compress() and return its LZ4 frame."""
+    def frame_view(self) -> memoryview:
+        """Wait for the last compress() and return its LZ4 frame as a view of a
+        persistent pinned host buffer (valid until the next frame_view call)."""
         self.done.synchronize()
         tot = int(self.total_host.item())
-        host = torch.empty(tot, dtype=torch.uint8, pin_memory=True)
+        if self._host is None:
+            self._host = torch.empty(self.frame.numel(), dtype=torch.uint8, pin_memory=True)
         with torch.cuda.stream(self.stream):
-            host.copy_(self.frame[:tot], non_blocking=True)
+            self._host[:tot].copy_(self.frame[:tot], non_blocking=True)
         self.stream.synchronize()
-        return host.numpy().tobytes()
+        return memoryview(self._host.numpy())[:tot]
+
+    def frame_bytes(self) -> bytes:
+        """Wait for the last compress() and return its LZ4 frame."""
+        return bytes(self.frame_view())
+
+    def _to_device(self, raw) -> torch.Tensor:
+        nb = len(raw)
+        if self._stage is None or self._stage.numel() < nb:
+            cap = max(nb, self.frame.numel())
+            self._stage = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            self._dframe = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        if self._h2d_done is not None:
+            self._h2d_done.synchronize()
+        self._stage.numpy()[:nb] = np.frombuffer(raw, dtype=np.uint8)
+        self._dframe[:nb].copy_(self._stage[:nb], non_blocking=True)
+        self._h2d_done = torch.cuda.Event()
+        self._h2d_done.record(torch.cuda.current_stream(self.device))
+        return self._dframe
 
     def decompress(self, frame, out: torch.Tensor) -> torch.Tensor:
         """Decode an LZ4 frame (bytes, or a uint8 device tensor) into `out` (on the
@@ -85,8 +109,7 @@ class GpuLZ4:
             data = np.frombuffer(runtime().lz4_decompress(raw), dtype=np.uint8)
             out.view(torch.uint8).reshape(-1).copy_(torch.from_numpy(data.copy()))
             return out
-        dev_frame = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device, non_blocking=False) \
-            if not isinstance(frame, torch.Tensor) else frame
+        dev_frame = self._to_device(raw) if not isinstance(frame, torch.Tensor) else frame
         d_offs = torch.from_numpy(offs.astype(np.int32)).to(self.device)
         d_words = torch.from_numpy(words.astype(np.int64).astype(np.uint32).view(np.int32)).to(self.device)
         self.err.zero_()

@@ -42,6 +42,10 @@ class GpuZVC:
         self.total_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         self.stream = torch.cuda.Stream(device=self.device)
         self.done = torch.cuda.Event()
+        self._host: Optional[torch.Tensor] = None     # persistent pinned D2H buffer (stream_view)
+        self._stage: Optional[torch.Tensor] = None    # persistent pinned H2D staging (decompress)
+        self._dstream: Optional[torch.Tensor] = None
+        self._h2d_done: Optional[torch.cuda.Event] = None
 
     def compress(self, t: torch.Tensor, after: Optional[torch.cuda.Event] = None) -> torch.cuda.Event:
         if not t.is_contiguous() or t.device != self.device or t.element_size() != self.esz:
@@ -63,22 +67,43 @@ class GpuZVC:
         t.record_stream(self.stream)
         return self.done
 
-    def stream_bytes(self) -> bytes:
+    def stream_view(self) -> memoryview:
+        """Wait for the last compress() and return its stream as a view of a
+        persistent pinned host buffer (valid until the next stream_view call)."""
         self.done.synchronize()
         tot = int(self.total_host.item())
-        host = torch.empty(tot, dtype=torch.uint8, pin_memory=True)
+        if self._host is None:
+            self._host = torch.empty(self.out.numel(), dtype=torch.uint8, pin_memory=True)
         with torch.cuda.stream(self.stream):
-            host.copy_(self.out[:tot], non_blocking=True)
+            self._host[:tot].copy_(self.out[:tot], non_blocking=True)
         self.stream.synchronize()
-        return host.numpy().tobytes()
+        return memoryview(self._host.numpy())[:tot]
+
+    def stream_bytes(self) -> bytes:
+        return bytes(self.stream_view())
+
+    def _to_device(self, raw) -> torch.Tensor:
+        """Host stream -> device copy through a reused pinned staging buffer
+        (one host memcpy + an async DMA on the current stream)."""
+        nb = len(raw)
+        if self._stage is None or self._stage.numel() < nb:
+            cap = max(nb, self.out.numel())
+            self._stage = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            self._dstream = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        if self._h2d_done is not None:
+            self._h2d_done.synchronize()            # the previous DMA has left the staging buffer
+        self._stage.numpy()[:nb] = np.frombuffer(raw, dtype=np.uint8)
+        self._dstream[:nb].copy_(self._stage[:nb], non_blocking=True)
+        self._h2d_done = torch.cuda.Event()
+        self._h2d_done.record(torch.cuda.current_stream(self.device))
+        return self._dstream
 
     def decompress(self, buf, out: torch.Tensor) -> torch.Tensor:
         raw = buf if isinstance(buf, (bytes, bytearray, memoryview)) else buf.cpu().numpy().tobytes()
         n, esz, nseg, offs = runtime().zvc_info(raw)
         if n != out.numel() or esz != out.element_size():
             raise ValueError(f"ZVC stream holds {n} x {esz} B, destination {out.numel()} x {out.element_size()} B")
-        dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device) if not isinstance(buf, torch.Tensor) \
-            else buf
+        dev = self._to_device(raw) if not isinstance(buf, torch.Tensor) else buf
         d_offs = torch.from_numpy(offs.astype(np.uint32).view(np.int32)).to(self.device)
         self.K.zvc_gpu_decompress(dev.data_ptr(), d_offs.data_ptr(), int(nseg), int(n), int(esz), out.data_ptr(),
                                   int(torch.cuda.current_stream(self.device).cuda_stream))

@@ -416,7 +416,7 @@ class DEFER:
         pred = m.tensors[0]
         if m.bf16 and m.bf16[0]:
             pred = (pred.astype(np.uint32) << 16).view(np.float32)
-        pred = pred[: m.count]
+        pred = np.array(pred[: m.count])             # own, writable copy for the caller
         self._completed += 1
         self.completion_times.append(time.time())
         if self.ordered:

@@ -80,7 +80,8 @@ class StageRuntime:
         # while the next micro-batch computes (two buffer sets ping-pong)
         self.gpu_codec = self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")
         self.compute = StageCompute(g, weights, int(cfg["batch"]), node.device,
-                                    graph_capture=cfg.get("graph", True), num_sets=2 if self.gpu_codec else 1)
+                                    graph_capture=cfg.get("graph", True), num_sets=2 if self.gpu_codec else 1,
+                                    host_ring=int(cfg.get("queue", 4)) + 4)
         if self.gpu_codec:
             self._init_gpu_codec()
         self.inq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
@@ -127,7 +128,8 @@ class StageRuntime:
     def _recv_loop(self) -> None:
         try:
             while not self.stop.is_set():
-                m = recv_message(self.upstream, self.node.state.chunk_size)
+                m = recv_message(self.upstream, self.node.state.chunk_size,
+                                 keep_encoded=("zvc", "lz4") if self.gpu_codec else ())
                 if m is None:
                     break
                 if m.epoch != self.epoch:
@@ -158,6 +160,37 @@ class StageRuntime:
             self.codecs.append(per)
         self._set_free = [None, None]     # codec-done events guarding each output set
         self._tick = 0
+        self.decoders: Dict[Tuple[str, str], object] = {}   # (input, codec) -> device decoder
+
+    def _gpu_decode(self, name: str, buf, dst) -> bool:
+        """Decode an encoded input container straight into its device buffer;
+        False when the container does not match the buffer (host fallback)."""
+        from . import codec as C
+        from .codec.gpu_lz4 import GpuLZ4
+        from .codec.gpu_zvc import GpuZVC
+        cname, _dt, shape, payload = C.payload_of(buf)
+        n = 1
+        for v in shape:
+            n *= int(v)
+        if n != dst.numel():
+            return False
+        key = (name, cname)
+        dec = self.decoders.get(key)
+        if dec is None:
+            if cname == "zvc":
+                dec = GpuZVC(dst.numel(), dst.element_size(), self.compute.device)
+            else:
+                dec = GpuLZ4(dst.numel() * dst.element_size(), self.compute.device)
+            self.decoders[key] = dec
+        if cname == "zvc" and dst.element_size() != int(self._zvc_esz(payload)):
+            return False
+        dec.decompress(payload, dst)
+        return True
+
+    @staticmethod
+    def _zvc_esz(payload) -> int:
+        from .native import runtime
+        return runtime().zvc_info(payload)[1]
 
     def _compute_gpu(self, m: Message) -> Message:
         import torch
@@ -169,6 +202,11 @@ class StageRuntime:
             ev.synchronize()                  # the encoders reading set j are done
         for name, a, b in zip(self.compute.inputs, m.tensors, m.bf16):
             dst = ex.input_buf(name, j)
+            if isinstance(a, (bytes, bytearray, memoryview)):
+                if self._gpu_decode(name, a, dst):
+                    continue
+                from . import codec as C
+                a = C.decode(a, copy=False)
             t = to_torch(a, b, dst.device)
             if t.dtype != dst.dtype:
                 t = t.to(dst.dtype)
@@ -199,12 +237,14 @@ class StageRuntime:
         bufs = []
         for (_, j, k), shp, dt in zip(m.tensors, shapes, dtypes):
             c = self.codecs[j][k]
-            payload = c.stream_bytes() if hasattr(c, "stream_bytes") else c.frame_bytes()
-            name = "zvc" if hasattr(c, "stream_bytes") else "lz4"
+            # a view of the codec's pinned host buffer: valid until its next
+            # use, which comes after this message has been sent (same thread)
+            payload = c.stream_view() if hasattr(c, "stream_view") else c.frame_view()
+            name = "zvc" if hasattr(c, "stream_view") else "lz4"
             np_dt = np.uint16 if dt == torch.bfloat16 else np.float32
             # the receiver only needs the first `count` images: a partial batch is
             # still sent whole (padding rows are zeros, cheap under either codec)
-            bufs.append(C.wrap(payload, name, np_dt, shp, bf16=(dt == torch.bfloat16)))
+            bufs.append((C.wrap(b"", name, np_dt, shp, bf16=(dt == torch.bfloat16)), payload))
         return Message(m.partition, m.req_id, m.epoch, m.count, bufs, m.bf16)
 
     def _compute_loop(self) -> None:

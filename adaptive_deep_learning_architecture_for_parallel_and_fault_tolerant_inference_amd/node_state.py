@@ -36,6 +36,13 @@ def socket_send(bytes_to_send, sock: socket.socket, chunk_size: int, timeout_ms:
     runtime().send_frame(sock.fileno(), memoryview(bytes_to_send).cast("B"), int(chunk_size), timeout_ms)
 
 
+def socket_send_parts(parts, sock: socket.socket, chunk_size: int, timeout_ms: int = -1) -> None:
+    """Send one frame whose body is the concatenation of `parts` (buffers), without
+    joining them in memory first."""
+    runtime().send_frame_parts(sock.fileno(), [memoryview(p).cast("B") for p in parts], int(chunk_size),
+                               timeout_ms)
+
+
 def socket_recv(sock: socket.socket, chunk_size: int, timeout_ms: int = -1) -> bytes:
     """Receive one frame; returns b'' on a clean close before any header byte."""
     data = runtime().recv_frame(sock.fileno(), int(chunk_size), timeout_ms, 0)

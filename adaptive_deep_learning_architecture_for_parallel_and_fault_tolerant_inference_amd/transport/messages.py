@@ -24,7 +24,7 @@ from typing import List, Optional
 import numpy as np
 
 from .. import codec as C
-from ..node_state import socket_recv, socket_send
+from ..node_state import socket_recv, socket_send, socket_send_parts
 
 MAGIC = b"ADPT"
 HDR = struct.Struct(">4sIQIII")
@@ -46,12 +46,22 @@ def send_message(sock: socket.socket, m: Message, codec: str = "lz4", chunk_size
                 timeout_ms)
     flags = m.bf16 or [False] * len(m.tensors)
     for t, b in zip(m.tensors, flags):
-        # bytes = a container already encoded elsewhere (GPU side-stream codec)
-        buf = t if isinstance(t, (bytes, bytearray)) else C.encode(t, codec, bf16=b)
-        socket_send(buf, sock, chunk_size, timeout_ms)
+        if isinstance(t, tuple):
+            # (container header, payload view) from the GPU side-stream codec
+            socket_send_parts(list(t), sock, chunk_size, timeout_ms)
+        elif isinstance(t, (bytes, bytearray)):
+            # a container already encoded elsewhere (GPU side-stream codec)
+            socket_send(t, sock, chunk_size, timeout_ms)
+        else:
+            # header + payload as one frame; a raw payload goes out straight from
+            # the array's memory (no tobytes / concatenation copies)
+            socket_send_parts(C.encode_parts(t, codec, bf16=b), sock, chunk_size, timeout_ms)
 
 
-def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int = -1) -> Optional[Message]:
+def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int = -1,
+                 keep_encoded: tuple = ()) -> Optional[Message]:
+    """Receive one message.  Tensors whose codec is in `keep_encoded` stay as the
+    received container bytes (a GPU stage decodes them on the device)."""
     h = socket_recv(sock, chunk_size, timeout_ms)
     if not h:
         return None
@@ -64,7 +74,10 @@ def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int 
         if not buf:
             raise ConnectionError("closed inside a message")
         bf.append(C.is_bf16(buf))
-        ts.append(C.decode(buf))
+        if keep_encoded and C.codec_of(buf) in keep_encoded:
+            ts.append(buf)
+        else:
+            ts.append(C.decode(buf, copy=False))      # read-only view of the received frame
     return Message(part, rid, epoch, count, ts, bf)
 
 

@@ -49,6 +49,19 @@ PYBIND11_MODULE(_runtime, m) {
     NoGil nogil;
     send_frame(fd, v.first, v.second, chunk, timeout_ms);
   }, py::arg("fd"), py::arg("data"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
+  m.def("send_frame_parts", [](int fd, py::list parts, size_t chunk, int timeout_ms) {
+    std::vector<py::buffer_info> infos;
+    std::vector<std::pair<const uint8_t*, size_t>> v;
+    infos.reserve(parts.size());
+    for (auto h : parts) {
+      py::buffer b = py::reinterpret_borrow<py::buffer>(h);
+      infos.emplace_back();
+      auto pv = view(b, infos.back());
+      v.emplace_back(pv.first, pv.second);
+    }
+    NoGil nogil;
+    send_frame_parts(fd, v, chunk, timeout_ms);
+  }, py::arg("fd"), py::arg("parts"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
   m.def("send_all", [](int fd, py::buffer data, size_t chunk, int timeout_ms) {
     py::buffer_info info;
     auto v = view(data, info);
@@ -56,14 +69,28 @@ PYBIND11_MODULE(_runtime, m) {
     send_all(fd, v.first, v.second, chunk, timeout_ms);
   }, py::arg("fd"), py::arg("data"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
   m.def("recv_frame", [](int fd, size_t chunk, int timeout_ms, size_t max_len) -> py::object {
-    std::vector<uint8_t> out;
+    // header first, then receive straight into an uninitialised bytes object:
+    // no zero-fill, no staging vector, no second copy (a 57 MB frame used to
+    // pay two fresh-page faults passes, a memset and a memcpy)
+    uint8_t hdr[8];
+    uint64_t n = 0;
     bool ok;
     {
       NoGil nogil;
-      ok = recv_frame(fd, out, chunk, timeout_ms, max_len);
+      ok = recv_exact(fd, hdr, 8, 8, timeout_ms, true);
     }
     if (!ok) return py::none();
-    return to_bytes(out);
+    for (int i = 0; i < 8; ++i) n = (n << 8) | hdr[i];
+    if (max_len && n > max_len) throw std::runtime_error("frame larger than max_len");
+    PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)n);
+    if (!b) throw py::error_already_set();
+    py::object obj = py::reinterpret_steal<py::object>(b);
+    if (n) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(PyBytes_AS_STRING(b));
+      NoGil nogil;
+      recv_exact(fd, dst, (size_t)n, chunk, timeout_ms, false);
+    }
+    return obj;
   }, py::arg("fd"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1, py::arg("max_len") = 0);
   m.def("recv_exact", [](int fd, size_t n, int timeout_ms) -> py::object {
     std::vector<uint8_t> out(n);
@@ -81,13 +108,17 @@ PYBIND11_MODULE(_runtime, m) {
     size_t cap = (size_t)(info.size * info.itemsize);
     uint8_t hdr[8];
     uint64_t n = 0;
+    bool ok;
     {
       NoGil nogil;
-      if (!recv_exact(fd, hdr, 8, 8, timeout_ms, true)) return py::none();
-      for (int i = 0; i < 8; ++i) n = (n << 8) | hdr[i];
-      if (n > cap) throw std::runtime_error("frame larger than destination buffer");
-      if (n) recv_exact(fd, static_cast<uint8_t*>(info.ptr), (size_t)n, chunk, timeout_ms, false);
+      ok = recv_exact(fd, hdr, 8, 8, timeout_ms, true);
+      if (ok) {
+        for (int i = 0; i < 8; ++i) n = (n << 8) | hdr[i];
+        if (n > cap) throw std::runtime_error("frame larger than destination buffer");
+        if (n) recv_exact(fd, static_cast<uint8_t*>(info.ptr), (size_t)n, chunk, timeout_ms, false);
+      }
     }
+    if (!ok) return py::none();
     return py::int_(n);
   }, py::arg("fd"), py::arg("dst"), py::arg("chunk") = 512000, py::arg("timeout_ms") = -1);
 

@@ -66,6 +66,19 @@ void send_frame(int fd, const uint8_t* p, size_t n, size_t chunk, int timeout_ms
   send_all(fd, p, n, chunk, timeout_ms);
 }
 
+void send_frame_parts(int fd, const std::vector<std::pair<const uint8_t*, size_t>>& parts, size_t chunk,
+                      int timeout_ms) {
+  uint64_t v = 0;
+  for (auto& pr : parts) v += pr.second;
+  uint8_t hdr[8];
+  for (int i = 7; i >= 0; --i) {
+    hdr[i] = (uint8_t)(v & 0xFF);
+    v >>= 8;
+  }
+  send_all(fd, hdr, 8, 8, timeout_ms);
+  for (auto& pr : parts) send_all(fd, pr.first, pr.second, chunk, timeout_ms);
+}
+
 bool recv_exact(int fd, uint8_t* p, size_t n, size_t chunk, int timeout_ms, bool eof_ok_at_start) {
   if (chunk == 0) chunk = n ? n : 1;
   size_t off = 0;

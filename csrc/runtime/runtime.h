@@ -49,6 +49,9 @@ void zfp_decompress(const uint8_t* data, size_t n, void* dst, int threads);
 // recv_frame returns false on a clean EOF before any header byte.
 void send_all(int fd, const uint8_t* p, size_t n, size_t chunk, int timeout_ms);
 void send_frame(int fd, const uint8_t* p, size_t n, size_t chunk, int timeout_ms);
+// one frame whose body is the concatenation of `parts` (no staging copy)
+void send_frame_parts(int fd, const std::vector<std::pair<const uint8_t*, size_t>>& parts, size_t chunk,
+                      int timeout_ms);
 bool recv_exact(int fd, uint8_t* p, size_t n, size_t chunk, int timeout_ms, bool eof_ok_at_start);
 bool recv_frame(int fd, std::vector<uint8_t>& out, size_t chunk, int timeout_ms, size_t max_len);
 
