@@ -107,11 +107,18 @@ def cmd_serve(argv):
 
     threading.Thread(target=feed, daemon=True).start()
     try:
+        t_first = None
         for i in range(a.requests):
             outq.get(timeout=600)
-        run = time.time() - start
-        print(f"{a.requests} results in {run:.3f} seconds")
+            if t_first is None:
+                t_first = time.time()
+        end = time.time()
+        run = end - start
+        print(f"{a.requests} results in {run:.3f} seconds (incl. partition + slice push)")
         print(f"Throughput: {a.requests * cfg.batch / run:.2f} img/s ({a.requests / run:.2f} req/s)")
+        if a.requests > 1 and end > t_first:
+            steady = (a.requests - 1) / (end - t_first)
+            print(f"Steady-state: {steady * cfg.batch:.2f} img/s ({steady:.2f} req/s) after the first result")
         for ts, ev in d.events:
             print(f"  [{ts - start:8.3f}s] {ev}")
     finally:
@@ -175,7 +182,21 @@ def main(argv=None):
     if not argv or argv[0] not in COMMANDS:
         print(__doc__)
         sys.exit(0 if not argv else 2)
-    COMMANDS[argv[0]](argv[1:])
+    code = 0
+    try:
+        COMMANDS[argv[0]](argv[1:])
+    except SystemExit as e:
+        code = e.code if isinstance(e.code, int) else (0 if e.code is None else 1)
+    except BaseException:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        code = 1
+    # Leave without interpreter finalization: daemon I/O threads may still sit in
+    # native recv() calls with the GIL released, and CPython 3.10 retires such
+    # threads with a forced unwind that aborts the process (node.py does the same).
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
 
 
 if __name__ == "__main__":

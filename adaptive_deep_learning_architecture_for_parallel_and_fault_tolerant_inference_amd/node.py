@@ -158,7 +158,11 @@ class StageRuntime:
                 else:
                     per.append(GpuLZ4(t.numel() * t.element_size(), self.compute.device))
             self.codecs.append(per)
-        self._set_free = [None, None]     # codec-done events guarding each output set
+        # set j (its output buffers and its codecs' device streams) is reusable only
+        # after the send thread has copied set j's compressed bytes to the host
+        self._set_free = [threading.Event(), threading.Event()]
+        for e in self._set_free:
+            e.set()
         self._tick = 0
         self.decoders: Dict[Tuple[str, str], object] = {}   # (input, codec) -> device decoder
 
@@ -198,8 +202,10 @@ class StageRuntime:
         j = self._tick % 2
         self._tick += 1
         ex = self.compute.ex
-        for ev in self._set_free[j] or []:
-            ev.synchronize()                  # the encoders reading set j are done
+        while not self._set_free[j].wait(0.1):    # set j's previous message has left the GPU
+            if self.stop.is_set():
+                raise RuntimeError("stage stopped")
+        self._set_free[j].clear()
         for name, a, b in zip(self.compute.inputs, m.tensors, m.bf16):
             dst = ex.input_buf(name, j)
             if isinstance(a, (bytes, bytearray, memoryview)):
@@ -221,9 +227,6 @@ class StageRuntime:
         dones = []
         for o, codec in zip(self.compute.outputs, self.codecs[j]):
             dones.append(codec.compress(outs[o], after=ev))
-        self._set_free[j] = [torch.cuda.Event() for _ in dones]
-        for e, c in zip(self._set_free[j], self.codecs[j]):
-            e.record(c.stream)
         shapes = [tuple(outs[o].shape) for o in self.compute.outputs]
         dtypes = [outs[o].dtype for o in self.compute.outputs]
         return Message(self.stage + 2, m.req_id, m.epoch, m.count, [("gpu", j, k) for k in range(len(shapes))],
@@ -245,6 +248,7 @@ class StageRuntime:
             # the receiver only needs the first `count` images: a partial batch is
             # still sent whole (padding rows are zeros, cheap under either codec)
             bufs.append((C.wrap(b"", name, np_dt, shp, bf16=(dt == torch.bfloat16)), payload))
+        self._set_free[m.tensors[0][1]].set()     # all of set j's bytes are on the host now
         return Message(m.partition, m.req_id, m.epoch, m.count, bufs, m.bf16)
 
     def _compute_loop(self) -> None:

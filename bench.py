@@ -51,6 +51,7 @@ def parse():
 
 
 BASELINE_IMG_S = None   # the reference publishes no absolute number
+MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152"}
 
 
 def main():
@@ -110,7 +111,7 @@ def main():
     value = images / elapsed
     if rank == 0:
         rec = {
-            "metric": "images/sec (whole node) ResNet-50 bs=32",
+            "metric": (f"images/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} bs={args.batch}"),
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,

@@ -140,3 +140,5 @@ def main():
 
 if __name__ == "__main__":
     main()
+    sys.stdout.flush()
+    os._exit(0)        # daemon I/O threads may sit in native recv(); skip finalization

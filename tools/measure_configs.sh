@@ -15,11 +15,12 @@ run() {   # secs name cmd...
   echo "=== [$name] rc=$rc"; tail -4 "$out/$name.log"
   [ $rc -eq 0 ] || exit $rc
 }
-run 300 local_cpu_bs1 $M local-infer --model resnet50 --batch 1 --requests 10 --device cpu
-run 300 local_gpu_bs1 $M local-infer --model resnet50 --batch 1 --requests 200 --device cuda
-run 300 local_gpu_bs32 $M local-infer --model resnet50 --batch 32 --requests 200 --device cuda
-run 300 bench_r152 python bench.py --model resnet152 --steps 50 --warmup 10
+[ -n "$SKIP_LOCAL" ] || run 300 local_cpu_bs1 $M local-infer --model resnet50 --batch 1 --requests 10 --device cpu
+[ -n "$SKIP_LOCAL" ] || run 300 local_gpu_bs1 $M local-infer --model resnet50 --batch 1 --requests 200 --device cuda
+[ -n "$SKIP_LOCAL" ] || run 300 local_gpu_bs32 $M local-infer --model resnet50 --batch 32 --requests 200 --device cuda
+[ -n "$SKIP_LOCAL" ] || run 300 bench_r152 python bench.py --model resnet152 --steps 50 --warmup 10
 run 400 serve_2stage_tcp $M serve --model resnet50 --batch 32 --part-at conv3_block1_1_conv --spawn 2 --device cuda:0 --codec none --requests 300
+run 300 serve_2stage_bs1 $M serve --model resnet50 --batch 1 --part-at conv3_block1_1_conv --spawn 2 --device cuda:0 --codec none --requests 500
 run 400 serve_2stage_zvc $M serve --model resnet50 --batch 32 --part-at conv3_block1_1_conv --spawn 2 --device cuda:0 --codec zvc --requests 300
 run 500 serve_4stage_r152 $M serve --model resnet152 --batch 32 --part-at auto:4 --spawn 4 --device cuda:0 --codec none --requests 200
 run 500 fault_r50_4w python tools/fault_bench.py --workers 4 --device cuda:0 --model resnet50 --image 224 --batch 32 --duration 25 --kill-at 10 --codec zvc --inflight 8 --json "$out/fault_r50_4w.json"
