@@ -17,6 +17,7 @@
 //   DMA never needs a mask.
 // * Fused epilogue identical to v1 (LDS fp32 tile -> 16-byte row segments).
 #include "kernels.h"
+#include "epilogue.h"
 
 namespace adapt {
 
@@ -272,8 +273,12 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     }
     return;
   }
+  if (sk.slot < 0) {
+    fused_epilogue<BM, BN, NT, EPI_LD, OUT_F32>(p, epi, m0, n0, tid);
+    return;
+  }
   const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);
-  if (sk.slot >= 0) {
+  {
     // Stream-K partial tile: publish it with 16-B sc1 stores, then one lane
     // counts the arrival; the last of the tile's segments combines all partials
     // in segment order (deterministic) and runs the epilogue.  Nobody waits
@@ -306,11 +311,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     if (m >= p.M || n >= p.N) continue;
     const float* e = epi + row * EPI_LD + cc * 8;
     float v[8];
-    if (sk.slot < 0) {
-      f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
-      v[0] = v0[0]; v[1] = v0[1]; v[2] = v0[2]; v[3] = v0[3];
-      v[4] = v1[0]; v[5] = v1[1]; v[6] = v1[2]; v[7] = v1[3];
-    } else {
+    {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = 0.f;
       for (int sg = 0; sg < sk.nseg; ++sg) {

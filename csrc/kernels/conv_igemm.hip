@@ -18,6 +18,7 @@
 // Split-K (ksplit > 1): each K-slice writes an fp32 partial slab
 // ws[slice][M][N]; conv_splitk_reduce applies the epilogue.
 #include "kernels.h"
+#include "epilogue.h"
 
 namespace adapt {
 
@@ -196,39 +197,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvParams p) {
     }
     return;
   }
-  for (int c = tid; c < NCH; c += NTHREADS) {
-    const int row = c / CPR, cc = c % CPR;
-    const int m = m0 + row, n = n0 + cc * 8;
-    if (m >= p.M || n >= p.N) continue;
-    const float* e = epi + row * EPI_LD + cc * 8;
-    f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    if (p.bias) {
-      f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
-      v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
-      v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
-    }
-    if (p.res) {
-      V8 r;
-      r.u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] += bf2f(r.e[t]);
-    }
-    if (p.relu) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
-    }
-    if (OUT_F32) {
-      float* o = (float*)p.out + (size_t)m * p.ldo + n;
-      *(f32x4*)o = (f32x4){v[0], v[1], v[2], v[3]};
-      *(f32x4*)(o + 4) = (f32x4){v[4], v[5], v[6], v[7]};
-    } else {
-      V8 o;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-      *(u32x4*)((bf16*)p.out + (size_t)m * p.ldo + n) = o.u;
-    }
-  }
+  fused_epilogue<BM, BN, NTHREADS, EPI_LD, OUT_F32>(p, epi, m0, n0, tid);
 }
 
 // split-K reduction + epilogue: out = act(sum_s ws[s] + bias (+res))
