@@ -26,15 +26,36 @@ CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64
              6: (128, 128), 7: (128, 128), 8: (128, 64), 9: (64, 128), 10: (64, 64), 11: (256, 64), 12: (64, 256),
              13: (128, 128), 14: (128, 128), 15: (64, 128), 16: (64, 64), 17: (128, 64), 18: (64, 128),
              19: (256, 64), 20: (128, 128), 21: (64, 64), 22: (128, 128), 23: (64, 128), 24: (64, 64),
-             25: (128, 64), 26: (256, 64), 27: (64, 256), 28: (128, 256), 29: (256, 128)}
+             25: (128, 64), 26: (256, 64), 27: (64, 256), 28: (128, 256), 29: (256, 128),
+             # v3: 3x3 halo-patch kernel (conv_halo.hip); BM = pixels of TH whole output rows
+             40: (224, 64), 41: (112, 128), 42: (224, 64), 43: (64, 128), 44: (112, 64), 45: (224, 64),
+             46: (224, 64), 47: (112, 128), 48: (224, 64), 49: (64, 128), 50: (224, 64), 51: (224, 64),
+             52: (112, 64)}
 V1_CFGS = (0, 1, 2, 3, 4, 5)
+# halo configs: patch capacity in pixels (must match ADAPT_HALO_CFGS)
+HALO_PATCH = {40: 352, 41: 192, 42: 288, 43: 96, 44: 144, 45: 384, 46: 352, 47: 192, 48: 384, 49: 96, 50: 320,
+              51: 288, 52: 144}
+
+
+def halo_rows(cfg: int, pc: "PackedConv", H: int, W: int) -> int:
+    """Output rows per tile for a halo config, 0 if the conv/shape does not fit it."""
+    if (pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) != (3, 3, 1, 1, 1, 1, 1) or pc.cin % 64:
+        return 0
+    bm = CFG_TILES[cfg][0]
+    th = min(H, bm // W if W else 0)
+    while th >= 1 and (th + 2) * (W + 2) > HALO_PATCH[cfg]:
+        th -= 1
+    return max(th, 0)
 _CFG_EFF = {0: 1.0, 4: 0.97, 1: 0.86, 2: 0.86, 3: 0.66, 5: 0.42}
 
 
 def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
-    """v2 configs walk K tap-major in 64-channel slices: they need Cin % 64 == 0."""
+    """v2 configs walk K tap-major in 64-channel slices: they need Cin % 64 == 0;
+    v3 (halo) configs take 3x3/s1/p1 convs only (the row count is checked at launch)."""
     if cfg in V1_CFGS:
         return True
+    if cfg in HALO_PATCH:
+        return (pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l) == (3, 3, 1, 1, 1) and pc.cin % 64 == 0
     return pc.cin % 64 == 0
 NUM_CUS = 256
 
@@ -176,9 +197,14 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         raise ValueError("packed weights not padded to the tile's N")
     pure = pc.kh == 1 and pc.kw == 1 and pc.stride == 1 and pc.pad_t == 0 and pc.pad_l == 0 and OH == H and OW == W
     if not cfg_supported(cfg, pc, pure):
-        raise ValueError(f"tile config {cfg} needs a power-of-two input channel count (got {pc.cin})")
-    if ksplit == 0 or (ksplit < 0 and cfg in V1_CFGS):
+        raise ValueError(f"tile config {cfg} does not support this conv (Cin {pc.cin}, {pc.kh}x{pc.kw}/s{pc.stride})")
+    if ksplit == 0 or (ksplit < 0 and cfg in V1_CFGS) or (ksplit != 1 and cfg in HALO_PATCH):
         raise ValueError(f"ksplit {ksplit} not supported by tile config {cfg}")
+    th = 0
+    if cfg in HALO_PATCH:
+        th = halo_rows(cfg, pc, H, W)
+        if th < 1:
+            raise ValueError(f"halo config {cfg} cannot tile a {H}x{W} 3x3 conv")
     ws_ptr = ctr_ptr = 0
     sk_iters = 0
     need = workspace_elems(M, N, pc.Kpad, cfg, ksplit)
@@ -195,7 +221,7 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         if counters.numel() < tiles or counters.dtype != torch.int32:
             raise ValueError(f"stream-K needs {tiles} int32 tile counters")
         ctr_ptr = ptr(counters)
-    kernels().conv_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, ctr_ptr, sk_iters,
+    kernels().conv_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, ctr_ptr, sk_iters, th,
                            B, H, W, C, OH, OW, N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l,
                            pc.K, pc.Kpad, N, int(relu), int(ksplit), int(cfg), bool(out_f32),
                            stream_handle(stream))

@@ -20,6 +20,7 @@ allocator and the stream / graph API only.
 from __future__ import annotations
 
 import json
+import os
 import threading
 from collections import ChainMap
 from pathlib import Path
@@ -324,7 +325,13 @@ class SliceExecutor:
     # -------------------------------------------------------------- run
     def _launch(self, set_idx: int = 0, stream=None) -> None:
         b = self.bufs(set_idx)
+        # ADAPT_DEBUG_SYNC=1: synchronize after every step so a faulting or
+        # failing kernel is reported with its step (the AMD_SERIALIZE_KERNEL
+        # idea at plan level; never active under hipGraph capture)
+        debug = os.environ.get("ADAPT_DEBUG_SYNC", "0") == "1" and not torch.cuda.is_current_stream_capturing()
         for i, st in enumerate(self.steps):
+            if debug and i:
+                self._debug_check(i - 1)
             k = st.kind
             if k == "pack":
                 E.input_pack(b[st.ins[0]], b[st.out], stream=stream)
@@ -363,6 +370,8 @@ class SliceExecutor:
                 E.softmax_rows(b[st.ins[0]], b[st.out], stream=stream)
             else:
                 raise NotImplementedError(k)
+        if debug and self.steps:
+            self._debug_check(len(self.steps) - 1)
         # relay frontier tensors: device copy into the output set (no aliasing with the
         # input buffer that the next micro-batch's receive will overwrite)
         for r in self.relay:
@@ -372,6 +381,13 @@ class SliceExecutor:
                     s[r + "#out"].copy_(s[r], non_blocking=True)
             else:
                 s[r + "#out"].copy_(s[r], non_blocking=True)
+
+    def _debug_check(self, i: int) -> None:
+        try:
+            torch.cuda.synchronize(self.device)
+        except RuntimeError as e:
+            st = self.steps[i]
+            raise RuntimeError(f"step {i} ({st.kind} -> {st.out}, cfg {self.cfg.get(i)}) failed: {e}") from e
 
     def capture(self) -> None:
         """Record the step list of every buffer set into its own hipGraph."""

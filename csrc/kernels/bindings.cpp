@@ -26,6 +26,11 @@ static hipStream_t S(u64 v) { return reinterpret_cast<hipStream_t>(v); }
 PYBIND11_MODULE(_C, m) {
   m.doc() = "ADAPT MI355X (gfx950) HIP kernels";
   m.def("conv_num_cfgs", &adapt::conv_num_cfgs);
+  m.def("conv_halo_cfg", [](int cfg) -> py::object {
+    int bm, bn, pp;
+    if (!adapt::conv_halo_cfg(cfg, &bm, &bn, &pp)) return py::none();
+    return py::make_tuple(bm, bn, pp);
+  });
   m.def("conv_sk_plan", [](int tiles, int kt, int mult) {
     int g, it;
     adapt::conv_sk_plan(tiles, kt, mult, &g, &it);
@@ -38,7 +43,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def(
       "conv_forward",
-      [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, u64 counters, int sk_iters, int B, int H, int W,
+      [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, u64 counters, int sk_iters, int th, int B, int H, int W,
          int Cin, int OH, int OW, int N, int KH, int KW, int stride, int pad_t, int pad_l, int K, int Kpad, int ldo,
          int relu, int ksplit, int cfg, bool out_f32, u64 stream) {
         adapt::ConvParams p;
@@ -50,6 +55,7 @@ PYBIND11_MODULE(_C, m) {
         p.ws = P<float>(ws);
         p.counters = P<int>(counters);
         p.sk_iters = sk_iters;
+        p.th = th;
         p.B = B; p.H = H; p.W = W; p.Cin = Cin;
         p.OH = OH; p.OW = OW; p.N = N;
         p.KH = KH; p.KW = KW; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;

@@ -274,7 +274,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     return;
   }
   if (sk.slot < 0) {
-    fused_epilogue<BM, BN, NT, EPI_LD, OUT_F32>(p, epi, m0, n0, tid);
+    fused_epilogue<BM, BN, NT, EPI_LD, OUT_F32>(p, epi, m0, n0, tid, p.M);
     return;
   }
   const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvParams p) {
     }
     return;
   }
-  fused_epilogue<BM, BN, NTHREADS, EPI_LD, OUT_F32>(p, epi, m0, n0, tid);
+  fused_epilogue<BM, BN, NTHREADS, EPI_LD, OUT_F32>(p, epi, m0, n0, tid, p.M);
 }
 
 // split-K reduction + epilogue: out = act(sum_s ws[s] + bias (+res))
@@ -288,6 +288,7 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
     ADAPT_CONV_CFGS(X)
 #undef X
     default:
+      if (cfg >= 40) return conv_halo_launch(p, cfg, s, out_f32);   // v3: 3x3 halo-patch kernel
       // v2 (LDS-DMA ring) configs walk K tap-major in 64-channel slices
       if (p.Cin % 64) return hipErrorInvalidValue;
       e = conv_glds_launch(p, cfg, s, pure, out_f32);

@@ -1,7 +1,7 @@
 // Fused conv epilogue shared by the implicit-GEMM kernels:
 //   out[m][n] = act(tile[m][n] + bias[n] (+ res[m][n]))   (bf16 or fp32 out)
 // over a BM x BN fp32 tile staged in LDS (row stride EPI_LD), written as 16-byte
-// row segments.
+// row segments; rows m >= m_end are not written.
 //
 // Latency: one block per CU is the common case, so nothing hides a dependent
 // global load here.  A thread's column chunk is the same for all its
@@ -15,7 +15,8 @@
 namespace adapt {
 
 template <int BM, int BN, int NT, int EPI_LD, bool OUT_F32>
-__device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float* epi, int m0, int n0, int tid) {
+__device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float* epi, int m0, int n0, int tid,
+                                               int m_end) {
   constexpr int CPR = BN / 8;                 // 8-wide chunks per row
   constexpr int NCH = BM * CPR;
   constexpr int RPI = NT / CPR;               // rows covered per iteration
@@ -41,13 +42,13 @@ __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float*
       const int row = row0 + (g + u) * RPI;
       const int m = m0 + row;
       r[u].u = (u32x4){0u, 0u, 0u, 0u};
-      if (p.res && g + u < IT && row < BM && m < p.M) r[u].u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
+      if (p.res && g + u < IT && row < BM && m < m_end) r[u].u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
     }
 #pragma unroll
     for (int u = 0; u < EPI_G; ++u) {
       const int row = row0 + (g + u) * RPI;
       const int m = m0 + row;
-      if (g + u >= IT || row >= BM || m >= p.M) continue;
+      if (g + u >= IT || row >= BM || m >= m_end) continue;
       const float* e = epi + row * EPI_LD + cc * 8;
       const f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
       float v[8] = {v0[0] + b[0], v0[1] + b[1], v0[2] + b[2], v0[3] + b[3],

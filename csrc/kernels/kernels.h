@@ -18,7 +18,10 @@ struct ConvParams {
   int ksplit;       // >= 1: split-K slices (fp32 slabs in ws + reduce); < 0: stream-K over -ksplit x 256 blocks
   int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
   int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_sk_plan)
+  int th;           // halo 3x3 kernel: output rows per tile
 };
+hipError_t conv_halo_launch(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
+bool conv_halo_cfg(int cfg, int* bm, int* bn, int* patch_pix);
 void conv_sk_plan(int tiles, int kt, int mult, int* grid, int* iters);
 hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
 int zvc_seg();

@@ -111,3 +111,56 @@ def test_fault_injection_sigkill_repartition_replay(tiny, transport):
             except ProcessLookupError:
                 pass
             p.wait(timeout=10)
+
+
+@pytest.mark.slow
+def test_elastic_join_scales_up(tiny):
+    """SURVEY §5.3 "a join triggers the same flow (scale-up)": with elastic=True a
+    worker registering mid-stream bumps the epoch, the cuts are re-planned over
+    the larger set and every request is still answered exactly once."""
+    d = DEFER(membership_port=0, result_port=0, worker_wait=60, max_inflight=4, task_timeout=20, min_workers=2,
+              weight_codec="lz4", elastic=True)
+    d.membership_server.start()
+    procs = [_spawn_worker(d.membership_port, f"j{i}") for i in range(2)]
+    try:
+        inq, outq, _ = _start(d, tiny, ["conv3_block1_out"])
+        rng = np.random.default_rng(2)
+        x = rng.standard_normal((1, 32, 32, 3)).astype(np.float32)
+        want = tiny.predict(x, device="cpu")
+        n_req = 30
+        results = []
+
+        def feeder():
+            for _ in range(n_req):
+                inq.put(x)
+                time.sleep(0.02)
+
+        threading.Thread(target=feeder, daemon=True).start()
+        for _ in range(6):
+            results.append(outq.get(timeout=120))
+        assert len(d.pipeline.workers) == 2
+        epoch0 = d.pipeline.epoch
+        procs.append(_spawn_worker(d.membership_port, "j2"))        # scale up mid-stream
+        while len(results) < n_req:
+            results.append(outq.get(timeout=120))
+        def nworkers():
+            p = d.pipeline                                           # None while an epoch is being formed
+            return len(p.workers) if p is not None else 0
+        deadline = time.time() + 60
+        while nworkers() < 3 and time.time() < deadline:
+            time.sleep(0.1)
+        time.sleep(0.5)
+        assert outq.empty()                                          # exactly-once
+        for y in results:
+            np.testing.assert_allclose(y, want, rtol=1e-4, atol=1e-5)
+        p = d.pipeline
+        assert p is not None and len(p.workers) == 3 and p.epoch > epoch0
+        assert len(p.part_at) == 2
+    finally:
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait(timeout=10)

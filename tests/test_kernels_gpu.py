@@ -44,6 +44,8 @@ CONV_CASES = [
     (2, 56, 56, 256, 128, 1, 2, 0),
     (2, 28, 28, 128, 128, 3, 1, 1),
     (4, 7, 7, 512, 512, 3, 1, 1),
+    (2, 14, 14, 256, 256, 3, 1, 1),
+    (3, 13, 11, 128, 64, 3, 1, 1),     # odd spatial sizes for the halo tiles
     (2, 14, 14, 1024, 2048, 1, 2, 0),
     (2, 224, 224, 8, 64, 7, 2, 3),     # stem (input padded to 8 channels)
     (3, 9, 11, 24, 40, 3, 2, 1),       # odd sizes, M/N tails
@@ -69,11 +71,12 @@ def test_conv_vs_torch(ops, case, cfg):
     out = torch.empty(B, OH, OW, Cout, device=dev, dtype=torch.bfloat16)
     ks = 1
     ws = None
-    if cfg is not None and pc.Kpad // 64 >= 4:
+    halo = cfg in conv.HALO_PATCH
+    if cfg is not None and pc.Kpad // 64 >= 4 and not halo:
         ks = 2 if cfg % 2 == 0 else 3
         ws = torch.empty(ks * B * OH * OW * Cout, device=dev, dtype=torch.float32)
     pure = k == 1 and s == 1 and p == 0
-    if cfg is not None and not conv.cfg_supported(cfg, pc, pure):
+    if cfg is not None and (not conv.cfg_supported(cfg, pc, pure) or (halo and conv.halo_rows(cfg, pc, H, W) < 1)):
         with pytest.raises(ValueError):
             conv.conv_forward(x, pc, out, residual=res, relu=True, cfg=cfg, ksplit=ks, workspace=ws)
         return
@@ -117,7 +120,7 @@ def test_stem_vs_torch(ops, B, H, W, pool):
     assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
 
 
-V2_CFGS = [c for c in ALL_CFGS if c >= 6]
+V2_CFGS = [c for c in ALL_CFGS if 6 <= c < 40]
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] % 64 == 0])
