@@ -263,10 +263,15 @@ class SliceExecutor:
         if tune:
             self.autotune()
 
-    def autotune(self, reps: int = 20, persist: bool = True) -> Dict[str, List]:
-        """Time every (tile cfg, split-K) candidate per conv problem; keep the fastest."""
+    def autotune(self, reps: int = 20, persist: bool = True, refine: int = 3) -> Dict[str, List]:
+        """Time every (tile cfg, split-K) candidate per conv problem in isolation,
+        then (refine > 1) re-decide each problem among its `refine` best
+        candidates by replaying the WHOLE captured slice: isolated timings miss
+        how a kernel's tail and grid overlap with its neighbours."""
         results: Dict[str, List] = {}
         done: Dict[str, Tuple[int, int]] = {}
+        ranked: Dict[str, List[Tuple[float, int, int]]] = {}
+        prev = dict(load_tuning())              # the table in force: a known-good starting point
         for i, st in enumerate(self.steps):
             if st.kind not in ("conv", "dense"):
                 continue
@@ -311,6 +316,7 @@ class SliceExecutor:
                         del gg
                     except (RuntimeError, ValueError):
                         continue
+                    ranked.setdefault(key, []).append((t, cfg, ks))
                     if best is None or t < best[0]:
                         best = (t, cfg, ks)
             if best:
@@ -318,9 +324,74 @@ class SliceExecutor:
                 done[key] = (best[1], best[2])
                 self.cfg[i] = (best[1], best[2])
         self._ensure_ws()
+        if refine > 1 and ranked:
+            self._refine_in_graph(ranked, results, refine, prev)
         if persist:
             save_tuning(results)
         return results
+
+    def _graph_time(self, rounds: int = 5, reps: int = 10) -> float:
+        """Median ms per replay of the whole slice, freshly captured."""
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._launch(0)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            self._launch(0)
+        g.replay()
+        times = []
+        for _ in range(rounds):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                g.replay()
+            b.record()
+            b.synchronize()
+            times.append(a.elapsed_time(b) / reps)
+        del g
+        return sorted(times)[len(times) // 2]
+
+    def _refine_in_graph(self, ranked, results, top: int, prev: Optional[Dict[str, List]] = None) -> None:
+        steps_of: Dict[str, List[int]] = {}
+        for i, st in enumerate(self.steps):
+            if st.kind in ("conv", "dense"):
+                B, H, W, C, OH, OW, pc = self._conv_geom(i)
+                steps_of.setdefault(conv_key(B, H, W, C, pc), []).append(i)
+        # start from the previous table where it is still a valid candidate, so a
+        # re-tune can only keep or improve the whole-slice time
+        for key, idx in steps_of.items():
+            old = (prev or {}).get(key)
+            if old and any((c, k) == (int(old[0]), int(old[1])) for _, c, k in ranked.get(key, [])):
+                for i in idx:
+                    self.cfg[i] = (int(old[0]), int(old[1]))
+                results[key] = list(old)
+        self._ensure_ws()
+        base = self._graph_time()
+        # most expensive problems first (isolated time x occurrences)
+        order = sorted(ranked, key=lambda k: -min(ranked[k])[0] * len(steps_of.get(k, [])))
+        for key in order:
+            if key not in steps_of:
+                continue
+            cands = sorted(ranked[key])[:top]
+            cur = self.cfg[steps_of[key][0]]
+            for t, cfg, ks in cands:
+                if (cfg, ks) == cur:
+                    continue
+                for i in steps_of[key]:
+                    self.cfg[i] = (cfg, ks)
+                self._ensure_ws()
+                tt = self._graph_time()
+                if tt < base * 0.997:
+                    base, cur = tt, (cfg, ks)
+                    results[key] = [cfg, ks, round(t * 1000, 2)]
+                else:
+                    for i in steps_of[key]:
+                        self.cfg[i] = cur
+        self._ensure_ws()
+        self.tuned_graph_ms = base
 
     # -------------------------------------------------------------- run
     def _launch(self, set_idx: int = 0, stream=None) -> None:

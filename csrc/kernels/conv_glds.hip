@@ -425,9 +425,14 @@ __device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
   X(26, 256, 64, 4, 2, 3, true)     \
   X(27, 64, 256, 2, 4, 3, true)     \
   X(28, 128, 256, 4, 2, 3, true)    \
-  X(29, 256, 128, 4, 2, 3, true)
+  X(29, 256, 128, 4, 2, 3, true)    \
+  X(30, 128, 128, 4, 2, 2, true)    \
+  X(31, 64, 128, 2, 4, 3, true)     \
+  X(32, 128, 64, 4, 2, 3, true)     \
+  X(33, 128, 128, 2, 2, 2, true)    \
+  X(34, 64, 64, 2, 2, 3, true)
 
-int conv_glds_num_cfgs() { return 24; }
+int conv_glds_num_cfgs() { return 29; }
 
 // stream-K grid: `mult` x 256 blocks (one per CU), each taking ceil(total / G)
 // consecutive (tile, K-tile) iterations
