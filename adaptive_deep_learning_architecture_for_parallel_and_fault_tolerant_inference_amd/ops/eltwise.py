@@ -93,6 +93,29 @@ def gap(x: torch.Tensor, out: Optional[torch.Tensor] = None, out32: Optional[tor
     return out if out is not None else out32
 
 
+def dense_small_scratch(M: int, N: int, K: int) -> int:
+    """fp32 elements of the split-K scratch `dense_small` needs."""
+    return kernels().dense_small_kslices(K) * M * N
+
+
+def dense_small(x: torch.Tensor, pc, part: torch.Tensor, logits: Optional[torch.Tensor] = None,
+                probs: Optional[torch.Tensor] = None, stream=None) -> None:
+    """Classifier GEMM for M <= 32 rows (csrc/kernels/head.hip): x [M][K] bf16,
+    packed weights `pc` (ops.conv.PackedConv, 1x1), fp32 logits and/or softmax probs."""
+    _chk(x, name="x")
+    M, K = x.shape[0], x.numel() // x.shape[0]
+    N = pc.cout
+    if M > 32 or K != pc.K:
+        raise ValueError(f"dense_small: M={M} (<= 32) and K={K} (== {pc.K}) required")
+    if part.dtype != torch.float32 or part.numel() < dense_small_scratch(M, N, K):
+        raise ValueError("dense_small: scratch too small")
+    for t in (logits, probs):
+        if t is not None and (t.dtype != torch.float32 or t.numel() != M * N or not t.is_contiguous()):
+            raise ValueError("dense_small: outputs must be contiguous fp32 [M][N]")
+    kernels().dense_small(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(part), ptr(logits), ptr(probs), M, N, K, pc.Kpad,
+                          stream_handle(stream))
+
+
 def softmax_rows(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
     _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
     rows, n = x.shape

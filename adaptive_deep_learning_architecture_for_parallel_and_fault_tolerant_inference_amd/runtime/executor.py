@@ -195,8 +195,14 @@ class SliceExecutor:
                     if src is not None and "_buf" in src.p:
                         free.append(src.p["_buf"])
         self._logits: Dict[int, torch.Tensor] = {}
+        self._dense_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
-            if st.kind == "dense" and st.p["softmax"]:
+            if st.kind == "dense" and self.batch <= 32:
+                # small-M head GEMM (csrc/kernels/head.hip): split-K scratch
+                pc = self.packed[i]
+                n = E.dense_small_scratch(self.batch, pc.cout, pc.K)
+                self._dense_part[i] = torch.empty(n, dtype=torch.float32, device=dev)
+            elif st.kind == "dense" and st.p["softmax"]:
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
         self._ws: Optional[torch.Tensor] = None
         self._ctr: Optional[torch.Tensor] = None
@@ -273,7 +279,7 @@ class SliceExecutor:
         ranked: Dict[str, List[Tuple[float, int, int]]] = {}
         prev = dict(load_tuning())              # the table in force: a known-good starting point
         for i, st in enumerate(self.steps):
-            if st.kind not in ("conv", "dense"):
+            if st.kind not in ("conv", "dense") or i in self._dense_part:
                 continue
             B, H, W, C, OH, OW, pc = self._conv_geom(i)
             M, N = B * OH * OW, pc.cout
@@ -357,7 +363,7 @@ class SliceExecutor:
     def _refine_in_graph(self, ranked, results, top: int, prev: Optional[Dict[str, List]] = None) -> None:
         steps_of: Dict[str, List[int]] = {}
         for i, st in enumerate(self.steps):
-            if st.kind in ("conv", "dense"):
+            if st.kind in ("conv", "dense") and i not in self._dense_part:
                 B, H, W, C, OH, OW, pc = self._conv_geom(i)
                 steps_of.setdefault(conv_key(B, H, W, C, pc), []).append(i)
         # start from the previous table where it is still a valid candidate, so a
@@ -429,6 +435,12 @@ class SliceExecutor:
                 E.pad(b[st.ins[0]], b[st.out], pt, pl, stream=stream)
             elif k == "gap":
                 E.gap(b[st.ins[0]], out=b[st.out], stream=stream)
+            elif k == "dense" and i in self._dense_part:
+                x = b[st.ins[0]].reshape(self.batch, -1)
+                if st.p["softmax"]:
+                    E.dense_small(x, self.packed[i], self._dense_part[i], probs=b[st.out], stream=stream)
+                else:
+                    E.dense_small(x, self.packed[i], self._dense_part[i], logits=b[st.out], stream=stream)
             elif k == "dense":
                 cfg, ks = self.cfg[i]
                 x = b[st.ins[0]].reshape(self.batch, -1)

@@ -115,6 +115,13 @@ PYBIND11_MODULE(_C, m) {
     check(adapt::maxpool(P<const bf16>(x), P<bf16>(y), B, H, W, C, OH, OW, K, Sd, pad_t, pad_l, pad_zero, S(s)),
           "maxpool");
   });
+  m.def("dense_small_kslices", &adapt::dense_small_kslices);
+  m.def("dense_small", [](u64 x, u64 w, u64 bias, u64 part, u64 logits, u64 probs, int M, int N, int K, int Kpad,
+                          u64 s) {
+    check(adapt::dense_small(P<const bf16>(x), P<const bf16>(w), P<const float>(bias), P<float>(part),
+                             P<float>(logits), P<float>(probs), M, N, K, Kpad, S(s)),
+          "dense_small");
+  });
   m.def("gap", [](u64 x, u64 y, u64 y32, int B, int HW, int C, u64 s) {
     check(adapt::gap(P<const bf16>(x), P<bf16>(y), P<float>(y32), B, HW, C, S(s)), "gap");
   });

@@ -8,7 +8,7 @@
 //  * add_act       y = a + b (+ReLU)                          (unfused Keras Add)
 //  * relu          y = max(x, 0)
 //  * maxpool       KxK/s with explicit zero padding (Keras ZeroPadding2D + MaxPooling2D)
-//  * gap           global average pool -> bf16 [B][C] (+ optional fp32 copy)
+//  * gap           -> head.hip
 //  * softmax_rows  fp32 row softmax (Dense activation='softmax')
 //  * cast          bf16 <-> fp32 for frontier / host I/O
 #include "kernels.h"
@@ -120,35 +120,6 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const bf16* __restrict__ x
   }
 }
 
-// one block per (image, 256*8-channel slab); threads over channels chunks, loop over HW
-__global__ __launch_bounds__(256) void gap_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                                  float* __restrict__ y32, int HW, int C) {
-  const int b = blockIdx.y;
-  const int cc = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cc * 8 >= C) return;
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bf16* base = x + (size_t)b * HW * C + cc * 8;
-  for (int i = 0; i < HW; ++i) {
-    V8 v;
-    v.u = *(const u32x4*)(base + (size_t)i * C);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) s[t] += bf2f(v.e[t]);
-  }
-  const float inv = 1.f / (float)HW;
-  V8 o;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    s[t] *= inv;
-    o.e[t] = f2bf(s[t]);
-  }
-  if (y) *(u32x4*)(y + (size_t)b * C + cc * 8) = o.u;
-  if (y32) {
-    float* d = y32 + (size_t)b * C + cc * 8;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) d[t] = s[t];
-  }
-}
-
 // one block (256 threads) per row
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ x, float* __restrict__ y, int N,
                                                            int ldx) {
@@ -232,11 +203,6 @@ hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, i
   size_t total = (size_t)B * OH * OW * (C / 8);
   hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(total)), dim3(256), 0, s, x, y, B, H, W, C, OH, OW, K, S, pad_t,
                      pad_l, pad_zero);
-  return hipGetLastError();
-}
-hipError_t gap(const bf16* x, bf16* y, float* y32, int B, int HW, int C, hipStream_t s) {
-  dim3 grid((C / 8 + 255) / 256, B);
-  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, y, y32, HW, C);
   return hipGetLastError();
 }
 hipError_t softmax_rows(const float* x, float* y, int rows, int N, int ldx, hipStream_t s) {

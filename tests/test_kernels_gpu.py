@@ -173,6 +173,39 @@ def test_conv_f32_out_dense(ops):
     assert torch.allclose(out, ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M,K,N", [(32, 2048, 1000), (1, 2048, 1000), (7, 512, 10), (20, 1000, 37)])
+def test_dense_small_head(ops, M, K, N):
+    """Small-M classifier GEMM (+bias, + softmax) of csrc/kernels/head.hip vs torch fp32."""
+    conv, E = ops
+    dev = "cuda"
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, N) / math.sqrt(K)).numpy()
+    b = (torch.randn(N) * 0.1).numpy()
+    pc = conv.pack_conv(w.reshape(1, 1, K, N), b, 1, ((0, 0), (0, 0)), dev)
+    part = torch.empty(E.dense_small_scratch(M, N, K), device=dev)
+    logits = torch.empty(M, N, device=dev)
+    probs = torch.empty(M, N, device=dev)
+    E.dense_small(x, pc, part, logits=logits, probs=probs)
+    torch.cuda.synchronize()
+    ref = x.float() @ torch.from_numpy(w).to(dev).to(torch.bfloat16).float() + torch.from_numpy(b).to(dev)
+    assert torch.allclose(logits, ref, atol=2e-2, rtol=2e-2)
+    assert torch.allclose(probs, torch.softmax(ref, -1), atol=1e-3, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,H,W,C", [(32, 7, 7, 2048), (3, 5, 9, 64), (2, 1, 1, 520)])
+def test_gap(ops, B, H, W, C):
+    _, E = ops
+    x = torch.randn(B, H, W, C, device="cuda").to(torch.bfloat16)
+    y = torch.empty(B, C, device="cuda", dtype=torch.bfloat16)
+    y32 = torch.empty(B, C, device="cuda")
+    E.gap(x, out=y, out32=y32)
+    torch.cuda.synchronize()
+    ref = x.float().mean(dim=(1, 2))
+    assert torch.allclose(y32, ref, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(y.float(), ref, atol=1e-2, rtol=1e-2)
+
+
 def test_eltwise(ops):
     _, E = ops
     dev = "cuda"

@@ -58,6 +58,8 @@ def main():
         ex.cfg = {0: cfg_saved[i]} if i in cfg_saved else {}
         logits_saved = ex._logits
         ex._logits = {0: logits_saved[i]} if i in logits_saved else {}
+        dense_saved = ex._dense_part
+        ex._dense_part = {0: dense_saved[i]} if i in dense_saved else {}
         relay_saved = ex.relay
         ex.relay = []
         try:
@@ -72,6 +74,7 @@ def main():
             t = time_fn(lambda: gg.replay(), reps=5, warm=2) / 20
         finally:
             ex.steps, ex.packed, ex.cfg, ex._logits, ex.relay = saved, packed_saved, cfg_saved, logits_saved, relay_saved
+            ex._dense_part = dense_saved
         flop = 0
         if st.kind in ("conv", "dense"):
             B, H, W, C, OH, OW, pc = ex._conv_geom(i)
