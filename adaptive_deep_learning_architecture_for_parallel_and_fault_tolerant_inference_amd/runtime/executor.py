@@ -172,6 +172,11 @@ class SliceExecutor:
         for i, st in enumerate(self.steps):
             for t in st.ins:
                 last_use[t] = i
+        # independent branches run on a side stream: their inputs stay live until the join
+        self._side = self._side_schedule()
+        for i, j in self._side.items():
+            for t in self.steps[i].ins:
+                last_use[t] = max(last_use.get(t, j), j)
         by_out = {st.out: st for st in self.steps}
         free: List[torch.Tensor] = []
         self.internal: Dict[str, torch.Tensor] = {}
@@ -206,6 +211,36 @@ class SliceExecutor:
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
         self._ws: Optional[torch.Tensor] = None
         self._ctr: Optional[torch.Tensor] = None
+        self._ws_side: Optional[torch.Tensor] = None
+        self._ctr_side: Optional[torch.Tensor] = None
+        self._side_stream: Optional[torch.cuda.Stream] = None
+
+    def _side_schedule(self) -> Dict[int, int]:
+        """{step i: join step j} for convs that form an independent branch: the
+        first of several consumers of their input whose only consumer comes
+        later than the next step (ResNet: the projection shortcut X_0 of each
+        stage's first block runs beside X_1 -> X_2 and joins at X_3's residual
+        add).  Run on a second HIP stream inside the same hipGraph.
+
+        Opt-in (ADAPT_BRANCH_STREAMS=1): measured on MI355X at bs=32 the
+        concurrent branch slows the slice down (0.877 vs 0.815 ms/batch): both
+        sides are bandwidth-bound and the shortcut conv steals the CUs the
+        critical path needs."""
+        if self.device.type != "cuda" or os.environ.get("ADAPT_BRANCH_STREAMS", "0") != "1":
+            return {}
+        cons: Dict[str, List[int]] = {}
+        for i, st in enumerate(self.steps):
+            for t in set(st.ins):
+                cons.setdefault(t, []).append(i)
+        side: Dict[int, int] = {}
+        for i, st in enumerate(self.steps):
+            if st.kind != "conv" or st.out in self.outputs:
+                continue
+            c_in = cons.get(st.ins[0], [])
+            users = cons.get(st.out, [])
+            if len(c_in) >= 2 and c_in[0] == i and len(users) == 1 and users[0] > i + 1:
+                side[i] = users[0]
+        return side
 
     def bufs(self, set_idx: int = 0):
         return ChainMap(self.sets[set_idx], self.internal)
@@ -248,9 +283,13 @@ class SliceExecutor:
                     ctr = max(ctr, conv_ops.sk_plan(B * OH * OW, pc.cout, pc.Kpad, cfg, -ks)[0])
         if need and (self._ws is None or self._ws.numel() < need):
             self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+            if self._side:                     # side-stream convs must not share scratch with the main stream
+                self._ws_side = torch.empty(need, dtype=torch.float32, device=self.device)
         if ctr and (self._ctr is None or self._ctr.numel() < ctr):
             # stream-K arrival counters: zero once, every launch leaves them zero
             self._ctr = torch.zeros(ctr, dtype=torch.int32, device=self.device)
+            if self._side:
+                self._ctr_side = torch.zeros(ctr, dtype=torch.int32, device=self.device)
 
     def _select_configs(self, tune: bool) -> None:
         table = load_tuning()
@@ -406,9 +445,26 @@ class SliceExecutor:
         # failing kernel is reported with its step (the AMD_SERIALIZE_KERNEL
         # idea at plan level; never active under hipGraph capture)
         debug = os.environ.get("ADAPT_DEBUG_SYNC", "0") == "1" and not torch.cuda.is_current_stream_capturing()
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        side = self._side
+        joins: Dict[int, List[int]] = {}
+        for a, j in side.items():
+            joins.setdefault(j, []).append(a)
+        if side and self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(device=self.device)
+        done: Dict[int, torch.cuda.Event] = {}
+        main_stream = stream
         for i, st in enumerate(self.steps):
             if debug and i:
                 self._debug_check(i - 1)
+            for a in joins.get(i, []):
+                main.wait_event(done[a])              # join: the branch result is ready
+            stream, ws, ctr = main_stream, self._ws, self._ctr
+            if i in side:                             # fork: the branch starts after everything before it
+                fork = torch.cuda.Event()
+                fork.record(main)
+                self._side_stream.wait_event(fork)
+                stream, ws, ctr = self._side_stream, self._ws_side, self._ctr_side
             k = st.kind
             if k == "pack":
                 E.input_pack(b[st.ins[0]], b[st.out], stream=stream)
@@ -419,7 +475,7 @@ class SliceExecutor:
                 cfg, ks = self.cfg[i]
                 res = b[st.ins[1]] if len(st.ins) > 1 else None
                 conv_ops.conv_forward(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
-                                      cfg=cfg, ksplit=ks, workspace=self._ws, stream=stream, counters=self._ctr)
+                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr)
             elif k == "maxpool":
                 (pt, _), (pl, _) = st.p["pads"]
                 E.maxpool(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, True, stream=stream)
@@ -453,6 +509,14 @@ class SliceExecutor:
                 E.softmax_rows(b[st.ins[0]], b[st.out], stream=stream)
             else:
                 raise NotImplementedError(k)
+            if i in side:
+                ev = torch.cuda.Event()
+                ev.record(self._side_stream)
+                done[i] = ev
+        stream = main_stream
+        for a in done:                                # every branch joined (normally at its consumer)
+            if a not in side or side[a] >= len(self.steps):
+                main.wait_event(done[a])
         if debug and self.steps:
             self._debug_check(len(self.steps) - 1)
         # relay frontier tensors: device copy into the output set (no aliasing with the

@@ -60,6 +60,8 @@ def main():
         ex._logits = {0: logits_saved[i]} if i in logits_saved else {}
         dense_saved = ex._dense_part
         ex._dense_part = {0: dense_saved[i]} if i in dense_saved else {}
+        side_saved = ex._side
+        ex._side = {}
         relay_saved = ex.relay
         ex.relay = []
         try:
@@ -75,6 +77,7 @@ def main():
         finally:
             ex.steps, ex.packed, ex.cfg, ex._logits, ex.relay = saved, packed_saved, cfg_saved, logits_saved, relay_saved
             ex._dense_part = dense_saved
+            ex._side = side_saved
         flop = 0
         if st.kind in ("conv", "dense"):
             B, H, W, C, OH, OW, pc = ex._conv_geom(i)
