@@ -88,6 +88,7 @@ class PackedConv:
     pad_l: int
     pad_b: int
     pad_r: int
+    n_split: int = 0         # > 0: two sibling convs packed along N (outputs [0, n_split) and [n_split, cout))
 
     @property
     def K(self) -> int:
@@ -171,11 +172,14 @@ def workspace_elems(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int:
 def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: Optional[torch.Tensor] = None,
                  relu: bool = False, cfg: Optional[int] = None, ksplit: int = 1,
                  workspace: Optional[torch.Tensor] = None, stream=None,
-                 counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 counters: Optional[torch.Tensor] = None, out2: Optional[torch.Tensor] = None,
+                 relu2: bool = False) -> torch.Tensor:
     """x: [B,H,W,Cin] bf16 NHWC; out: [B,OH,OW,Cout] bf16 (or fp32 [M][Cout] for GEMM use).
 
     ksplit > 1: split-K (fp32 slabs + reduce launch); ksplit < 0: stream-K over
-    -ksplit x 256 blocks (v2 configs; needs `counters`, int32 zeros, one per tile)."""
+    -ksplit x 256 blocks (v2 configs; needs `counters`, int32 zeros, one per tile).
+    Dual output (``pc.n_split > 0``, two sibling convs packed along N): channels
+    [0, n_split) go to `out` (ReLU `relu`), the rest to `out2` (ReLU `relu2`)."""
     if x.dim() == 2:
         B, H, W, C = x.shape[0], 1, 1, x.shape[1]
     else:
@@ -188,7 +192,16 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
     M = B * OH * OW
     N = pc.cout
     out_f32 = out.dtype == torch.float32
-    if out.numel() != M * N or not out.is_contiguous():
+    ns = pc.n_split
+    if ns:
+        if out2 is None or residual is not None or out_f32:
+            raise ValueError("dual-output conv needs a bf16 out2 and no residual")
+        if out.numel() != M * ns or out2.numel() != M * (N - ns) or not out.is_contiguous() \
+                or not out2.is_contiguous() or out2.dtype != torch.bfloat16:
+            raise ValueError(f"dual-output conv buffers need {M * ns} + {M * (N - ns)} bf16 elements")
+    elif out2 is not None:
+        raise ValueError("out2 given for a single-output conv")
+    elif out.numel() != M * N or not out.is_contiguous():
         raise ValueError(f"conv output buffer has {out.numel()} elements, need {M * N}")
     if residual is not None and (residual.numel() != M * N or residual.dtype != torch.bfloat16):
         raise ValueError("residual must be bf16 with the output's shape")
@@ -197,6 +210,8 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
     bm, bn = CFG_TILES[cfg]
     if pc.w.shape[0] < math.ceil(N / bn) * bn:
         raise ValueError("packed weights not padded to the tile's N")
+    if ns and ns % 8:
+        raise ValueError("dual-output split must be a multiple of 8 channels")
     pure = pc.kh == 1 and pc.kw == 1 and pc.stride == 1 and pc.pad_t == 0 and pc.pad_l == 0 and OH == H and OW == W
     if not cfg_supported(cfg, pc, pure):
         raise ValueError(f"tile config {cfg} does not support this conv (Cin {pc.cin}, {pc.kh}x{pc.kw}/s{pc.stride})")
@@ -225,8 +240,8 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         ctr_ptr = ptr(counters)
     kernels().conv_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, ctr_ptr, sk_iters, th,
                            B, H, W, C, OH, OW, N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l,
-                           pc.K, pc.Kpad, N, int(relu), int(ksplit), int(cfg), bool(out_f32),
-                           stream_handle(stream))
+                           pc.K, pc.Kpad, ns or N, int(relu), int(ksplit), int(cfg), bool(out_f32),
+                           stream_handle(stream), ptr(out2), int(ns), int(relu2))
     return out
 
 

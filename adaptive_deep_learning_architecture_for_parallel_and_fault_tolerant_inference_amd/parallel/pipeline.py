@@ -130,6 +130,176 @@ class StageLink:
             self.send_work[j] = None
 
 
+class CompressedStageLink(StageLink):
+    """StageLink whose frontier tensors travel compressed (BASELINE config 3:
+    "8-stage pipeline with lz4 activation compression"; the reference
+    compresses every hop, `src/dispatcher.py:92-98`, `src/node.py:178`).
+
+    Per frontier tensor and buffer set a `codec.wire.WireCodec` turns the
+    stage output into one device byte buffer.  A point-to-point receive must
+    know its length, so each tick sends two messages:
+
+    * the byte counts, int64[n_out], on a host (gloo) control group, tag 7;
+    * the wire buffers on the data group (RCCL over xGMI, or gloo).
+
+    Schedule of a stage at tick t (set j = t % nsets):
+
+    1. receive t's byte counts, post the data receives, decode into the
+       slice's input set j on the compute stream (device-side scan + decode);
+    2. compute(j);
+    3. enqueue the encode of t's outputs on the codec's side stream behind an
+       event of the compute stream;
+    4. post the messages of tick t-1: its encode ran beside compute(t).
+
+    The receiver learns a length one tick later than an uncompressed link
+    would; with two buffer sets the compute stream still has the next
+    micro-batch queued while the host waits.
+    """
+
+    SIZE_TAG = 7
+
+    def __init__(self, compute: Callable[[int], None], in_bufs: List[List[torch.Tensor]],
+                 out_bufs: List[List[torch.Tensor]], prev_rank: Optional[int], next_rank: Optional[int],
+                 codec: str = "lz4", group=None, ctl_group=None, host_staged: bool = False):
+        StageLink.__init__(self, compute, in_bufs, out_bufs, prev_rank, next_rank, group=group, host_staged=False)
+        from ..codec.wire import WireCodec
+        self.host_staged = host_staged
+        self.ctl = ctl_group
+        self.codec = codec
+        ref = (out_bufs or in_bufs)[0][0]
+        self.gpu = ref.device.type == "cuda"
+        self.side = torch.cuda.Stream(device=ref.device) if self.gpu else None
+        self.enc = [[WireCodec(codec, t, self.side) for t in s] for s in out_bufs] if next_rank is not None else []
+        self.dec = [[WireCodec(codec, t) for t in s] for s in in_bufs] if prev_rank is not None else []
+        n_out = len(out_bufs[0]) if out_bufs and out_bufs[0] else 1
+        n_in = len(in_bufs[0]) if in_bufs and in_bufs[0] else 1
+        self.size_out = [torch.zeros(n_out, dtype=torch.int64) for _ in range(self.nsets)]
+        self.size_in = [torch.zeros(n_in, dtype=torch.int64) for _ in range(self.nsets)]
+        self.size_recv: List[Optional[object]] = [None] * self.nsets
+        self.size_send: List[Optional[object]] = [None] * self.nsets
+        self.enc_done: List[Optional[torch.cuda.Event]] = [None] * self.nsets
+        self.pending: List[int] = []
+        self.raw_bytes = 0
+        self.wire_bytes = 0
+        self.staged = host_staged and self.gpu
+        if self.staged:
+            self.host_out = [[torch.empty(e.wire.numel(), dtype=torch.uint8, pin_memory=True) for e in s]
+                             for s in self.enc]
+            self.host_in = [[torch.empty(d.wire.numel(), dtype=torch.uint8, pin_memory=True) for d in s]
+                            for s in self.dec]
+
+    @property
+    def ratio(self) -> Optional[float]:
+        return self.raw_bytes / self.wire_bytes if self.wire_bytes else None
+
+    def _post_size_recv(self, j: int) -> None:
+        self.size_recv[j] = dist.irecv(self.size_in[j], src=self.prev, group=self.ctl, tag=self.SIZE_TAG)
+
+    def prime(self, total_ticks: Optional[int] = None) -> None:
+        self.total_ticks = total_ticks
+        if self.prev is not None:
+            for j in range(self.nsets):
+                if total_ticks is None or j < total_ticks:
+                    self._post_size_recv(j)
+
+    def _recv(self, j: int) -> None:
+        self.size_recv[j].wait()
+        self.size_recv[j] = None
+        sizes = [int(v) for v in self.size_in[j].tolist()]
+        works = []
+        for k, (d, nb) in enumerate(zip(self.dec[j], sizes)):
+            if self.staged:
+                h = self.host_in[j][k]
+                dist.recv(h[:nb], src=self.prev, group=self.group)
+                d.wire[:nb].copy_(h[:nb], non_blocking=False)
+            else:
+                works.append(dist.irecv(d.wire[:nb], src=self.prev, group=self.group))
+        for w in works:
+            w.wait()                 # RCCL: the compute stream waits for the receive; gloo: host wait
+        for d, nb, buf in zip(self.dec[j], sizes, self.in_bufs[j]):
+            d.decode(nb, buf)
+        total = getattr(self, "total_ticks", None)
+        if total is None or self.tick + self.nsets < total:
+            self._post_size_recv(j)
+
+    def _send(self, j: int) -> None:
+        sizes = [e.nbytes() for e in self.enc[j]]          # waits for set j's encode only
+        if self.size_send[j] is not None:
+            self.size_send[j].wait()
+        self.size_out[j].copy_(torch.tensor(sizes, dtype=torch.int64))
+        self.size_send[j] = dist.isend(self.size_out[j], dst=self.next, group=self.ctl, tag=self.SIZE_TAG)
+        works = []
+        for k, (e, nb) in enumerate(zip(self.enc[j], sizes)):
+            self.raw_bytes += e.n
+            self.wire_bytes += nb
+            if self.staged:
+                h = self.host_out[j][k]
+                h[:nb].copy_(e.wire[:nb])                   # the encode is complete (nbytes waited)
+                works.append(dist.isend(h[:nb], dst=self.next, group=self.group))
+            elif self.gpu:
+                with torch.cuda.stream(self.side):          # RCCL orders the send after the encode
+                    works.append(dist.isend(e.wire[:nb], dst=self.next, group=self.group))
+            else:
+                works.append(dist.isend(e.wire[:nb], dst=self.next, group=self.group))
+        self.send_work[j] = works
+
+    def _release(self, j: int) -> None:
+        """Set j's wire buffers are about to be re-encoded: their send must be done."""
+        works = self.send_work[j]
+        if not works:
+            return
+        if self.gpu and not self.staged:
+            with torch.cuda.stream(self.side):
+                for w in works:
+                    w.wait()
+        else:
+            for w in works:
+                w.wait()
+        self.send_work[j] = None
+
+    def step(self) -> int:
+        j = self.tick % self.nsets
+        if self.prev is not None:
+            self._recv(j)
+        if self.gpu and self.enc_done[j] is not None:
+            # compute(j) overwrites the outputs that set j's last encode reads
+            torch.cuda.current_stream().wait_event(self.enc_done[j])
+        self.compute(j)
+        if self.next is not None:
+            self._release(j)
+            if self.gpu:
+                ev = torch.cuda.Event()
+                ev.record()
+                for e, t in zip(self.enc[j], self.out_bufs[j]):
+                    self.enc_done[j] = e.encode(t, after=ev)
+            else:
+                for e, t in zip(self.enc[j], self.out_bufs[j]):
+                    e.encode(t)
+            for p in self.pending:
+                self._send(p)
+            self.pending = [j]
+        self.tick += 1
+        return j
+
+    def flush(self) -> None:
+        """Post the deferred messages now (a host-side sync point follows, e.g. a
+        barrier: the peer must not wait for a tick this rank will not run)."""
+        for p in self.pending:
+            self._send(p)
+        self.pending = []
+
+    def drain(self) -> None:
+        self.flush()
+        for j in range(self.nsets):
+            self._release(j)
+            if self.size_send[j] is not None:
+                self.size_send[j].wait()
+                self.size_send[j] = None
+        for row in self.dec:
+            for d in row:
+                d.check()
+
+
 def stage_ranks(stage: int, stages: int, replica: int) -> Dict[str, Optional[int]]:
     base = replica * stages
     return {

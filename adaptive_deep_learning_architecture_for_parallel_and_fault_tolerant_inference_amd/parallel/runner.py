@@ -21,7 +21,7 @@ import torch.distributed as dist
 from ..graph.planner import plan_cuts
 from ..graph.slicer import partition, subgraph
 from ..runtime.executor import SliceExecutor
-from .pipeline import StageLink, stage_ranks
+from .pipeline import CompressedStageLink, StageLink, stage_ranks
 
 
 class DPJob:
@@ -80,7 +80,7 @@ class PipelineJob:
 
     def __init__(self, g, weights, world: int, rank: int, device, batch: int, stages: int,
                  part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False, nsets: int = 2,
-                 host_staged: bool = False):
+                 host_staged: bool = False, codec: str = "none"):
         if world % stages:
             raise ValueError(f"world {world} not divisible by stages {stages}")
         self.stages = stages
@@ -104,8 +104,16 @@ class PipelineJob:
         self.prev, self.next = rk["prev"], rk["next"]
         in_bufs = [[self.ex.input_buf(n, j) for n in sl.inputs] for j in range(nsets)]
         out_bufs = [[self.ex.output_buf(n, j) for n in sl.outputs] for j in range(nsets)]
-        self.link = StageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next,
-                              host_staged=host_staged)
+        self.codec = codec
+        if codec == "none":
+            self.link = StageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next,
+                                  host_staged=host_staged)
+        else:
+            # byte counts ride a host (gloo) control group; with host staging the
+            # default group already is gloo
+            ctl = None if host_staged else dist.new_group(backend="gloo")
+            self.link = CompressedStageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next,
+                                            codec=codec, ctl_group=ctl, host_staged=host_staged)
         self.images_per_step = batch * world          # stages ticks x replicas x batch / stages-per-image
         self.global_batch = batch * world
         self.parallelism = f"pp{stages}" if self.replicas == 1 else f"pp{stages}xdp{self.replicas}"
@@ -127,6 +135,8 @@ class PipelineJob:
             self._primed = True
         for _ in range(self.stages):
             self.link.step()
+        if hasattr(self.link, "flush"):
+            self.link.flush()            # a step ends with every message posted (callers barrier between steps)
 
     def finish(self) -> None:
         self.link.drain()
@@ -134,7 +144,7 @@ class PipelineJob:
 
 def build_job(g, weights, mode: str, world: int, rank: int, device, batch: int = 32, stages: int = 0,
               part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False,
-              host_staged: bool = False, streams: int = 1):
+              host_staged: bool = False, streams: int = 1, codec: str = "none"):
     if mode == "dp" or world == 1 and not part_at:
         return DPJob(g, weights, world, rank, device, batch, graph=graph, tune=tune, streams=streams)
     if mode == "pp":
@@ -142,9 +152,9 @@ def build_job(g, weights, mode: str, world: int, rank: int, device, batch: int =
         if k != world:
             raise ValueError(f"pp mode: {k} stages for {world} ranks")
         return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune,
-                           host_staged=host_staged)
+                           host_staged=host_staged, codec=codec)
     if mode == "ppdp":
         k = stages or (len(part_at) + 1 if part_at else 2)
         return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune,
-                           host_staged=host_staged)
+                           host_staged=host_staged, codec=codec)
     raise ValueError(f"unknown mode {mode}")

@@ -115,17 +115,16 @@ class SliceExecutor:
         for i, st in enumerate(self.steps):
             if st.kind == "conv":
                 p = st.p
-                cname = p["conv"]
-                k = weights[f"{cname}/kernel"]
-                b = weights.get(f"{cname}/bias")
-                bn = None
-                eps = 1e-3
-                if p["bn"]:
-                    bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
-                    eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
-                kf, bf = conv_ops.fold_bn(k, b, bn, eps)
-                cin_pad = ((k.shape[2] + 7) // 8) * 8
-                self.packed[i] = conv_ops.pack_conv(kf, bf, p["stride"], p["pads"], dev, cin_pad=cin_pad)
+                kf, bf = self._folded(weights, p)
+                cin_pad = ((kf.shape[2] + 7) // 8) * 8
+                n_split = 0
+                if p.get("sibling"):                  # merged sibling convs: one GEMM, N = N0 + N1
+                    k2, b2 = self._folded(weights, p["sibling"])
+                    n_split = kf.shape[-1]
+                    kf, bf = np.concatenate([kf, k2], axis=-1), np.concatenate([bf, b2])
+                pc = conv_ops.pack_conv(kf, bf, p["stride"], p["pads"], dev, cin_pad=cin_pad)
+                pc.n_split = n_split
+                self.packed[i] = pc
             elif st.kind == "stem":
                 p = st.p
                 k = weights[f"{p['conv']}/kernel"]
@@ -150,6 +149,16 @@ class SliceExecutor:
                 s = gm / np.sqrt(var + eps)
                 self.packed[i] = (torch.tensor(s, dtype=torch.float32, device=dev),
                                   torch.tensor(bt - mu * s, dtype=torch.float32, device=dev))
+
+    def _folded(self, weights: Dict[str, np.ndarray], p: Dict):
+        """BN-folded (kernel HWIO, bias) of a conv step's parameters."""
+        cname = p["conv"]
+        bn = None
+        eps = 1e-3
+        if p["bn"]:
+            bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
+            eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
+        return conv_ops.fold_bn(weights[f"{cname}/kernel"], weights.get(f"{cname}/bias"), bn, eps)
 
     # ----------------------------------------------------------- buffers
     def _alloc(self) -> None:
@@ -177,13 +186,15 @@ class SliceExecutor:
         for i, j in self._side.items():
             for t in self.steps[i].ins:
                 last_use[t] = max(last_use.get(t, j), j)
-        by_out = {st.out: st for st in self.steps}
+        owner: Dict[str, torch.Tensor] = {}          # internal tensor -> arena block backing it
         free: List[torch.Tensor] = []
         self.internal: Dict[str, torch.Tensor] = {}
         self._arena: List[torch.Tensor] = []
         for i, st in enumerate(self.steps):
-            if st.out not in keep:
-                shp, dt = self.shape_of(st.out), self.dtype_of(st.out)
+            for name in [st.out] + ([st.p["out2"]] if st.p.get("out2") else []):
+                if name in keep:
+                    continue
+                shp, dt = self.shape_of(name), self.dtype_of(name)
                 nb = _nbytes(shp, dt)
                 cand = [k for k, b in enumerate(free) if b.numel() >= nb]
                 if cand:
@@ -192,13 +203,11 @@ class SliceExecutor:
                 else:
                     b = torch.empty(max(nb, 1 << 16), dtype=torch.uint8, device=dev)
                     self._arena.append(b)
-                self.internal[st.out] = b[:nb].view(dt).view(shp)
-                st.p["_buf"] = b
+                self.internal[name] = b[:nb].view(dt).view(shp)
+                owner[name] = b
             for tname in set(st.ins):
-                if last_use.get(tname) == i and tname not in keep:
-                    src = by_out.get(tname)
-                    if src is not None and "_buf" in src.p:
-                        free.append(src.p["_buf"])
+                if last_use.get(tname) == i and tname not in keep and tname in owner:
+                    free.append(owner.pop(tname))
         self._logits: Dict[int, torch.Tensor] = {}
         self._dense_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
@@ -234,7 +243,7 @@ class SliceExecutor:
                 cons.setdefault(t, []).append(i)
         side: Dict[int, int] = {}
         for i, st in enumerate(self.steps):
-            if st.kind != "conv" or st.out in self.outputs:
+            if st.kind != "conv" or st.out in self.outputs or st.p.get("out2"):
                 continue
             c_in = cons.get(st.ins[0], [])
             users = cons.get(st.out, [])
@@ -474,8 +483,10 @@ class SliceExecutor:
             elif k == "conv":
                 cfg, ks = self.cfg[i]
                 res = b[st.ins[1]] if len(st.ins) > 1 else None
+                out2 = b[st.p["out2"]] if st.p.get("out2") else None
                 conv_ops.conv_forward(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
-                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr)
+                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr,
+                                      out2=out2, relu2=st.p.get("relu2", False))
             elif k == "maxpool":
                 (pt, _), (pl, _) = st.p["pads"]
                 E.maxpool(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, True, stream=stream)

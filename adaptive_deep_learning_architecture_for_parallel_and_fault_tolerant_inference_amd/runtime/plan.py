@@ -181,7 +181,42 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
         raise RuntimeError(f"plan does not produce outputs {missing}")
     if os.environ.get("ADAPT_NO_STEM", "0") != "1":
         steps = _fuse_stem(g, steps, outset)
+    if os.environ.get("ADAPT_NO_SIBLINGS", "0") != "1":
+        steps = merge_siblings(steps)
     return steps
+
+
+def merge_siblings(steps: List[Step]) -> List[Step]:
+    """Two 1x1 convs that read the same tensor with the same stride and no
+    residual become ONE GEMM with N = N0 + N1 and two outputs: ResNet's
+    projection shortcut ``conv{s}_block1_0`` and ``conv{s}_block1_1`` (one
+    launch and one read of the block input instead of two; the kernels route
+    columns >= N0 to the second output, csrc/kernels/kernels.h `epi_dst`).
+    The merged step sits at the first sibling's position (its input is ready
+    there); the second output merely becomes available earlier."""
+    out: List[Step] = []
+    taken: Set[int] = set()
+    for i, st in enumerate(steps):
+        if i in taken:
+            continue
+        p = st.p
+        if st.kind == "conv" and not p.get("residual") and p.get("kernel") == (1, 1) and not p.get("packed_input"):
+            for j in range(i + 1, min(i + 4, len(steps))):
+                sj = steps[j]
+                q = sj.p
+                if (j not in taken and sj.kind == "conv" and sj.ins[0] == st.ins[0] and not q.get("residual")
+                        and q.get("kernel") == (1, 1) and q["stride"] == p["stride"] and q["pads"] == p["pads"]
+                        and p["filters"] % 256 == 0 and q["filters"] % 8 == 0):
+                    # nothing between them may consume the first sibling's output before
+                    # ... (it is produced at i either way) -- only the second moves earlier
+                    p["sibling"] = dict(q)
+                    p["out2"] = sj.out
+                    p["relu2"] = q["relu"]
+                    st.covers = st.covers + sj.covers
+                    taken.add(j)
+                    break
+        out.append(st)
+    return out
 
 
 STEM_MAX_OW = 112     # csrc/kernels/stem.hip ST_OWMAX

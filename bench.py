@@ -47,6 +47,8 @@ def parse():
                     help="independent bs=--batch micro-batches in flight per GPU (dp mode)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = host-staged rehearsal (several ranks per GPU)")
+    ap.add_argument("--codec", default="none", choices=["none", "lz4", "zvc"],
+                    help="pp/ppdp: compress stage-boundary activations on a side stream (BASELINE config 3)")
     return ap.parse_args()
 
 
@@ -79,7 +81,7 @@ def main():
     part_at = [s for s in args.part_at.split(",") if s]
     job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
                            stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune,
-                           host_staged=(backend != "nccl"), streams=args.streams)
+                           host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec)
     # synthetic input, resident on device (data="synthetic")
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     job.set_synthetic_input(torch.randn((args.batch, 224, 224, 3), generator=gen, device=dev))
@@ -127,6 +129,10 @@ def main():
                        "image": [224, 224, 3], "parallelism": job.parallelism, "part_at": job.part_at,
                        "micro_batch": args.batch, "hipgraph": not args.no_graph},
         }
+        link = getattr(job, "link", None)
+        if args.codec != "none" and link is not None:
+            rec["config"]["codec"] = args.codec
+            rec["config"]["wire_ratio"] = round(link.ratio, 4) if link.ratio else None
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

@@ -45,7 +45,7 @@ PYBIND11_MODULE(_C, m) {
       "conv_forward",
       [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, u64 counters, int sk_iters, int th, int B, int H, int W,
          int Cin, int OH, int OW, int N, int KH, int KW, int stride, int pad_t, int pad_l, int K, int Kpad, int ldo,
-         int relu, int ksplit, int cfg, bool out_f32, u64 stream) {
+         int relu, int ksplit, int cfg, bool out_f32, u64 stream, u64 out2, int n_split, int relu2) {
         adapt::ConvParams p;
         p.x = P<const bf16>(x);
         p.w = P<const bf16>(w);
@@ -60,10 +60,17 @@ PYBIND11_MODULE(_C, m) {
         p.OH = OH; p.OW = OW; p.N = N;
         p.KH = KH; p.KW = KW; p.stride = stride; p.pad_t = pad_t; p.pad_l = pad_l;
         p.M = B * OH * OW; p.K = K; p.Kpad = Kpad; p.ldo = ldo;
-        p.relu = relu; p.ksplit = ksplit < 1 ? 1 : ksplit;
+        // ksplit > 1: split-K slabs; < 0: stream-K over -ksplit x 256 blocks (v2 configs)
+        p.relu = relu; p.ksplit = ksplit == 0 ? 1 : ksplit;
+        p.n_split = n_split; p.out2 = P<void>(out2); p.relu2 = relu2; p.ldo2 = N - n_split;
         py::gil_scoped_release nogil;
         check(adapt::conv_forward(p, cfg, S(stream), out_f32), "conv_forward");
-      });
+      },
+      py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("out"), py::arg("ws"), py::arg("counters"),
+      py::arg("sk_iters"), py::arg("th"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"),
+      py::arg("OW"), py::arg("N"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"),
+      py::arg("K"), py::arg("Kpad"), py::arg("ldo"), py::arg("relu"), py::arg("ksplit"), py::arg("cfg"),
+      py::arg("out_f32"), py::arg("stream"), py::arg("out2") = 0, py::arg("n_split") = 0, py::arg("relu2") = 0);
   m.def("zvc_seg", &adapt::zvc_seg);
   m.def("zvc_scratch_bytes", &adapt::zvc_scratch_bytes);
   m.def("zvc_max_stream", &adapt::zvc_max_stream);
@@ -90,6 +97,15 @@ PYBIND11_MODULE(_C, m) {
     check(adapt::lz4_gpu_decompress(P<const uint8_t>(frame), P<const uint32_t>(offs), P<const uint32_t>(sizes),
                                     nchunks, P<uint8_t>(out), n, P<int>(err), S(s)),
           "lz4_gpu_decompress");
+  });
+  m.def("lz4_gpu_decompress_dev", [](u64 frame, u64 sizes, int nchunks, u64 offs, u64 out, size_t n, u64 err, u64 s) {
+    check(adapt::lz4_gpu_decompress_dev(P<const uint8_t>(frame), P<const uint32_t>(sizes), nchunks, P<uint32_t>(offs),
+                                        P<uint8_t>(out), n, P<int>(err), S(s)),
+          "lz4_gpu_decompress_dev");
+  });
+  m.def("zvc_gpu_decompress_dev", [](u64 stream, int nseg, size_t n, int esz, u64 out, u64 offs, u64 s) {
+    check(adapt::zvc_gpu_decompress_dev(P<const uint8_t>(stream), nseg, n, esz, P<void>(out), P<uint32_t>(offs), S(s)),
+          "zvc_gpu_decompress_dev");
   });
   m.def("stem_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW, int pad_t,
                            int pad_l, int pool, int PH, int PW, int pool_pad, u64 s) {

@@ -341,19 +341,20 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += bf2f(r.e[t]);
     }
-    if (p.relu) {
+    const EpiDst d = epi_dst(p, n);
+    if (d.relu) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
     }
     if (OUT_F32) {
-      float* o = (float*)p.out + (size_t)m * p.ldo + n;
+      float* o = (float*)d.base + (size_t)m * d.ld + d.col;
       *(f32x4*)o = (f32x4){v[0], v[1], v[2], v[3]};
       *(f32x4*)(o + 4) = (f32x4){v[4], v[5], v[6], v[7]};
     } else {
       V8 o;
 #pragma unroll
       for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-      *(u32x4*)((bf16*)p.out + (size_t)m * p.ldo + n) = o.u;
+      *(u32x4*)((bf16*)d.base + (size_t)m * d.ld + d.col) = o.u;
     }
   }
 }

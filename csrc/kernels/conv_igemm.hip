@@ -224,19 +224,20 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvParams p) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += bf2f(r.e[t]);
     }
-    if (p.relu) {
+    const EpiDst d = epi_dst(p, n);
+    if (d.relu) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
     }
     if (OUT_F32) {
-      float* o = (float*)p.out + (size_t)m * p.ldo + n;
+      float* o = (float*)d.base + (size_t)m * d.ld + d.col;
 #pragma unroll
       for (int t = 0; t < 8; ++t) o[t] = v[t];
     } else {
       V8 o;
 #pragma unroll
       for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-      *(u32x4*)((bf16*)p.out + (size_t)m * p.ldo + n) = o.u;
+      *(u32x4*)((bf16*)d.base + (size_t)m * d.ld + d.col) = o.u;
     }
   }
 }

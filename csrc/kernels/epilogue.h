@@ -26,6 +26,7 @@ __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float*
   const int cc = tid % CPR, row0 = tid / CPR;
   const int n = n0 + cc * 8;
   if (n >= p.N) return;
+  const EpiDst d = epi_dst(p, n);             // n_split is a multiple of 8: one destination per chunk
   float b[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) b[t] = 0.f;
@@ -57,19 +58,19 @@ __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float*
 #pragma unroll
         for (int t = 0; t < 8; ++t) v[t] += bf2f(r[u].e[t]);
       }
-      if (p.relu) {
+      if (d.relu) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
       }
       if (OUT_F32) {
-        float* o = (float*)p.out + (size_t)m * p.ldo + n;
+        float* o = (float*)d.base + (size_t)m * d.ld + d.col;
         *(f32x4*)o = (f32x4){v[0], v[1], v[2], v[3]};
         *(f32x4*)(o + 4) = (f32x4){v[4], v[5], v[6], v[7]};
       } else {
         V8 o;
 #pragma unroll
         for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-        *(u32x4*)((bf16*)p.out + (size_t)m * p.ldo + n) = o.u;
+        *(u32x4*)((bf16*)d.base + (size_t)m * d.ld + d.col) = o.u;
       }
     }
   }

@@ -19,7 +19,23 @@ struct ConvParams {
   int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
   int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_sk_plan)
   int th;           // halo 3x3 kernel: output rows per tile
+  // dual-output GEMM (two sibling convs over one input, runtime/plan.py
+  // merge_siblings): columns [0, n_split) -> out (row stride ldo, ReLU relu),
+  // columns [n_split, N) -> out2 (row stride ldo2, ReLU relu2); 0 = one output
+  int n_split;
+  void* out2;
+  int ldo2, relu2;
 };
+
+// where column n of the GEMM goes: destination base, column within it, row stride, ReLU
+struct EpiDst {
+  void* base;
+  int col, ld, relu;
+};
+__device__ __forceinline__ EpiDst epi_dst(const ConvParams& p, int n) {
+  if (p.n_split > 0 && n >= p.n_split) return EpiDst{p.out2, n - p.n_split, p.ldo2, p.relu2};
+  return EpiDst{p.out, n, p.ldo, p.relu};
+}
 hipError_t conv_halo_launch(const ConvParams& p, int cfg, hipStream_t s, bool out_f32);
 bool conv_halo_cfg(int cfg, int* bm, int* bn, int* patch_pix);
 void conv_sk_plan(int tiles, int kt, int mult, int* grid, int* iters);
@@ -38,6 +54,11 @@ hipError_t lz4_gpu_compress(const uint8_t* in, size_t n, uint8_t* scratch, uint3
                             uint8_t* out, uint64_t* total, hipStream_t s);
 hipError_t lz4_gpu_decompress(const uint8_t* frame, const uint32_t* offs, const uint32_t* sizes, int nchunks,
                               uint8_t* out, size_t n, int* err, hipStream_t s);
+// device-resident frame + block-size table -> out (offsets scanned on the device)
+hipError_t lz4_gpu_decompress_dev(const uint8_t* frame, const uint32_t* sizes, int nchunks, uint32_t* offs_scratch,
+                                  uint8_t* out, size_t n, int* err, hipStream_t s);
+hipError_t zvc_gpu_decompress_dev(const uint8_t* stream, int nseg, size_t n, int esz, void* out, uint32_t* offs_scratch,
+                                  hipStream_t s);
 hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pure, bool out_f32);
 bool conv_glds_cfg_tile(int cfg, int* bm, int* bn);
 int conv_num_cfgs();

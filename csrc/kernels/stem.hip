@@ -179,6 +179,146 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
   }
 }
 
+// ---- v2 pooled stem: one block per (image, group of S2_SP pool rows) ------------
+//
+// v1 (stem_kernel<true>) recomputes 3 conv rows per pool row (1.5x the conv
+// work) and re-stages 11 input rows per 2 new conv rows: 1792 blocks of 4
+// waves, 52.9 us at bs=32 (profiles/stem_bench.txt; PMC: VALU-heavy staging,
+// waits).  v2 walks S2_SP pool rows per block with a 3-row ring of conv rows
+// in LDS: each step computes conv rows 2t, 2t+1 once (only the block's first
+// pool row also computes row 2t-1) and emits pool row t from rows 2t-1..2t+1.
+// The (4*S2_SP+7)-row input patch is staged once.  224x224 at bs=32: 8 row
+// groups x 32 images = 256 blocks, one per CU; 7 waves = the 14 16-pixel conv
+// tiles of a two-row step, two per wave.
+namespace {
+constexpr int S2_SP = 7;                                   // pool rows per block
+constexpr int S2_WAVES = 7;
+constexpr int S2_NT = S2_WAVES * 64;
+constexpr int S2_PROWS = 4 * S2_SP + 7;                    // input rows of a block's patch (35)
+constexpr int S2_ITEMS = (S2_PROWS * ST_PWC + S2_NT - 1) / S2_NT;
+}  // namespace
+
+__global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __restrict__ x,
+                                                                const bf16* __restrict__ w,
+                                                                const float* __restrict__ bias,
+                                                                bf16* __restrict__ out, int H, int W, int C, int OH,
+                                                                int OW, int pad_t, int pad_l, int PH, int PW,
+                                                                int pool_pad, int groups) {
+  __shared__ __attribute__((aligned(16))) bf16 patch[S2_PROWS * ST_PWC * 4];        // 63.4 KiB
+  __shared__ __attribute__((aligned(16))) bf16 ring[ST_CROWS_POOL * ST_OWMAX * 64];  // 42 KiB
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = logical / groups;
+  const int t0 = (logical - img * groups) * S2_SP;
+  const int t1 = min(PH, t0 + S2_SP);                      // pool rows [t0, t1)
+  const int r_first = 2 * t0 - pool_pad;                   // first conv row (may be -1)
+  const int ih0 = 2 * r_first - pad_t;                     // input row of patch row 0
+  const int nrows = 4 * (t1 - t0) + 7;                     // input rows in use (2R+5 for R = 2(t1-t0)+1 conv rows)
+  const int tpr = (OW + 15) >> 4;
+  const int pwc = 2 * tpr * 16 + 8;
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 bw[7][4];
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bw[s][n] = *(const bf16x8*)(w + (size_t)(n * 16 + fr) * ST_K + s * 32 + fq * 8);
+  float b4[4][4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b4[n][r] = bias[n * 16 + 4 * fq + r];
+
+  // ---- stage the patch: fp32 NHWC -> bf16 [row][col][4]; all loads issued first
+  {
+    const float* xi = x + (size_t)img * H * W * C;
+    float pv[S2_ITEMS][4];
+#pragma unroll
+    for (int k = 0; k < S2_ITEMS; ++k) {
+      const int idx = tid + k * S2_NT;
+      const int i = idx / ST_PWC, j = idx - i * ST_PWC;
+      const int ih = ih0 + i, iw = j - pad_l;
+      const bool ok = i < nrows && j < pwc && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const float* px = xi + (ok ? ((size_t)ih * W + iw) * C : 0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pv[k][c] = (ok && c < C) ? px[c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < S2_ITEMS; ++k) {
+      const int idx = tid + k * S2_NT;
+      if (idx < S2_PROWS * ST_PWC) {
+        bf16x4s v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v.v[c] = f2bf(pv[k][c]);
+        *(bf16x4s*)(patch + idx * 4) = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  for (int t = t0; t < t1; ++t) {
+    // conv rows of this step: 2t-pp+1 .. 2t-pp+2, plus 2t-pp on the block's first step
+    const int ra = 2 * t - pool_pad + (t == t0 ? 0 : 1);
+    const int nr = 2 * t - pool_pad + 3 - ra;
+    const int ntiles = nr * tpr;
+    for (int mt = wave; mt < ntiles; mt += S2_WAVES) {
+      const int q = mt / tpr;
+      const int r = ra + q;
+      if (r < 0 || r >= OH) continue;                      // wave-uniform
+      const int c0 = (mt - q * tpr) * 16;
+      const int prow = 2 * (r - r_first);
+      f32x4 acc[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const int ow = c0 + fr;
+#pragma unroll
+      for (int s = 0; s < 7; ++s) {
+        const bf16x8 a = *(const bf16x8*)(patch + ((prow + s) * ST_PWC + 2 * ow + 2 * fq) * 4);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][n], a, acc[n], 0, 0, 0);
+      }
+      const int slot = r % ST_CROWS_POOL;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        bf16x4s v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v.v[e] = f2bf(fmaxf(acc[n][e] + b4[n][e], 0.f));
+        *(bf16x4s*)(ring + stage_off(slot, ow, 2 * n + (fq >> 1)) + 4 * (fq & 1)) = v;
+      }
+    }
+    __syncthreads();
+    // pool row t from conv rows 2t-pp .. 2t-pp+2 (post-ReLU >= 0: padding is the 0 the max starts from)
+    for (int idx = tid; idx < PW * 8; idx += S2_NT) {
+      const int ch8 = idx & 7, pw = idx >> 3;
+      float m[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = 0.f;
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const int oh = 2 * t - pool_pad + dr;
+        if ((unsigned)oh >= (unsigned)OH) continue;
+        const int slot = oh % ST_CROWS_POOL;
+#pragma unroll
+        for (int dc = 0; dc < 3; ++dc) {
+          const int ow = 2 * pw - pool_pad + dc;
+          if ((unsigned)ow >= (unsigned)OW) continue;
+          V8 v;
+          v.u = *(const u32x4*)(ring + stage_off(slot, ow, ch8));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], bf2f(v.e[e]));
+        }
+      }
+      V8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.e[e] = f2bf(m[e]);
+      *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = o.u;
+    }
+    __syncthreads();                                       // ring slots of rows 2t-pp, 2t-pp+1 are free
+  }
+}
+
 hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
                         int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
                         hipStream_t s) {
@@ -186,6 +326,13 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
   if (pool) {
     if (PH < 1 || PW < 1 || PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1)
       return hipErrorInvalidValue;
+    const char* v1 = getenv("ADAPT_STEM_V1");           // A/B switch to the v1 kernel
+    if (!(v1 && v1[0] == '1')) {
+      const int groups = (PH + S2_SP - 1) / S2_SP;
+      hipLaunchKernelGGL(stem_pool_v2_kernel, dim3(groups * B), dim3(S2_NT), 0, s, x, w, bias, out, H, W, C, OH, OW,
+                         pad_t, pad_l, PH, PW, pool_pad, groups);
+      return hipGetLastError();
+    }
     dim3 grid(PH * B);
     hipLaunchKernelGGL(stem_kernel<true>, grid, dim3(ST_NT), 0, s, x, w, bias, out, H, W, C, OH, OW, pad_t, pad_l,
                        PH, PW, pool_pad);

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(1024) void zvc_scan(const uint32_t* __restrict__ si
     offs[i] = run;
     run += sizes[i];
   }
-  if (t == 1023) *total = (uint64_t)HDR + 4ull * nseg + part[1023];
+  if (t == 1023 && total) *total = (uint64_t)HDR + 4ull * nseg + part[1023];
 }
 
 __global__ __launch_bounds__(256) void zvc_pack(const uint8_t* __restrict__ scratch, const uint32_t* __restrict__ sizes,
@@ -190,6 +190,16 @@ hipError_t zvc_gpu_decompress(const uint8_t* stream, const uint32_t* offs, int n
   else if (esz == 4) hipLaunchKernelGGL(zvc_dec<uint32_t>, dim3(nseg), dim3(256), 0, s, stream, offs, nseg, n, (uint32_t*)out);
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+// device-resident stream (e.g. received over RCCL): the segment offsets come
+// from a scan of the stream's own size table, no host round trip
+hipError_t zvc_gpu_decompress_dev(const uint8_t* stream, int nseg, size_t n, int esz, void* out, uint32_t* offs_scratch,
+                                  hipStream_t s) {
+  if (nseg < 1 || (size_t)nseg != (n + SEG - 1) / SEG || (((uintptr_t)stream) & 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(zvc_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)(stream + HDR), offs_scratch, nseg,
+                     (uint64_t*)nullptr);
+  return zvc_gpu_decompress(stream, offs_scratch, nseg, n, esz, out, s);
 }
 
 }  // namespace adapt

@@ -99,12 +99,26 @@ def test_plan_fuses_resnet(r50):
     steps = compile_plan(r50)
     kinds = [s.kind for s in steps]
     assert kinds.count("bn") == 0 and kinds.count("add") == 0
-    assert kinds.count("conv") == 52 and kinds[0] == "stem" and kinds[-2:] == ["gap", "dense"]
+    # 52 convs: the 4 projection shortcuts share a GEMM with their block's first 1x1 conv
+    assert kinds.count("conv") == 48 and kinds[0] == "stem" and kinds[-2:] == ["gap", "dense"]
+    dual = [s for s in steps if s.p.get("out2")]
+    assert [(s.out, s.p["out2"]) for s in dual] == [(f"conv{k}_block1_0_bn", f"conv{k}_block1_1_relu")
+                                                    for k in (2, 3, 4, 5)]
+    assert all(s.p["relu2"] and not s.p["relu"] for s in dual)
     st = steps[0]
     assert st.p["pads"] == ((3, 3), (3, 3)) and st.p["pool"] and st.out == "pool1_pool" and st.ins == ["input_1"]
     assert st.covers == ["conv1_pad", "conv1_conv", "conv1_bn", "conv1_relu", "pool1_pad", "pool1_pool"]
     res = [s for s in steps if s.kind == "conv" and s.p["residual"]]
     assert len(res) == 16 and all(s.out.endswith("_out") for s in res)
+
+
+def test_plan_siblings_respect_cuts(r50):
+    # a cut that exposes conv3_block1_1_conv leaves that conv unfused: no merge with the shortcut
+    s = partition(r50, ["conv3_block1_1_conv"])
+    st0 = compile_plan(subgraph(r50, s[0]))
+    assert not any(x.p.get("out2", "").startswith("conv3") for x in st0)
+    st1 = compile_plan(subgraph(r50, s[1]))
+    assert all(x.p.get("out2") is None or x.out.startswith(("conv4", "conv5")) for x in st1)
 
 
 def test_plan_stem_respects_cuts(r50, monkeypatch):
@@ -119,7 +133,7 @@ def test_plan_stem_respects_cuts(r50, monkeypatch):
     assert [x.kind for x in compile_plan(subgraph(r50, s[0]))] == ["pack", "conv"]
     monkeypatch.setenv("ADAPT_NO_STEM", "1")
     kinds = [x.kind for x in compile_plan(r50)]
-    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds.count("conv") == 53
+    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds.count("conv") == 49   # 53 convs, 4 sibling pairs merged
 
 
 def test_plan_unfused_at_cut(r50):

@@ -90,9 +90,15 @@ def test_conv_vs_torch(ops, case, cfg):
 
 
 @pytest.mark.parametrize("B,H,W,pool", [(4, 224, 224, True), (3, 224, 224, False), (2, 64, 48, True),
-                                         (2, 37, 29, True), (1, 21, 30, False)])
-def test_stem_vs_torch(ops, B, H, W, pool):
-    """Fused fp32-image -> conv1(7x7/s2)+BN+ReLU [-> 3x3/s2 max-pool] vs F.conv2d/F.max_pool2d."""
+                                         (2, 37, 29, True), (1, 21, 30, False), (3, 230, 218, True)])
+@pytest.mark.parametrize("version", ["v2", "v1"])
+def test_stem_vs_torch(ops, B, H, W, pool, version, monkeypatch):
+    """Fused fp32-image -> conv1(7x7/s2)+BN+ReLU [-> 3x3/s2 max-pool] vs F.conv2d/F.max_pool2d
+    (v2 = row-group kernel with the conv-row ring; v1 = one pool row per block)."""
+    if version == "v1":
+        monkeypatch.setenv("ADAPT_STEM_V1", "1")
+    else:
+        monkeypatch.delenv("ADAPT_STEM_V1", raising=False)
     conv, _ = ops
     dev = "cuda"
     torch.manual_seed(1)
@@ -293,3 +299,47 @@ def test_gpu_zvc_matches_host_codec(ops, n_elems, dtype):
     assert torch.equal(y.view(torch.uint8), x.view(torch.uint8))
     if n_elems > 4096:
         assert len(s) < 0.65 * x.numel() * esz            # ~half zeros removed
+
+
+@pytest.mark.parametrize("cfg", [None, 3, 4, 20, 22, 23, 28])
+@pytest.mark.parametrize("ks", [1, 2, -1])
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256, 512, 128, 2), (2, 9, 11, 64, 256, 64, 1)])
+def test_conv_dual_output_matches_two_convs(ops, cfg, ks, shape):
+    """Sibling 1x1 convs packed along N (runtime/plan.py merge_siblings): columns
+    [0, n_split) -> out (no ReLU), the rest -> out2 (ReLU), for plain, split-K and
+    stream-K launches, equal to the two convs run separately."""
+    conv, _ = ops
+    if ks < 0 and (cfg is None or cfg in conv.V1_CFGS):
+        pytest.skip("stream-K is a v2-config mode")
+    B, H, W, Cin, N0, N1, s = shape
+    dev = "cuda"
+    torch.manual_seed(4)
+    x = torch.randn(B, H, W, Cin, device=dev).to(torch.bfloat16)
+    k0 = (torch.randn(1, 1, Cin, N0) / math.sqrt(Cin)).numpy()
+    k1 = (torch.randn(1, 1, Cin, N1) / math.sqrt(Cin)).numpy()
+    b0, b1 = (torch.randn(N0) * 0.1).numpy(), (torch.randn(N1) * 0.1).numpy()
+    pads = ((0, 0), (0, 0))
+    pc0, pc1 = conv.pack_conv(k0, b0, s, pads, dev), conv.pack_conv(k1, b1, s, pads, dev)
+    pcd = conv.pack_conv(np.concatenate([k0, k1], -1), np.concatenate([b0, b1]), s, pads, dev)
+    pcd.n_split = N0
+    OH, OW = pc0.out_hw(H, W)
+    M = B * OH * OW
+    r0 = torch.empty(B, OH, OW, N0, device=dev, dtype=torch.bfloat16)
+    r1 = torch.empty(B, OH, OW, N1, device=dev, dtype=torch.bfloat16)
+    conv.conv_forward(x, pc0, r0, relu=False)
+    conv.conv_forward(x, pc1, r1, relu=True)
+    o0, o1 = torch.full_like(r0, 7.0), torch.full_like(r1, 7.0)
+    ws = ctr = None
+    if cfg is not None:
+        need = conv.workspace_elems(M, N0 + N1, pcd.Kpad, cfg, ks)
+        ws = torch.empty(max(need, 1), device=dev, dtype=torch.float32)
+        if ks < 0:
+            ctr = torch.zeros(conv.sk_plan(M, N0 + N1, pcd.Kpad, cfg, -ks)[0], device=dev, dtype=torch.int32)
+    if cfg is not None and ks > 1 and pcd.Kpad // 64 // ks < 1:
+        pytest.skip("K too short to split")
+    conv.conv_forward(x, pcd, o0, relu=False, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr, out2=o1, relu2=True)
+    torch.cuda.synchronize()
+    for got, want in ((o0, r0), (o1, r1)):
+        err = (got.float() - want.float()).abs().max().item()
+        assert err <= 2e-2 * (want.float().abs().max().item() + 1e-6) + 1e-2, err
+    assert (o1.float() >= 0).all()

@@ -47,7 +47,12 @@ def main():
     pooled = torch.empty(B, 56, 56, 64, device=dev, dtype=torch.bfloat16)
     res = {}
     if a.only in ("", "fused"):
-        res["fused stem (conv+pool)"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
+        res["fused stem v2 (conv+pool, row groups)"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
+        ref = pooled.clone()
+        os.environ["ADAPT_STEM_V1"] = "1"
+        res["fused stem v1 (conv+pool)"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
+        del os.environ["ADAPT_STEM_V1"]
+        print("v1 == v2:", bool(torch.equal(ref, pooled)))
         full = torch.empty(B, 112, 112, 64, device=dev, dtype=torch.bfloat16)
         res["fused stem (conv only)"] = graph_time(lambda: C.stem_forward(x, ps, full, pool=False))
     if a.only in ("", "unfused"):
