@@ -365,12 +365,73 @@ class DEFER:
                         break
                 if self._shutdown_event.is_set():
                     return
-                rid = self._next_req
-                self._next_req += 1
-                with self.inflight_lock:
-                    self.inflight_tasks[rid] = {"partition": 1, "data": chunk, "start_time": time.time(),
-                                                "epoch": None}
-                self._send_to_stage0(rid, chunk)
+                self._wait_and_forward(1, chunk)
+
+    def _wait_and_forward(self, partition_index: int, data: np.ndarray) -> Optional[int]:
+        """`src/dispatcher.py:176-201`: register the task in the in-flight registry
+        (retained input = the replay source of the watchdog) and forward it.  The
+        dispatcher feeds partition 1 only; later partitions are fed stage to
+        stage by the workers (TCP or RCCL), not relayed through this hub."""
+        if partition_index != 1:
+            raise ValueError("the dispatcher forwards to partition 1; stages feed each other")
+        rid = self._next_req
+        self._next_req += 1
+        with self.inflight_lock:
+            self.inflight_tasks[rid] = {"partition": partition_index, "data": data, "start_time": time.time(),
+                                        "epoch": None}
+        self._forward_data_to_worker(rid, data)
+        return rid
+
+    def _forward_data_to_worker(self, rid: int, data: np.ndarray) -> bool:
+        """`src/dispatcher.py:204-220` (one persistent framed connection per epoch
+        instead of a new TCP connection per message)."""
+        return self._send_to_stage0(rid, data)
+
+    # ------------------------------------------- reference-named helpers
+    @staticmethod
+    def _comp(arr: np.ndarray) -> bytes:
+        """`src/dispatcher.py:92-93`: zfp (reversible) then LZ4 frame, native codecs."""
+        from . import codec
+        return codec.comp(arr)
+
+    @staticmethod
+    def _decomp(byts) -> np.ndarray:
+        """`src/dispatcher.py:94-98`."""
+        from . import codec
+        return codec.decomp(byts)
+
+    def _send_weights(self, weights: Sequence[np.ndarray], sock: socket.socket,
+                      chunk_size: Optional[int] = None) -> None:
+        """`src/dispatcher.py:76-89`: u64be array count, then one framed `_comp(array)`
+        per array in Keras `get_weights()` order (read back by `Node._recv_weights`)."""
+        sock.sendall(len(weights).to_bytes(8, "big"))
+        for w in weights:
+            socket_send(self._comp(np.ascontiguousarray(w)), sock, chunk_size or self.chunk_size)
+
+    def _update_localhost(self, conn, raw_ip: str, worker_cli: dict) -> None:
+        """`src/dispatcher.py:164-173`: a peer address outside `computeNodes` maps to
+        127.0.0.1 when the deployment is all-local."""
+        final_ip = raw_ip
+        with self.worker_lock:
+            if raw_ip not in self.computeNodes and "127.0.0.1" in self.computeNodes:
+                final_ip = "127.0.0.1"
+        worker_cli[conn] = final_ip
+
+    def _result_server(self, output_stream: "queue.Queue") -> None:
+        """Gen-1 result sink (`src/dispatcher.py:109-119`) = the gen-2 server here."""
+        self._intermediate_result_server(output_stream)
+
+    def _dispatchModels(self, models: Optional[Sequence[str]], nodeIPs: Sequence[str]) -> bool:
+        """Gen-1 static placement (`src/dispatcher.py:55-73`, dead code there): restrict
+        the pipeline to the workers on `nodeIPs` (host or worker id) and configure
+        one slice per worker as a new epoch.  `models`: the cut list (layer names),
+        or None to keep the current cuts.  Needs the model of a running `run_defer`."""
+        if self._model is None:
+            raise RuntimeError("_dispatchModels needs the model of a running run_defer")
+        if models is not None:
+            self._user_cuts = list(models)
+        self.computeNodes = list(nodeIPs)
+        return self._form_pipeline()
 
     # ------------------------------------------------------ data: results
     def _intermediate_result_server(self, output_stream: "queue.Queue") -> None:

@@ -29,6 +29,8 @@ CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64
              25: (128, 64), 26: (256, 64), 27: (64, 256), 28: (128, 256), 29: (256, 128),
              # v2, sized for 2+ blocks per CU
              30: (128, 128), 31: (64, 128), 32: (128, 64), 33: (128, 128), 34: (64, 64),
+             # v2, deep rings (5-8 stages)
+             35: (64, 128), 36: (128, 64), 37: (64, 64), 38: (64, 128), 39: (64, 64),
              # v3: 3x3 halo-patch kernel (conv_halo.hip); BM = pixels of TH whole output rows
              40: (224, 64), 41: (112, 128), 42: (224, 64), 43: (64, 128), 44: (112, 64), 45: (224, 64),
              46: (224, 64), 47: (112, 128), 48: (224, 64), 49: (64, 128), 50: (224, 64), 51: (224, 64),

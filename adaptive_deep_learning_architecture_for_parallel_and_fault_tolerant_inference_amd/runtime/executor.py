@@ -336,7 +336,9 @@ class SliceExecutor:
                 self.cfg[i] = done[key]
                 continue
             x = torch.randn(self.bufs(0)[st.ins[0]].shape, device=self.device).to(torch.bfloat16)
-            out = torch.empty(M * N, dtype=torch.bfloat16, device=self.device)
+            ns = pc.n_split                       # merged sibling convs write two outputs
+            out = torch.empty(M * (ns or N), dtype=torch.bfloat16, device=self.device)
+            extra = {"out2": torch.empty(M * (N - ns), dtype=torch.bfloat16, device=self.device)} if ns else {}
             best = None
             ktiles = pc.Kpad // conv_ops.BK
             for cfg in conv_ops.CFG_TILES:
@@ -352,13 +354,14 @@ class SliceExecutor:
                         if ks < 0:
                             ctr = torch.zeros(conv_ops.sk_plan(M, N, pc.Kpad, cfg, -ks)[0], dtype=torch.int32,
                                               device=self.device)
-                        conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr)
+                        conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr, **extra)
                         torch.cuda.synchronize(self.device)
                         # time device work only: `reps` launches captured in one hipGraph
                         gg = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(gg):
                             for _ in range(reps):
-                                conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr)
+                                conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr,
+                                                      **extra)
                         gg.replay()
                         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         s.record()

@@ -431,9 +431,17 @@ __device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
   X(31, 64, 128, 2, 4, 3, true)     \
   X(32, 128, 64, 4, 2, 3, true)     \
   X(33, 128, 128, 2, 2, 2, true)    \
-  X(34, 64, 64, 2, 2, 3, true)
+  X(34, 64, 64, 2, 2, 3, true)     \
+  X(35, 64, 128, 2, 4, 6, true)    \
+  X(36, 128, 64, 4, 2, 6, true)    \
+  X(37, 64, 64, 2, 2, 8, true)     \
+  X(38, 64, 128, 2, 4, 5, true)    \
+  X(39, 64, 64, 2, 4, 8, true)
 
-int conv_glds_num_cfgs() { return 29; }
+// 35-39: deeper rings (5-8 stages) for the small-grid layers, where one block
+// per CU streams ~30 K-tiles whose ~0.2 us of MFMA work each cannot cover the
+// L2/HBM latency with 2-3 tiles in flight
+int conv_glds_num_cfgs() { return 34; }
 
 // stream-K grid: `mult` x 256 blocks (one per CU), each taking ceil(total / G)
 // consecutive (tile, K-tile) iterations
