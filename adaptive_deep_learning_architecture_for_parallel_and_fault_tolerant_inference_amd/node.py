@@ -21,7 +21,7 @@ etcd for it.  Here:
   epoch's links (sockets closed => blocked peers unblock) and starts the new
   one — this is how survivors re-form a pipeline after a failure;
 * **links**: TCP framed messages (any host, CPU or GPU; codec per link), or
-  RCCL point-to-point over xGMI between GPU stages (parallel/rccl_link.py).
+  RCCL point-to-point over xGMI between GPU stages (parallel/stage_runtime.py).
 
 CLI:  python -m <pkg>.node --dispatcher 127.0.0.1 --membership-port 2379 \
           --data-port 6000 --config-port 6001 --device cuda:0
@@ -413,6 +413,37 @@ class Node:
                 self.registration.put(**kw)
             except (OSError, ConnectionError, RuntimeError):
                 pass
+
+    # ------------------------------------------- reference-named helpers
+    @staticmethod
+    def _comp(arr: np.ndarray) -> bytes:
+        """`src/node.py:122-123`: zfp (reversible) then LZ4 frame, native codecs."""
+        from . import codec
+        return codec.comp(arr)
+
+    @staticmethod
+    def _decomp(byts) -> np.ndarray:
+        """`src/node.py:124-125`."""
+        from . import codec
+        return codec.decomp(byts)
+
+    def _recv_weights(self, sock: socket.socket, chunk_size: Optional[int] = None) -> list:
+        """`src/node.py:101-119`: u64be array count, then one framed compressed
+        array each (written by `DEFER._send_weights`); Keras `get_weights()` order."""
+        head = b""
+        while len(head) < 8:
+            part = sock.recv(8 - len(head))
+            if not part:
+                raise ConnectionError("connection closed before the weight count")
+            head += part
+        count = int.from_bytes(head, "big")
+        out = []
+        for _ in range(count):
+            frame = socket_recv(sock, chunk_size or self.state.chunk_size)
+            if not frame:
+                raise ConnectionError("connection closed inside the weight list")
+            out.append(self._decomp(frame))
+        return out
 
     # ------------------------------------------------------- config plane
     def _config_server(self) -> None:

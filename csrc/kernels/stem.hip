@@ -195,8 +195,41 @@ constexpr int S2_SP = 7;                                   // pool rows per bloc
 constexpr int S2_WAVES = 7;
 constexpr int S2_NT = S2_WAVES * 64;
 constexpr int S2_PROWS = 4 * S2_SP + 7;                    // input rows of a block's patch (35)
-constexpr int S2_ITEMS = (S2_PROWS * ST_PWC + S2_NT - 1) / S2_NT;
+constexpr int S2_ROWS0 = 11;                              // patch rows the first step needs
+constexpr int S2_ITEMS0 = (S2_ROWS0 * ST_PWC + S2_NT - 1) / S2_NT;
+constexpr int S2_ITEMS1 = (4 * ST_PWC + S2_NT - 1) / S2_NT;  // 4 new input rows per later step
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 }  // namespace
+
+// fp32 NHWC patch rows [row0, row0 + nrows) -> registers (loads only; `put_rows` converts + stores)
+template <int ITEMS>
+__device__ __forceinline__ void get_rows(float (&pv)[ITEMS][4], const float* __restrict__ xi, int tid, int row0,
+                                         int nrows, int row_end, int ih0, int H, int W, int C, int pwc, int pad_l) {
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int idx = tid + k * S2_NT;
+    const int i = row0 + idx / ST_PWC, j = idx % ST_PWC;
+    const int ih = ih0 + i, iw = j - pad_l;
+    const bool ok = idx < nrows * ST_PWC && i < row_end && j < pwc && (unsigned)ih < (unsigned)H &&
+                    (unsigned)iw < (unsigned)W;
+    const float* px = xi + (ok ? ((size_t)ih * W + iw) * C : 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pv[k][c] = (ok && c < C) ? px[c] : 0.f;
+  }
+}
+template <int ITEMS>
+__device__ __forceinline__ void put_rows(const float (&pv)[ITEMS][4], bf16* patch, int tid, int row0, int nrows) {
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int idx = tid + k * S2_NT;
+    if (idx < nrows * ST_PWC && row0 * ST_PWC + idx < S2_PROWS * ST_PWC) {
+      bf16x4s v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v.v[c] = f2bf(pv[k][c]);
+      *(bf16x4s*)(patch + (row0 * ST_PWC + idx) * 4) = v;
+    }
+  }
+}
 
 __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __restrict__ x,
                                                                 const bf16* __restrict__ w,
@@ -215,10 +248,17 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
   const int t1 = min(PH, t0 + S2_SP);                      // pool rows [t0, t1)
   const int r_first = 2 * t0 - pool_pad;                   // first conv row (may be -1)
   const int ih0 = 2 * r_first - pad_t;                     // input row of patch row 0
-  const int nrows = 4 * (t1 - t0) + 7;                     // input rows in use (2R+5 for R = 2(t1-t0)+1 conv rows)
+  const int row_end = 4 * (t1 - t0) + 7;                   // patch rows in use (2R+5 for R = 2(t1-t0)+1 conv rows)
   const int tpr = (OW + 15) >> 4;
   const int pwc = 2 * tpr * 16 + 8;
+  const float* xi = x + (size_t)img * H * W * C;
 
+  // first step's 11 input rows: loads in flight while the weight panel loads
+  {
+    float pv0[S2_ITEMS0][4];
+    get_rows<S2_ITEMS0>(pv0, xi, tid, 0, S2_ROWS0, row_end, ih0, H, W, C, pwc, pad_l);
+    put_rows<S2_ITEMS0>(pv0, patch, tid, 0, S2_ROWS0);
+  }
   const int fr = lane & 15, fq = lane >> 4;
   bf16x8 bw[7][4];
 #pragma unroll
@@ -230,35 +270,14 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
   for (int n = 0; n < 4; ++n)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b4[n][r] = bias[n * 16 + 4 * fq + r];
-
-  // ---- stage the patch: fp32 NHWC -> bf16 [row][col][4]; all loads issued first
-  {
-    const float* xi = x + (size_t)img * H * W * C;
-    float pv[S2_ITEMS][4];
-#pragma unroll
-    for (int k = 0; k < S2_ITEMS; ++k) {
-      const int idx = tid + k * S2_NT;
-      const int i = idx / ST_PWC, j = idx - i * ST_PWC;
-      const int ih = ih0 + i, iw = j - pad_l;
-      const bool ok = i < nrows && j < pwc && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      const float* px = xi + (ok ? ((size_t)ih * W + iw) * C : 0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) pv[k][c] = (ok && c < C) ? px[c] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < S2_ITEMS; ++k) {
-      const int idx = tid + k * S2_NT;
-      if (idx < S2_PROWS * ST_PWC) {
-        bf16x4s v;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v.v[c] = f2bf(pv[k][c]);
-        *(bf16x4s*)(patch + idx * 4) = v;
-      }
-    }
-  }
   __syncthreads();
 
   for (int t = t0; t < t1; ++t) {
+    // the NEXT step's 4 input rows: issued now, landed in LDS after this step's MFMAs
+    const int nrow0 = 4 * (t - t0) + S2_ROWS0;
+    float pv[S2_ITEMS1][4];
+    const bool more = t + 1 < t1;
+    if (more) get_rows<S2_ITEMS1>(pv, xi, tid, nrow0, 4, row_end, ih0, H, W, C, pwc, pad_l);
     // conv rows of this step: 2t-pp+1 .. 2t-pp+2, plus 2t-pp on the block's first step
     const int ra = 2 * t - pool_pad + (t == t0 ? 0 : 1);
     const int nr = 2 * t - pool_pad + 3 - ra;
@@ -284,17 +303,23 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
       for (int n = 0; n < 4; ++n) {
         bf16x4s v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v.v[e] = f2bf(fmaxf(acc[n][e] + b4[n][e], 0.f));
+        for (int e = 0; e < 4; ++e) {
+          const float y = acc[n][e] + b4[n][e];
+          v.v[e] = f2bf(y > 0.f ? y : 0.f);               // +0 for y <= 0: staged values are non-negative bit patterns
+        }
         *(bf16x4s*)(ring + stage_off(slot, ow, 2 * n + (fq >> 1)) + 4 * (fq & 1)) = v;
       }
     }
+    if (more) put_rows<S2_ITEMS1>(pv, patch, tid, nrow0, 4);
     __syncthreads();
-    // pool row t from conv rows 2t-pp .. 2t-pp+2 (post-ReLU >= 0: padding is the 0 the max starts from)
+    // pool row t from conv rows 2t-pp .. 2t-pp+2.  Non-negative bf16 values order
+    // like their u16 bit patterns: packed integer max, 2 values per instruction;
+    // the zero padding is the 0 the max starts from.
     for (int idx = tid; idx < PW * 8; idx += S2_NT) {
       const int ch8 = idx & 7, pw = idx >> 3;
-      float m[8];
+      u16x2 m[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m[e] = 0.f;
+      for (int e = 0; e < 4; ++e) m[e] = (u16x2){0, 0};
 #pragma unroll
       for (int dr = 0; dr < 3; ++dr) {
         const int oh = 2 * t - pool_pad + dr;
@@ -304,16 +329,15 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
         for (int dc = 0; dc < 3; ++dc) {
           const int ow = 2 * pw - pool_pad + dc;
           if ((unsigned)ow >= (unsigned)OW) continue;
-          V8 v;
-          v.u = *(const u32x4*)(ring + stage_off(slot, ow, ch8));
+          const u32x4 v = *(const u32x4*)(ring + stage_off(slot, ow, ch8));
 #pragma unroll
-          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], bf2f(v.e[e]));
+          for (int e = 0; e < 4; ++e) m[e] = __builtin_elementwise_max(m[e], __builtin_bit_cast(u16x2, v[e]));
         }
       }
-      V8 o;
+      u32x4 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o.e[e] = f2bf(m[e]);
-      *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = o.u;
+      for (int e = 0; e < 4; ++e) o[e] = __builtin_bit_cast(uint32_t, m[e]);
+      *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = o;
     }
     __syncthreads();                                       // ring slots of rows 2t-pp, 2t-pp+1 are free
   }
