@@ -199,6 +199,10 @@ constexpr int S2_ROWS0 = 11;                              // patch rows the firs
 constexpr int S2_ITEMS0 = (S2_ROWS0 * ST_PWC + S2_NT - 1) / S2_NT;
 constexpr int S2_ITEMS1 = (4 * ST_PWC + S2_NT - 1) / S2_NT;  // 4 new input rows per later step
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+union P8 {                                                 // 8 bf16 as 16 B or as 4 packed u16 pairs
+  u32x4 u;
+  u16x2 h[4];
+};
 }  // namespace
 
 // fp32 NHWC patch rows [row0, row0 + nrows) -> registers (loads only; `put_rows` converts + stores)
@@ -317,9 +321,9 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
     // the zero padding is the 0 the max starts from.
     for (int idx = tid; idx < PW * 8; idx += S2_NT) {
       const int ch8 = idx & 7, pw = idx >> 3;
-      u16x2 m[4];
+      P8 m;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) m[e] = (u16x2){0, 0};
+      for (int e = 0; e < 4; ++e) m.h[e] = (u16x2){0, 0};
 #pragma unroll
       for (int dr = 0; dr < 3; ++dr) {
         const int oh = 2 * t - pool_pad + dr;
@@ -329,15 +333,13 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
         for (int dc = 0; dc < 3; ++dc) {
           const int ow = 2 * pw - pool_pad + dc;
           if ((unsigned)ow >= (unsigned)OW) continue;
-          const u32x4 v = *(const u32x4*)(ring + stage_off(slot, ow, ch8));
+          P8 v;
+          v.u = *(const u32x4*)(ring + stage_off(slot, ow, ch8));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) m[e] = __builtin_elementwise_max(m[e], __builtin_bit_cast(u16x2, v[e]));
+          for (int e = 0; e < 4; ++e) m.h[e] = __builtin_elementwise_max(m.h[e], v.h[e]);
         }
       }
-      u32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = __builtin_bit_cast(uint32_t, m[e]);
-      *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = o;
+      *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = m.u;
     }
     __syncthreads();                                       // ring slots of rows 2t-pp, 2t-pp+1 are free
   }
