@@ -63,7 +63,7 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
     out_dir = BUILD / "kernels"
     out_dir.mkdir(parents=True, exist_ok=True)
     inc = _py_includes() + [f"-I{src_dir}"]
-    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1",
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
               "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-result"] + inc
 
     def compile_one(src: Path) -> Path:

@@ -60,3 +60,16 @@ def test_tracer_and_metrics(tmp_path):
     m.inc("n", 3)
     s = m.summary()
     assert s["lat"]["n"] == 100 and 40 < s["lat"]["p50"] < 60 and s["counters"]["n"] == 3
+
+
+def test_reference_demo_driver_runs_on_cpu():
+    """examples/test.py = the reference's distributed demo (`test/test.py`): DEFER +
+    two local CPU workers, multi-tensor cut, prints results and req/s."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "examples", "test.py"), "--devices", "cpu,cpu",
+                        "--model", "resnet_tiny", "--task-size", "3", "--part-at", "conv3_block1_1_conv"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("(1, 10)") == 3 and "3 results in" in r.stdout and "Throughput:" in r.stdout
