@@ -199,6 +199,11 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
+  // data-parallel tile with a residual: its loads go out before the K loop
+  // (older than every LDS-DMA piece, so the counted vmcnt waits stay valid)
+  EpiRes<BM, BN, NT> rpre;
+  const bool use_pre = sk.slot < 0 && p.ksplit == 1 && p.res != nullptr;
+  if (use_pre) rpre.prefetch(p, m0, n0, tid, p.M);
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s);
 
@@ -274,7 +279,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     return;
   }
   if (sk.slot < 0) {
-    fused_epilogue<BM, BN, NT, EPI_LD, OUT_F32>(p, epi, m0, n0, tid, p.M);
+    fused_epilogue<BM, BN, NT, EPI_LD, OUT_F32>(p, epi, m0, n0, tid, p.M, &rpre, use_pre);
     return;
   }
   const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);

@@ -136,6 +136,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvParams p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
+  EpiRes<BM, BN, NTHREADS> rpre;
+  const bool use_pre = p.ksplit == 1 && p.res != nullptr;
+  if (use_pre) rpre.prefetch(p, m0, n0, tid, p.M);
   if (kt0 < kt1) {
     load_tile(kt0);
     store_tile(0);
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvParams p) {
     }
     return;
   }
-  fused_epilogue<BM, BN, NTHREADS, EPI_LD, OUT_F32>(p, epi, m0, n0, tid, p.M);
+  fused_epilogue<BM, BN, NTHREADS, EPI_LD, OUT_F32>(p, epi, m0, n0, tid, p.M, &rpre, use_pre);
 }
 
 // split-K reduction + epilogue: out = act(sum_s ws[s] + bias (+res))

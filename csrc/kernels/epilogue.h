@@ -14,9 +14,29 @@
 
 namespace adapt {
 
+// Residual chunks of this thread's epilogue iterations, loaded BEFORE the main
+// loop so their HBM latency overlaps the GEMM (the small-K 1x1 "_3" convs of
+// ResNet spend a large share of each block in that epilogue round trip).
+template <int BM, int BN, int NT>
+struct EpiRes {
+  static constexpr int CPR = BN / 8, NCH = BM * CPR, RPI = NT / CPR, IT = (NCH + NT - 1) / NT;
+  V8 r[IT];
+  __device__ __forceinline__ void prefetch(const ConvParams& p, int m0, int n0, int tid, int m_end) {
+    const int cc = tid % CPR, row0 = tid / CPR;
+    const int n = n0 + cc * 8;
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int row = row0 + u * RPI, m = m0 + row;
+      r[u].u = (u32x4){0u, 0u, 0u, 0u};
+      if (p.res && n < p.N && row < BM && m < m_end) r[u].u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
+    }
+  }
+};
+
 template <int BM, int BN, int NT, int EPI_LD, bool OUT_F32>
 __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float* epi, int m0, int n0, int tid,
-                                               int m_end) {
+                                               int m_end, const EpiRes<BM, BN, NT>* rp = nullptr,
+                                               bool use_pre = false) {
   constexpr int CPR = BN / 8;                 // 8-wide chunks per row
   constexpr int NCH = BM * CPR;
   constexpr int RPI = NT / CPR;               // rows covered per iteration
@@ -43,7 +63,11 @@ __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float*
       const int row = row0 + (g + u) * RPI;
       const int m = m0 + row;
       r[u].u = (u32x4){0u, 0u, 0u, 0u};
-      if (p.res && g + u < IT && row < BM && m < m_end) r[u].u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
+      if (use_pre) {
+        if (g + u < IT) r[u] = rp->r[g + u];       // compile-time index: stays in registers
+      } else if (p.res && g + u < IT && row < BM && m < m_end) {
+        r[u].u = *(const u32x4*)(p.res + (size_t)m * p.N + n);
+      }
     }
 #pragma unroll
     for (int u = 0; u < EPI_G; ++u) {
