@@ -77,12 +77,15 @@ class DEFER:
                  batch: int = 1, codec: str = "lz4", weight_codec: str = "zfp+lz4", max_inflight: int = 8,
                  task_timeout: float = 30.0, worker_wait: float = 5.0, elastic: bool = False,
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
-                 transport: str = "tcp") -> None:
-        """transport: stage-to-stage links — "tcp" (framed, codec; any host),
+                 transport: str = "tcp", link_codec: str = "none") -> None:
+        """link_codec: compression of the collective stage-to-stage links ("none",
+        "lz4", "zvc"; codec/wire.py, on a side stream); `codec` applies to TCP hops.
+        transport: stage-to-stage links — "tcp" (framed, codec; any host),
         "rccl" (RCCL p2p over xGMI between GPU workers), "gloo" (CPU workers)."""
         if transport not in ("tcp", "rccl", "gloo"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
+        self.link_codec = link_codec
         self._store_server = None
         self._store_port = 0
         if transport != "tcp":
@@ -296,6 +299,7 @@ class DEFER:
                        "next": nxt, "result_addr": [self._result_host(rec), self.result_port],
                        "codec": self.codec, "graph": self.device_graph, "transport": self.transport}
                 if self.transport != "tcp":
+                    cfg["link_codec"] = self.link_codec
                     cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
                                          "store_host": self._result_host(rec), "store_port": self._store_port,
                                          "timeout": 30}

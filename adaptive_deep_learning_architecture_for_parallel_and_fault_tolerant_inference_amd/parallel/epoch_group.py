@@ -35,7 +35,7 @@ def make_store_server(host: str = "0.0.0.0", port: int = 0) -> dist.TCPStore:
 
 class EpochGroup:
     def __init__(self, backend: str, store_host: str, store_port: int, epoch: int, rank: int, world: int,
-                 device: Optional[torch.device] = None, timeout_s: float = 30.0):
+                 device: Optional[torch.device] = None, timeout_s: float = 30.0, ctl: bool = False):
         self.backend = backend
         self.rank, self.world, self.epoch = rank, world, epoch
         self.device = device
@@ -53,6 +53,11 @@ class EpochGroup:
             self.pg = dist.ProcessGroupGloo(self.store, rank, world, to)
         else:
             raise ValueError(f"unknown backend {backend}")
+        # host control group (compressed links: per-message byte counts travel here,
+        # so a receiver can size its data receive without a device round trip)
+        self.ctl = None
+        if ctl:
+            self.ctl = dist.ProcessGroupGloo(dist.PrefixStore("ctl/", self.store), rank, world, to)
 
     # ------------------------------------------------------------- p2p
     def isend(self, t: torch.Tensor, dst: int, tag: int = 0):
@@ -70,8 +75,13 @@ class EpochGroup:
         if self.backend == "nccl":
             work.wait()
             return
-        # gloo p2p work only progresses inside wait(): run it on a helper thread
-        # and poll, so an abort can abandon a wait on a dead peer
+        self.wait_host(work, poll_s)
+
+    def wait_host(self, work, poll_s: float = 0.0002) -> None:
+        """Abortable wait on a host (gloo) work item: gloo p2p work only progresses
+        inside wait(), so it runs on a helper thread that an abort can abandon."""
+        if work is None:
+            return
         done = threading.Event()
         err: list = []
 
@@ -98,9 +108,18 @@ class EpochGroup:
                 raise Aborted(f"epoch {self.epoch} aborted")
             time.sleep(poll_s)
 
+    def ctl_isend(self, t: torch.Tensor, dst: int, tag: int = 0):
+        return self.ctl.send([t], dst, tag)
+
+    def ctl_irecv(self, t: torch.Tensor, src: int, tag: int = 0):
+        return self.ctl.recv([t], src, tag)
+
     def abort(self) -> None:
         self.abort_flag.set()
-        try:
-            self.pg.abort()
-        except Exception:  # noqa: BLE001 - best effort; the group is discarded either way
-            pass
+        for pg in (self.pg, self.ctl):
+            if pg is None:
+                continue
+            try:
+                pg.abort()
+            except Exception:  # noqa: BLE001 - best effort; the group is discarded either way
+                pass

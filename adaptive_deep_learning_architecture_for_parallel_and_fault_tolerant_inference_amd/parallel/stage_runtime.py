@@ -41,7 +41,8 @@ class CollectiveStageRuntime:
         self.stage = int(cfg["stage"])
         self.stages = int(cfg["stages"])
         self.batch = int(cfg["batch"])
-        self.codec = cfg.get("codec", "lz4")
+        self.codec = cfg.get("codec", "lz4")                 # TCP edges (dispatcher <-> first / last stage)
+        self.link_codec = cfg.get("link_codec", "none")      # stage-to-stage collective links
         self.manifest = manifest
         self.nsets = int(cfg.get("nsets", 2))
         g = manifest.graph()
@@ -78,6 +79,18 @@ class CollectiveStageRuntime:
         self.meta_in = [torch.zeros(4, dtype=torch.int64, device=mdev) for _ in range(self.nsets)]
         self.meta_out = [torch.zeros(4, dtype=torch.int64, device=mdev) for _ in range(self.nsets)]
         self.events = [None] * self.nsets
+        self.cur_meta = [torch.zeros(4, dtype=torch.int64) for _ in range(self.nsets)]   # host copy per set
+        self.enc = self.dec = None
+        if self.link_codec != "none":
+            from ..codec.wire import WireCodec
+            self.side = torch.cuda.Stream(device=self.dev) if self.gpu else None
+            if self.next is not None:
+                self.enc = [[WireCodec(self.link_codec, t, self.side) for t in st] for st in self.out_bufs]
+            if self.prev is not None:
+                self.dec = [[WireCodec(self.link_codec, t) for t in st] for st in self.in_bufs]
+            # host meta: request id, count, epoch, 1, then the byte count of each wire buffer
+            self.hmeta_in = [torch.zeros(4 + len(self.in_bufs[0]), dtype=torch.int64) for _ in range(self.nsets)]
+            self.hmeta_out = [torch.zeros(4 + len(self.out_bufs[0]), dtype=torch.int64) for _ in range(self.nsets)]
 
     # ----------------------------------------------------------- lifecycle
     def attach_upstream(self, sock) -> None:
@@ -174,7 +187,8 @@ class CollectiveStageRuntime:
                 t = torch.nn.functional.pad(t, (0, buf.shape[-1] - t.shape[-1]))
             buf.zero_() if t.shape[0] < buf.shape[0] else None
             buf[: t.shape[0]].copy_(t)
-        self.meta_in[j].copy_(torch.tensor([m.req_id, m.count, self.epoch, 1], dtype=torch.int64))
+        self.cur_meta[j] = torch.tensor([m.req_id, m.count, self.epoch, 1], dtype=torch.int64)
+        self.meta_in[j].copy_(self.cur_meta[j])
         return True
 
     def _compute(self, j: int) -> None:
@@ -208,7 +222,8 @@ class CollectiveStageRuntime:
         cc = self.cfg["collective"]
         try:
             self.group = EpochGroup(cc["backend"], cc["store_host"], int(cc["store_port"]), self.epoch, self.stage,
-                                    self.stages, self.dev if self.gpu else None, float(cc.get("timeout", 30)))
+                                    self.stages, self.dev if self.gpu else None, float(cc.get("timeout", 30)),
+                                    ctl=self.link_codec != "none")
         except Exception as e:  # noqa: BLE001 - rendezvous failed (a member died): epoch is dead
             self._fail("rendezvous", e)
             return
@@ -216,16 +231,42 @@ class CollectiveStageRuntime:
             self.group.abort()
             return
         G = self.group
+        if self.link_codec != "none":
+            try:
+                self._codec_loop(G)
+            except Exception as e:  # noqa: BLE001
+                if not isinstance(e, Aborted):
+                    traceback.print_exc()
+                self._fail("data", e)
+            return
         recv_w: List[Optional[list]] = [None] * self.nsets
         send_w: List[Optional[list]] = [None] * self.nsets
+        # gloo between GPU stages (the rehearsal of the RCCL path on one device):
+        # device tensors are staged through pinned host mirrors, one bulk copy each
+        staged = self.gpu and G.backend != "nccl"
+        if staged:
+            def pinned(t):
+                return torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h_in = [[pinned(t) for t in [self.meta_in[j]] + self.in_bufs[j]] for j in range(self.nsets)]
+            h_out = [[pinned(t) for t in [self.meta_out[j]] + self.out_bufs[j]] for j in range(self.nsets)]
 
         def post_recv(j):
-            return [G.irecv(self.meta_in[j], self.prev, 2 * j)] + \
-                   [G.irecv(t, self.prev, 2 * j + 1) for t in self.in_bufs[j]]
+            dst = h_in[j] if staged else [self.meta_in[j]] + self.in_bufs[j]
+            return [G.irecv(t, self.prev, 2 * j + (1 if k else 0)) for k, t in enumerate(dst)]
+
+        def land(j):
+            if staged:                                   # pinned -> device (the next irecv reuses the mirror)
+                for h, d in zip(h_in[j], [self.meta_in[j]] + self.in_bufs[j]):
+                    d.copy_(h, non_blocking=False)
 
         def post_send(j):
-            return [G.isend(self.meta_out[j], self.next, 2 * j)] + \
-                   [G.isend(t, self.next, 2 * j + 1) for t in self.out_bufs[j]]
+            src = [self.meta_out[j]] + self.out_bufs[j]
+            if staged:
+                G.wait_event(self.events[j])             # abortable: the compute that filled set j is done
+                for h, d in zip(h_out[j], src):
+                    h.copy_(d)
+                src = h_out[j]
+            return [G.isend(t, self.next, 2 * j + (1 if k else 0)) for k, t in enumerate(src)]
 
         tick = 0
         try:
@@ -242,6 +283,7 @@ class CollectiveStageRuntime:
                     for w in recv_w[j]:
                         G.wait(w)
                     recv_w[j] = None
+                    land(j)
                 for w in send_w[j] or []:
                     G.wait(w)
                 send_w[j] = None
@@ -264,3 +306,113 @@ class CollectiveStageRuntime:
             if not isinstance(e, Aborted):
                 traceback.print_exc()
             self._fail("data", e)
+
+    # ------------------------------------------------ compressed links
+    def _codec_loop(self, G: EpochGroup) -> None:
+        """Data loop of a compressed collective link (DEFER ``link_codec``; the
+        reference compresses every hop, `src/node.py:178`).  Per frontier tensor a
+        `codec.wire.WireCodec` turns the stage output into one wire buffer; the
+        request meta and the byte counts travel on the epoch's host control
+        group, the wire buffers on the data group (RCCL over xGMI, or gloo).
+        Encodes run on a side stream and a sender thread posts them, so the
+        compute of the next micro-batch is queued while this one's encode and
+        send are in flight."""
+        staged = self.gpu and G.backend != "nccl"           # gloo between GPU stages: host-staged wire
+        if staged:
+            h_out = [[torch.empty(e.wire.numel(), dtype=torch.uint8, pin_memory=True) for e in st]
+                     for st in (self.enc or [])]
+            h_in = [[torch.empty(d.wire.numel(), dtype=torch.uint8, pin_memory=True) for d in st]
+                    for st in (self.dec or [])]
+        released = [threading.Event() for _ in range(self.nsets)]
+        for e in released:
+            e.set()
+        sendq: "queue.Queue" = queue.Queue()
+
+        def sender():
+            try:
+                while not self.stop.is_set():
+                    try:
+                        j = sendq.get(timeout=0.05)
+                    except queue.Empty:
+                        continue
+                    hm = self.hmeta_out[j]
+                    sizes = [e.nbytes() for e in self.enc[j]]     # waits for set j's encode only
+                    for k, nb in enumerate(sizes):
+                        hm[4 + k] = nb
+                    wm = G.ctl_isend(hm, self.next, 2 * j)
+                    works = []
+                    for k, (e, nb) in enumerate(zip(self.enc[j], sizes)):
+                        if staged:
+                            h_out[j][k][:nb].copy_(e.wire[:nb])
+                            works.append(G.isend(h_out[j][k][:nb], self.next, 2 * j + 1))
+                        elif self.gpu:
+                            with torch.cuda.stream(self.side):  # RCCL orders the send after the encode
+                                works.append(G.isend(e.wire[:nb], self.next, 2 * j + 1))
+                        else:
+                            works.append(G.isend(e.wire[:nb], self.next, 2 * j + 1))
+                    G.wait_host(wm)
+                    for w in works:
+                        if self.gpu and not staged:
+                            with torch.cuda.stream(self.side):  # the next encode into this wire waits for it
+                                w.wait()
+                        else:
+                            G.wait_host(w)
+                    released[j].set()
+            except Exception as e:  # noqa: BLE001
+                if not isinstance(e, Aborted):
+                    traceback.print_exc()
+                self._fail("send", e)
+
+        if self.next is not None:
+            t = threading.Thread(target=sender, daemon=True, name=f"cstage{self.stage}-send-e{self.epoch}")
+            t.start()
+            self.threads.append(t)
+        meta_w: List[Optional[object]] = [None] * self.nsets
+        if self.prev is not None:
+            for j in range(self.nsets):
+                meta_w[j] = G.ctl_irecv(self.hmeta_in[j], self.prev, 2 * j)
+        tick = 0
+        while not self.stop.is_set():
+            j = tick % self.nsets
+            if self.prev is None:
+                self._next_request(j)
+            else:
+                G.wait_host(meta_w[j])
+                hm = self.hmeta_in[j]
+                sizes = [int(v) for v in hm[4:].tolist()]
+                works = []
+                for k, (d, nb) in enumerate(zip(self.dec[j], sizes)):
+                    if staged:
+                        G.wait_host(G.irecv(h_in[j][k][:nb], self.prev, 2 * j + 1))
+                        d.wire[:nb].copy_(h_in[j][k][:nb])
+                    else:
+                        works.append(G.irecv(d.wire[:nb], self.prev, 2 * j + 1))
+                for w in works:
+                    G.wait(w)
+                for d, nb, buf in zip(self.dec[j], sizes, self.in_bufs[j]):
+                    d.decode(nb, buf)
+                self.cur_meta[j] = hm[:4].clone()             # before the next meta may land in hm
+                self.meta_in[j].copy_(self.cur_meta[j])
+                meta_w[j] = G.ctl_irecv(self.hmeta_in[j], self.prev, 2 * j)
+            while not released[j].wait(0.05):                 # set j's previous send has left
+                if self.stop.is_set():
+                    raise Aborted("stopped")
+            if self.gpu and self.enc is not None and self.enc[j]:
+                torch.cuda.current_stream(self.dev).wait_event(self.enc[j][-1].done)
+            self._compute(j)
+            if self.gpu:
+                ev = torch.cuda.Event()
+                ev.record()
+                self.events[j] = ev
+            if self.next is not None:
+                self.hmeta_out[j][:4].copy_(self.cur_meta[j])
+                for e, tns in zip(self.enc[j], self.out_bufs[j]):
+                    e.encode(tns, after=self.events[j])
+                released[j].clear()
+                sendq.put(j)
+            else:
+                if self.gpu:
+                    G.wait_event(self.events[j])
+                self._emit_result(j)
+            self.processed += 1
+            tick += 1

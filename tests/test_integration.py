@@ -164,3 +164,31 @@ def test_elastic_join_scales_up(tiny):
             except ProcessLookupError:
                 pass
             p.wait(timeout=10)
+
+
+@pytest.mark.parametrize("link_codec", ["lz4", "zvc"])
+def test_defer_collective_links_compressed(tiny, link_codec):
+    """DEFER over collective stage links (gloo here; RCCL on GPUs) with the
+    frontier compressed per hop (`link_codec`: meta + byte counts on the epoch's
+    host control group, one wire buffer per tensor): lossless, in order."""
+    d = DEFER(membership_port=0, result_port=0, worker_wait=10, ordered=True, batch=2, weight_codec="lz4",
+              transport="gloo", link_codec=link_codec, min_workers=3)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu", node_id=f"c{i}",
+                  heartbeat_ttl=0.5) for i in range(3)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq, _ = _start(d, tiny, ["conv3_block1_1_conv", "conv4_block1_out"])   # multi-tensor frontier + relay
+        rng = np.random.default_rng(1)
+        xs = [np.maximum(rng.standard_normal((2, 32, 32, 3)), 0).astype(np.float32) for _ in range(5)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=60) for _ in range(5)])
+        want = tiny.predict(np.concatenate(xs), device="cpu")
+        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+        assert len(d.pipeline.workers) == 3
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
