@@ -69,3 +69,32 @@ def test_defer_two_gpu_stages_side_stream_codec(codec):
         d.shutdown(stop_workers=True)
         for n in nodes:
             n.stop()
+
+
+@pytest.mark.parametrize("link_codec", ["none", "lz4", "zvc"])
+def test_defer_two_gpu_stages_collective_links(link_codec):
+    """Two GPU stages over the collective data plane (gloo rehearsal of the RCCL
+    path: both Nodes share the box's one GPU), uncompressed and with the GPU wire
+    codecs on the stage-to-stage link (DEFER `link_codec`)."""
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
+              min_workers=2, transport="gloo", link_codec=link_codec)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"k{i}",
+                  heartbeat_ttl=1.0) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["conv3_block1_1_conv"], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(2)
+        xs = [rng.standard_normal((4, 224, 224, 3)).astype(np.float32) for _ in range(4)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=120) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert np.abs(got - want).sum(-1).max() < 0.1
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
