@@ -131,6 +131,12 @@ class CollectiveStageRuntime:
                     s.close()
                 except OSError:
                     pass
+        # bounded join: the loops poll `stop` every <=0.1 s, so a stopped runtime
+        # has no thread left inside a device call when the process tears down
+        me = threading.current_thread()
+        for t in self.threads:
+            if t is not me:
+                t.join(timeout=2.0)
 
     # ------------------------------------------------------- TCP edges
     def _tcp_recv_loop(self) -> None:
