@@ -81,7 +81,8 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
   constexpr int LPW = A_INS + B_INS;
   constexpr int TILE_A = BM * 128, STAGE_BYTES = S::STAGE_BYTES;
   constexpr int EPI_LD = BN + 4;
-  static_assert((NW == 4 || NW == 8) && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "waves / tile split");
+  static_assert((NW == 4 || NW == 8 || NW == 16) && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN,
+                "waves / tile split");
   static_assert(STAGES >= 2 && S::LDS_BYTES + 16 <= 160 * 1024, "stages");
   static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
 
@@ -441,8 +442,19 @@ __device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
   X(36, 128, 64, 4, 2, 6, true)    \
   X(37, 64, 64, 2, 2, 8, true)     \
   X(38, 64, 128, 2, 4, 5, true)    \
-  X(39, 64, 64, 2, 4, 8, true)
+  X(39, 64, 64, 2, 4, 8, true)     \
+  X(53, 128, 128, 4, 4, 4, true)   \
+  X(54, 128, 128, 4, 4, 3, true)   \
+  X(55, 256, 128, 8, 2, 3, true)   \
+  X(56, 128, 256, 2, 8, 3, true)   \
+  X(57, 256, 128, 4, 4, 3, true)   \
+  X(58, 128, 128, 4, 4, 2, true)
 
+// 53-58: 16 waves (4 per SIMD) per block: twice the LDS-DMA pieces in flight per
+// CU at the same tile size.  Measured (profiles/conv_bench_v7_16w.txt): within
+// 1-2 % of the 8-wave tiles on every ResNet-50 shape (ahead only on the stage-3
+// 1x1 512->128), so per-CU issue depth is not what bounds these layers; kept as
+// autotuner candidates.
 // 35-39: deeper rings (5-8 stages) for the small-grid layers, where one block
 // per CU streams ~30 K-tiles whose ~0.2 us of MFMA work each cannot cover the
 // L2/HBM latency with 2-3 tiles in flight

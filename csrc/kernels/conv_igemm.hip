@@ -292,7 +292,7 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
     ADAPT_CONV_CFGS(X)
 #undef X
     default:
-      if (cfg >= 40) return conv_halo_launch(p, cfg, s, out_f32);   // v3: 3x3 halo-patch kernel
+      if (cfg >= 40 && cfg < 53) return conv_halo_launch(p, cfg, s, out_f32);   // v3: 3x3 halo-patch kernel
       // v2 (LDS-DMA ring) configs walk K tap-major in 64-channel slices
       if (p.Cin % 64) return hipErrorInvalidValue;
       e = conv_glds_launch(p, cfg, s, pure, out_f32);
