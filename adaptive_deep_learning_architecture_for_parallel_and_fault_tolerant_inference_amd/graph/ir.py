@@ -21,15 +21,31 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 OPS = (
     "input",      # graph input, attrs: shape
     "zeropad",    # attrs: pad=((t,b),(l,r))
-    "conv",       # attrs: filters, kernel=(kh,kw), stride, padding('valid'|'same'), use_bias
+    "conv",       # attrs: filters, kernel=(kh,kw), stride, padding('valid'|'same'), use_bias, activation
+    "dwconv",     # DepthwiseConv2D, multiplier 1: kernel, stride, padding, use_bias, activation
     "bn",         # attrs: epsilon
-    "relu",
+    "relu",       # attrs: max_value (None | 6.0: Keras ReLU(6.))
     "add",
+    "concat",     # channel concat (Keras Concatenate(axis=-1))
     "maxpool",    # attrs: pool, stride, padding
+    "avgpool",    # attrs: pool, stride, padding (padding excluded from the mean)
     "gap",        # global average pool
-    "dense",      # attrs: units, activation(None|'softmax'), use_bias
+    "flatten",    # NHWC -> (H*W*C,) in Keras channels_last order
+    "identity",   # Dropout / Activation('linear') at inference
+    "dense",      # attrs: units, activation(None|'relu'|'softmax'), use_bias
     "softmax",
 )
+
+
+def same_pads(size: int, k: int, s: int) -> Tuple[int, int]:
+    """TF/Keras 'same' padding of one spatial dim: (before, after), the odd pixel after."""
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    return total // 2, total - total // 2
+
+
+def _pair(v) -> Tuple[int, int]:
+    return (v, v) if isinstance(v, int) else (int(v[0]), int(v[1]))
 
 
 @dataclass
@@ -57,6 +73,13 @@ class Layer:
         if self.op == "bn":
             c = in_shapes[0][-1]
             return [(f"{self.name}/{n}", (c,)) for n in ("gamma", "beta", "moving_mean", "moving_variance")]
+        if self.op == "dwconv":
+            kh, kw = self.attrs["kernel"]
+            cin = in_shapes[0][-1]
+            out = [(f"{self.name}/depthwise_kernel", (kh, kw, cin, 1))]
+            if self.attrs.get("use_bias", True):
+                out.append((f"{self.name}/bias", (cin,)))
+            return out
         if self.op == "dense":
             cin = in_shapes[0][-1]
             out = [(f"{self.name}/kernel", (cin, self.attrs["units"]))]
@@ -71,6 +94,10 @@ class Layer:
             kh, kw = self.attrs["kernel"]
             oh, ow, co = self.out_shape
             return oh * ow * co * kh * kw * in_shapes[0][-1]
+        if self.op == "dwconv":
+            kh, kw = self.attrs["kernel"]
+            oh, ow, co = self.out_shape
+            return oh * ow * co * kh * kw
         if self.op == "dense":
             return in_shapes[0][-1] * self.attrs["units"]
         return 0
@@ -82,7 +109,7 @@ class Layer:
     @staticmethod
     def from_json(d: Dict) -> "Layer":
         attrs = dict(d.get("attrs", {}))
-        for k in ("kernel", "pad"):
+        for k in ("kernel", "pad", "pool"):
             if k in attrs and isinstance(attrs[k], list):
                 attrs[k] = _tuplify(attrs[k])
         return Layer(d["name"], d["op"], list(d["inputs"]), attrs, tuple(d.get("out_shape", ())))
@@ -137,25 +164,35 @@ class Graph:
             (t, b), (l, r) = a["pad"]
             h, w, c = ins[0]
             return (h + t + b, w + l + r, c)
-        if layer.op == "conv":
-            h, w, _ = ins[0]
+        if layer.op in ("conv", "dwconv"):
+            h, w, c = ins[0]
             kh, kw = a["kernel"]
             s = a.get("stride", 1)
+            co = a["filters"] if layer.op == "conv" else c
             if a.get("padding", "valid") == "same":
-                return (-(-h // s), -(-w // s), a["filters"])
-            return ((h - kh) // s + 1, (w - kw) // s + 1, a["filters"])
-        if layer.op in ("bn", "relu", "softmax"):
+                return (-(-h // s), -(-w // s), co)
+            return ((h - kh) // s + 1, (w - kw) // s + 1, co)
+        if layer.op in ("bn", "relu", "softmax", "identity"):
             return ins[0]
+        if layer.op == "flatten":
+            n = 1
+            for d in ins[0]:
+                n *= d
+            return (n,)
+        if layer.op == "concat":
+            if len(ins) < 2 or any(len(s) != 3 or s[:2] != ins[0][:2] for s in ins):
+                raise ValueError(f"concat {layer.name}: inputs {ins} do not share H x W")
+            return ins[0][:2] + (sum(s[2] for s in ins),)
         if layer.op == "add":
             if any(s != ins[0] for s in ins):
                 raise ValueError(f"add {layer.name}: mismatched shapes {ins}")
             return ins[0]
-        if layer.op == "maxpool":
+        if layer.op in ("maxpool", "avgpool"):
             h, w, c = ins[0]
-            p, s = a["pool"], a["stride"]
+            (ph, pw), s = _pair(a["pool"]), a["stride"]
             if a.get("padding", "valid") == "same":
                 return (-(-h // s), -(-w // s), c)
-            return ((h - p) // s + 1, (w - p) // s + 1, c)
+            return ((h - ph) // s + 1, (w - pw) // s + 1, c)
         if layer.op == "gap":
             return (ins[0][-1],)
         if layer.op == "dense":

@@ -84,10 +84,30 @@ def articulation_points(g: Graph) -> List[str]:
 
 
 def default_candidates(g: Graph) -> List[str]:
-    """Articulation points at fusion-group ends (post-activation tensors): cutting
-    there never splits a conv+BN+add+ReLU epilogue across stages."""
-    return [n for n in articulation_points(g)
-            if g.layers[n].op in ("relu", "maxpool") and (n.endswith("_out") or n.endswith("_pool"))]
+    """Articulation points at fusion-group ends: cutting there never splits a
+    conv+BN+add+ReLU (or dwconv+BN+ReLU6) epilogue across stages.  ResNet:
+    ``pool1_pool`` and the ``*_out`` block outputs; MobileNetV2: the block
+    outputs (``*_add`` or ``*_project_BN``); DenseNet: the ``*_concat`` /
+    ``pool*_pool`` tensors; VGG: the conv outputs and pools.  A tensor whose
+    only consumer is a ZeroPadding2D is skipped (the pad folds into the next op)."""
+    cons = g.consumers()
+
+    def group_end(n: str) -> bool:
+        L = g.layers[n]
+        c = cons.get(n, [])
+        nxt = g.layers[c[0]].op if len(c) == 1 else None
+        if nxt == "zeropad":
+            return False
+        if L.op in ("relu", "maxpool", "avgpool", "concat"):
+            return True
+        if L.op == "add":
+            return nxt != "relu"
+        if L.op == "bn":
+            return nxt not in ("relu", "add")
+        if L.op in ("conv", "dwconv"):
+            return L.attrs.get("activation") == "relu"
+        return False
+    return [n for n in articulation_points(g) if group_end(n)]
 
 
 def plan_cuts(g: Graph, stages: int, batch: int = 32, hw: Optional[HwModel] = None,

@@ -45,6 +45,27 @@ class Model:
     def to_json(self) -> str:
         return self.graph.to_json()
 
+    def to_keras_json(self) -> str:
+        """Keras functional-model JSON (what the reference's `model.to_json()` ships)."""
+        from ..graph.keras_json import to_keras_json
+        return to_keras_json(self.graph)
+
+    @staticmethod
+    def from_keras_json(s, weights=None, seed: int = 0) -> "Model":
+        """`tf.keras.models.model_from_json` analogue (`src/node.py:40,77`): a Keras
+        JSON architecture plus, optionally, its `get_weights()` list (or a
+        name -> array dict); random-init (seeded) when no weights are given."""
+        from ..graph.keras_json import from_keras_json
+        from .resnet import init_weights, set_weights
+        g = from_keras_json(s)
+        if weights is None:
+            w = init_weights(g, seed)
+        elif isinstance(weights, dict):
+            w = dict(weights)
+        else:
+            w = set_weights(g, list(weights))
+        return Model(g, w)
+
     def summary(self, print_fn=print) -> str:
         s = self.graph.summary()
         if print_fn:
@@ -89,7 +110,14 @@ class Model:
 
 
 def resnet(depth: str = "resnet50", seed: int = 0, weights: Optional[Dict[str, np.ndarray]] = None, **kw) -> Model:
-    """`ResNet50(weights=...)` analogue: random-init (seeded) or given weights."""
-    from .resnet import build_resnet, init_weights
-    g = build_resnet(depth, **kw)
+    """`ResNet50(weights=...)` analogue: random-init (seeded) or given weights.
+    Any family of `models/zoo.py` is accepted by name too (vgg16, mobilenet_v2, densenet121, ...)."""
+    from .resnet import init_weights
+    from .zoo import build_model
+    g = build_model(depth, **kw)
     return Model(g, weights if weights is not None else init_weights(g, seed))
+
+
+def application(name: str, seed: int = 0, weights: Optional[Dict[str, np.ndarray]] = None, **kw) -> Model:
+    """`tf.keras.applications.<Name>(...)` analogue for every family we build."""
+    return resnet(name, seed=seed, weights=weights, **kw)

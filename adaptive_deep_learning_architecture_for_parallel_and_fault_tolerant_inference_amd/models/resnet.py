@@ -118,9 +118,16 @@ def init_weights(g: Graph, seed: int = 0, layers: Optional[List[str]] = None) ->
             out[specs[0][0]] = (rng.standard_normal((kh, kw, cin, cout)) * std).astype(np.float32)
             if len(specs) > 1:
                 out[specs[1][0]] = (rng.standard_normal(cout) * 0.01).astype(np.float32)
+        elif L.op == "dwconv":
+            kh, kw, cin, mult = specs[0][1]
+            std = np.sqrt(2.0 / (kh * kw))
+            out[specs[0][0]] = (rng.standard_normal((kh, kw, cin, mult)) * std).astype(np.float32)
+            if len(specs) > 1:
+                out[specs[1][0]] = (rng.standard_normal(cin * mult) * 0.01).astype(np.float32)
         elif L.op == "bn":
             c = specs[0][1][0]
-            damp = 0.2 if n.endswith("_3_bn") else 1.0
+            # last BN of a residual branch (ResNet `_3_bn`, MobileNetV2 `project_BN`) damped
+            damp = 0.2 if n.endswith("_3_bn") or n.endswith("project_BN") else 1.0
             out[specs[0][0]] = (damp * rng.uniform(0.8, 1.2, c)).astype(np.float32)
             out[specs[1][0]] = (rng.standard_normal(c) * 0.05).astype(np.float32)
             out[specs[2][0]] = (rng.standard_normal(c) * 0.05).astype(np.float32)

@@ -1,0 +1,166 @@
+"""Other `tf.keras.applications` families, rebuilt in our IR with Keras layer
+names, creation order and `get_weights()` order.
+
+The reference's dispatcher is model-agnostic: `DEFER.run_defer(model, ...)`
+takes any Keras functional model and `dag_util.construct_model` cuts it at
+named layers (`src/dispatcher.py:39-53`, `src/dag_util.py:50-62`); its demo
+happens to use ResNet50 (`test/test.py:13`).  These builders give that
+generality a concrete footing beyond ResNet (and `graph/keras_import.py`
+takes an arbitrary Keras JSON):
+
+* VGG16 / VGG19  (plain conv stacks, Conv2D(activation='relu'), Flatten, Dense relu)
+* MobileNetV2    (ReLU6, DepthwiseConv2D, 'same' padding at stride 2, inverted residuals)
+* DenseNet121/169/201 (pre-activation BN-ReLU, Concatenate, AveragePooling2D)
+
+Parameter totals (Keras, include_top, 1000 classes; checked by tests):
+VGG16 138,357,544; VGG19 143,667,240; MobileNetV2 3,538,984; DenseNet121 8,062,504.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict
+
+from ..graph.ir import Graph, Layer
+
+
+def _conv(g: Graph, x: str, name: str, filters: int, k: int, stride: int = 1, padding: str = "valid",
+          use_bias: bool = True, activation=None) -> str:
+    a = {"filters": filters, "kernel": (k, k), "stride": stride, "padding": padding, "use_bias": use_bias}
+    if activation:
+        a["activation"] = activation
+    return g.add(Layer(name, "conv", [x], a))
+
+
+# ------------------------------------------------------------------- VGG
+VGG_BLOCKS = {"vgg16": (2, 2, 3, 3, 3), "vgg19": (2, 2, 4, 4, 4)}
+
+
+def build_vgg(name: str = "vgg16", classes: int = 1000, input_shape=(224, 224, 3)) -> Graph:
+    """`keras.applications.vgg16/vgg19` with include_top=True."""
+    g = Graph(name)
+    x = g.add(Layer("input_1", "input", [], {"shape": tuple(input_shape)}))
+    for b, (n, f) in enumerate(zip(VGG_BLOCKS[name], (64, 128, 256, 512, 512)), start=1):
+        for i in range(1, n + 1):
+            x = _conv(g, x, f"block{b}_conv{i}", f, 3, padding="same", activation="relu")
+        x = g.add(Layer(f"block{b}_pool", "maxpool", [x], {"pool": 2, "stride": 2, "padding": "valid"}))
+    x = g.add(Layer("flatten", "flatten", [x]))
+    x = g.add(Layer("fc1", "dense", [x], {"units": 4096, "activation": "relu", "use_bias": True}))
+    x = g.add(Layer("fc2", "dense", [x], {"units": 4096, "activation": "relu", "use_bias": True}))
+    g.add(Layer("predictions", "dense", [x], {"units": classes, "activation": "softmax", "use_bias": True}))
+    g.output_names = ["predictions"]
+    return g
+
+
+# ------------------------------------------------------------- MobileNetV2
+MBV2_EPS = 1e-3
+# (filters, stride, expansion) per inverted-residual block, block_id = index
+MBV2_BLOCKS = [(16, 1, 1), (24, 2, 6), (24, 1, 6), (32, 2, 6), (32, 1, 6), (32, 1, 6), (64, 2, 6), (64, 1, 6),
+               (64, 1, 6), (64, 1, 6), (96, 1, 6), (96, 1, 6), (96, 1, 6), (160, 2, 6), (160, 1, 6), (160, 1, 6),
+               (320, 1, 6)]
+
+
+def _make_divisible(v: float, divisor: int = 8) -> int:
+    new_v = max(divisor, int(v + divisor / 2) // divisor * divisor)
+    return new_v + divisor if new_v < 0.9 * v else new_v
+
+
+def build_mobilenet_v2(name: str = "mobilenetv2_1.00_224", classes: int = 1000, input_shape=(224, 224, 3),
+                       alpha: float = 1.0) -> Graph:
+    """`keras.applications.MobileNetV2(alpha=1.0, include_top=True)`."""
+    g = Graph(name)
+    x = g.add(Layer("input_1", "input", [], {"shape": tuple(input_shape)}))
+    x = _conv(g, x, "Conv1", _make_divisible(32 * alpha), 3, stride=2, padding="same", use_bias=False)
+    x = g.add(Layer("bn_Conv1", "bn", [x], {"epsilon": MBV2_EPS}))
+    x = g.add(Layer("Conv1_relu", "relu", [x], {"max_value": 6.0}))
+    for block_id, (filters, stride, expansion) in enumerate(MBV2_BLOCKS):
+        inp = x
+        cin = g.layers[x].out_shape[-1]
+        out_c = _make_divisible(int(filters * alpha), 8)
+        if block_id:
+            prefix = f"block_{block_id}_"
+            x = _conv(g, x, prefix + "expand", expansion * cin, 1, padding="same", use_bias=False)
+            x = g.add(Layer(prefix + "expand_BN", "bn", [x], {"epsilon": MBV2_EPS}))
+            x = g.add(Layer(prefix + "expand_relu", "relu", [x], {"max_value": 6.0}))
+        else:
+            prefix = "expanded_conv_"
+        if stride == 2:
+            h = g.layers[x].out_shape[0]
+            adj = 1 - h % 2                    # imagenet_utils.correct_pad(x, 3)
+            x = g.add(Layer(prefix + "pad", "zeropad", [x], {"pad": ((1 - adj, 1), (1 - adj, 1))}))
+        x = g.add(Layer(prefix + "depthwise", "dwconv", [x],
+                        {"kernel": (3, 3), "stride": stride, "padding": "same" if stride == 1 else "valid",
+                         "use_bias": False}))
+        x = g.add(Layer(prefix + "depthwise_BN", "bn", [x], {"epsilon": MBV2_EPS}))
+        x = g.add(Layer(prefix + "depthwise_relu", "relu", [x], {"max_value": 6.0}))
+        x = _conv(g, x, prefix + "project", out_c, 1, padding="same", use_bias=False)
+        x = g.add(Layer(prefix + "project_BN", "bn", [x], {"epsilon": MBV2_EPS}))
+        if cin == out_c and stride == 1:
+            x = g.add(Layer(prefix + "add", "add", [inp, x]))
+    last = _make_divisible(1280 * alpha, 8) if alpha > 1.0 else 1280
+    x = _conv(g, x, "Conv_1", last, 1, use_bias=False)
+    x = g.add(Layer("Conv_1_bn", "bn", [x], {"epsilon": MBV2_EPS}))
+    x = g.add(Layer("out_relu", "relu", [x], {"max_value": 6.0}))
+    x = g.add(Layer("global_average_pooling2d", "gap", [x]))
+    g.add(Layer("predictions", "dense", [x], {"units": classes, "activation": "softmax", "use_bias": True}))
+    g.output_names = ["predictions"]
+    return g
+
+
+# ---------------------------------------------------------------- DenseNet
+DENSENET_BLOCKS = {"densenet121": (6, 12, 24, 16), "densenet169": (6, 12, 32, 32), "densenet201": (6, 12, 48, 32)}
+DN_EPS = 1.001e-5
+
+
+def build_densenet(name: str = "densenet121", classes: int = 1000, input_shape=(224, 224, 3)) -> Graph:
+    """`keras.applications.DenseNet121/169/201(include_top=True)`."""
+    g = Graph(name)
+    x = g.add(Layer("input_1", "input", [], {"shape": tuple(input_shape)}))
+    x = g.add(Layer("zero_padding2d", "zeropad", [x], {"pad": ((3, 3), (3, 3))}))
+    x = _conv(g, x, "conv1/conv", 64, 7, stride=2, use_bias=False)
+    x = g.add(Layer("conv1/bn", "bn", [x], {"epsilon": DN_EPS}))
+    x = g.add(Layer("conv1/relu", "relu", [x]))
+    x = g.add(Layer("zero_padding2d_1", "zeropad", [x], {"pad": ((1, 1), (1, 1))}))
+    x = g.add(Layer("pool1", "maxpool", [x], {"pool": 3, "stride": 2, "padding": "valid"}))
+    blocks = DENSENET_BLOCKS[name]
+    for s, n in enumerate(blocks, start=2):
+        for i in range(1, n + 1):
+            p = f"conv{s}_block{i}"
+            y = g.add(Layer(p + "_0_bn", "bn", [x], {"epsilon": DN_EPS}))
+            y = g.add(Layer(p + "_0_relu", "relu", [y]))
+            y = _conv(g, y, p + "_1_conv", 128, 1, use_bias=False)
+            y = g.add(Layer(p + "_1_bn", "bn", [y], {"epsilon": DN_EPS}))
+            y = g.add(Layer(p + "_1_relu", "relu", [y]))
+            y = _conv(g, y, p + "_2_conv", 32, 3, padding="same", use_bias=False)
+            x = g.add(Layer(p + "_concat", "concat", [x, y]))
+        if s < 2 + len(blocks) - 1:
+            p = f"pool{s}"
+            c = g.layers[x].out_shape[-1]
+            y = g.add(Layer(p + "_bn", "bn", [x], {"epsilon": DN_EPS}))
+            y = g.add(Layer(p + "_relu", "relu", [y]))
+            y = _conv(g, y, p + "_conv", int(c * 0.5), 1, use_bias=False)
+            x = g.add(Layer(p + "_pool", "avgpool", [y], {"pool": 2, "stride": 2, "padding": "valid"}))
+    x = g.add(Layer("bn", "bn", [x], {"epsilon": DN_EPS}))
+    x = g.add(Layer("relu", "relu", [x]))
+    x = g.add(Layer("avg_pool", "gap", [x]))
+    g.add(Layer("predictions", "dense", [x], {"units": classes, "activation": "softmax", "use_bias": True}))
+    g.output_names = ["predictions"]
+    return g
+
+
+BUILDERS: Dict[str, Callable[..., Graph]] = {
+    "vgg16": lambda **kw: build_vgg("vgg16", **kw),
+    "vgg19": lambda **kw: build_vgg("vgg19", **kw),
+    "mobilenet_v2": lambda **kw: build_mobilenet_v2(**kw),
+    "densenet121": lambda **kw: build_densenet("densenet121", **kw),
+    "densenet169": lambda **kw: build_densenet("densenet169", **kw),
+    "densenet201": lambda **kw: build_densenet("densenet201", **kw),
+}
+
+
+def build_model(name: str, **kw) -> Graph:
+    """Any supported family by name: resnet50/101/152 (+ test sizes) or a key of BUILDERS."""
+    from .resnet import STACKS, build_resnet
+    if name in STACKS:
+        return build_resnet(name, **kw)
+    if name not in BUILDERS:
+        raise KeyError(f"unknown model {name!r}; known: {sorted(STACKS) + sorted(BUILDERS)}")
+    return BUILDERS[name](**kw)

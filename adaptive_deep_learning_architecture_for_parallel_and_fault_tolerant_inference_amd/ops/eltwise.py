@@ -41,7 +41,7 @@ def bn_act(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, out: torch
     C = x.shape[-1]
     if C % 8 or scale.numel() != C or shift.numel() != C or out.numel() != x.numel():
         raise ValueError("bn_act: bad shapes")
-    kernels().bn_act(ptr(x), ptr(out), ptr(scale), ptr(shift), x.numel(), C, int(relu), stream_handle(stream))
+    kernels().bn_act(ptr(x), ptr(out), ptr(scale), ptr(shift), x.numel(), C, int(relu), stream_handle(stream))   # 2 = ReLU6
     return out
 
 
@@ -53,11 +53,62 @@ def add_act(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, relu: bool = Fa
     return out
 
 
-def relu(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+def relu(x: torch.Tensor, out: torch.Tensor, mode: int = 1, stream=None) -> torch.Tensor:
+    """mode 1: ReLU; mode 2: ReLU6 (Keras ``ReLU(max_value=6)``)."""
     _chk(x, name="x"); _chk(out, name="out")
-    if x.numel() != out.numel() or x.numel() % 8:
-        raise ValueError("relu: bad shapes")
-    kernels().relu(ptr(x), ptr(out), x.numel(), stream_handle(stream))
+    if x.numel() != out.numel() or x.numel() % 8 or mode not in (1, 2):
+        raise ValueError("relu: bad shapes or mode")
+    kernels().relu(ptr(x), ptr(out), x.numel(), int(mode), stream_handle(stream))
+    return out
+
+
+def dwconv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, stride: int,
+           pads=((0, 0), (0, 0)), act: int = 0, stream=None) -> torch.Tensor:
+    """Depthwise conv (csrc/kernels/layers.hip): x [B,H,W,Cp] bf16, w fp32 [KH,KW,Cp] (BN folded),
+    bias fp32 [Cp], out [B,OH,OW,Cp] bf16; act 0 / 1 ReLU / 2 ReLU6."""
+    _chk(x, name="x"); _chk(out, name="out")
+    _chk(w, torch.float32, "w"); _chk(bias, torch.float32, "bias")
+    B, H, W, Cp = x.shape
+    KH, KW, Cw = w.shape
+    Bo, OH, OW, Co = out.shape
+    (pt, pb), (pl, pr) = pads
+    if (Bo != B or Co != Cp or Cw != Cp or bias.numel() != Cp or Cp % 8
+            or OH != (H + pt + pb - KH) // stride + 1 or OW != (W + pl + pr - KW) // stride + 1):
+        raise ValueError(f"dwconv: bad shapes x{tuple(x.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
+    kernels().dwconv(ptr(x), ptr(w), ptr(bias), ptr(out), B, H, W, Cp, OH, OW, KH, KW, stride, pt, pl, int(act),
+                     stream_handle(stream))
+    return out
+
+
+def avgpool(x: torch.Tensor, out: torch.Tensor, k, s: int, pads=((0, 0), (0, 0)), stream=None) -> torch.Tensor:
+    """Average pool (padding excluded from the count, Keras semantics)."""
+    _chk(x, name="x"); _chk(out, name="out")
+    kh, kw = (k, k) if isinstance(k, int) else k
+    B, H, W, Cp = x.shape
+    Bo, OH, OW, Co = out.shape
+    (pt, pb), (pl, pr) = pads
+    if (Bo != B or Co != Cp or Cp % 8 or OH != (H + pt + pb - kh) // s + 1 or OW != (W + pl + pr - kw) // s + 1):
+        raise ValueError("avgpool: bad shapes")
+    kernels().avgpool(ptr(x), ptr(out), B, H, W, Cp, OH, OW, kh, kw, s, pt, pl, stream_handle(stream))
+    return out
+
+
+def concat(xs, channels, out: torch.Tensor, out_channels: int, stream=None) -> torch.Tensor:
+    """Channel concat of NHWC tensors whose channel dims are padded (xs[i] holds
+    `channels[i]` real channels); the padding channels of `out` are zeroed."""
+    _chk(out, name="out")
+    Cpy = out.shape[-1]
+    pixels = out.numel() // Cpy
+    if sum(channels) != out_channels or out_channels > Cpy:
+        raise ValueError("concat: channel counts do not add up")
+    off = 0
+    for i, (x, c) in enumerate(zip(xs, channels)):
+        _chk(x, name=f"x{i}")
+        if x.numel() // x.shape[-1] != pixels or c > x.shape[-1]:
+            raise ValueError(f"concat: input {i} shape {tuple(x.shape)} does not match {tuple(out.shape)}")
+        zero_from = out_channels if i == len(xs) - 1 else Cpy
+        kernels().concat_into(ptr(x), c, x.shape[-1], ptr(out), Cpy, off, zero_from, pixels, stream_handle(stream))
+        off += c
     return out
 
 

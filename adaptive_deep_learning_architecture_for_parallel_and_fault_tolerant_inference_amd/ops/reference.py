@@ -13,7 +13,24 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from ..graph.ir import Graph
+from ..graph.ir import Graph, _pair, same_pads
+
+
+def _same(x: torch.Tensor, kh: int, kw: int, s: int, value: float = 0.0) -> torch.Tensor:
+    """TF 'same' padding of an NCHW tensor (the odd pixel goes after)."""
+    t, b = same_pads(x.shape[2], kh, s)
+    l, r = same_pads(x.shape[3], kw, s)
+    return F.pad(x, (l, r, t, b), value=value)
+
+
+def _act(y: torch.Tensor, act) -> torch.Tensor:
+    if act in (None, "linear"):
+        return y
+    if act == "relu":
+        return torch.relu(y)
+    if act == "softmax":
+        return torch.softmax(y, dim=-1)
+    raise ValueError(f"unsupported activation {act!r}")
 
 
 class ReferenceExecutor:
@@ -38,27 +55,52 @@ class ReferenceExecutor:
             bias = self.w.get(f"{L.name}/bias")
             s = a.get("stride", 1)
             if a.get("padding", "valid") == "same":
-                kh, kw = a["kernel"]
-                H, W = x.shape[2], x.shape[3]
-                oh, ow = -(-H // s), -(-W // s)
-                ph = max((oh - 1) * s + kh - H, 0)
-                pw = max((ow - 1) * s + kw - W, 0)
-                x = F.pad(x, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
+                x = _same(x, *a["kernel"], s)
             y = F.conv2d(x, k, bias, stride=s)
-            return y.permute(0, 2, 3, 1)
+            return _act(y.permute(0, 2, 3, 1), a.get("activation"))
+        if L.op == "dwconv":
+            x = ins[0].permute(0, 3, 1, 2)
+            c = x.shape[1]
+            k = self.w[f"{L.name}/depthwise_kernel"].permute(2, 3, 0, 1)      # (C, 1, kh, kw)
+            bias = self.w.get(f"{L.name}/bias")
+            s = a.get("stride", 1)
+            if a.get("padding", "valid") == "same":
+                x = _same(x, *a["kernel"], s)
+            y = F.conv2d(x, k, bias, stride=s, groups=c)
+            return _act(y.permute(0, 2, 3, 1), a.get("activation"))
         if L.op == "bn":
             g_, b_, m_, v_ = (self.w[f"{L.name}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance"))
             return (ins[0] - m_) / torch.sqrt(v_ + a.get("epsilon", 1e-3)) * g_ + b_
         if L.op == "relu":
-            return torch.relu(ins[0])
+            y = torch.relu(ins[0])
+            return y if a.get("max_value") is None else torch.clamp(y, max=float(a["max_value"]))
+        if L.op == "identity":
+            return ins[0]
+        if L.op == "flatten":
+            return ins[0].reshape(ins[0].shape[0], -1)
+        if L.op == "concat":
+            return torch.cat(ins, dim=-1)
         if L.op == "add":
             y = ins[0]
             for t in ins[1:]:
                 y = y + t
             return y
-        if L.op == "maxpool":
+        if L.op in ("maxpool", "avgpool"):
             x = ins[0].permute(0, 3, 1, 2)
-            y = F.max_pool2d(x, a["pool"], a["stride"])
+            kh, kw = _pair(a["pool"])
+            s = a["stride"]
+            if L.op == "maxpool":
+                if a.get("padding", "valid") == "same":
+                    x = _same(x, kh, kw, s, value=float("-inf"))
+                y = F.max_pool2d(x, (kh, kw), s)
+            elif a.get("padding", "valid") == "same":
+                # mean over the in-image part of each window (TF excludes the padding)
+                ones = torch.ones_like(x[:, :1])
+                num = F.avg_pool2d(_same(x, kh, kw, s), (kh, kw), s, divisor_override=1)
+                den = F.avg_pool2d(_same(ones, kh, kw, s), (kh, kw), s, divisor_override=1)
+                y = num / den
+            else:
+                y = F.avg_pool2d(x, (kh, kw), s)
             return y.permute(0, 2, 3, 1)
         if L.op == "gap":
             return ins[0].mean(dim=(1, 2))
@@ -66,9 +108,7 @@ class ReferenceExecutor:
             y = ins[0] @ self.w[f"{L.name}/kernel"]
             if f"{L.name}/bias" in self.w:
                 y = y + self.w[f"{L.name}/bias"]
-            if a.get("activation") == "softmax":
-                y = torch.softmax(y, dim=-1)
-            return y
+            return _act(y, a.get("activation"))
         if L.op == "softmax":
             return torch.softmax(ins[0], dim=-1)
         raise ValueError(f"unsupported op {L.op}")

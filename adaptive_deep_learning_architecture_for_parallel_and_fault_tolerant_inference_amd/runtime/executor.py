@@ -104,8 +104,8 @@ class SliceExecutor:
         if (L.op == "input" and base == name and len(L.out_shape) == 3
                 and L.attrs.get("stands_for", "input") == "input"):
             return torch.float32          # user image input (Keras float32 NHWC)
-        if L.op in ("dense", "softmax"):
-            return torch.float32
+        if L.op == "softmax" or (L.op == "dense" and L.attrs.get("activation") != "relu"):
+            return torch.float32          # logits / probabilities; a Dense(relu) feeds the next GEMM in bf16
         return torch.bfloat16
 
     # ----------------------------------------------------------- weights
@@ -141,6 +141,23 @@ class SliceExecutor:
                 b = weights.get(f"{name}/bias", np.zeros(k.shape[1], np.float32))
                 self.packed[i] = conv_ops.pack_conv(k.reshape(1, 1, k.shape[0], k.shape[1]), b, 1,
                                                     ((0, 0), (0, 0)), dev)
+            elif st.kind == "dwconv":
+                p = st.p
+                k = weights[f"{p['conv']}/depthwise_kernel"][..., 0]          # (kh, kw, C), multiplier 1
+                bn = None
+                eps = 1e-3
+                if p["bn"]:
+                    bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
+                    eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
+                # as an HWIO kernel with one input channel: BN scales the last (channel) axis
+                kf, bf = conv_ops.fold_bn(k[:, :, None, :], weights.get(f"{p['conv']}/bias"), bn, eps)
+                kf = kf[:, :, 0, :]
+                cp = ((kf.shape[-1] + 7) // 8) * 8
+                wp = np.zeros(kf.shape[:2] + (cp,), np.float32)
+                wp[..., :kf.shape[-1]] = kf
+                bp = np.zeros(cp, np.float32)
+                bp[:bf.shape[0]] = bf
+                self.packed[i] = (torch.tensor(wp, device=dev), torch.tensor(bp, device=dev))
             elif st.kind == "bn":
                 name = st.p["bn"]
                 gm, bt, mu, var = (weights[f"{name}/{n}"].astype(np.float64) for n in
@@ -211,7 +228,7 @@ class SliceExecutor:
         self._logits: Dict[int, torch.Tensor] = {}
         self._dense_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
-            if st.kind == "dense" and self.batch <= 32:
+            if st.kind == "dense" and self.batch <= 32 and not st.p.get("relu"):
                 # small-M head GEMM (csrc/kernels/head.hip): split-K scratch
                 pc = self.packed[i]
                 n = E.dense_small_scratch(self.batch, pc.cout, pc.K)
@@ -274,6 +291,8 @@ class SliceExecutor:
     def _conv_geom(self, i: int):
         st = self.steps[i]
         x = self.bufs(0)[st.ins[0]]
+        if st.kind == "dense":                     # a GEMM over the flattened input (Flatten aliases into it)
+            x = x.reshape(self.batch, -1)
         if x.dim() == 2:
             B, H, W, C = x.shape[0], 1, 1, x.shape[1]
         else:
@@ -304,9 +323,12 @@ class SliceExecutor:
         table = load_tuning()
         self.cfg: Dict[int, Tuple[int, int]] = {}
         for i, st in enumerate(self.steps):
-            if st.kind not in ("conv", "dense"):
+            if st.kind not in ("conv", "dense") or i in self._dense_part:    # small-M heads: head.hip
                 continue
             B, H, W, C, OH, OW, pc = self._conv_geom(i)
+            if pc.cout % 8:
+                raise NotImplementedError(f"{st.kind} {st.out}: {pc.cout} output channels (the MFMA GEMM path "
+                                          f"needs a multiple of 8)")
             key = conv_key(B, H, W, C, pc)
             if key in table:
                 cfg, ks = table[key][:2]
@@ -492,14 +514,32 @@ class SliceExecutor:
                                       out2=out2, relu2=st.p.get("relu2", False))
             elif k == "maxpool":
                 (pt, _), (pl, _) = st.p["pads"]
-                E.maxpool(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, True, stream=stream)
+                E.maxpool(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, st.p.get("pad_zero", True),
+                          stream=stream)
+            elif k == "avgpool":
+                E.avgpool(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], st.p["pads"], stream=stream)
+            elif k == "dwconv":
+                w, bias = self.packed[i]
+                E.dwconv(b[st.ins[0]], w, bias, b[st.out], st.p["stride"], st.p["pads"], act=st.p["relu"],
+                         stream=stream)
+            elif k == "concat":
+                E.concat([b[t] for t in st.ins], st.p["channels"], b[st.out], sum(st.p["channels"]), stream=stream)
+            elif k == "copy":
+                src, dst = b[st.ins[0]], b[st.out]
+                if src.numel() != dst.numel() or src.dtype != dst.dtype:
+                    raise RuntimeError(f"copy {st.ins[0]} -> {st.out}: {tuple(src.shape)} vs {tuple(dst.shape)}")
+                if stream is not None:
+                    with torch.cuda.stream(stream):
+                        dst.view(-1).copy_(src.view(-1), non_blocking=True)
+                else:
+                    dst.view(-1).copy_(src.view(-1), non_blocking=True)
             elif k == "bn":
                 sc, sh = self.packed[i]
                 E.bn_act(b[st.ins[0]], sc, sh, b[st.out], relu=st.p["relu"], stream=stream)
             elif k == "add":
                 E.add_act(b[st.ins[0]], b[st.ins[1]], b[st.out], relu=st.p["relu"], stream=stream)
             elif k == "relu":
-                E.relu(b[st.ins[0]], b[st.out], stream=stream)
+                E.relu(b[st.ins[0]], b[st.out], mode=st.p.get("mode", 1) or 1, stream=stream)
             elif k == "pad":
                 (pt, _), (pl, _) = st.p["pad"]
                 E.pad(b[st.ins[0]], b[st.out], pt, pl, stream=stream)
@@ -515,8 +555,8 @@ class SliceExecutor:
                 cfg, ks = self.cfg[i]
                 x = b[st.ins[0]].reshape(self.batch, -1)
                 dst = self._logits[i] if st.p["softmax"] else b[st.out]
-                conv_ops.conv_forward(x, self.packed[i], dst, cfg=cfg, ksplit=ks, workspace=self._ws, stream=stream,
-                                      counters=self._ctr)
+                conv_ops.conv_forward(x, self.packed[i], dst, relu=st.p.get("relu", 0), cfg=cfg, ksplit=ks,
+                                      workspace=self._ws, stream=stream, counters=self._ctr)
                 if st.p["softmax"]:
                     E.softmax_rows(dst, b[st.out], stream=stream)
             elif k == "softmax":

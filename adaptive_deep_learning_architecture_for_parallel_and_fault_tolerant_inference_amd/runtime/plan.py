@@ -6,9 +6,16 @@ The reference re-creates each slice as a Keras model on the worker
 compiled once into a short list of fused steps that map 1:1 onto our HIP
 kernels:
 
-* ``conv``     Conv2D [+BN folded] [+Add residual] [+ReLU]; a preceding
-               ZeroPadding2D is folded into the conv's address math
-* ``maxpool``  [ZeroPadding2D +] MaxPooling2D
+* ``conv``     Conv2D [+BN folded] [+Add residual] [+ReLU / ReLU6, or the
+               Conv2D's own activation='relu']; a preceding ZeroPadding2D or
+               'same' padding (any stride, TF placement) becomes explicit pads
+* ``maxpool``  [ZeroPadding2D +] MaxPooling2D ('same' padding excluded from the max)
+* ``avgpool``  AveragePooling2D (padding excluded from the mean)
+* ``dwconv``   DepthwiseConv2D [+BN folded] [+ReLU/ReLU6], explicit pads
+* ``concat``   Concatenate along channels (one copy launch per input)
+* ``copy``     a Flatten/Dropout that the slice emits under its own name
+               (otherwise they alias their input: Dropout everywhere,
+               Flatten when a Dense consumes it)
 * ``bn``       standalone BN [+ReLU] (only when a cut exposes the raw conv output)
 * ``add``      standalone Add [+ReLU]
 * ``relu``, ``pad`` (materialised ZeroPadding2D), ``gap``,
@@ -28,7 +35,7 @@ import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set
 
-from ..graph.ir import Graph
+from ..graph.ir import Graph, _pair, same_pads
 
 
 @dataclass
@@ -72,6 +79,29 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
             packed.add(n)
             steps.append(Step("pack", n + "#packed", [n], [], {"cin": c, "cpad": ((c + 7) // 8) * 8}))
 
+    alias: Dict[str, str] = {}          # identity / flatten-into-dense layers -> the tensor they pass on
+
+    def R(t: str) -> str:
+        return _phys(alias.get(t, t), packed)
+
+    def same(n: str, L, k) -> tuple:
+        """Explicit pads of a 'same' conv / pool (TF: the odd pixel after)."""
+        h, w = g.layers[L.inputs[0]].out_shape[:2]
+        kh, kw = _pair(k)
+        s = L.attrs.get("stride", 1)
+        return same_pads(h, kh, s), same_pads(w, kw, s)
+
+    def act_mode(c: Optional[str]) -> int:
+        """ReLU mode of a fusible activation layer: 1 ReLU, 2 ReLU6, 0 not a ReLU."""
+        if c is None or g.layers[c].op != "relu":
+            return 0
+        mv = g.layers[c].attrs.get("max_value")
+        if mv is None:
+            return 1
+        if float(mv) == 6.0:
+            return 2
+        raise NotImplementedError(f"ReLU(max_value={mv}) ({c})")
+
     for n in g.order:
         if n in done:
             continue
@@ -79,12 +109,13 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
         a = L.attrs
         if L.op == "zeropad":
             c = single(n)
-            if c is not None and g.layers[c].op in ("conv", "maxpool") and g.layers[c].attrs.get("padding", "valid") == "valid":
+            if (c is not None and g.layers[c].op in ("conv", "dwconv", "maxpool", "avgpool")
+                    and g.layers[c].attrs.get("padding", "valid") == "valid"):
                 pad_fold[c] = (L.inputs[0], a["pad"])
                 done.add(n)
                 continue
-            steps.append(Step("pad", n, [_phys(L.inputs[0], packed)], [n], {"pad": a["pad"]}))
-        elif L.op == "conv":
+            steps.append(Step("pad", n, [R(L.inputs[0])], [n], {"pad": a["pad"]}))
+        elif L.op in ("conv", "dwconv"):
             src = L.inputs[0]
             pads = ((0, 0), (0, 0))
             cover = [n]
@@ -92,86 +123,128 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
                 src, pads = pad_fold[n]
                 cover = [g.layers[n].inputs[0], n]
             if a.get("padding", "valid") == "same":
-                kh, kw = a["kernel"]
-                pads = (((kh - 1) // 2, kh - 1 - (kh - 1) // 2), ((kw - 1) // 2, kw - 1 - (kw - 1) // 2))
-                if a.get("stride", 1) != 1:
-                    raise NotImplementedError("'same' padding with stride > 1")
+                pads = same(n, L, a["kernel"])
             bn = None
-            relu = False
+            relu = 0
             res = None
             out = n
-            c1 = single(n)
-            if c1 is not None and g.layers[c1].op == "bn":
-                bn = c1
-                cover.append(c1)
-                out = c1
-                c2 = single(c1)
-                if c2 is not None and g.layers[c2].op == "relu":
-                    relu = True
-                    cover.append(c2)
-                    out = c2
-                elif c2 is not None and g.layers[c2].op == "add" and len(g.layers[c2].inputs) == 2:
-                    other = [i for i in g.layers[c2].inputs if i != c1]
-                    if len(other) == 1 and other[0] in produced:
-                        res = other[0]
+            act = a.get("activation")
+            if act not in (None, "linear", "relu"):
+                raise NotImplementedError(f"{L.op} activation {act!r} ({n})")
+            if act == "relu":
+                relu = 1                        # Conv2D(activation='relu'): nothing after it fuses
+            else:
+                c1 = single(n)
+                if c1 is not None and g.layers[c1].op == "bn":
+                    bn = c1
+                    cover.append(c1)
+                    out = c1
+                    c2 = single(c1)
+                    if act_mode(c2):
+                        relu = act_mode(c2)
                         cover.append(c2)
                         out = c2
-                        c3 = single(c2)
-                        if c3 is not None and g.layers[c3].op == "relu":
-                            relu = True
-                            cover.append(c3)
-                            out = c3
-            steps.append(Step("conv", out, [_phys(src, packed)] + ([res] if res else []), cover,
-                              {"conv": n, "bn": bn, "relu": relu, "residual": res, "pads": pads,
-                               "stride": a.get("stride", 1), "kernel": tuple(a["kernel"]),
-                               "filters": a["filters"], "packed_input": src in packed}))
+                    elif (L.op == "conv" and c2 is not None and g.layers[c2].op == "add"
+                          and len(g.layers[c2].inputs) == 2):
+                        other = [i for i in g.layers[c2].inputs if i != c1]
+                        if len(other) == 1 and alias.get(other[0], other[0]) in produced:
+                            res = alias.get(other[0], other[0])
+                            cover.append(c2)
+                            out = c2
+                            c3 = single(c2)
+                            if act_mode(c3):
+                                relu = act_mode(c3)
+                                cover.append(c3)
+                                out = c3
+                elif act_mode(c1):
+                    relu = act_mode(c1)
+                    cover.append(c1)
+                    out = c1
+            kernel = tuple(_pair(a["kernel"]))
+            if L.op == "dwconv":
+                steps.append(Step("dwconv", out, [R(src)], cover,
+                                  {"conv": n, "bn": bn, "relu": relu, "pads": pads, "stride": a.get("stride", 1),
+                                   "kernel": kernel}))
+            else:
+                steps.append(Step("conv", out, [R(src)] + ([res] if res else []), cover,
+                                  {"conv": n, "bn": bn, "relu": relu, "residual": res, "pads": pads,
+                                   "stride": a.get("stride", 1), "kernel": kernel,
+                                   "filters": a["filters"], "packed_input": src in packed}))
             done.update(cover)
-        elif L.op == "maxpool":
+        elif L.op in ("maxpool", "avgpool"):
             src = L.inputs[0]
             pads = ((0, 0), (0, 0))
             cover = [n]
+            pad_zero = True                     # a folded ZeroPadding2D: the zeros take part
             if n in pad_fold:
                 src, pads = pad_fold[n]
                 cover = [L.inputs[0], n]
-            steps.append(Step("maxpool", n, [_phys(src, packed)], cover,
-                              {"pool": a["pool"], "stride": a["stride"], "pads": pads}))
+            if a.get("padding", "valid") == "same":
+                pads = same(n, L, a["pool"])
+                pad_zero = False                # Keras 'same' pooling ignores the padding
+            if L.op == "avgpool" and n in pad_fold:
+                raise NotImplementedError(f"ZeroPadding2D before AveragePooling2D ({n})")
+            steps.append(Step(L.op, n, [R(src)], cover,
+                              {"pool": a["pool"], "stride": a["stride"], "pads": pads, "pad_zero": pad_zero}))
             done.update(cover)
         elif L.op == "bn":
             cover = [n]
-            relu = False
+            relu = 0
             out = n
             c = single(n)
-            if c is not None and g.layers[c].op == "relu":
-                relu = True
+            if act_mode(c):
+                relu = act_mode(c)
                 cover.append(c)
                 out = c
-            steps.append(Step("bn", out, [L.inputs[0]], cover, {"bn": n, "relu": relu}))
+            steps.append(Step("bn", out, [R(L.inputs[0])], cover, {"bn": n, "relu": relu}))
             done.update(cover)
         elif L.op == "add":
             cover = [n]
-            relu = False
+            relu = 0
             out = n
             c = single(n)
-            if c is not None and g.layers[c].op == "relu":
-                relu = True
+            if act_mode(c):
+                relu = act_mode(c)
                 cover.append(c)
                 out = c
             if len(L.inputs) != 2:
                 raise NotImplementedError("add with != 2 inputs")
-            steps.append(Step("add", out, list(L.inputs), cover, {"relu": relu}))
+            steps.append(Step("add", out, [R(i) for i in L.inputs], cover, {"relu": relu}))
             done.update(cover)
         elif L.op == "relu":
-            steps.append(Step("relu", n, [L.inputs[0]], [n]))
+            steps.append(Step("relu", n, [R(L.inputs[0])], [n], {"mode": act_mode(n)}))
+            done.add(n)
+        elif L.op == "concat":
+            steps.append(Step("concat", n, [R(i) for i in L.inputs], [n],
+                              {"channels": [g.layers[i].out_shape[-1] for i in L.inputs]}))
+            done.add(n)
+        elif L.op in ("identity", "flatten"):
+            c = single(n)
+            src_shape = g.layers[L.inputs[0]].out_shape
+            if L.op == "identity" or (c is not None and g.layers[c].op == "dense"):
+                if n in outset:                 # the slice must emit it under its own name
+                    steps.append(Step("copy", n, [R(L.inputs[0])], [n]))
+                else:
+                    alias[n] = alias.get(L.inputs[0], L.inputs[0])
+                    done.add(n)
+                    continue
+            else:
+                steps.append(Step("copy", n, [R(L.inputs[0])], [n]))
+            if L.op == "flatten" and len(src_shape) == 3 and src_shape[-1] % 8:
+                raise NotImplementedError(f"Flatten of a {src_shape[-1]}-channel tensor ({n}): channels are padded to 8")
             done.add(n)
         elif L.op == "gap":
-            steps.append(Step("gap", n, [L.inputs[0]], [n]))
+            steps.append(Step("gap", n, [R(L.inputs[0])], [n]))
             done.add(n)
         elif L.op == "dense":
-            steps.append(Step("dense", n, [L.inputs[0]], [n],
-                              {"units": a["units"], "softmax": a.get("activation") == "softmax"}))
+            act = a.get("activation")
+            if act not in (None, "linear", "relu", "softmax"):
+                raise NotImplementedError(f"Dense activation {act!r} ({n})")
+            steps.append(Step("dense", n, [R(L.inputs[0])], [n],
+                              {"units": a["units"], "softmax": act == "softmax", "relu": int(act == "relu")}))
             done.add(n)
         elif L.op == "softmax":
-            steps.append(Step("softmax", n, [L.inputs[0]], [n]))
+            steps.append(Step("softmax", n, [R(L.inputs[0])], [n]))
             done.add(n)
         else:
             raise NotImplementedError(f"op {L.op}")
@@ -236,7 +309,7 @@ def _fuse_stem(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
         cv = steps[u[0]]
         p = cv.p
         oh, ow = g.layers[p["conv"]].out_shape[:2]
-        if (p["kernel"] != (7, 7) or p["stride"] != 2 or p["filters"] != 64 or not p["relu"] or p["residual"]
+        if (p["kernel"] != (7, 7) or p["stride"] != 2 or p["filters"] != 64 or p["relu"] != 1 or p["residual"]
                 or ow > STEM_MAX_OW):
             continue
         drop = {i, u[0]}

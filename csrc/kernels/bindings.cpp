@@ -123,8 +123,22 @@ PYBIND11_MODULE(_C, m) {
   m.def("add_act", [](u64 a, u64 b, u64 y, size_t elems, int relu, u64 s) {
     check(adapt::add_act(P<const bf16>(a), P<const bf16>(b), P<bf16>(y), elems, relu, S(s)), "add_act");
   });
-  m.def("relu", [](u64 x, u64 y, size_t elems, u64 s) {
-    check(adapt::relu(P<const bf16>(x), P<bf16>(y), elems, S(s)), "relu");
+  m.def("relu", [](u64 x, u64 y, size_t elems, int mode, u64 s) {
+    check(adapt::relu(P<const bf16>(x), P<bf16>(y), elems, mode, S(s)), "relu");
+  });
+  m.def("dwconv", [](u64 x, u64 w, u64 bias, u64 y, int B, int H, int W, int Cp, int OH, int OW, int KH, int KW,
+                     int stride, int pad_t, int pad_l, int act, u64 s) {
+    check(adapt::dwconv(P<const bf16>(x), P<const float>(w), P<const float>(bias), P<bf16>(y), B, H, W, Cp, OH, OW,
+                        KH, KW, stride, pad_t, pad_l, act, S(s)), "dwconv");
+  });
+  m.def("avgpool", [](u64 x, u64 y, int B, int H, int W, int Cp, int OH, int OW, int KH, int KW, int Sd, int pad_t,
+                      int pad_l, u64 s) {
+    check(adapt::avgpool(P<const bf16>(x), P<bf16>(y), B, H, W, Cp, OH, OW, KH, KW, Sd, pad_t, pad_l, S(s)),
+          "avgpool");
+  });
+  m.def("concat_into", [](u64 x, int Cx, int Cpx, u64 y, int Cpy, int off, int zero_from, size_t pixels, u64 s) {
+    check(adapt::concat_into(P<const bf16>(x), Cx, Cpx, P<bf16>(y), Cpy, off, zero_from, pixels, S(s)),
+          "concat_into");
   });
   m.def("maxpool", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int K, int Sd, int pad_t, int pad_l,
                       int pad_zero, u64 s) {

@@ -20,6 +20,13 @@ union V8 {
   bf16 e[8];
 };
 
+// Fused activation of the epilogues and eltwise kernels: 0 none, 1 ReLU,
+// 2 ReLU6 (Keras ReLU(max_value=6), MobileNetV2).
+__device__ __forceinline__ float act_f(float v, int mode) {
+  v = mode ? fmaxf(v, 0.f) : v;
+  return mode == 2 ? fminf(v, 6.f) : v;
+}
+
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): consecutive logical tiles land on the same XCD so neighbouring
 // tiles that share an A panel hit the same L2.

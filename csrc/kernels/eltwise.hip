@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const bf16* __restrict__ x,
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float f = bf2f(v.e[t]) * scale[c0 + t] + shift[c0 + t];
-      o.e[t] = f2bf(relu ? fmaxf(f, 0.f) : f);
+      o.e[t] = f2bf(act_f(f, relu));
     }
     ((u32x4*)y)[i] = o.u;
   }
@@ -65,18 +65,19 @@ __global__ __launch_bounds__(256) void add_act_kernel(const bf16* __restrict__ a
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float f = bf2f(va.e[t]) + bf2f(vb.e[t]);
-      o.e[t] = f2bf(relu ? fmaxf(f, 0.f) : f);
+      o.e[t] = f2bf(act_f(f, relu));
     }
     ((u32x4*)y)[i] = o.u;
   }
 }
 
-__global__ __launch_bounds__(256) void relu_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, size_t chunks) {
+__global__ __launch_bounds__(256) void relu_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, size_t chunks,
+                                                   int mode) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < chunks; i += (size_t)gridDim.x * blockDim.x) {
     V8 v, o;
     v.u = ((const u32x4*)x)[i];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(fmaxf(bf2f(v.e[t]), 0.f));
+    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(bf2f(v.e[t]), mode));
     ((u32x4*)y)[i] = o.u;
   }
 }
@@ -193,9 +194,9 @@ hipError_t add_act(const bf16* a, const bf16* b, bf16* y, size_t elems, int relu
   hipLaunchKernelGGL(add_act_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a, b, y, chunks, relu);
   return hipGetLastError();
 }
-hipError_t relu(const bf16* x, bf16* y, size_t elems, hipStream_t s) {
+hipError_t relu(const bf16* x, bf16* y, size_t elems, int mode, hipStream_t s) {
   size_t chunks = elems / 8;
-  hipLaunchKernelGGL(relu_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, chunks);
+  hipLaunchKernelGGL(relu_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, chunks, mode);
   return hipGetLastError();
 }
 hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,

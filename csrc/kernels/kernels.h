@@ -14,7 +14,7 @@ struct ConvParams {
   int OH, OW, N;
   int KH, KW, stride, pad_t, pad_l;
   int M, K, Kpad, ldo;
-  int relu;
+  int relu;         // fused activation: 0 none, 1 ReLU, 2 ReLU6 (common.h act_f)
   int ksplit;       // >= 1: split-K slices (fp32 slabs in ws + reduce); < 0: stream-K over -ksplit x 256 blocks
   int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
   int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_sk_plan)
@@ -67,7 +67,14 @@ hipError_t input_pack(const float* x, bf16* y, size_t pixels, int C, int Cp, hip
 hipError_t bn_act(const bf16* x, bf16* y, const float* scale, const float* shift, size_t elems, int C, int relu,
                   hipStream_t s);
 hipError_t add_act(const bf16* a, const bf16* b, bf16* y, size_t elems, int relu, hipStream_t s);
-hipError_t relu(const bf16* x, bf16* y, size_t elems, hipStream_t s);
+hipError_t relu(const bf16* x, bf16* y, size_t elems, int mode, hipStream_t s);   // mode: 1 ReLU, 2 ReLU6
+// layers beyond ResNet (layers.hip): depthwise conv, average pool, channel concat
+hipError_t dwconv(const bf16* x, const float* w, const float* bias, bf16* y, int B, int H, int W, int Cp, int OH,
+                  int OW, int KH, int KW, int stride, int pad_t, int pad_l, int act, hipStream_t s);
+hipError_t avgpool(const bf16* x, bf16* y, int B, int H, int W, int Cp, int OH, int OW, int KH, int KW, int S,
+                   int pad_t, int pad_l, hipStream_t s);
+hipError_t concat_into(const bf16* x, int Cx, int Cpx, bf16* y, int Cpy, int off, int zero_from, size_t pixels,
+                       hipStream_t s);
 hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
                    int pad_l, int pad_zero, hipStream_t s);
 hipError_t gap(const bf16* x, bf16* y, float* y32, int B, int HW, int C, hipStream_t s);

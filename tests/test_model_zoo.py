@@ -1,0 +1,213 @@
+"""Model families beyond ResNet and the Keras JSON bridge (CPU).
+
+The reference's DEFER takes any Keras functional model (`src/dispatcher.py:
+39-53`) and ships it as `model.to_json()` (`src/dispatcher.py:234-236`); these
+tests pin our builders to the Keras applications (parameter totals and
+`get_weights()` lengths of `tf.keras.applications` with include_top=True),
+check the Keras JSON reader/writer on both serialisation formats, and run
+sliced == unsliced through the fp32 oracle.  Parity with real TF outputs is
+unpinned (no TensorFlow in this environment)."""
+import json
+import queue
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.dispatcher import DEFER
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph import planner, slicer
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph.keras_json import (
+    from_keras_json, to_keras_json)
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.model import Model, application
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import init_weights
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.zoo import build_model
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.node import Node
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.reference import ReferenceExecutor
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.plan import compile_plan
+
+KERAS_PARAMS = {"vgg16": 138_357_544, "vgg19": 143_667_240, "mobilenet_v2": 3_538_984,
+                "densenet121": 8_062_504, "densenet169": 14_307_880, "densenet201": 20_242_984}
+
+
+@pytest.mark.parametrize("name", sorted(KERAS_PARAMS))
+def test_param_totals_match_keras(name):
+    g = build_model(name)
+    assert g.count_params() == KERAS_PARAMS[name]
+    assert g.layers[g.output].out_shape == (1000,)
+
+
+def test_keras_names_and_weight_lists():
+    vgg = build_model("vgg16")
+    assert [n for n in vgg.order if vgg.layers[n].op == "dense"] == ["fc1", "fc2", "predictions"]
+    assert len(vgg.weight_specs()) == 32
+    mb = build_model("mobilenet_v2")
+    assert len(mb.weight_specs()) == 262
+    for n in ("Conv1", "bn_Conv1", "Conv1_relu", "expanded_conv_depthwise", "block_1_pad", "block_2_add",
+              "block_16_project_BN", "Conv_1", "out_relu", "global_average_pooling2d"):
+        assert n in mb.layers
+    assert mb.layers["block_1_pad"].attrs["pad"] == ((0, 1), (0, 1))          # imagenet_utils.correct_pad
+    assert mb.layers["Conv1_relu"].attrs["max_value"] == 6.0
+    dn = build_model("densenet121")
+    assert dn.layers["conv5_block16_concat"].out_shape == (7, 7, 1024)
+    assert dn.layers["pool4_pool"].out_shape == (7, 7, 512)
+
+
+@pytest.mark.parametrize("name", ["resnet50", "vgg16", "mobilenet_v2", "densenet121"])
+def test_keras_json_round_trip(name):
+    g = build_model(name)
+    s = to_keras_json(g)
+    d = json.loads(s)
+    assert d["class_name"] == "Functional" and d["config"]["layers"][0]["class_name"] == "InputLayer"
+    g2 = from_keras_json(s)
+    assert json.loads(g2.to_json()) == json.loads(g.to_json())
+
+
+def _k2(cls, name, inbound, **cfg):
+    cfg["name"] = name
+    return {"class_name": cls, "config": cfg, "name": name,
+            "inbound_nodes": [[[i, 0, 0, {}] for i in inbound]] if inbound else []}
+
+
+def _k3(cls, name, inbound, **cfg):
+    cfg["name"] = name
+    t = [{"class_name": "__keras_tensor__", "config": {"shape": [None], "dtype": "float32",
+                                                       "keras_history": [i, 0, 0]}} for i in inbound]
+    args = [t] if len(t) > 1 else t
+    return {"module": "keras.layers", "class_name": cls, "config": cfg, "name": name,
+            "inbound_nodes": [{"args": args, "kwargs": {}}] if inbound else []}
+
+
+def _small_keras(fmt):
+    """A hand-written Keras functional model touching every supported layer class."""
+    L = _k2 if fmt == 2 else _k3
+    inp = ({"batch_input_shape": [None, 16, 16, 3]} if fmt == 2 else {"batch_shape": [None, 16, 16, 3]})
+    layers = [
+        L("InputLayer", "img", [], dtype="float32", **inp),
+        L("Conv2D", "c1", ["img"], filters=16, kernel_size=[3, 3], strides=[1, 1], padding="same",
+          activation="relu", use_bias=True, dilation_rate=[1, 1], groups=1, data_format="channels_last"),
+        L("ZeroPadding2D", "pad", ["c1"], padding=[[0, 1], [0, 1]]),
+        L("DepthwiseConv2D", "dw", ["pad"], kernel_size=[3, 3], strides=[2, 2], padding="valid",
+          depth_multiplier=1, use_bias=False, activation="linear"),
+        L("BatchNormalization", "dw_bn", ["dw"], axis=[3], epsilon=1e-3, center=True, scale=True),
+        L("ReLU", "dw_relu", ["dw_bn"], max_value=6.0, negative_slope=0.0, threshold=0.0),
+        L("Conv2D", "pw", ["dw_relu"], filters=16, kernel_size=1, strides=1, padding="valid", use_bias=False),
+        L("BatchNormalization", "pw_bn", ["pw"], axis=-1, epsilon=1e-3),
+        L("Add", "add", ["pw_bn", "dw_relu"]),
+        L("Activation", "act", ["add"], activation="relu"),
+        L("Conv2D", "branch", ["act"], filters=8, kernel_size=[1, 1], padding="valid", use_bias=True),
+        L("Concatenate", "cat", ["act", "branch"], axis=-1),
+        L("MaxPooling2D", "mp", ["cat"], pool_size=[2, 2], strides=[1, 1], padding="same"),
+        L("AveragePooling2D", "ap", ["mp"], pool_size=[2, 2], strides=[2, 2], padding="valid"),
+        L("Dropout", "drop", ["ap"], rate=0.5),
+        L("Flatten", "flat", ["drop"]),
+        L("Dense", "fc", ["flat"], units=32, activation="relu", use_bias=True),
+        L("Dense", "predictions", ["fc"], units=10, activation="softmax", use_bias=True),
+    ]
+    io = ({"input_layers": [["img", 0, 0]], "output_layers": [["predictions", 0, 0]]} if fmt == 2 else
+          {"input_layers": ["img", 0, 0], "output_layers": ["predictions", 0, 0]})
+    return json.dumps({"class_name": "Functional", "config": {"name": "small", "layers": layers, **io}})
+
+
+@pytest.mark.parametrize("fmt", [2, 3])
+def test_keras_json_import_every_layer_class(fmt):
+    g = from_keras_json(_small_keras(fmt))
+    ops = [g.layers[n].op for n in g.order]
+    assert ops == ["input", "conv", "zeropad", "dwconv", "bn", "relu", "conv", "bn", "add", "relu", "conv",
+                   "concat", "maxpool", "avgpool", "identity", "flatten", "dense", "dense"]
+    assert g.layers["cat"].out_shape == (8, 8, 24) and g.layers["flat"].out_shape == (384,)
+    m = Model.from_keras_json(_small_keras(fmt), seed=3)
+    x = np.random.default_rng(0).standard_normal((2, 16, 16, 3)).astype(np.float32)
+    y = m.predict(x, device="cpu")
+    assert y.shape == (2, 10) and np.allclose(y.sum(-1), 1.0, atol=1e-5)
+    # the same graph from the Keras-ordered weight list
+    m2 = Model.from_keras_json(_small_keras(fmt), weights=m.get_weights())
+    np.testing.assert_allclose(m2.predict(x, device="cpu"), y, rtol=1e-6, atol=1e-7)
+    steps = compile_plan(g)
+    kinds = [s.kind for s in steps]
+    assert kinds == ["pack", "conv", "dwconv", "conv", "conv", "concat", "maxpool", "avgpool", "dense", "dense"]
+    dw = steps[2]
+    assert dw.p["pads"] == ((0, 1), (0, 1)) and dw.p["relu"] == 2 and dw.p["bn"] == "dw_bn"
+    assert steps[3].p["residual"] == "dw_relu" and steps[3].p["relu"] == 1
+    assert steps[8].ins == ["ap"] and steps[8].p["relu"] == 1            # Dropout + Flatten alias into the Dense
+
+
+def test_keras_json_rejects_unsupported():
+    d = json.loads(_small_keras(2))
+    d["config"]["layers"][9]["config"]["activation"] = "gelu"
+    with pytest.raises(NotImplementedError, match="gelu"):
+        from_keras_json(json.dumps(d))
+    d = json.loads(_small_keras(2))
+    d["config"]["layers"][1]["class_name"] = "SeparableConv2D"
+    with pytest.raises(NotImplementedError, match="SeparableConv2D"):
+        from_keras_json(json.dumps(d))
+
+
+def test_reference_pooling_same_excludes_padding():
+    g = from_keras_json(_small_keras(2))
+    ex = ReferenceExecutor(g, init_weights(g, 0))
+    x = torch.arange(2 * 3 * 3 * 1, dtype=torch.float32).reshape(2, 3, 3, 1)
+    L = g.layers["mp"]
+    y = ex._layer(L, [x])                          # 2x2/s1 'same': pad after, -inf
+    assert y.shape == (2, 3, 3, 1) and float(y[0, 2, 2, 0]) == 8.0 and float(y[0, 0, 0, 0]) == 4.0
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph.ir import Layer
+    ap = Layer("ap2", "avgpool", ["x"], {"pool": 2, "stride": 1, "padding": "same"})
+    z = ex._layer(ap, [x])
+    assert float(z[0, 2, 2, 0]) == 8.0                # corner window sees one real pixel
+    assert float(z[0, 0, 0, 0]) == (0 + 1 + 3 + 4) / 4
+
+
+@pytest.mark.parametrize("name,shape", [("vgg16", (32, 32, 3)), ("mobilenet_v2", (64, 64, 3)),
+                                        ("densenet121", (64, 64, 3))])
+def test_sliced_equals_unsliced(name, shape):
+    g = build_model(name, input_shape=shape)
+    w = init_weights(g, 0)
+    cuts, _ = planner.plan_cuts(g, 4, batch=32)
+    assert len(cuts) == 3
+    x = torch.randn(2, *shape)
+    full = ReferenceExecutor(g, w)(x)
+    vals = {g.input_names[0]: x}
+    for s in slicer.partition(g, cuts):
+        sg = slicer.subgraph(g, s)
+        compile_plan(sg, sg.output_names)
+        vals.update(ReferenceExecutor(sg, w).run({k: vals[k] for k in sg.input_names}))
+    torch.testing.assert_close(vals[g.output], full, rtol=1e-5, atol=1e-6)
+
+
+def test_mobilenet_plan_fuses_relu6_and_residuals():
+    steps = compile_plan(build_model("mobilenet_v2"))
+    kinds = [s.kind for s in steps]
+    assert kinds.count("dwconv") == 17 and "relu" not in kinds and "bn" not in kinds and "add" not in kinds
+    assert sum(1 for s in steps if s.kind == "conv" and s.p["residual"]) == 10
+    assert all(s.p["relu"] == 2 for s in steps if s.kind == "dwconv")
+    conv1 = steps[1]
+    assert conv1.p["conv"] == "Conv1" and conv1.p["pads"] == ((0, 1), (0, 1)) and conv1.p["relu"] == 2
+
+
+def test_defer_serves_a_keras_json_model():
+    """DEFER + two CPU Nodes on a model imported from Keras JSON, cut at a
+    multi-tensor frontier (the concat consumes both sides)."""
+    m = Model.from_keras_json(_small_keras(2), seed=1)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=10, ordered=True, batch=2)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu", node_id=f"k{i}",
+                  heartbeat_ttl=0.5) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["branch"], inq, outq), daemon=True).start()
+        xs = [np.random.default_rng(i).standard_normal((2, 16, 16, 3)).astype(np.float32) for i in range(3)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=60) for _ in xs])
+        np.testing.assert_allclose(got, m.predict(np.concatenate(xs), device="cpu"), rtol=1e-4, atol=1e-6)
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
+
+
+def test_application_factory():
+    m = application("mobilenet_v2", input_shape=(32, 32, 3), classes=5, seed=2)
+    assert m.count_params() > 0 and m.predict(np.zeros((1, 32, 32, 3), np.float32), device="cpu").shape == (1, 5)
