@@ -53,7 +53,8 @@ def parse():
 
 
 BASELINE_IMG_S = None   # the reference publishes no absolute number
-MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152"}
+MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152", "vgg16": "VGG16",
+               "vgg19": "VGG19", "mobilenet_v2": "MobileNetV2", "densenet121": "DenseNet121"}
 
 
 def main():
@@ -74,9 +75,10 @@ def main():
 
     from importlib import import_module
     resnet = import_module(f"{PKG}.models.resnet")
+    zoo = import_module(f"{PKG}.models.zoo")
     runner = import_module(f"{PKG}.parallel.runner")
 
-    g = resnet.build_resnet(args.model)
+    g = zoo.build_model(args.model)
     weights = resnet.init_weights(g, seed=args.seed)
     part_at = [s for s in args.part_at.split(",") if s]
     job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,

@@ -61,6 +61,77 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16* __restrict__ x,
   }
 }
 
+// 3x3 specialisation: a thread owns OWG consecutive output pixels of one row and one 8-channel chunk, so
+// each input column of the (OWG-1)*S+3 it touches is loaded once per filter row (6 loads per row instead of
+// 12 at stride 1, 9 instead of 12 at stride 2) and the row's three weight vectors stay in registers.
+template <int S, int OWG>
+__global__ __launch_bounds__(256) void dwconv3_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, bf16* __restrict__ y, int B,
+                                                      int H, int W, int Cp, int OH, int OW, int pad_t, int pad_l,
+                                                      int act) {
+  constexpr int COLS = (OWG - 1) * S + 3;
+  const int cpr = Cp / 8;
+  const int owg = (OW + OWG - 1) / OWG;
+  const size_t total = (size_t)B * OH * owg * cpr;
+  for (size_t i = gtid(); i < total; i += gstride()) {
+    const int c0 = (int)(i % cpr) * 8;
+    size_t pix = i / cpr;
+    const int ow0 = (int)(pix % owg) * OWG;
+    pix /= owg;
+    const int oh = (int)(pix % OH);
+    const int b = (int)(pix / OH);
+    float acc[OWG][8];
+    {
+      const f32x4 b0 = *(const f32x4*)(bias + c0), b1 = *(const f32x4*)(bias + c0 + 4);
+#pragma unroll
+      for (int j = 0; j < OWG; ++j) {
+        acc[j][0] = b0[0]; acc[j][1] = b0[1]; acc[j][2] = b0[2]; acc[j][3] = b0[3];
+        acc[j][4] = b1[0]; acc[j][5] = b1[1]; acc[j][6] = b1[2]; acc[j][7] = b1[3];
+      }
+    }
+    const int iw0 = ow0 * S - pad_l;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * S - pad_t + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      float wk[3][8];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const float* wt = w + ((size_t)kh * 3 + kw) * Cp + c0;
+        const f32x4 w0 = *(const f32x4*)wt, w1 = *(const f32x4*)(wt + 4);
+        wk[kw][0] = w0[0]; wk[kw][1] = w0[1]; wk[kw][2] = w0[2]; wk[kw][3] = w0[3];
+        wk[kw][4] = w1[0]; wk[kw][5] = w1[1]; wk[kw][6] = w1[2]; wk[kw][7] = w1[3];
+      }
+      const bf16* row = x + ((size_t)b * H + ih) * W * Cp + c0;
+#pragma unroll
+      for (int c = 0; c < COLS; ++c) {
+        const int iw = iw0 + c;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        V8 v;
+        v.u = *(const u32x4*)(row + (size_t)iw * Cp);
+        float xf[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xf[t] = bf2f(v.e[t]);
+#pragma unroll
+        for (int j = 0; j < OWG; ++j) {
+          const int kw = c - j * S;
+          if (kw < 0 || kw > 2) continue;      // compile-time after unrolling
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[j][t] += xf[t] * wk[kw][t];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < OWG; ++j) {
+      if (ow0 + j >= OW) break;
+      V8 o;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(acc[j][t], act));
+      *(u32x4*)(y + (((size_t)b * OH + oh) * OW + ow0 + j) * Cp + c0) = o.u;
+    }
+  }
+}
+
 // Average pool; padded positions are excluded from the count (TF/Keras 'same'), 'valid' has none.
 __global__ __launch_bounds__(256) void avgpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int H,
                                                       int W, int Cp, int OH, int OW, int KH, int KW, int S,
@@ -125,6 +196,16 @@ __global__ __launch_bounds__(256) void concat_scalar_kernel(const bf16* __restri
 hipError_t dwconv(const bf16* x, const float* w, const float* bias, bf16* y, int B, int H, int W, int Cp, int OH,
                   int OW, int KH, int KW, int stride, int pad_t, int pad_l, int act, hipStream_t s) {
   if (Cp % 8) return hipErrorInvalidValue;
+  // The register-blocked 3x3 kernel pays off at stride 1 on large maps; measured on MobileNetV2 bs=32
+  // (profiles/mbv2_bs32_steps_v*.json) it lost at stride 2 and on grids under ~512 blocks, where the
+  // thread-per-pixel kernel keeps 4x more loads in flight.
+  constexpr int OWG = 4;
+  const size_t t3 = (size_t)B * OH * ((OW + OWG - 1) / OWG) * (Cp / 8);
+  if (KH == 3 && KW == 3 && stride == 1 && t3 >= 512 * 256) {
+    hipLaunchKernelGGL((dwconv3_kernel<1, OWG>), dim3(grid_of(t3)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp, OH,
+                       OW, pad_t, pad_l, act);
+    return hipGetLastError();
+  }
   const size_t total = (size_t)B * OH * OW * (Cp / 8);
   hipLaunchKernelGGL(dwconv_kernel, dim3(grid_of(total)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp, OH, OW, KH,
                      KW, stride, pad_t, pad_l, act);

@@ -21,7 +21,9 @@ def ops():
 @pytest.mark.parametrize("B,H,W,C,k,s,pads,act", [
     (2, 56, 56, 32, 3, 1, ((1, 1), (1, 1)), 2), (2, 112, 112, 96, 3, 2, ((0, 1), (0, 1)), 2),
     (3, 14, 14, 576, 3, 1, ((1, 1), (1, 1)), 0), (1, 7, 9, 40, 3, 2, ((1, 1), (1, 1)), 1),
-    (2, 10, 10, 16, 5, 1, ((2, 2), (2, 2)), 2)])
+    (2, 10, 10, 16, 5, 1, ((2, 2), (2, 2)), 2),
+    # large stride-1 maps take the register-blocked 3x3 kernel (OW tail of 2 in the last case)
+    (16, 112, 112, 32, 3, 1, ((1, 1), (1, 1)), 2), (64, 30, 30, 96, 3, 1, ((1, 1), (1, 1)), 1)])
 def test_dwconv_vs_torch(ops, B, H, W, C, k, s, pads, act):
     E, _ = ops
     torch.manual_seed(0)

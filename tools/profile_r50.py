@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet, init_weights  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import init_weights  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.zoo import build_model  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.reference import ReferenceExecutor  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import SliceExecutor  # noqa: E402
 
@@ -41,7 +42,7 @@ def main():
     ap.add_argument("--baseline", action="store_true")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
-    g = build_resnet(a.model)
+    g = build_model(a.model)
     w = init_weights(g, 0)
     ex = SliceExecutor(g, w, a.batch, tune=a.tune)
     x = torch.randn(a.batch, 224, 224, 3, device="cuda")
@@ -82,6 +83,9 @@ def main():
         if st.kind in ("conv", "dense"):
             B, H, W, C, OH, OW, pc = ex._conv_geom(i)
             flop = 2 * B * OH * OW * pc.cout * pc.kh * pc.kw * pc.cin
+        elif st.kind == "dwconv":
+            o = ex.bufs(0)[st.out]
+            flop = 2 * o.numel() * st.p["kernel"][0] * st.p["kernel"][1]
         total_flop += flop
         per.append({"i": i, "kind": st.kind, "out": st.out, "ms": round(t, 4),
                     "tflops": round(flop / t / 1e9, 1) if flop else None, "cfg": ex.cfg.get(i)})
