@@ -12,6 +12,10 @@ worker list / cut list in the source) (`README.md:36-56`).  Subcommands:
   plan         balanced cut planner: cuts, per-stage cost, frontier bytes
   summary      model summary (layers, shapes, params)
 
+--model takes a family name (resnet50/101/152, vgg16/19, mobilenet_v2,
+densenet121/169/201) or a Keras ``model.to_json()`` file (*.json), with
+--weights pointing at its ``get_weights()`` list saved as .npz.
+
 All take --config FILE (YAML) plus ADAPT_* environment overrides (utils/config.py).
 """
 from __future__ import annotations
@@ -48,7 +52,13 @@ def _cfg(a, **extra) -> AdaptConfig:
 def _model(cfg: AdaptConfig):
     from .graph.manifest import load_keras_weight_list, load_model
     from .models.model import Model, resnet
-    m = resnet(cfg.model, seed=cfg.seed, input_shape=tuple(cfg.image), classes=cfg.classes)
+    if cfg.model.endswith(".json"):
+        # a Keras architecture (`model.to_json()`, what the reference ships to its workers);
+        # weights: --weights <Keras get_weights() .npz>, else seeded random init
+        with open(cfg.model) as f:
+            m = Model.from_keras_json(f.read(), seed=cfg.seed)
+    else:
+        m = resnet(cfg.model, seed=cfg.seed, input_shape=tuple(cfg.image), classes=cfg.classes)
     if cfg.weights:
         if cfg.weights.endswith(".npz"):
             m.weights = load_keras_weight_list(m.graph, cfg.weights)
