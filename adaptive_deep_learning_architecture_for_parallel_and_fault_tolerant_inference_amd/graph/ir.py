@@ -32,9 +32,24 @@ OPS = (
     "gap",        # global average pool
     "flatten",    # NHWC -> (H*W*C,) in Keras channels_last order
     "identity",   # Dropout / Activation('linear') at inference
-    "dense",      # attrs: units, activation(None|'relu'|'softmax'), use_bias
+    "dense",      # attrs: units, activation(None|'relu'|'softmax'|any ACTIVATIONS), use_bias
     "softmax",
+    "act",        # Keras Activation / LeakyReLU: attrs fn (ACTIVATIONS), alpha (LeakyReLU slope)
+    "binary",     # Multiply / Subtract / Maximum / Minimum / Average: attrs fn; the 2nd input may be one
+                  # channel row per image (squeeze-excite broadcast)
+    "gmp",        # GlobalMaxPooling2D
+    "reshape",    # attrs: shape (element order unchanged: NHWC row-major)
+    "rescale",    # Keras Rescaling: attrs scale, offset (scalars or per-channel lists)
+    "normalization",  # Keras Normalization(axis=-1): weights mean, variance, count
 )
+
+# activations the runtime executes (fused into conv / dense / eltwise epilogues,
+# csrc/kernels/common.h ActMode), by their Keras names
+ACTIVATIONS = ("linear", "relu", "relu6", "swish", "silu", "sigmoid", "tanh", "hard_sigmoid", "hard_swish", "gelu",
+               "elu", "selu", "softplus", "leaky_relu")
+# Keras activation name -> kernel ActMode (csrc/kernels/common.h); leaky_relu also takes its slope
+ACT_MODE = {None: 0, "linear": 0, "relu": 1, "relu6": 2, "swish": 3, "silu": 3, "sigmoid": 4, "tanh": 5,
+            "hard_sigmoid": 6, "hard_swish": 7, "gelu": 8, "elu": 9, "selu": 10, "softplus": 11, "leaky_relu": 12}
 
 
 def same_pads(size: int, k: int, s: int) -> Tuple[int, int]:
@@ -80,6 +95,9 @@ class Layer:
             if self.attrs.get("use_bias", True):
                 out.append((f"{self.name}/bias", (cin,)))
             return out
+        if self.op == "normalization":
+            c = in_shapes[0][-1]
+            return [(f"{self.name}/mean", (c,)), (f"{self.name}/variance", (c,)), (f"{self.name}/count", ())]
         if self.op == "dense":
             cin = in_shapes[0][-1]
             out = [(f"{self.name}/kernel", (cin, self.attrs["units"]))]
@@ -172,8 +190,20 @@ class Graph:
             if a.get("padding", "valid") == "same":
                 return (-(-h // s), -(-w // s), co)
             return ((h - kh) // s + 1, (w - kw) // s + 1, co)
-        if layer.op in ("bn", "relu", "softmax", "identity"):
+        if layer.op in ("bn", "relu", "softmax", "identity", "act", "rescale", "normalization"):
             return ins[0]
+        if layer.op == "binary":
+            return ins[0]
+        if layer.op == "reshape":
+            shp = tuple(int(d) for d in a["shape"])
+            n_in = n_out = 1
+            for d in ins[0]:
+                n_in *= d
+            for d in shp:
+                n_out *= d
+            if n_in != n_out:
+                raise ValueError(f"reshape {layer.name}: {ins[0]} -> {shp}")
+            return shp
         if layer.op == "flatten":
             n = 1
             for d in ins[0]:
@@ -193,8 +223,8 @@ class Graph:
             if a.get("padding", "valid") == "same":
                 return (-(-h // s), -(-w // s), c)
             return ((h - ph) // s + 1, (w - pw) // s + 1, c)
-        if layer.op == "gap":
-            return (ins[0][-1],)
+        if layer.op in ("gap", "gmp"):
+            return (1, 1, ins[0][-1]) if a.get("keepdims") else (ins[0][-1],)
         if layer.op == "dense":
             return (a["units"],)
         raise ValueError(f"unknown op {layer.op}")

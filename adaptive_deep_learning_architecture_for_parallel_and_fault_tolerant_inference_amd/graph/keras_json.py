@@ -27,7 +27,9 @@ from __future__ import annotations
 import json
 from typing import Any, Dict, List, Tuple
 
-from .ir import Graph, Layer, _pair
+from .ir import ACTIVATIONS, Graph, Layer, _pair
+
+_BINARY = {"Multiply": "mul", "Subtract": "sub", "Maximum": "max", "Minimum": "min", "Average": "avg"}
 
 
 def _inbound_names(layer: Dict[str, Any]) -> List[str]:
@@ -76,6 +78,36 @@ def _check_channels_last(cfg: Dict[str, Any], name: str) -> None:
         raise NotImplementedError(f"{name}: data_format {cfg['data_format']!r}")
 
 
+def _activation(act, name: str):
+    """A Keras activation config (a name, or a serialized function in Keras 3) -> our name."""
+    if isinstance(act, dict):
+        act = act.get("config", {}).get("name", act.get("class_name"))
+    if act in (None, "linear"):
+        return None
+    if act not in ACTIVATIONS and act != "softmax":
+        raise NotImplementedError(f"{name}: activation {act!r}")
+    return act
+
+
+def _layers_from_keras(cls: str, cfg: Dict[str, Any], name: str, inputs: List[str]) -> List[Layer]:
+    """Most classes map to one IR layer; SeparableConv2D lowers to a depthwise + a pointwise conv (same
+    get_weights() order: depthwise_kernel, pointwise_kernel, bias), the pointwise one keeping the Keras name."""
+    if cls == "SeparableConv2D":
+        _check_channels_last(cfg, name)
+        if int(cfg.get("depth_multiplier", 1)) != 1 or _pair(cfg.get("dilation_rate", 1)) != (1, 1):
+            raise NotImplementedError(f"{name}: SeparableConv2D with depth_multiplier / dilation")
+        dw = Layer(f"{name}/depthwise", "dwconv", inputs,
+                   {"kernel": _pair(cfg["kernel_size"]), "stride": _stride(cfg, name),
+                    "padding": cfg.get("padding", "valid"), "use_bias": False})
+        a = {"filters": int(cfg["filters"]), "kernel": (1, 1), "stride": 1, "padding": "valid",
+             "use_bias": bool(cfg.get("use_bias", True))}
+        act = _activation(cfg.get("activation"), name)
+        if act:
+            a["activation"] = act
+        return [dw, Layer(name, "conv", [dw.name], a)]
+    return [_layer_from_keras(cls, cfg, name, inputs)]
+
+
 def _layer_from_keras(cls: str, cfg: Dict[str, Any], name: str, inputs: List[str]) -> Layer:
     if cls == "InputLayer":
         shp = cfg.get("batch_input_shape") or cfg.get("batch_shape")
@@ -88,8 +120,10 @@ def _layer_from_keras(cls: str, cfg: Dict[str, Any], name: str, inputs: List[str
             raise NotImplementedError(f"{name}: dilated / grouped convolution")
         a = {"kernel": _pair(cfg["kernel_size"]), "stride": _stride(cfg, name),
              "padding": cfg.get("padding", "valid"), "use_bias": bool(cfg.get("use_bias", True))}
-        act = cfg.get("activation", "linear")
-        if act not in (None, "linear"):
+        act = _activation(cfg.get("activation", "linear"), name)
+        if act == "softmax":
+            raise NotImplementedError(f"{name}: softmax on a convolution")
+        if act:
             a["activation"] = act
         if cls == "Conv2D":
             a["filters"] = int(cfg["filters"])
@@ -104,19 +138,45 @@ def _layer_from_keras(cls: str, cfg: Dict[str, Any], name: str, inputs: List[str
             raise NotImplementedError(f"{name}: BatchNormalization needs axis=-1, center and scale")
         return Layer(name, "bn", inputs, {"epsilon": float(cfg.get("epsilon", 1e-3))})
     if cls == "ReLU":
-        if float(cfg.get("negative_slope", 0.0) or 0.0) != 0.0 or float(cfg.get("threshold", 0.0) or 0.0) != 0.0:
-            raise NotImplementedError(f"{name}: leaky / thresholded ReLU")
+        if float(cfg.get("threshold", 0.0) or 0.0) != 0.0:
+            raise NotImplementedError(f"{name}: thresholded ReLU")
         mv = cfg.get("max_value")
+        slope = float(cfg.get("negative_slope", 0.0) or 0.0)
+        if slope:
+            if mv is not None:
+                raise NotImplementedError(f"{name}: ReLU with both max_value and negative_slope")
+            return Layer(name, "act", inputs, {"fn": "leaky_relu", "alpha": slope})
+        if mv is not None and float(mv) != 6.0:
+            raise NotImplementedError(f"{name}: ReLU(max_value={mv})")
         return Layer(name, "relu", inputs, {"max_value": float(mv)} if mv is not None else {})
+    if cls == "LeakyReLU":
+        alpha = cfg.get("alpha", cfg.get("negative_slope", 0.3))
+        return Layer(name, "act", inputs, {"fn": "leaky_relu", "alpha": float(alpha)})
     if cls == "Activation":
-        act = cfg["activation"]
+        act = _activation(cfg["activation"], name)
+        if act is None:
+            return Layer(name, "identity", inputs)
         if act == "relu":
             return Layer(name, "relu", inputs)
         if act == "softmax":
             return Layer(name, "softmax", inputs)
-        if act == "linear":
-            return Layer(name, "identity", inputs)
-        raise NotImplementedError(f"{name}: Activation({act!r})")
+        return Layer(name, "act", inputs, {"fn": act})
+    if cls in _BINARY:
+        if len(inputs) != 2:
+            raise NotImplementedError(f"{name}: {cls} of {len(inputs)} inputs")
+        return Layer(name, "binary", inputs, {"fn": _BINARY[cls]})
+    if cls == "GlobalMaxPooling2D":
+        return Layer(name, "gmp", inputs, {"keepdims": True} if cfg.get("keepdims") else {})
+    if cls == "Reshape":
+        return Layer(name, "reshape", inputs, {"shape": tuple(int(d) for d in cfg["target_shape"])})
+    if cls == "Rescaling":
+        return Layer(name, "rescale", inputs, {"scale": cfg.get("scale", 1.0), "offset": cfg.get("offset", 0.0)})
+    if cls == "Normalization":
+        axis = cfg.get("axis", -1)
+        axis = axis[0] if isinstance(axis, list) and len(axis) == 1 else axis
+        if axis not in (-1, 3) or cfg.get("invert"):
+            raise NotImplementedError(f"{name}: Normalization needs axis=-1")
+        return Layer(name, "normalization", inputs)
     if cls == "Softmax":
         return Layer(name, "softmax", inputs)
     if cls == "Add":
@@ -135,17 +195,15 @@ def _layer_from_keras(cls: str, cfg: Dict[str, Any], name: str, inputs: List[str
                      {"pool": pool if pool[0] != pool[1] else pool[0], "stride": sh,
                       "padding": cfg.get("padding", "valid")})
     if cls == "GlobalAveragePooling2D":
-        if cfg.get("keepdims"):
-            raise NotImplementedError(f"{name}: keepdims=True")
-        return Layer(name, "gap", inputs)
+        return Layer(name, "gap", inputs, {"keepdims": True} if cfg.get("keepdims") else {})
     if cls == "Flatten":
         return Layer(name, "flatten", inputs)
     if cls in ("Dropout", "SpatialDropout2D", "GaussianDropout", "GaussianNoise", "ActivityRegularization"):
         return Layer(name, "identity", inputs)
     if cls == "Dense":
-        act = cfg.get("activation", "linear")
+        act = _activation(cfg.get("activation", "linear"), name)
         a = {"units": int(cfg["units"]), "use_bias": bool(cfg.get("use_bias", True))}
-        if act not in (None, "linear"):
+        if act:
             a["activation"] = act
         return Layer(name, "dense", inputs, a)
     raise NotImplementedError(f"layer {name!r}: Keras class {cls!r} is not supported by the runtime")
@@ -160,7 +218,8 @@ def from_keras_json(s) -> Graph:
     g = Graph(cfg.get("name", "model"))
     for ld in cfg["layers"]:
         name = ld.get("name") or ld["config"]["name"]
-        g.add(_layer_from_keras(ld["class_name"], ld["config"], name, _inbound_names(ld)))
+        for layer in _layers_from_keras(ld["class_name"], ld["config"], name, _inbound_names(ld)):
+            g.add(layer)
 
     def names(v) -> List[str]:
         if isinstance(v, list) and v and isinstance(v[0], str):
@@ -210,9 +269,27 @@ def _keras_layer(L: Layer, g: Graph) -> Dict[str, Any]:
         cls = "MaxPooling2D" if L.op == "maxpool" else "AveragePooling2D"
         cfg.update(pool_size=list(_pair(a["pool"])), strides=[a["stride"]] * 2, padding=a.get("padding", "valid"),
                    data_format="channels_last")
-    elif L.op == "gap":
-        cls = "GlobalAveragePooling2D"
-        cfg.update(data_format="channels_last", keepdims=False)
+    elif L.op in ("gap", "gmp"):
+        cls = "GlobalAveragePooling2D" if L.op == "gap" else "GlobalMaxPooling2D"
+        cfg.update(data_format="channels_last", keepdims=bool(a.get("keepdims", False)))
+    elif L.op == "act":
+        if a["fn"] == "leaky_relu":
+            cls = "LeakyReLU"
+            cfg.update(alpha=a.get("alpha", 0.3))
+        else:
+            cls = "Activation"
+            cfg.update(activation=a["fn"])
+    elif L.op == "binary":
+        cls = {v: k for k, v in _BINARY.items()}[a["fn"]]
+    elif L.op == "reshape":
+        cls = "Reshape"
+        cfg.update(target_shape=list(a["shape"]))
+    elif L.op == "rescale":
+        cls = "Rescaling"
+        cfg.update(scale=a.get("scale", 1.0), offset=a.get("offset", 0.0))
+    elif L.op == "normalization":
+        cls = "Normalization"
+        cfg.update(axis=[-1], invert=False)
     elif L.op == "flatten":
         cls = "Flatten"
         cfg.update(data_format="channels_last")

@@ -132,6 +132,11 @@ def init_weights(g: Graph, seed: int = 0, layers: Optional[List[str]] = None) ->
             out[specs[1][0]] = (rng.standard_normal(c) * 0.05).astype(np.float32)
             out[specs[2][0]] = (rng.standard_normal(c) * 0.05).astype(np.float32)
             out[specs[3][0]] = rng.uniform(0.5, 1.5, c).astype(np.float32)
+        elif L.op == "normalization":
+            c = specs[0][1][0]
+            out[specs[0][0]] = (rng.standard_normal(c) * 0.1).astype(np.float32)
+            out[specs[1][0]] = rng.uniform(0.5, 1.5, c).astype(np.float32)
+            out[specs[2][0]] = np.array(1000.0, np.float32)
         elif L.op == "dense":
             cin, units = specs[0][1]
             lim = np.sqrt(6.0 / (cin + units))

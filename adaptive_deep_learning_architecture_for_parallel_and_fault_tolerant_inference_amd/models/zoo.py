@@ -5,15 +5,17 @@ The reference's dispatcher is model-agnostic: `DEFER.run_defer(model, ...)`
 takes any Keras functional model and `dag_util.construct_model` cuts it at
 named layers (`src/dispatcher.py:39-53`, `src/dag_util.py:50-62`); its demo
 happens to use ResNet50 (`test/test.py:13`).  These builders give that
-generality a concrete footing beyond ResNet (and `graph/keras_import.py`
+generality a concrete footing beyond ResNet (and `graph/keras_json.py`
 takes an arbitrary Keras JSON):
 
 * VGG16 / VGG19  (plain conv stacks, Conv2D(activation='relu'), Flatten, Dense relu)
 * MobileNetV2    (ReLU6, DepthwiseConv2D, 'same' padding at stride 2, inverted residuals)
 * DenseNet121/169/201 (pre-activation BN-ReLU, Concatenate, AveragePooling2D)
+* EfficientNetB0-B7   (Rescaling/Normalization inside the model, swish, squeeze-excite Multiply)
 
 Parameter totals (Keras, include_top, 1000 classes; checked by tests):
-VGG16 138,357,544; VGG19 143,667,240; MobileNetV2 3,538,984; DenseNet121 8,062,504.
+VGG16 138,357,544; VGG19 143,667,240; MobileNetV2 3,538,984; DenseNet121 8,062,504;
+EfficientNetB0 5,330,571.
 """
 from __future__ import annotations
 
@@ -146,6 +148,89 @@ def build_densenet(name: str = "densenet121", classes: int = 1000, input_shape=(
     return g
 
 
+# ---------------------------------------------------------------- EfficientNet
+EFFNET_BLOCKS = [  # kernel, repeats, filters_in, filters_out, expand_ratio, strides (se_ratio 0.25, id_skip)
+    (3, 1, 32, 16, 1, 1), (3, 2, 16, 24, 6, 2), (5, 2, 24, 40, 6, 2), (3, 3, 40, 80, 6, 2),
+    (5, 3, 80, 112, 6, 1), (5, 4, 112, 192, 6, 2), (3, 1, 192, 320, 6, 1)]
+EFFNET_SCALE = {  # width, depth, resolution
+    "efficientnetb0": (1.0, 1.0, 224), "efficientnetb1": (1.0, 1.1, 240), "efficientnetb2": (1.1, 1.2, 260),
+    "efficientnetb3": (1.2, 1.4, 300), "efficientnetb4": (1.4, 1.8, 380), "efficientnetb5": (1.6, 2.2, 456),
+    "efficientnetb6": (1.8, 2.6, 528), "efficientnetb7": (2.0, 3.1, 600)}
+
+
+def build_efficientnet(name: str = "efficientnetb0", classes: int = 1000, input_shape=None) -> Graph:
+    """`keras.applications.EfficientNetB0..B7(include_top=True, weights=None)` (tf.keras 2.15): Rescaling +
+    Normalization preprocessing inside the model, swish, squeeze-excite (GAP -> Reshape -> 1x1 swish ->
+    1x1 sigmoid -> Multiply), drop-connect Dropout before the residual Add (identity at inference)."""
+    import math
+    width, depth, res = EFFNET_SCALE[name]
+    input_shape = tuple(input_shape or (res, res, 3))
+
+    def round_filters(f: float) -> int:
+        f *= width
+        new = max(8, int(f + 4) // 8 * 8)
+        return int(new + 8 if new < 0.9 * f else new)
+
+    g = Graph(name)
+    x = g.add(Layer("input_1", "input", [], {"shape": input_shape}))
+    x = g.add(Layer("rescaling", "rescale", [x], {"scale": 1.0 / 255.0, "offset": 0.0}))
+    x = g.add(Layer("normalization", "normalization", [x]))
+
+    def correct_pad(t: str, k: int):
+        h = g.layers[t].out_shape[0]
+        adj = 1 - h % 2
+        c = k // 2
+        return ((c - adj, c), (c - adj, c))
+
+    x = g.add(Layer("stem_conv_pad", "zeropad", [x], {"pad": correct_pad(x, 3)}))
+    x = _conv(g, x, "stem_conv", round_filters(32), 3, stride=2, use_bias=False)
+    x = g.add(Layer("stem_bn", "bn", [x], {"epsilon": 1e-3}))
+    x = g.add(Layer("stem_activation", "act", [x], {"fn": "swish"}))
+    total = float(sum(int(math.ceil(depth * r)) for _, r, *_ in EFFNET_BLOCKS))
+    b = 0
+    for i, (k, reps, f_in, f_out, expand, stride) in enumerate(EFFNET_BLOCKS):
+        f_in, f_out = round_filters(f_in), round_filters(f_out)
+        for j in range(int(math.ceil(depth * reps))):
+            if j > 0:
+                stride, f_in = 1, f_out
+            p = f"block{i + 1}{chr(j + 97)}_"
+            drop_rate = 0.2 * b / total
+            inp = x
+            filters = f_in * expand
+            if expand != 1:
+                x = _conv(g, x, p + "expand_conv", filters, 1, padding="same", use_bias=False)
+                x = g.add(Layer(p + "expand_bn", "bn", [x], {"epsilon": 1e-3}))
+                x = g.add(Layer(p + "expand_activation", "act", [x], {"fn": "swish"}))
+            if stride == 2:
+                x = g.add(Layer(p + "dwconv_pad", "zeropad", [x], {"pad": correct_pad(x, k)}))
+            x = g.add(Layer(p + "dwconv", "dwconv", [x], {"kernel": (k, k), "stride": stride,
+                                                        "padding": "valid" if stride == 2 else "same",
+                                                        "use_bias": False}))
+            x = g.add(Layer(p + "bn", "bn", [x], {"epsilon": 1e-3}))
+            x = g.add(Layer(p + "activation", "act", [x], {"fn": "swish"}))
+            se_f = max(1, int(f_in * 0.25))
+            se = g.add(Layer(p + "se_squeeze", "gap", [x]))
+            se = g.add(Layer(p + "se_reshape", "reshape", [se], {"shape": (1, 1, filters)}))
+            se = _conv(g, se, p + "se_reduce", se_f, 1, padding="same", activation="swish")
+            se = _conv(g, se, p + "se_expand", filters, 1, padding="same", activation="sigmoid")
+            x = g.add(Layer(p + "se_excite", "binary", [x, se], {"fn": "mul"}))
+            x = _conv(g, x, p + "project_conv", f_out, 1, padding="same", use_bias=False)
+            x = g.add(Layer(p + "project_bn", "bn", [x], {"epsilon": 1e-3}))
+            if stride == 1 and f_in == f_out:
+                if drop_rate > 0:
+                    x = g.add(Layer(p + "drop", "identity", [x]))
+                x = g.add(Layer(p + "add", "add", [x, inp]))
+            b += 1
+    x = _conv(g, x, "top_conv", round_filters(1280), 1, padding="same", use_bias=False)
+    x = g.add(Layer("top_bn", "bn", [x], {"epsilon": 1e-3}))
+    x = g.add(Layer("top_activation", "act", [x], {"fn": "swish"}))
+    x = g.add(Layer("avg_pool", "gap", [x]))
+    x = g.add(Layer("top_dropout", "identity", [x]))
+    g.add(Layer("predictions", "dense", [x], {"units": classes, "activation": "softmax", "use_bias": True}))
+    g.output_names = ["predictions"]
+    return g
+
+
 BUILDERS: Dict[str, Callable[..., Graph]] = {
     "vgg16": lambda **kw: build_vgg("vgg16", **kw),
     "vgg19": lambda **kw: build_vgg("vgg19", **kw),
@@ -153,6 +238,7 @@ BUILDERS: Dict[str, Callable[..., Graph]] = {
     "densenet121": lambda **kw: build_densenet("densenet121", **kw),
     "densenet169": lambda **kw: build_densenet("densenet169", **kw),
     "densenet201": lambda **kw: build_densenet("densenet201", **kw),
+    **{n: (lambda n: lambda **kw: build_efficientnet(n, **kw))(n) for n in EFFNET_SCALE},
 }
 
 

@@ -190,6 +190,8 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         B, H, W, C = x.shape
     if C != pc.cin:
         raise ValueError(f"conv expects {pc.cin} input channels, got {C}")
+    if int(relu) not in (0, 1, 2) or int(relu2) not in (0, 1, 2):
+        raise ValueError("conv epilogue activation must be 0 (none), 1 (ReLU) or 2 (ReLU6)")
     if x.dtype != torch.bfloat16 or not x.is_contiguous():
         raise ValueError("conv input must be contiguous bf16 NHWC")
     OH, OW = pc.out_hw(H, W)

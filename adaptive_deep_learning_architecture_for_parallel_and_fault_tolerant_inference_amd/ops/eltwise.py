@@ -54,9 +54,9 @@ def add_act(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, relu: bool = Fa
 
 
 def relu(x: torch.Tensor, out: torch.Tensor, mode: int = 1, stream=None) -> torch.Tensor:
-    """mode 1: ReLU; mode 2: ReLU6 (Keras ``ReLU(max_value=6)``)."""
+    """mode 1: ReLU; mode 2: ReLU6 (Keras ``ReLU(max_value=6)``); any other ActMode works too."""
     _chk(x, name="x"); _chk(out, name="out")
-    if x.numel() != out.numel() or x.numel() % 8 or mode not in (1, 2):
+    if x.numel() != out.numel() or x.numel() % 8 or not 0 <= mode <= 11:
         raise ValueError("relu: bad shapes or mode")
     kernels().relu(ptr(x), ptr(out), x.numel(), int(mode), stream_handle(stream))
     return out
@@ -65,7 +65,7 @@ def relu(x: torch.Tensor, out: torch.Tensor, mode: int = 1, stream=None) -> torc
 def dwconv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, stride: int,
            pads=((0, 0), (0, 0)), act: int = 0, stream=None) -> torch.Tensor:
     """Depthwise conv (csrc/kernels/layers.hip): x [B,H,W,Cp] bf16, w fp32 [KH,KW,Cp] (BN folded),
-    bias fp32 [Cp], out [B,OH,OW,Cp] bf16; act 0 / 1 ReLU / 2 ReLU6."""
+    bias fp32 [Cp], out [B,OH,OW,Cp] bf16; `act` (ActMode: 0 none, 1 ReLU, 2 ReLU6, 3 swish, ...)."""
     _chk(x, name="x"); _chk(out, name="out")
     _chk(w, torch.float32, "w"); _chk(bias, torch.float32, "bias")
     B, H, W, Cp = x.shape
@@ -126,8 +126,18 @@ def maxpool(x: torch.Tensor, out: torch.Tensor, k: int, s: int, pad_t: int = 0, 
     return out
 
 
+GAP_LARGE_HW = 1024      # from this many pixels per image the sliced two-pass GAP is used
+
+
+def gap_scratch_elems(B: int, HW: int, C: int) -> int:
+    """fp32 scratch the large-map GAP needs (0: the one-pass kernel serves this shape)."""
+    return B * kernels().gap_large_slices(B, HW) * C if HW >= GAP_LARGE_HW else 0
+
+
 def gap(x: torch.Tensor, out: Optional[torch.Tensor] = None, out32: Optional[torch.Tensor] = None,
-        stream=None) -> torch.Tensor:
+        stream=None, scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Global average pool [B,H,W,C] -> [B,C] (bf16 `out` and/or fp32 `out32`).  Maps of
+    >= GAP_LARGE_HW pixels take the sliced two-pass kernel and need `scratch`."""
     _chk(x, name="x")
     B, H, W, C = x.shape
     if C % 8:
@@ -140,7 +150,13 @@ def gap(x: torch.Tensor, out: Optional[torch.Tensor] = None, out32: Optional[tor
         _chk(out32, torch.float32, "out32")
         if out32.numel() != B * C:
             raise ValueError("gap: bad out32")
-    kernels().gap(ptr(x), ptr(out), ptr(out32), B, H * W, C, stream_handle(stream))
+    need = gap_scratch_elems(B, H * W, C)
+    if need:
+        if scratch is None or scratch.numel() < need or scratch.dtype != torch.float32:
+            raise ValueError(f"gap over {H}x{W}: needs an fp32 scratch of {need} elements")
+        kernels().gap_large(ptr(x), ptr(out), ptr(out32), ptr(scratch), B, H * W, C, stream_handle(stream))
+    else:
+        kernels().gap(ptr(x), ptr(out), ptr(out32), B, H * W, C, stream_handle(stream))
     return out if out is not None else out32
 
 
@@ -200,4 +216,47 @@ def pad(x: torch.Tensor, out: torch.Tensor, pad_t: int, pad_l: int, stream=None)
     if Bo != B or Co != C or C % 8 or OH < H + pad_t or OW < W + pad_l:
         raise ValueError("pad: bad shapes")
     kernels().pad(ptr(x), ptr(out), B, H, W, C, OH, OW, pad_t, pad_l, stream_handle(stream))
+    return out
+
+
+from ..graph.ir import ACT_MODE as ACT_MODES  # noqa: E402  (Keras name -> csrc/kernels/common.h ActMode)
+
+BIN_OPS = {"add": 0, "sub": 1, "mul": 2, "max": 3, "min": 4, "avg": 5}
+
+
+def act(x: torch.Tensor, out: torch.Tensor, mode: int, alpha: float = 0.3, stream=None) -> torch.Tensor:
+    """Standalone activation (ActMode `mode`; `alpha` = LeakyReLU slope)."""
+    _chk(x, name="x"); _chk(out, name="out")
+    if x.numel() != out.numel() or x.numel() % 8 or not 0 <= mode <= 12:
+        raise ValueError("act: bad shapes or mode")
+    kernels().act(ptr(x), ptr(out), x.numel(), int(mode), float(alpha), stream_handle(stream))
+    return out
+
+
+def binary(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, op: str, act_mode: int = 0,
+           stream=None) -> torch.Tensor:
+    """out = act(a <op> b); b has a's shape, or one channel row per image ([B,1,1,Cp] / [B,Cp]) broadcast over
+    a's pixels."""
+    _chk(a, name="a"); _chk(b, name="b"); _chk(out, name="out")
+    Cp = a.shape[-1]
+    if out.numel() != a.numel() or Cp % 8 or b.shape[-1] != Cp:
+        raise ValueError("binary: bad shapes")
+    bcast = 0
+    if b.numel() != a.numel():
+        B = a.shape[0]
+        if b.numel() != B * Cp:
+            raise ValueError(f"binary: cannot broadcast {tuple(b.shape)} over {tuple(a.shape)}")
+        bcast = a.numel() // (B * Cp)
+    kernels().binary(ptr(a), ptr(b), ptr(out), a.numel(), Cp, bcast, BIN_OPS[op], int(act_mode),
+                     stream_handle(stream))
+    return out
+
+
+def gmp(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    """GlobalMaxPooling2D: [B,H,W,Cp] -> [B,Cp]."""
+    _chk(x, name="x"); _chk(out, name="out")
+    B, H, W, Cp = x.shape
+    if out.numel() != B * Cp or Cp % 8:
+        raise ValueError("gmp: bad shapes")
+    kernels().gmp(ptr(x), ptr(out), B, H * W, Cp, stream_handle(stream))
     return out

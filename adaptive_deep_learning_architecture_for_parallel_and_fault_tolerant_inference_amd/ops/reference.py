@@ -23,13 +23,36 @@ def _same(x: torch.Tensor, kh: int, kw: int, s: int, value: float = 0.0) -> torc
     return F.pad(x, (l, r, t, b), value=value)
 
 
-def _act(y: torch.Tensor, act) -> torch.Tensor:
+def _act(y: torch.Tensor, act, alpha: float = 0.3) -> torch.Tensor:
+    """Keras activations by name (tf.keras 2.15 definitions)."""
     if act in (None, "linear"):
         return y
     if act == "relu":
         return torch.relu(y)
+    if act == "relu6":
+        return torch.clamp(y, 0.0, 6.0)
     if act == "softmax":
         return torch.softmax(y, dim=-1)
+    if act in ("swish", "silu"):
+        return y * torch.sigmoid(y)
+    if act == "sigmoid":
+        return torch.sigmoid(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    if act == "hard_sigmoid":
+        return torch.clamp(0.2 * y + 0.5, 0.0, 1.0)
+    if act == "hard_swish":
+        return y * torch.clamp(y + 3.0, 0.0, 6.0) / 6.0
+    if act == "gelu":
+        return F.gelu(y)
+    if act == "elu":
+        return F.elu(y)
+    if act == "selu":
+        return F.selu(y)
+    if act == "softplus":
+        return F.softplus(y)
+    if act == "leaky_relu":
+        return F.leaky_relu(y, alpha)
     raise ValueError(f"unsupported activation {act!r}")
 
 
@@ -43,6 +66,10 @@ class ReferenceExecutor:
             L = g.layers[n]
             for wname, _ in L.weight_shapes(g.in_shapes(n)) if L.op != "input" else []:
                 self.w[wname] = torch.from_numpy(np.asarray(weights[wname], np.float32)).to(self.device, dtype)
+            if L.op == "rescale":           # per-channel Rescaling factors: device tensors made once (graph capture)
+                for k in ("scale", "offset"):
+                    if isinstance(L.attrs.get(k), (list, tuple)):
+                        self.w[f"{n}/#{k}"] = torch.tensor(L.attrs[k], dtype=dtype, device=self.device)
 
     def _layer(self, L, ins: List[torch.Tensor]) -> torch.Tensor:
         a = L.attrs
@@ -57,7 +84,7 @@ class ReferenceExecutor:
             if a.get("padding", "valid") == "same":
                 x = _same(x, *a["kernel"], s)
             y = F.conv2d(x, k, bias, stride=s)
-            return _act(y.permute(0, 2, 3, 1), a.get("activation"))
+            return _act(y.permute(0, 2, 3, 1), a.get("activation"), a.get("alpha", 0.3))
         if L.op == "dwconv":
             x = ins[0].permute(0, 3, 1, 2)
             c = x.shape[1]
@@ -76,6 +103,39 @@ class ReferenceExecutor:
             return y if a.get("max_value") is None else torch.clamp(y, max=float(a["max_value"]))
         if L.op == "identity":
             return ins[0]
+        if L.op == "act":
+            return _act(ins[0], a["fn"], a.get("alpha", 0.3))
+        if L.op == "binary":
+            x, y = ins
+            if y.dim() != x.dim():                      # one channel row per image
+                y = y.reshape((y.shape[0],) + (1,) * (x.dim() - 2) + (y.shape[-1],))
+            fn = a["fn"]
+            if fn == "mul":
+                return x * y
+            if fn == "sub":
+                return x - y
+            if fn == "max":
+                return torch.maximum(x, y)
+            if fn == "min":
+                return torch.minimum(x, y)
+            if fn == "avg":
+                return 0.5 * (x + y)
+            raise ValueError(f"binary {fn}")
+        if L.op == "gmp":
+            y = ins[0].amax(dim=(1, 2))
+            return y.reshape(y.shape[0], 1, 1, -1) if a.get("keepdims") else y
+        if L.op == "reshape":
+            return ins[0].reshape((ins[0].shape[0],) + tuple(L.out_shape))
+        if L.op == "rescale":
+            sc, of = a.get("scale", 1.0), a.get("offset", 0.0)
+            if isinstance(sc, (list, tuple)):
+                sc = self.w[f"{L.name}/#scale"]
+            if isinstance(of, (list, tuple)):
+                of = self.w[f"{L.name}/#offset"]
+            return ins[0] * sc + of
+        if L.op == "normalization":
+            m, v = self.w[f"{L.name}/mean"], self.w[f"{L.name}/variance"]
+            return (ins[0] - m) / torch.clamp(torch.sqrt(v), min=1e-7)
         if L.op == "flatten":
             return ins[0].reshape(ins[0].shape[0], -1)
         if L.op == "concat":
@@ -103,7 +163,8 @@ class ReferenceExecutor:
                 y = F.avg_pool2d(x, (kh, kw), s)
             return y.permute(0, 2, 3, 1)
         if L.op == "gap":
-            return ins[0].mean(dim=(1, 2))
+            y = ins[0].mean(dim=(1, 2))
+            return y.reshape(y.shape[0], 1, 1, -1) if a.get("keepdims") else y
         if L.op == "dense":
             y = ins[0] @ self.w[f"{L.name}/kernel"]
             if f"{L.name}/bias" in self.w:

@@ -104,8 +104,8 @@ class SliceExecutor:
         if (L.op == "input" and base == name and len(L.out_shape) == 3
                 and L.attrs.get("stands_for", "input") == "input"):
             return torch.float32          # user image input (Keras float32 NHWC)
-        if L.op == "softmax" or (L.op == "dense" and L.attrs.get("activation") != "relu"):
-            return torch.float32          # logits / probabilities; a Dense(relu) feeds the next GEMM in bf16
+        if L.op == "softmax" or (L.op == "dense" and L.attrs.get("activation") in (None, "linear", "softmax")):
+            return torch.float32          # logits / probabilities; a Dense(relu, ...) feeds the next GEMM in bf16
         return torch.bfloat16
 
     # ----------------------------------------------------------- weights
@@ -117,6 +117,12 @@ class SliceExecutor:
                 p = st.p
                 kf, bf = self._folded(weights, p)
                 cin_pad = ((kf.shape[2] + 7) // 8) * 8
+                if kf.shape[-1] % 8 and not p.get("sibling"):
+                    # output channels padded to the 16-byte activation layout with zero filters
+                    # (EfficientNet's 4- / 6-channel squeeze-excite convs)
+                    extra = 8 - kf.shape[-1] % 8
+                    kf = np.concatenate([kf, np.zeros(kf.shape[:3] + (extra,), kf.dtype)], axis=-1)
+                    bf = np.concatenate([bf, np.zeros(extra, bf.dtype)])
                 n_split = 0
                 if p.get("sibling"):                  # merged sibling convs: one GEMM, N = N0 + N1
                     k2, b2 = self._folded(weights, p["sibling"])
@@ -158,6 +164,20 @@ class SliceExecutor:
                 bp = np.zeros(cp, np.float32)
                 bp[:bf.shape[0]] = bf
                 self.packed[i] = (torch.tensor(wp, device=dev), torch.tensor(bp, device=dev))
+            elif st.kind == "affine":            # Keras Rescaling / Normalization: y = x * scale + shift
+                L = self.g.layers[st.p["layer"]]
+                c = L.out_shape[-1]
+                if L.op == "rescale":
+                    sc = np.broadcast_to(np.asarray(L.attrs.get("scale", 1.0), np.float64), (c,))
+                    sh = np.broadcast_to(np.asarray(L.attrs.get("offset", 0.0), np.float64), (c,))
+                else:
+                    mu = weights[f"{L.name}/mean"].astype(np.float64)
+                    sd = np.maximum(np.sqrt(weights[f"{L.name}/variance"].astype(np.float64)), 1e-7)
+                    sc, sh = 1.0 / sd, -mu / sd
+                cp = ((c + 7) // 8) * 8
+                scp, shp = np.zeros(cp, np.float32), np.zeros(cp, np.float32)   # padding channels stay 0
+                scp[:c], shp[:c] = sc, sh
+                self.packed[i] = (torch.tensor(scp, device=dev), torch.tensor(shp, device=dev))
             elif st.kind == "bn":
                 name = st.p["bn"]
                 gm, bt, mu, var = (weights[f"{name}/{n}"].astype(np.float64) for n in
@@ -235,6 +255,14 @@ class SliceExecutor:
                 self._dense_part[i] = torch.empty(n, dtype=torch.float32, device=dev)
             elif st.kind == "dense" and st.p["softmax"]:
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
+        self._gap_part: Dict[int, torch.Tensor] = {}
+        for i, st in enumerate(self.steps):
+            if st.kind == "gap" and self.device.type == "cuda":
+                shp = self.shape_of(st.ins[0])
+                if len(shp) == 4:
+                    need = E.gap_scratch_elems(shp[0], shp[1] * shp[2], shp[3])
+                    if need:
+                        self._gap_part[i] = torch.empty(need, dtype=torch.float32, device=dev)
         self._ws: Optional[torch.Tensor] = None
         self._ctr: Optional[torch.Tensor] = None
         self._ws_side: Optional[torch.Tensor] = None
@@ -522,6 +550,15 @@ class SliceExecutor:
                 w, bias = self.packed[i]
                 E.dwconv(b[st.ins[0]], w, bias, b[st.out], st.p["stride"], st.p["pads"], act=st.p["relu"],
                          stream=stream)
+            elif k == "act":
+                E.act(b[st.ins[0]], b[st.out], st.p["mode"], st.p["alpha"], stream=stream)
+            elif k == "binary":
+                E.binary(b[st.ins[0]], b[st.ins[1]], b[st.out], st.p["fn"], st.p["act"], stream=stream)
+            elif k == "gmp":
+                E.gmp(b[st.ins[0]], b[st.out], stream=stream)
+            elif k == "affine":
+                sc, sh = self.packed[i]
+                E.bn_act(b[st.ins[0]], sc, sh, b[st.out], relu=0, stream=stream)
             elif k == "concat":
                 E.concat([b[t] for t in st.ins], st.p["channels"], b[st.out], sum(st.p["channels"]), stream=stream)
             elif k == "copy":
@@ -544,7 +581,7 @@ class SliceExecutor:
                 (pt, _), (pl, _) = st.p["pad"]
                 E.pad(b[st.ins[0]], b[st.out], pt, pl, stream=stream)
             elif k == "gap":
-                E.gap(b[st.ins[0]], out=b[st.out], stream=stream)
+                E.gap(b[st.ins[0]], out=b[st.out], stream=stream, scratch=self._gap_part.get(i))
             elif k == "dense" and i in self._dense_part:
                 x = b[st.ins[0]].reshape(self.batch, -1)
                 if st.p["softmax"]:

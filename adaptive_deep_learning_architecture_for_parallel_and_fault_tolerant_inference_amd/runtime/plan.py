@@ -35,7 +35,7 @@ import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set
 
-from ..graph.ir import Graph, _pair, same_pads
+from ..graph.ir import ACT_MODE, Graph, _pair, same_pads
 
 
 @dataclass
@@ -92,15 +92,30 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
         return same_pads(h, kh, s), same_pads(w, kw, s)
 
     def act_mode(c: Optional[str]) -> int:
-        """ReLU mode of a fusible activation layer: 1 ReLU, 2 ReLU6, 0 not a ReLU."""
-        if c is None or g.layers[c].op != "relu":
+        """Kernel ActMode of a fusible activation layer (ReLU, ReLU6, swish, sigmoid, ...), 0 if `c`
+        is not one (LeakyReLU needs its slope: it runs as its own step)."""
+        if c is None:
             return 0
-        mv = g.layers[c].attrs.get("max_value")
+        Lc = g.layers[c]
+        if Lc.op == "act":
+            return 0 if Lc.attrs["fn"] == "leaky_relu" else ACT_MODE[Lc.attrs["fn"]]
+        if Lc.op != "relu":
+            return 0
+        mv = Lc.attrs.get("max_value")
         if mv is None:
             return 1
         if float(mv) == 6.0:
             return 2
         raise NotImplementedError(f"ReLU(max_value={mv}) ({c})")
+
+    def own_act(n: str, L) -> int:
+        """ActMode of a conv / dense layer's own `activation` argument."""
+        act = L.attrs.get("activation")
+        if act in (None, "linear"):
+            return 0
+        if act not in ACT_MODE or act == "leaky_relu":
+            raise NotImplementedError(f"{L.op} activation {act!r} ({n})")
+        return ACT_MODE[act]
 
     for n in g.order:
         if n in done:
@@ -128,11 +143,11 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
             relu = 0
             res = None
             out = n
-            act = a.get("activation")
-            if act not in (None, "linear", "relu"):
-                raise NotImplementedError(f"{L.op} activation {act!r} ({n})")
-            if act == "relu":
-                relu = 1                        # Conv2D(activation='relu'): nothing after it fuses
+            post_act = 0                        # an activation the MFMA epilogue does not take (swish, ...)
+            if own_act(n, L):
+                relu = own_act(n, L)            # Conv2D(activation=...): nothing after it fuses
+                if L.op == "conv" and relu > 2:
+                    post_act, relu = relu, 0
             else:
                 c1 = single(n)
                 if c1 is not None and g.layers[c1].op == "bn":
@@ -140,23 +155,28 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
                     cover.append(c1)
                     out = c1
                     c2 = single(c1)
-                    if act_mode(c2):
+                    feed = c1                       # the tensor the residual Add sees from this branch
+                    while (c2 is not None and g.layers[c2].op == "identity"
+                           and single(c2) is not None and g.layers[single(c2)].op == "add"):
+                        cover.append(c2)            # drop-connect Dropout between the BN and the residual Add
+                        feed, c2 = c2, single(c2)
+                    if act_mode(c2) and (L.op == "dwconv" or act_mode(c2) <= 2):
                         relu = act_mode(c2)
                         cover.append(c2)
                         out = c2
                     elif (L.op == "conv" and c2 is not None and g.layers[c2].op == "add"
                           and len(g.layers[c2].inputs) == 2):
-                        other = [i for i in g.layers[c2].inputs if i != c1]
+                        other = [i for i in g.layers[c2].inputs if i != feed]
                         if len(other) == 1 and alias.get(other[0], other[0]) in produced:
                             res = alias.get(other[0], other[0])
                             cover.append(c2)
                             out = c2
                             c3 = single(c2)
-                            if act_mode(c3):
+                            if 0 < act_mode(c3) <= 2:
                                 relu = act_mode(c3)
                                 cover.append(c3)
                                 out = c3
-                elif act_mode(c1):
+                elif act_mode(c1) and (L.op == "dwconv" or act_mode(c1) <= 2):
                     relu = act_mode(c1)
                     cover.append(c1)
                     out = c1
@@ -166,10 +186,13 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
                                   {"conv": n, "bn": bn, "relu": relu, "pads": pads, "stride": a.get("stride", 1),
                                    "kernel": kernel}))
             else:
-                steps.append(Step("conv", out, [R(src)] + ([res] if res else []), cover,
+                cv_out = out if not post_act else n + "#preact"
+                steps.append(Step("conv", cv_out, [R(src)] + ([res] if res else []), cover,
                                   {"conv": n, "bn": bn, "relu": relu, "residual": res, "pads": pads,
                                    "stride": a.get("stride", 1), "kernel": kernel,
                                    "filters": a["filters"], "packed_input": src in packed}))
+                if post_act:
+                    steps.append(Step("act", out, [cv_out], [], {"mode": post_act, "alpha": 0.3}))
             done.update(cover)
         elif L.op in ("maxpool", "avgpool"):
             src = L.inputs[0]
@@ -214,6 +237,38 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
         elif L.op == "relu":
             steps.append(Step("relu", n, [R(L.inputs[0])], [n], {"mode": act_mode(n)}))
             done.add(n)
+        elif L.op == "act":
+            steps.append(Step("act", n, [R(L.inputs[0])], [n],
+                              {"mode": ACT_MODE[a["fn"]], "alpha": float(a.get("alpha", 0.3))}))
+            done.add(n)
+        elif L.op == "binary":
+            cover = [n]
+            out = n
+            mode = 0
+            c = single(n)
+            if act_mode(c):
+                mode = act_mode(c)
+                cover.append(c)
+                out = c
+            steps.append(Step("binary", out, [R(i) for i in L.inputs], cover, {"fn": a["fn"], "act": mode}))
+            done.update(cover)
+        elif L.op in ("rescale", "normalization"):
+            steps.append(Step("affine", n, [R(L.inputs[0])], [n], {"layer": n}))
+            done.add(n)
+        elif L.op == "gmp":
+            steps.append(Step("gmp", n, [R(L.inputs[0])], [n]))
+            done.add(n)
+        elif L.op == "reshape":
+            src_shape = g.layers[L.inputs[0]].out_shape
+            if src_shape[-1] != L.out_shape[-1] and (src_shape[-1] % 8 or L.out_shape[-1] % 8):
+                raise NotImplementedError(f"Reshape {src_shape} -> {L.out_shape} ({n}): channels are padded to 8")
+            if n in outset:
+                steps.append(Step("copy", n, [R(L.inputs[0])], [n]))
+                done.add(n)
+            else:
+                alias[n] = alias.get(L.inputs[0], L.inputs[0])
+                done.add(n)
+                continue
         elif L.op == "concat":
             steps.append(Step("concat", n, [R(i) for i in L.inputs], [n],
                               {"channels": [g.layers[i].out_shape[-1] for i in L.inputs]}))
@@ -238,10 +293,14 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
             done.add(n)
         elif L.op == "dense":
             act = a.get("activation")
-            if act not in (None, "linear", "relu", "softmax"):
-                raise NotImplementedError(f"Dense activation {act!r} ({n})")
-            steps.append(Step("dense", n, [R(L.inputs[0])], [n],
-                              {"units": a["units"], "softmax": act == "softmax", "relu": int(act == "relu")}))
+            mode = 0 if act == "softmax" else own_act(n, L)
+            if mode > 2:                        # not an MFMA-epilogue activation: its own step
+                steps.append(Step("dense", n + "#preact", [R(L.inputs[0])], [n],
+                                  {"units": a["units"], "softmax": False, "relu": 0}))
+                steps.append(Step("act", n, [n + "#preact"], [], {"mode": mode, "alpha": 0.3}))
+            else:
+                steps.append(Step("dense", n, [R(L.inputs[0])], [n],
+                                  {"units": a["units"], "softmax": act == "softmax", "relu": mode}))
             done.add(n)
         elif L.op == "softmax":
             steps.append(Step("softmax", n, [R(L.inputs[0])], [n]))

@@ -136,6 +136,21 @@ PYBIND11_MODULE(_C, m) {
     check(adapt::avgpool(P<const bf16>(x), P<bf16>(y), B, H, W, Cp, OH, OW, KH, KW, Sd, pad_t, pad_l, S(s)),
           "avgpool");
   });
+  m.def("act", [](u64 x, u64 y, size_t elems, int mode, float alpha, u64 s) {
+    check(adapt::act(P<const bf16>(x), P<bf16>(y), elems, mode, alpha, S(s)), "act");
+  });
+  m.def("binary", [](u64 a, u64 b, u64 y, size_t elems, int Cp, int bcast_hw, int op, int act_mode, u64 s) {
+    check(adapt::binary(P<const bf16>(a), P<const bf16>(b), P<bf16>(y), elems, Cp, bcast_hw, op, act_mode, S(s)),
+          "binary");
+  });
+  m.def("gap_large_slices", &adapt::gap_large_slices);
+  m.def("gap_large", [](u64 x, u64 y, u64 y32, u64 part, int B, int HW, int Cp, u64 s) {
+    check(adapt::gap_large(P<const bf16>(x), P<bf16>(y), P<float>(y32), P<float>(part), B, HW, Cp, S(s)),
+          "gap_large");
+  });
+  m.def("gmp", [](u64 x, u64 y, int B, int HW, int Cp, u64 s) {
+    check(adapt::gmp(P<const bf16>(x), P<bf16>(y), B, HW, Cp, S(s)), "gmp");
+  });
   m.def("concat_into", [](u64 x, int Cx, int Cpx, u64 y, int Cpy, int off, int zero_from, size_t pixels, u64 s) {
     check(adapt::concat_into(P<const bf16>(x), Cx, Cpx, P<bf16>(y), Cpy, off, zero_from, pixels, S(s)),
           "concat_into");

@@ -20,11 +20,35 @@ union V8 {
   bf16 e[8];
 };
 
-// Fused activation of the epilogues and eltwise kernels: 0 none, 1 ReLU,
-// 2 ReLU6 (Keras ReLU(max_value=6), MobileNetV2).
-__device__ __forceinline__ float act_f(float v, int mode) {
+// Activations of the fused epilogues and the eltwise kernels (Keras names):
+//   0 linear, 1 relu, 2 relu6 (ReLU(max_value=6)), 3 swish / silu, 4 sigmoid, 5 tanh,
+//   6 hard_sigmoid (Keras 2: clip(0.2x + 0.5)), 7 hard_swish (x * relu6(x + 3) / 6),
+//   8 gelu (erf form), 9 elu, 10 selu, 11 softplus, 12 leaky_relu (slope alpha)
+enum ActMode { ACT_LINEAR = 0, ACT_RELU, ACT_RELU6, ACT_SWISH, ACT_SIGMOID, ACT_TANH, ACT_HARD_SIGMOID,
+               ACT_HARD_SWISH, ACT_GELU, ACT_ELU, ACT_SELU, ACT_SOFTPLUS, ACT_LEAKY_RELU };
+// The MFMA conv epilogues take the ReLU family only (two selects; the wider
+// switch below, inlined into every tile config, doubled their code and compile
+// time): runtime/plan.py runs other activations after a conv as their own step.
+__device__ __forceinline__ float act_relu(float v, int mode) {
   v = mode ? fmaxf(v, 0.f) : v;
-  return mode == 2 ? fminf(v, 6.f) : v;
+  return mode == ACT_RELU6 ? fminf(v, 6.f) : v;
+}
+
+__device__ __forceinline__ float act_f(float v, int mode, float alpha = 0.3f) {
+  if (mode <= ACT_RELU6) return act_relu(v, mode);
+  switch (mode) {
+    case ACT_SWISH: return v / (1.f + __expf(-v));
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case ACT_TANH: return tanhf(v);
+    case ACT_HARD_SIGMOID: return fminf(fmaxf(0.2f * v + 0.5f, 0.f), 1.f);
+    case ACT_HARD_SWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678f));
+    case ACT_ELU: return v > 0.f ? v : __expf(v) - 1.f;
+    case ACT_SELU: return 1.0507009873554805f * (v > 0.f ? v : 1.6732632423543772f * (__expf(v) - 1.f));
+    case ACT_SOFTPLUS: return v > 20.f ? v : log1pf(__expf(v));
+    case ACT_LEAKY_RELU: return v > 0.f ? v : alpha * v;
+    default: return v;
+  }
 }
 
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be

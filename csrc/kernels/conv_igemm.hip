@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvParams p) {
     const EpiDst d = epi_dst(p, n);
     if (d.relu) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], d.relu);
+      for (int t = 0; t < 8; ++t) v[t] = act_relu(v[t], d.relu);
     }
     if (OUT_F32) {
       float* o = (float*)d.base + (size_t)m * d.ld + d.col;

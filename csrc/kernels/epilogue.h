@@ -84,7 +84,7 @@ __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float*
       }
       if (d.relu) {
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], d.relu);
+        for (int t = 0; t < 8; ++t) v[t] = act_relu(v[t], d.relu);
       }
       if (OUT_F32) {
         float* o = (float*)d.base + (size_t)m * d.ld + d.col;

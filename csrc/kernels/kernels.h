@@ -14,7 +14,7 @@ struct ConvParams {
   int OH, OW, N;
   int KH, KW, stride, pad_t, pad_l;
   int M, K, Kpad, ldo;
-  int relu;         // fused activation: 0 none, 1 ReLU, 2 ReLU6 (common.h act_f)
+  int relu;         // fused activation: 0 none, 1 ReLU, 2 ReLU6 (common.h act_relu)
   int ksplit;       // >= 1: split-K slices (fp32 slabs in ws + reduce); < 0: stream-K over -ksplit x 256 blocks
   int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
   int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_sk_plan)
@@ -73,6 +73,13 @@ hipError_t dwconv(const bf16* x, const float* w, const float* bias, bf16* y, int
                   int OW, int KH, int KW, int stride, int pad_t, int pad_l, int act, hipStream_t s);
 hipError_t avgpool(const bf16* x, bf16* y, int B, int H, int W, int Cp, int OH, int OW, int KH, int KW, int S,
                    int pad_t, int pad_l, hipStream_t s);
+hipError_t act(const bf16* x, bf16* y, size_t elems, int mode, float alpha, hipStream_t s);   // common.h ActMode
+hipError_t binary(const bf16* a, const bf16* b, bf16* y, size_t elems, int Cp, int bcast_hw, int op, int act_mode,
+                  hipStream_t s);
+hipError_t gmp(const bf16* x, bf16* y, int B, int HW, int Cp, hipStream_t s);
+int gap_large_slices(int B, int HW);
+// GAP over large maps: part = [B][gap_large_slices][Cp] fp32 scratch
+hipError_t gap_large(const bf16* x, bf16* y, float* y32, float* part, int B, int HW, int Cp, hipStream_t s);
 hipError_t concat_into(const bf16* x, int Cx, int Cpx, bf16* y, int Cpy, int off, int zero_from, size_t pixels,
                        hipStream_t s);
 hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,

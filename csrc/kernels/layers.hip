@@ -48,10 +48,13 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16* __restrict__ x,
         v.u = *(const u32x4*)(x + (((size_t)b * H + ih) * W + iw) * Cp + c0);
         const float* wt = w + ((size_t)kh * KW + kw) * Cp + c0;
         const f32x4 w0 = *(const f32x4*)wt, w1 = *(const f32x4*)(wt + 4);
-        acc[0] += bf2f(v.e[0]) * w0[0]; acc[1] += bf2f(v.e[1]) * w0[1];
-        acc[2] += bf2f(v.e[2]) * w0[2]; acc[3] += bf2f(v.e[3]) * w0[3];
-        acc[4] += bf2f(v.e[4]) * w1[0]; acc[5] += bf2f(v.e[5]) * w1[1];
-        acc[6] += bf2f(v.e[6]) * w1[2]; acc[7] += bf2f(v.e[7]) * w1[3];
+        float xf[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xf[t] = bf2f(v.e[t]);
+        acc[0] += xf[0] * w0[0]; acc[1] += xf[1] * w0[1];
+        acc[2] += xf[2] * w0[2]; acc[3] += xf[3] * w0[3];
+        acc[4] += xf[4] * w1[0]; acc[5] += xf[5] * w1[1];
+        acc[6] += xf[6] * w1[2]; acc[7] += xf[7] * w1[3];
       }
     }
     V8 o;
@@ -191,6 +194,171 @@ __global__ __launch_bounds__(256) void concat_scalar_kernel(const bf16* __restri
     if (c < Cx) y[p * Cpy + off + c] = x[p * Cpx + c];
     else y[p * Cpy + zero_from + (c - Cx)] = f2bf(0.f);
   }
+}
+
+// Standalone activation (any ActMode, LeakyReLU slope alpha) over bf16 chunks.
+__global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, size_t chunks,
+                                                  int mode, float alpha) {
+  for (size_t i = gtid(); i < chunks; i += gstride()) {
+    V8 v, o;
+    v.u = ((const u32x4*)x)[i];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(bf2f(v.e[t]), mode, alpha));
+    ((u32x4*)y)[i] = o.u;
+  }
+}
+
+// Element-wise binary op (Keras Multiply / Subtract / Maximum / Minimum / Average / Add) of a [P][Cp] tensor
+// with b, where b is either the same shape or one [Cp] row per image (bcast_hw = H*W pixels share it: the
+// squeeze-excite Multiply of EfficientNet, x * se[b, 1, 1, c]).
+enum BinOp { BIN_ADD = 0, BIN_SUB, BIN_MUL, BIN_MAX, BIN_MIN, BIN_AVG };
+__global__ __launch_bounds__(256) void binary_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                     bf16* __restrict__ y, size_t chunks, int cpr, int bcast_hw,
+                                                     int op, int act) {
+  for (size_t i = gtid(); i < chunks; i += gstride()) {
+    size_t bi = i;
+    if (bcast_hw) {
+      const size_t pix = i / cpr;
+      bi = (pix / bcast_hw) * cpr + (i % cpr);
+    }
+    V8 va, vb, o;
+    va.u = ((const u32x4*)a)[i];
+    vb.u = ((const u32x4*)b)[bi];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float p = bf2f(va.e[t]), q = bf2f(vb.e[t]);
+      float r;
+      switch (op) {
+        case BIN_SUB: r = p - q; break;
+        case BIN_MUL: r = p * q; break;
+        case BIN_MAX: r = fmaxf(p, q); break;
+        case BIN_MIN: r = fminf(p, q); break;
+        case BIN_AVG: r = 0.5f * (p + q); break;
+        default: r = p + q;
+      }
+      o.e[t] = f2bf(act_f(r, act));
+    }
+    ((u32x4*)y)[i] = o.u;
+  }
+}
+
+// Global max pool: block (image, 64 chunks), 4 pixel groups, LDS combine (as head.hip's GAP).
+__global__ __launch_bounds__(256) void gmp_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int HW, int Cp) {
+  __shared__ float part[4][64][9];
+  const int b = blockIdx.y;
+  const int ch = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int cc = blockIdx.x * 64 + ch;
+  const bool ok = cc * 8 < Cp;
+  float m[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) m[t] = -INFINITY;
+  if (ok) {
+    const bf16* base = x + (size_t)b * HW * Cp + cc * 8;
+    for (int i = grp; i < HW; i += 4) {
+      V8 v;
+      v.u = *(const u32x4*)(base + (size_t)i * Cp);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) m[t] = fmaxf(m[t], bf2f(v.e[t]));
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) part[grp][ch][t] = m[t];
+  __syncthreads();
+  if (grp != 0 || !ok) return;
+  V8 o;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    o.e[t] = f2bf(fmaxf(fmaxf(part[0][ch][t], part[1][ch][t]), fmaxf(part[2][ch][t], part[3][ch][t])));
+  *(u32x4*)(y + (size_t)b * Cp + cc * 8) = o.u;
+}
+
+// Global average pool over LARGE maps (EfficientNet's squeeze-excite at 112x112 .. 28x28), where head.hip's
+// one-block-per-image GAP leaves most of the chip idle.  Pass 1: grid (S pixel slices, B); a block sums its
+// slice for a group of up to 256 channel chunks (lane = chunk, the remaining threads stride the pixels) and
+// reduces in LDS to one fp32 partial per channel.  Pass 2: sum of the S partials / HW -> bf16.
+__global__ __launch_bounds__(256) void gap_part_kernel(const bf16* __restrict__ x, float* __restrict__ part,
+                                                       int HW, int Cp, int S) {
+  __shared__ float red[256][9];
+  const int b = blockIdx.y, sl = blockIdx.x;
+  const int cpr = Cp / 8;
+  const int p0 = (int)((long long)HW * sl / S), p1 = (int)((long long)HW * (sl + 1) / S);
+  for (int cg = 0; cg < cpr; cg += 256) {
+    const int nc = min(256, cpr - cg);
+    const int lanes = 256 / nc;                      // pixel lanes per chunk
+    const int ch = threadIdx.x % nc, pl = threadIdx.x / nc;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (pl < lanes) {
+      const bf16* base = x + (size_t)b * HW * Cp + (size_t)(cg + ch) * 8;
+      for (int p = p0 + pl; p < p1; p += lanes) {
+        V8 v;
+        v.u = *(const u32x4*)(base + (size_t)p * Cp);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] += bf2f(v.e[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) red[threadIdx.x][t] = acc[t];
+    __syncthreads();
+    if (threadIdx.x < nc) {
+      float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int l = 0; l < lanes; ++l)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sum[t] += red[l * nc + threadIdx.x][t];
+      float* d = part + ((size_t)b * S + sl) * Cp + (size_t)(cg + threadIdx.x) * 8;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) d[t] = sum[t];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void gap_finish_kernel(const float* __restrict__ part, bf16* __restrict__ y,
+                                                         float* __restrict__ y32, int B, int HW, int Cp, int S) {
+  const size_t total = (size_t)B * Cp;
+  const float inv = 1.f / (float)HW;
+  for (size_t i = gtid(); i < total; i += gstride()) {
+    const size_t b = i / Cp, c = i % Cp;
+    float sum = 0.f;
+    for (int sl = 0; sl < S; ++sl) sum += part[(b * S + sl) * Cp + c];
+    if (y) y[i] = f2bf(sum * inv);
+    if (y32) y32[i] = sum * inv;
+  }
+}
+
+int gap_large_slices(int B, int HW) {
+  int s = (512 + B - 1) / B;                       // ~2 blocks per CU in all
+  const int cap = HW / 64 > 0 ? HW / 64 : 1;       // >= 64 pixels per slice
+  return s < 1 ? 1 : (s > cap ? cap : s);
+}
+
+hipError_t gap_large(const bf16* x, bf16* y, float* y32, float* part, int B, int HW, int Cp, hipStream_t s) {
+  if (Cp % 8) return hipErrorInvalidValue;
+  const int S = gap_large_slices(B, HW);
+  hipLaunchKernelGGL(gap_part_kernel, dim3(S, B), dim3(256), 0, s, x, part, HW, Cp, S);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gap_finish_kernel, dim3(grid_of((size_t)B * Cp)), dim3(256), 0, s, part, y, y32, B, HW, Cp, S);
+  return hipGetLastError();
+}
+
+hipError_t act(const bf16* x, bf16* y, size_t elems, int mode, float alpha, hipStream_t s) {
+  if (elems % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(act_kernel, dim3(grid_of(elems / 8)), dim3(256), 0, s, x, y, elems / 8, mode, alpha);
+  return hipGetLastError();
+}
+
+hipError_t binary(const bf16* a, const bf16* b, bf16* y, size_t elems, int Cp, int bcast_hw, int op, int act_mode,
+                  hipStream_t s) {
+  if (elems % 8 || Cp % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(binary_kernel, dim3(grid_of(elems / 8)), dim3(256), 0, s, a, b, y, elems / 8, Cp / 8, bcast_hw,
+                     op, act_mode);
+  return hipGetLastError();
+}
+
+hipError_t gmp(const bf16* x, bf16* y, int B, int HW, int Cp, hipStream_t s) {
+  if (Cp % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gmp_kernel, dim3((Cp / 8 + 63) / 64, B), dim3(256), 0, s, x, y, HW, Cp);
+  return hipGetLastError();
 }
 
 hipError_t dwconv(const bf16* x, const float* w, const float* bias, bf16* y, int B, int H, int W, int Cp, int OH,

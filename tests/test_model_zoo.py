@@ -134,12 +134,12 @@ def test_keras_json_import_every_layer_class(fmt):
 
 def test_keras_json_rejects_unsupported():
     d = json.loads(_small_keras(2))
-    d["config"]["layers"][9]["config"]["activation"] = "gelu"
-    with pytest.raises(NotImplementedError, match="gelu"):
+    d["config"]["layers"][9]["config"]["activation"] = "mish"
+    with pytest.raises(NotImplementedError, match="mish"):
         from_keras_json(json.dumps(d))
     d = json.loads(_small_keras(2))
-    d["config"]["layers"][1]["class_name"] = "SeparableConv2D"
-    with pytest.raises(NotImplementedError, match="SeparableConv2D"):
+    d["config"]["layers"][1]["class_name"] = "Conv3D"
+    with pytest.raises(NotImplementedError, match="Conv3D"):
         from_keras_json(json.dumps(d))
 
 
@@ -227,3 +227,91 @@ def test_cli_takes_a_keras_json_file_and_weight_list(tmp_path, capsys):
     np.testing.assert_allclose(m.predict(x, device="cpu"), ref.predict(x, device="cpu"), rtol=1e-6, atol=1e-7)
     cli.cmd_summary(["--model", str(arch)])         # (cli.main ends the process with os._exit)
     assert "Total params" in capsys.readouterr().out
+
+
+EFFNET_PARAMS = {"efficientnetb0": 5_330_571, "efficientnetb1": 7_856_239, "efficientnetb2": 9_177_569,
+                 "efficientnetb3": 12_320_535, "efficientnetb4": 19_466_823, "efficientnetb7": 66_658_687}
+
+
+@pytest.mark.parametrize("name", sorted(EFFNET_PARAMS))
+def test_efficientnet_param_totals_match_keras(name):
+    g = build_model(name)
+    assert g.count_params() == EFFNET_PARAMS[name]
+
+
+def test_efficientnet_plan_and_slicing():
+    g = build_model("efficientnetb0", input_shape=(64, 64, 3))
+    steps = compile_plan(g)
+    kinds = [s.kind for s in steps]
+    assert kinds[:3] == ["pack", "affine", "affine"] and "add" not in kinds        # residual Adds fused (drop-connect skipped)
+    assert kinds.count("binary") == 16 and kinds.count("dwconv") == 16
+    assert all(s.p["relu"] <= 2 for s in steps if s.kind == "conv")                 # swish never inside an MFMA epilogue
+    w = init_weights(g, 0)
+    x = torch.rand(2, 64, 64, 3) * 255
+    full = ReferenceExecutor(g, w)(x)
+    cuts, _ = planner.plan_cuts(g, 3, batch=32)
+    vals = {g.input: x}
+    for s in slicer.partition(g, cuts):
+        sg = slicer.subgraph(g, s)
+        compile_plan(sg, sg.output_names)
+        vals.update(ReferenceExecutor(sg, w).run({k: vals[k] for k in sg.input_names}))
+    torch.testing.assert_close(vals[g.output], full, rtol=1e-5, atol=1e-6)
+    g2 = from_keras_json(to_keras_json(g))
+    assert json.loads(g2.to_json()) == json.loads(g.to_json())
+
+
+def _se_keras():
+    """Keras-2 JSON with the layer classes of squeeze-excite / Xception-style models."""
+    L = _k2
+    layers = [
+        L("InputLayer", "img", [], batch_input_shape=[None, 12, 12, 3], dtype="float32"),
+        L("Rescaling", "rescaling", ["img"], scale=1.0 / 255, offset=-0.5),
+        L("Normalization", "normalization", ["rescaling"], axis=[-1]),
+        L("SeparableConv2D", "sep", ["normalization"], filters=16, kernel_size=[3, 3], strides=[1, 1],
+          padding="same", depth_multiplier=1, activation="linear", use_bias=True),
+        L("LeakyReLU", "leaky", ["sep"], alpha=0.2),
+        L("Activation", "hs", ["leaky"], activation="hard_swish"),
+        L("GlobalAveragePooling2D", "sq", ["hs"], keepdims=True),
+        L("Conv2D", "se1", ["sq"], filters=8, kernel_size=[1, 1], activation="swish", use_bias=True),
+        L("Conv2D", "se2", ["se1"], filters=16, kernel_size=[1, 1], activation="sigmoid", use_bias=True),
+        L("Multiply", "excite", ["hs", "se2"]),
+        L("Subtract", "sub", ["excite", "hs"]),
+        L("Maximum", "mx", ["sub", "excite"]),
+        L("Activation", "gelu", ["mx"], activation="gelu"),
+        L("GlobalMaxPooling2D", "gmp", ["gelu"]),
+        L("Reshape", "rs", ["gmp"], target_shape=[1, 1, 16]),
+        L("Flatten", "fl", ["rs"]),
+        L("Dense", "predictions", ["fl"], units=8, activation="softmax", use_bias=True),
+    ]
+    return json.dumps({"class_name": "Functional", "config": {"name": "se", "layers": layers,
+                                                              "input_layers": [["img", 0, 0]],
+                                                              "output_layers": [["predictions", 0, 0]]}})
+
+
+def test_keras_json_se_and_activation_layers():
+    g = from_keras_json(_se_keras())
+    ops = [g.layers[n].op for n in g.order]
+    assert ops == ["input", "rescale", "normalization", "dwconv", "conv", "act", "act", "gap", "conv", "conv",
+                   "binary", "binary", "binary", "act", "gmp", "reshape", "flatten", "dense"]
+    assert g.layers["sep/depthwise"].out_shape == (12, 12, 3) and g.layers["sep"].out_shape == (12, 12, 16)
+    assert g.layers["sq"].out_shape == (1, 1, 16)
+    m = Model.from_keras_json(_se_keras(), seed=4)
+    assert len(m.get_weights()) == 3 + 3 + 2 + 2 + 2        # normalization, separable conv, se1, se2, dense
+    x = np.random.default_rng(0).uniform(0, 255, (2, 12, 12, 3)).astype(np.float32)
+    y = m.predict(x, device="cpu")
+    assert y.shape == (2, 8) and np.isfinite(y).all()
+    kinds = [s.kind for s in compile_plan(g)]
+    assert kinds == ["pack", "affine", "affine", "dwconv", "conv", "act", "act", "gap", "conv", "act", "conv",
+                     "act", "binary", "binary", "binary", "gmp", "dense"]
+    # the exporter writes the same layer classes back (SeparableConv2D as its two halves)
+    g2 = from_keras_json(to_keras_json(g))
+    assert json.loads(g2.to_json()) == json.loads(g.to_json())
+
+
+def test_reference_activations_match_keras_definitions():
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.reference import _act
+    x = torch.linspace(-5, 5, 101)
+    torch.testing.assert_close(_act(x, "hard_sigmoid"), torch.clamp(0.2 * x + 0.5, 0, 1))
+    torch.testing.assert_close(_act(x, "swish"), x * torch.sigmoid(x))
+    torch.testing.assert_close(_act(x, "relu6"), torch.clamp(x, 0, 6))
+    torch.testing.assert_close(_act(x, "leaky_relu", 0.2), torch.where(x > 0, x, 0.2 * x))

@@ -126,3 +126,69 @@ def test_keras_json_model_vs_oracle():
     g = kj.from_keras_json(kj.to_keras_json(zoo.build_model("mobilenet_v2", input_shape=(96, 96, 3), classes=10)))
     assert json.loads(g.to_json())["layers"][0]["op"] == "input"
     _model_check(g, res.init_weights(g, 1), 4, "out_relu", (96, 96, 3), rel_tol=5e-2)
+
+
+ACT_NAMES = ["relu", "relu6", "swish", "sigmoid", "tanh", "hard_sigmoid", "hard_swish", "gelu", "elu", "selu",
+             "softplus", "leaky_relu"]
+
+
+@pytest.mark.parametrize("fn", ACT_NAMES)
+def test_act_kernel_vs_keras_definition(ops, fn):
+    E, _ = ops
+    ref_mod = importlib.import_module(f"{PKG}.ops.reference")
+    x = (torch.randn(4, 9, 7, 24, device="cuda") * 3).to(torch.bfloat16)
+    out = torch.empty_like(x)
+    E.act(x, out, E.ACT_MODES[fn], alpha=0.2)
+    ref = ref_mod._act(x.float(), fn, 0.2)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("fn", ["add", "sub", "mul", "max", "min", "avg"])
+@pytest.mark.parametrize("bcast", [False, True])
+def test_binary_kernel(ops, fn, bcast):
+    E, _ = ops
+    a = torch.randn(3, 5, 6, 32, device="cuda").to(torch.bfloat16)
+    b = torch.randn(3, 1, 1, 32, device="cuda").to(torch.bfloat16) if bcast else torch.randn_like(a)
+    out = torch.empty_like(a)
+    E.binary(a, b, out, fn, act_mode=E.ACT_MODES["swish"] if fn == "mul" else 0)
+    af, bf = a.float(), b.float()
+    ref = {"add": af + bf, "sub": af - bf, "mul": af * bf, "max": torch.maximum(af, bf),
+           "min": torch.minimum(af, bf), "avg": 0.5 * (af + bf)}[fn]
+    if fn == "mul":
+        ref = ref * torch.sigmoid(ref)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_gmp_kernel(ops):
+    E, _ = ops
+    x = torch.randn(4, 7, 7, 1040, device="cuda").to(torch.bfloat16)
+    out = torch.empty(4, 1040, device="cuda", dtype=torch.bfloat16)
+    E.gmp(x, out)
+    torch.testing.assert_close(out, x.amax(dim=(1, 2)))
+
+
+def test_efficientnet_b0_vs_oracle():
+    zoo = importlib.import_module(f"{PKG}.models.zoo")
+    res = importlib.import_module(f"{PKG}.models.resnet")
+    g = zoo.build_model("efficientnetb0")
+    _model_check(g, res.init_weights(g, 0), 4, "avg_pool", (224, 224, 3), rel_tol=5e-2)
+
+
+def test_keras_json_se_model_vs_oracle():
+    kj = importlib.import_module(f"{PKG}.graph.keras_json")
+    res = importlib.import_module(f"{PKG}.models.resnet")
+    from tests.test_model_zoo import _se_keras
+    g = kj.from_keras_json(_se_keras())
+    _model_check(g, res.init_weights(g, 2), 4, "gelu", (12, 12, 3), rel_tol=5e-2)
+
+
+@pytest.mark.parametrize("B,H,W,C", [(32, 112, 112, 32), (4, 56, 56, 144), (3, 33, 37, 2056), (2, 7, 7, 2048)])
+def test_gap_large_and_small_maps(ops, B, H, W, C):
+    E, _ = ops
+    x = torch.randn(B, H, W, C, device="cuda").to(torch.bfloat16)
+    out = torch.empty(B, C, device="cuda", dtype=torch.bfloat16)
+    need = E.gap_scratch_elems(B, H * W, C)
+    scratch = torch.empty(max(need, 1), device="cuda", dtype=torch.float32)
+    E.gap(x, out=out, scratch=scratch)
+    torch.testing.assert_close(out.float(), x.float().mean(dim=(1, 2)), rtol=1e-2, atol=1e-2)
+    assert (need > 0) == (H * W >= E.GAP_LARGE_HW)

@@ -61,6 +61,8 @@ def main():
         ex._logits = {0: logits_saved[i]} if i in logits_saved else {}
         dense_saved = ex._dense_part
         ex._dense_part = {0: dense_saved[i]} if i in dense_saved else {}
+        gap_saved = ex._gap_part
+        ex._gap_part = {0: gap_saved[i]} if i in gap_saved else {}
         side_saved = ex._side
         ex._side = {}
         relay_saved = ex.relay
@@ -78,6 +80,7 @@ def main():
         finally:
             ex.steps, ex.packed, ex.cfg, ex._logits, ex.relay = saved, packed_saved, cfg_saved, logits_saved, relay_saved
             ex._dense_part = dense_saved
+            ex._gap_part = gap_saved
             ex._side = side_saved
         flop = 0
         if st.kind in ("conv", "dense"):
