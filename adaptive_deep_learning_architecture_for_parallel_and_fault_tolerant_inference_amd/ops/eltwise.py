@@ -137,7 +137,7 @@ def gap_scratch_elems(B: int, HW: int, C: int) -> int:
 def gap(x: torch.Tensor, out: Optional[torch.Tensor] = None, out32: Optional[torch.Tensor] = None,
         stream=None, scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Global average pool [B,H,W,C] -> [B,C] (bf16 `out` and/or fp32 `out32`).  Maps of
-    >= GAP_LARGE_HW pixels take the sliced two-pass kernel and need `scratch`."""
+    >= GAP_LARGE_HW pixels take the sliced two-pass kernel and its fp32 `scratch`."""
     _chk(x, name="x")
     B, H, W, C = x.shape
     if C % 8:
@@ -152,7 +152,9 @@ def gap(x: torch.Tensor, out: Optional[torch.Tensor] = None, out32: Optional[tor
             raise ValueError("gap: bad out32")
     need = gap_scratch_elems(B, H * W, C)
     if need:
-        if scratch is None or scratch.numel() < need or scratch.dtype != torch.float32:
+        if scratch is None:               # the executor passes a preallocated one
+            scratch = torch.empty(need, dtype=torch.float32, device=x.device)
+        if scratch.numel() < need or scratch.dtype != torch.float32:
             raise ValueError(f"gap over {H}x{W}: needs an fp32 scratch of {need} elements")
         kernels().gap_large(ptr(x), ptr(out), ptr(out32), ptr(scratch), B, H * W, C, stream_handle(stream))
     else:
