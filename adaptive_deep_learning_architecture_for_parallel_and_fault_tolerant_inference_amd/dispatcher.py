@@ -410,7 +410,7 @@ class DEFER:
         per array in Keras `get_weights()` order (read back by `Node._recv_weights`)."""
         sock.sendall(len(weights).to_bytes(8, "big"))
         for w in weights:
-            socket_send(self._comp(np.ascontiguousarray(w)), sock, chunk_size or self.chunk_size)
+            socket_send(self._comp(np.require(w, None, ["C"])), sock, chunk_size or self.chunk_size)
 
     def _update_localhost(self, conn, raw_ip: str, worker_cli: dict) -> None:
         """`src/dispatcher.py:164-173`: a peer address outside `computeNodes` maps to

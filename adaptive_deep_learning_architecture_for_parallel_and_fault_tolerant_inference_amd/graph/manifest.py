@@ -83,12 +83,12 @@ def build_manifest(g: Graph, s: Slice, weights: Dict[str, np.ndarray]) -> (Slice
     arrays = []
     wspecs = []
     for name, shp in g.weight_specs(s.layers):
-        a = np.ascontiguousarray(weights[name], dtype=np.float32)
+        a = np.require(weights[name], np.float32, ["C"])       # (ascontiguousarray makes 0-d 1-d)
         if tuple(a.shape) != tuple(shp):
             raise ValueError(f"{name}: shape {a.shape} != {shp}")
         arrays.append(a)
         wspecs.append({"name": name, "shape": list(shp), "dtype": "float32",
-                       "xxh32": int(runtime().xxh32(a.view(np.uint8).reshape(-1)))})
+                       "xxh32": int(runtime().xxh32(a.reshape(-1).view(np.uint8)))})
     m = SliceManifest(g.name, s.index + 1, s.name, sg.to_json(),
                       [_tensor_spec(g, t) for t in s.inputs], [_tensor_spec(g, t) for t in s.outputs],
                       wspecs, s.start, s.end)
@@ -101,7 +101,7 @@ def verify_arrays(m: SliceManifest, arrays: Sequence[np.ndarray]) -> None:
     for spec, a in zip(m.weights, arrays):
         if list(a.shape) != list(spec["shape"]):
             raise ValueError(f"{spec['name']}: shape {a.shape} != {spec['shape']}")
-        h = int(runtime().xxh32(np.ascontiguousarray(a).view(np.uint8).reshape(-1)))
+        h = int(runtime().xxh32(np.require(a, None, ["C"]).reshape(-1).view(np.uint8)))
         if "xxh32" in spec and h != spec["xxh32"]:
             raise ValueError(f"{spec['name']}: checksum mismatch")
 
@@ -160,7 +160,7 @@ def save_slice(path_prefix: str, m: SliceManifest, arrays: Sequence[np.ndarray])
     os.makedirs(os.path.dirname(os.path.abspath(path_prefix)), exist_ok=True)
     with open(path_prefix + ".json", "w") as f:
         f.write(m.to_json())
-    save_file({f"{i:05d}": np.ascontiguousarray(a) for i, a in enumerate(arrays)}, path_prefix + ".safetensors",
+    save_file({f"{i:05d}": np.require(a, None, ["C"]) for i, a in enumerate(arrays)}, path_prefix + ".safetensors",
               metadata={"format": FORMAT, "order": json.dumps(m.weight_names)})
 
 
@@ -180,7 +180,7 @@ def save_model(path: str, g: Graph, weights: Dict[str, np.ndarray]) -> None:
     with open(path + ".graph.json", "w") as f:
         f.write(g.to_json())
     names = [n for n, _ in g.weight_specs()]
-    save_file({n: np.ascontiguousarray(weights[n], np.float32) for n in names}, path + ".safetensors",
+    save_file({n: np.require(weights[n], np.float32, ["C"]) for n in names}, path + ".safetensors",
               metadata={"format": "adapt-model-v1"})
 
 

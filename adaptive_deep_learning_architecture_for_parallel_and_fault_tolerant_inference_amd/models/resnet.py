@@ -167,5 +167,5 @@ def set_weights(g: Graph, arrays: List[np.ndarray], layers: Optional[List[str]] 
     for (name, shp), arr in zip(specs, arrays):
         if tuple(arr.shape) != tuple(shp):
             raise ValueError(f"{name}: expected shape {shp}, got {arr.shape}")
-        out[name] = np.ascontiguousarray(arr, dtype=np.float32)
+        out[name] = np.require(arr, np.float32, ["C"])      # keeps 0-d weights (Normalization count) 0-d
     return out

@@ -98,3 +98,32 @@ def test_defer_two_gpu_stages_collective_links(link_codec):
         d.shutdown(stop_workers=True)
         for n in nodes:
             n.stop()
+
+
+@pytest.mark.parametrize("name,cut", [("mobilenet_v2", "block_6_project_BN"), ("efficientnetb0", "block4a_project_bn")])
+def test_defer_two_gpu_stages_other_families(name, cut):
+    """Model families beyond ResNet through DEFER: two GPU stages over the
+    collective data plane (gloo rehearsal of RCCL on the box's one GPU)."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.model import application
+    m = application(name, seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
+              min_workers=2, transport="gloo")
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"z{i}",
+                  heartbeat_ttl=1.0) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, [cut], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(3)
+        xs = [rng.uniform(0, 255, (4, 224, 224, 3)).astype(np.float32) for _ in range(3)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=120) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert np.abs(got - want).sum(-1).max() < 0.1
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()

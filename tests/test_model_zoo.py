@@ -184,10 +184,14 @@ def test_mobilenet_plan_fuses_relu6_and_residuals():
     assert conv1.p["conv"] == "Conv1" and conv1.p["pads"] == ((0, 1), (0, 1)) and conv1.p["relu"] == 2
 
 
-def test_defer_serves_a_keras_json_model():
-    """DEFER + two CPU Nodes on a model imported from Keras JSON, cut at a
-    multi-tensor frontier (the concat consumes both sides)."""
-    m = Model.from_keras_json(_small_keras(2), seed=1)
+@pytest.mark.parametrize("which", ["small", "se"])
+def test_defer_serves_a_keras_json_model(which):
+    """DEFER + two CPU Nodes on a model imported from Keras JSON: cut at a
+    multi-tensor frontier (the concat consumes both sides), and a squeeze-excite
+    model whose Normalization ships a 0-d weight (`count`)."""
+    js, cut = (_small_keras(2), "branch") if which == "small" else (_se_keras(), "hs")
+    m = Model.from_keras_json(js, seed=1)
+    shape = (2, 16, 16, 3) if which == "small" else (2, 12, 12, 3)
     d = DEFER(membership_port=0, result_port=0, worker_wait=10, ordered=True, batch=2)
     d.membership_server.start()
     nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu", node_id=f"k{i}",
@@ -196,8 +200,8 @@ def test_defer_serves_a_keras_json_model():
         n.run(block=False)
     try:
         inq, outq = queue.Queue(), queue.Queue()
-        threading.Thread(target=d.run_defer, args=(m, ["branch"], inq, outq), daemon=True).start()
-        xs = [np.random.default_rng(i).standard_normal((2, 16, 16, 3)).astype(np.float32) for i in range(3)]
+        threading.Thread(target=d.run_defer, args=(m, [cut], inq, outq), daemon=True).start()
+        xs = [np.random.default_rng(i).standard_normal(shape).astype(np.float32) for i in range(3)]
         for x in xs:
             inq.put(x)
         got = np.concatenate([outq.get(timeout=60) for _ in xs])
