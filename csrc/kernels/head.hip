@@ -8,8 +8,8 @@
 // ran M = 32 rows through 64-row tiles with a K loop of 32 latency-bound
 // steps plus a split-K reduce launch.  Here:
 //
-// * gap: a block takes (image, 512 channels); 4 pixel groups per channel chunk
-//   issue all their loads before summing, LDS reduction of the 4 partials;
+// * gap: a block takes (image, 256 channels); 8 pixel groups per channel chunk
+//   issue all their loads before summing, LDS reduction of the 8 partials;
 // * dense_partial: small-M GEMV on MFMA.  Block = 16 output columns x all M
 //   (<= 32) rows x one K slice; the whole K slice of A and B is loaded up front
 //   (one round trip), fp32 partials per K slice;
@@ -20,23 +20,25 @@
 namespace adapt {
 
 // ------------------------------------------------------------------ GAP
-// block (image b, channel block of 64 chunks = 512 channels); 256 threads = 64 chunks x 4 pixel groups
+// block (image b, channel block of 32 chunks = 256 channels); 256 threads = 32 chunks x 8 pixel groups
+// (bs=32 x 2048 channels: 256 blocks, one per CU)
+constexpr int GAP_CH = 32, GAP_PG = 8;
 __global__ __launch_bounds__(256) void gap2_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                    float* __restrict__ y32, int HW, int C) {
-  __shared__ float part[4][64][9];
+  __shared__ float part[GAP_PG][GAP_CH][9];
   const int b = blockIdx.y;
-  const int ch = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int cc = blockIdx.x * 64 + ch;                  // 8-channel chunk
+  const int ch = threadIdx.x % GAP_CH, grp = threadIdx.x / GAP_CH;
+  const int cc = blockIdx.x * GAP_CH + ch;              // 8-channel chunk
   const bool ok = cc * 8 < C;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (ok) {
     const bf16* base = x + (size_t)b * HW * C + cc * 8;
     constexpr int U = 4;
-    for (int i0 = grp; i0 < HW; i0 += 4 * U) {
+    for (int i0 = grp; i0 < HW; i0 += GAP_PG * U) {
       V8 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int i = i0 + 4 * u;
+        const int i = i0 + GAP_PG * u;
         v[u].u = i < HW ? *(const u32x4*)(base + (size_t)i * C) : (u32x4){0u, 0u, 0u, 0u};
       }
 #pragma unroll
@@ -54,7 +56,10 @@ __global__ __launch_bounds__(256) void gap2_kernel(const bf16* __restrict__ x, b
   float r[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    r[t] = (part[0][ch][t] + part[1][ch][t] + part[2][ch][t] + part[3][ch][t]) * inv;
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < GAP_PG; ++q) a += part[q][ch][t];
+    r[t] = a * inv;
     o.e[t] = f2bf(r[t]);
   }
   if (y) *(u32x4*)(y + (size_t)b * C + cc * 8) = o.u;
@@ -153,12 +158,65 @@ __global__ __launch_bounds__(256) void dense_finish_kernel(const float* __restri
 }
 
 hipError_t gap(const bf16* x, bf16* y, float* y32, int B, int HW, int C, hipStream_t s) {
-  dim3 grid((C / 8 + 63) / 64, B);
+  dim3 grid((C / 8 + GAP_CH - 1) / GAP_CH, B);
   hipLaunchKernelGGL(gap2_kernel, grid, dim3(256), 0, s, x, y, y32, HW, C);
   return hipGetLastError();
 }
 
 int dense_small_kslices(int K) { return (K + DH_MAXK - 1) / DH_MAXK; }
+
+// Register-resident finish for N <= 1024 (the ImageNet head): each thread owns up to 4 columns of the row,
+// issues all KS x 4 partial loads before the first add, and keeps the logits in registers through the
+// max / exp / sum passes (the generic kernel above round-trips them through LDS and loads serially).
+__global__ __launch_bounds__(256) void dense_finish_reg_kernel(const float* __restrict__ part,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ logits, float* __restrict__ probs,
+                                                               int M, int N, int KS) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float v[4];
+  bool ok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = tid + 256 * j;
+    ok[j] = i < N;
+    v[j] = (ok[j] && bias) ? bias[i] : 0.f;
+  }
+  for (int sl = 0; sl < KS; ++sl) {
+    const float* pr = part + ((size_t)sl * M + row) * N;
+    float t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j] = ok[j] ? pr[tid + 256 * j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += t[j];
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!ok[j]) continue;
+    if (logits) logits[(size_t)row * N + tid + 256 * j] = v[j];
+    mx = fmaxf(mx, v[j]);
+  }
+  if (!probs) return;
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) red[wv] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = ok[j] ? __expf(v[j] - mx) : 0.f;
+    sum += v[j];
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if (lane == 0) red[wv] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (ok[j]) probs[(size_t)row * N + tid + 256 * j] = v[j] * inv;
+}
 
 hipError_t dense_small(const bf16* x, const bf16* w, const float* bias, float* part, float* logits, float* probs,
                        int M, int N, int K, int Kpad, hipStream_t s) {
@@ -168,8 +226,11 @@ hipError_t dense_small(const bf16* x, const bf16* w, const float* bias, float* p
   hipLaunchKernelGGL(dense_partial_kernel, grid, dim3(64), 0, s, x, w, part, M, N, K, Kpad, DH_MAXK);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(dense_finish_kernel, dim3(M), dim3(256), (size_t)N * sizeof(float), s, part, bias, logits, probs,
-                     M, N, ks);
+  if (N <= 1024)
+    hipLaunchKernelGGL(dense_finish_reg_kernel, dim3(M), dim3(256), 0, s, part, bias, logits, probs, M, N, ks);
+  else
+    hipLaunchKernelGGL(dense_finish_kernel, dim3(M), dim3(256), (size_t)N * sizeof(float), s, part, bias, logits,
+                       probs, M, N, ks);
   return hipGetLastError();
 }
 

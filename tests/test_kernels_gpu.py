@@ -180,7 +180,7 @@ def test_conv_f32_out_dense(ops):
     assert torch.allclose(out, ref, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,K,N", [(32, 2048, 1000), (1, 2048, 1000), (7, 512, 10), (20, 1000, 37)])
+@pytest.mark.parametrize("M,K,N", [(32, 2048, 1000), (1, 2048, 1000), (7, 512, 10), (20, 1000, 37), (4, 512, 1500)])
 def test_dense_small_head(ops, M, K, N):
     """Small-M classifier GEMM (+bias, + softmax) of csrc/kernels/head.hip vs torch fp32."""
     conv, E = ops
