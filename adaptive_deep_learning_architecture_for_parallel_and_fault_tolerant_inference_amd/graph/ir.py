@@ -52,6 +52,16 @@ ACT_MODE = {None: 0, "linear": 0, "relu": 1, "relu6": 2, "swish": 3, "silu": 3, 
             "hard_sigmoid": 6, "hard_swish": 7, "gelu": 8, "elu": 9, "selu": 10, "softplus": 11, "leaky_relu": 12}
 
 
+def bn_params(weights, name: str) -> Dict:
+    """gamma / beta / moving statistics of BN layer `name`, with Keras' defaults
+    (gamma 1, beta 0) for a layer built with scale=False / center=False."""
+    import numpy as np
+    mu = weights[f"{name}/moving_mean"]
+    return {"gamma": weights.get(f"{name}/gamma", np.ones_like(mu)),
+            "beta": weights.get(f"{name}/beta", np.zeros_like(mu)),
+            "moving_mean": mu, "moving_variance": weights[f"{name}/moving_variance"]}
+
+
 def same_pads(size: int, k: int, s: int) -> Tuple[int, int]:
     """TF/Keras 'same' padding of one spatial dim: (before, after), the odd pixel after."""
     out = -(-size // s)
@@ -86,8 +96,11 @@ class Layer:
                 out.append((f"{self.name}/bias", (self.attrs["filters"],)))
             return out
         if self.op == "bn":
+            # Keras omits gamma for scale=False (InceptionV3) and beta for center=False
             c = in_shapes[0][-1]
-            return [(f"{self.name}/{n}", (c,)) for n in ("gamma", "beta", "moving_mean", "moving_variance")]
+            keep = (("gamma", self.attrs.get("scale", True)), ("beta", self.attrs.get("center", True)),
+                    ("moving_mean", True), ("moving_variance", True))
+            return [(f"{self.name}/{n}", (c,)) for n, k in keep if k]
         if self.op == "dwconv":
             kh, kw = self.attrs["kernel"]
             cin = in_shapes[0][-1]

@@ -134,9 +134,13 @@ def _layer_from_keras(cls: str, cfg: Dict[str, Any], name: str, inputs: List[str
     if cls == "BatchNormalization":
         axis = cfg.get("axis", -1)
         axis = axis[0] if isinstance(axis, list) else axis
-        if axis not in (-1, 3) or not cfg.get("center", True) or not cfg.get("scale", True):
-            raise NotImplementedError(f"{name}: BatchNormalization needs axis=-1, center and scale")
-        return Layer(name, "bn", inputs, {"epsilon": float(cfg.get("epsilon", 1e-3))})
+        if axis not in (-1, 3):
+            raise NotImplementedError(f"{name}: BatchNormalization needs axis=-1")
+        a = {"epsilon": float(cfg.get("epsilon", 1e-3))}
+        for k in ("center", "scale"):
+            if not cfg.get(k, True):
+                a[k] = False
+        return Layer(name, "bn", inputs, a)
     if cls == "ReLU":
         if float(cfg.get("threshold", 0.0) or 0.0) != 0.0:
             raise NotImplementedError(f"{name}: thresholded ReLU")
@@ -252,7 +256,8 @@ def _keras_layer(L: Layer, g: Graph) -> Dict[str, Any]:
             cfg.update(depth_multiplier=1)
     elif L.op == "bn":
         cls = "BatchNormalization"
-        cfg.update(axis=[3], momentum=0.99, epsilon=a.get("epsilon", 1e-3), center=True, scale=True)
+        cfg.update(axis=[3], momentum=0.99, epsilon=a.get("epsilon", 1e-3), center=a.get("center", True),
+                   scale=a.get("scale", True))
     elif L.op == "relu":
         if a.get("max_value") is None:
             cls = "Activation"

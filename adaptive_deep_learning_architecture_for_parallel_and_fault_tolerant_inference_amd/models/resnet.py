@@ -128,10 +128,12 @@ def init_weights(g: Graph, seed: int = 0, layers: Optional[List[str]] = None) ->
             c = specs[0][1][0]
             # last BN of a residual branch (ResNet `_3_bn`, MobileNetV2 `project_BN`) damped
             damp = 0.2 if n.endswith("_3_bn") or n.endswith("project_BN") else 1.0
-            out[specs[0][0]] = (damp * rng.uniform(0.8, 1.2, c)).astype(np.float32)
-            out[specs[1][0]] = (rng.standard_normal(c) * 0.05).astype(np.float32)
-            out[specs[2][0]] = (rng.standard_normal(c) * 0.05).astype(np.float32)
-            out[specs[3][0]] = rng.uniform(0.5, 1.5, c).astype(np.float32)
+            vals = {"gamma": (damp * rng.uniform(0.8, 1.2, c)).astype(np.float32),
+                    "beta": (rng.standard_normal(c) * 0.05).astype(np.float32),
+                    "moving_mean": (rng.standard_normal(c) * 0.05).astype(np.float32),
+                    "moving_variance": rng.uniform(0.5, 1.5, c).astype(np.float32)}
+            for wname, _ in specs:                 # scale=False / center=False drop gamma / beta
+                out[wname] = vals[wname.rsplit("/", 1)[1]]
         elif L.op == "normalization":
             c = specs[0][1][0]
             out[specs[0][0]] = (rng.standard_normal(c) * 0.1).astype(np.float32)

@@ -12,10 +12,11 @@ takes an arbitrary Keras JSON):
 * MobileNetV2    (ReLU6, DepthwiseConv2D, 'same' padding at stride 2, inverted residuals)
 * DenseNet121/169/201 (pre-activation BN-ReLU, Concatenate, AveragePooling2D)
 * EfficientNetB0-B7   (Rescaling/Normalization inside the model, swish, squeeze-excite Multiply)
+* InceptionV3         (BatchNormalization(scale=False), asymmetric 1x7 / 7x1 kernels, multi-branch concats)
 
 Parameter totals (Keras, include_top, 1000 classes; checked by tests):
 VGG16 138,357,544; VGG19 143,667,240; MobileNetV2 3,538,984; DenseNet121 8,062,504;
-EfficientNetB0 5,330,571.
+EfficientNetB0 5,330,571; InceptionV3 23,851,784.
 """
 from __future__ import annotations
 
@@ -231,6 +232,79 @@ def build_efficientnet(name: str = "efficientnetb0", classes: int = 1000, input_
     return g
 
 
+# ------------------------------------------------------------- InceptionV3
+def build_inception_v3(name: str = "inception_v3", classes: int = 1000, input_shape=(299, 299, 3)) -> Graph:
+    """`keras.applications.InceptionV3(include_top=True)`.  Its conv2d_bn units are unnamed, so the
+    layers carry Keras' auto-names of a fresh session (conv2d, conv2d_1, ..., batch_normalization_N,
+    activation_N, max_pooling2d_N, average_pooling2d_N, concatenate_N) in creation order;
+    BatchNormalization(scale=False) (no gamma), asymmetric 1x7 / 7x1 / 1x3 / 3x1 kernels.
+    Weight-list order follows creation order: Keras' own `get_weights()` order for this
+    multi-branch graph is unpinned here (no TensorFlow to compare with)."""
+    g = Graph(name)
+    cnt: Dict[str, int] = {}
+
+    def auto(kind: str) -> str:
+        i = cnt.get(kind, 0)
+        cnt[kind] = i + 1
+        return kind if i == 0 else f"{kind}_{i}"
+
+    def cbn(x: str, f: int, kh: int, kw: int, padding: str = "same", stride: int = 1) -> str:
+        x = g.add(Layer(auto("conv2d"), "conv", [x], {"filters": f, "kernel": (kh, kw), "stride": stride,
+                                                       "padding": padding, "use_bias": False}))
+        x = g.add(Layer(auto("batch_normalization"), "bn", [x], {"epsilon": 1e-3, "scale": False}))
+        return g.add(Layer(auto("activation"), "relu", [x]))
+
+    def maxpool(x: str) -> str:
+        return g.add(Layer(auto("max_pooling2d"), "maxpool", [x], {"pool": 3, "stride": 2, "padding": "valid"}))
+
+    def avgpool(x: str) -> str:
+        return g.add(Layer(auto("average_pooling2d"), "avgpool", [x], {"pool": 3, "stride": 1, "padding": "same"}))
+
+    def cat(xs, nm=None) -> str:
+        return g.add(Layer(nm or auto("concatenate"), "concat", list(xs)))
+
+    x = g.add(Layer("input_1", "input", [], {"shape": tuple(input_shape)}))
+    x = cbn(x, 32, 3, 3, "valid", 2)
+    x = cbn(x, 32, 3, 3, "valid")
+    x = cbn(x, 64, 3, 3)
+    x = maxpool(x)
+    x = cbn(x, 80, 1, 1, "valid")
+    x = cbn(x, 192, 3, 3, "valid")
+    x = maxpool(x)
+    for i, pool_f in enumerate((32, 64, 64)):                     # mixed0-2: 35 x 35
+        b1 = cbn(x, 64, 1, 1)
+        b5 = cbn(cbn(x, 48, 1, 1), 64, 5, 5)
+        b3 = cbn(cbn(cbn(x, 64, 1, 1), 96, 3, 3), 96, 3, 3)
+        bp = cbn(avgpool(x), pool_f, 1, 1)
+        x = cat([b1, b5, b3, bp], f"mixed{i}")
+    b3 = cbn(x, 384, 3, 3, "valid", 2)                            # mixed3: 17 x 17
+    bd = cbn(cbn(cbn(x, 64, 1, 1), 96, 3, 3), 96, 3, 3, "valid", 2)
+    x = cat([b3, bd, maxpool(x)], "mixed3")
+    for i, c7 in enumerate((128, 160, 160, 192)):                 # mixed4-7
+        b1 = cbn(x, 192, 1, 1)
+        b7 = cbn(cbn(cbn(x, c7, 1, 1), c7, 1, 7), 192, 7, 1)
+        bd = cbn(x, c7, 1, 1)
+        for f, (kh, kw) in ((c7, (7, 1)), (c7, (1, 7)), (c7, (7, 1)), (192, (1, 7))):
+            bd = cbn(bd, f, kh, kw)
+        bp = cbn(avgpool(x), 192, 1, 1)
+        x = cat([b1, b7, bd, bp], f"mixed{4 + i}")
+    b3 = cbn(cbn(x, 192, 1, 1), 320, 3, 3, "valid", 2)            # mixed8: 8 x 8
+    b7 = cbn(cbn(cbn(cbn(x, 192, 1, 1), 192, 1, 7), 192, 7, 1), 192, 3, 3, "valid", 2)
+    x = cat([b3, b7, maxpool(x)], "mixed8")
+    for i in range(2):                                            # mixed9, mixed10
+        b1 = cbn(x, 320, 1, 1)
+        b3 = cbn(x, 384, 1, 1)
+        b3 = cat([cbn(b3, 384, 1, 3), cbn(b3, 384, 3, 1)], f"mixed9_{i}")
+        bd = cbn(cbn(x, 448, 1, 1), 384, 3, 3)
+        bd = cat([cbn(bd, 384, 1, 3), cbn(bd, 384, 3, 1)])
+        bp = cbn(avgpool(x), 192, 1, 1)
+        x = cat([b1, b3, bd, bp], f"mixed{9 + i}")
+    x = g.add(Layer("avg_pool", "gap", [x]))
+    g.add(Layer("predictions", "dense", [x], {"units": classes, "activation": "softmax", "use_bias": True}))
+    g.output_names = ["predictions"]
+    return g
+
+
 BUILDERS: Dict[str, Callable[..., Graph]] = {
     "vgg16": lambda **kw: build_vgg("vgg16", **kw),
     "vgg19": lambda **kw: build_vgg("vgg19", **kw),
@@ -239,6 +313,7 @@ BUILDERS: Dict[str, Callable[..., Graph]] = {
     "densenet169": lambda **kw: build_densenet("densenet169", **kw),
     "densenet201": lambda **kw: build_densenet("densenet201", **kw),
     **{n: (lambda n: lambda **kw: build_efficientnet(n, **kw))(n) for n in EFFNET_SCALE},
+    "inception_v3": lambda **kw: build_inception_v3(**kw),
 }
 
 

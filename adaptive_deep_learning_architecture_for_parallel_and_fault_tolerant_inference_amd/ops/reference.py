@@ -96,7 +96,9 @@ class ReferenceExecutor:
             y = F.conv2d(x, k, bias, stride=s, groups=c)
             return _act(y.permute(0, 2, 3, 1), a.get("activation"))
         if L.op == "bn":
-            g_, b_, m_, v_ = (self.w[f"{L.name}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance"))
+            m_, v_ = self.w[f"{L.name}/moving_mean"], self.w[f"{L.name}/moving_variance"]
+            g_ = self.w.get(f"{L.name}/gamma", 1.0)         # scale=False / center=False defaults
+            b_ = self.w.get(f"{L.name}/beta", 0.0)
             return (ins[0] - m_) / torch.sqrt(v_ + a.get("epsilon", 1e-3)) * g_ + b_
         if L.op == "relu":
             y = torch.relu(ins[0])

@@ -29,7 +29,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..graph.ir import Graph
+from ..graph.ir import Graph, bn_params
 from ..ops import conv as conv_ops
 from ..ops import eltwise as E
 from .plan import Step, compile_plan
@@ -137,7 +137,7 @@ class SliceExecutor:
                 bn = None
                 eps = 1e-3
                 if p["bn"]:
-                    bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
+                    bn = bn_params(weights, p["bn"])
                     eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
                 kf, bf = conv_ops.fold_bn(k, weights.get(f"{p['conv']}/bias"), bn, eps)
                 self.packed[i] = conv_ops.pack_stem(kf, bf, p["pads"], dev)
@@ -153,7 +153,7 @@ class SliceExecutor:
                 bn = None
                 eps = 1e-3
                 if p["bn"]:
-                    bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
+                    bn = bn_params(weights, p["bn"])
                     eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
                 # as an HWIO kernel with one input channel: BN scales the last (channel) axis
                 kf, bf = conv_ops.fold_bn(k[:, :, None, :], weights.get(f"{p['conv']}/bias"), bn, eps)
@@ -180,7 +180,8 @@ class SliceExecutor:
                 self.packed[i] = (torch.tensor(scp, device=dev), torch.tensor(shp, device=dev))
             elif st.kind == "bn":
                 name = st.p["bn"]
-                gm, bt, mu, var = (weights[f"{name}/{n}"].astype(np.float64) for n in
+                bp_ = bn_params(weights, name)
+                gm, bt, mu, var = (np.asarray(bp_[n], np.float64) for n in
                                    ("gamma", "beta", "moving_mean", "moving_variance"))
                 eps = self.g.layers[name].attrs.get("epsilon", 1e-3)
                 s = gm / np.sqrt(var + eps)
@@ -193,7 +194,7 @@ class SliceExecutor:
         bn = None
         eps = 1e-3
         if p["bn"]:
-            bn = {n: weights[f"{p['bn']}/{n}"] for n in ("gamma", "beta", "moving_mean", "moving_variance")}
+            bn = bn_params(weights, p["bn"])
             eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
         return conv_ops.fold_bn(weights[f"{cname}/kernel"], weights.get(f"{cname}/bias"), bn, eps)
 

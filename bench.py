@@ -54,7 +54,8 @@ def parse():
 
 BASELINE_IMG_S = None   # the reference publishes no absolute number
 MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152", "vgg16": "VGG16",
-               "vgg19": "VGG19", "mobilenet_v2": "MobileNetV2", "densenet121": "DenseNet121"}
+               "vgg19": "VGG19", "mobilenet_v2": "MobileNetV2", "densenet121": "DenseNet121",
+               "efficientnetb0": "EfficientNetB0", "inception_v3": "InceptionV3"}
 
 
 def main():
@@ -86,7 +87,8 @@ def main():
                            host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec)
     # synthetic input, resident on device (data="synthetic")
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    job.set_synthetic_input(torch.randn((args.batch, 224, 224, 3), generator=gen, device=dev))
+    image = tuple(g.layers[g.input].out_shape)          # 224x224x3 (ResNet-50); the model's own size otherwise
+    job.set_synthetic_input(torch.randn((args.batch,) + image, generator=gen, device=dev))
 
     if hasattr(job, "set_total_steps"):
         job.set_total_steps(args.warmup + args.steps)
@@ -126,9 +128,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_IMG_S, 4) if BASELINE_IMG_S else None),
             "dtype": "bf16",
-            "data": "synthetic 224x224x3 NHWC fp32 input, random-init weights (seeded)",
+            "data": f"synthetic {'x'.join(map(str, image))} NHWC fp32 input, random-init weights (seeded)",
             "config": {"model": args.model, "global_batch": job.global_batch, "seq_len": None,
-                       "image": [224, 224, 3], "parallelism": job.parallelism, "part_at": job.part_at,
+                       "image": list(image), "parallelism": job.parallelism, "part_at": job.part_at,
                        "micro_batch": args.batch, "hipgraph": not args.no_graph},
         }
         link = getattr(job, "link", None)

@@ -27,7 +27,8 @@ from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inferen
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.plan import compile_plan
 
 KERAS_PARAMS = {"vgg16": 138_357_544, "vgg19": 143_667_240, "mobilenet_v2": 3_538_984,
-                "densenet121": 8_062_504, "densenet169": 14_307_880, "densenet201": 20_242_984}
+                "densenet121": 8_062_504, "densenet169": 14_307_880, "densenet201": 20_242_984,
+                "inception_v3": 23_851_784}
 
 
 @pytest.mark.parametrize("name", sorted(KERAS_PARAMS))
@@ -53,7 +54,7 @@ def test_keras_names_and_weight_lists():
     assert dn.layers["pool4_pool"].out_shape == (7, 7, 512)
 
 
-@pytest.mark.parametrize("name", ["resnet50", "vgg16", "mobilenet_v2", "densenet121"])
+@pytest.mark.parametrize("name", ["resnet50", "vgg16", "mobilenet_v2", "densenet121", "inception_v3"])
 def test_keras_json_round_trip(name):
     g = build_model(name)
     s = to_keras_json(g)
@@ -319,3 +320,23 @@ def test_reference_activations_match_keras_definitions():
     torch.testing.assert_close(_act(x, "swish"), x * torch.sigmoid(x))
     torch.testing.assert_close(_act(x, "relu6"), torch.clamp(x, 0, 6))
     torch.testing.assert_close(_act(x, "leaky_relu", 0.2), torch.where(x > 0, x, 0.2 * x))
+
+
+def test_inception_v3_keras_auto_names_and_bn_without_scale():
+    g = build_model("inception_v3")
+    assert len(g) == 313 and g.layers["mixed10"].out_shape == (8, 8, 2048)
+    assert [n for n in g.order if g.layers[n].op == "conv"][-1] == "conv2d_93"
+    assert "concatenate_1" in g.layers and "mixed9_1" in g.layers
+    assert g.layers["conv2d_7"].attrs["kernel"] == (5, 5) and g.layers["conv2d_32"].attrs["kernel"] == (1, 7)
+    specs = dict(g.weight_specs(["batch_normalization"]))
+    assert list(specs) == ["batch_normalization/beta", "batch_normalization/moving_mean",
+                           "batch_normalization/moving_variance"]          # scale=False: no gamma
+    kinds = [s.kind for s in compile_plan(g)]
+    assert "bn" not in kinds and kinds.count("conv") == 94 and kinds.count("concat") == 15
+    # BatchNormalization(scale=False, center=False) through the Keras JSON reader and the oracle
+    d = json.loads(_small_keras(2))
+    d["config"]["layers"][4]["config"].update(scale=False, center=False)
+    m = Model.from_keras_json(json.dumps(d), seed=0)
+    assert [n for n, _ in m.graph.weight_specs(["dw_bn"])] == ["dw_bn/moving_mean", "dw_bn/moving_variance"]
+    y = m.predict(np.zeros((1, 16, 16, 3), np.float32), device="cpu")
+    assert np.isfinite(y).all()

@@ -110,12 +110,13 @@ def _model_check(g, w, batch, feat, size, rel_tol=3e-2):
 
 
 @pytest.mark.parametrize("name,batch,feat", [("vgg16", 2, "fc2"), ("mobilenet_v2", 4, "global_average_pooling2d"),
-                                             ("densenet121", 2, "avg_pool")])
+                                             ("densenet121", 2, "avg_pool"), ("inception_v3", 2, "avg_pool")])
 def test_zoo_model_vs_oracle(name, batch, feat):
     zoo = importlib.import_module(f"{PKG}.models.zoo")
     res = importlib.import_module(f"{PKG}.models.resnet")
     g = zoo.build_model(name)
-    _model_check(g, res.init_weights(g, 0), batch, feat, (224, 224, 3), rel_tol=5e-2)
+    size = (299, 299, 3) if name == "inception_v3" else (224, 224, 3)
+    _model_check(g, res.init_weights(g, 0), batch, feat, size, rel_tol=5e-2)
 
 
 def test_keras_json_model_vs_oracle():

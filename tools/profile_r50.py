@@ -45,7 +45,7 @@ def main():
     g = build_model(a.model)
     w = init_weights(g, 0)
     ex = SliceExecutor(g, w, a.batch, tune=a.tune)
-    x = torch.randn(a.batch, 224, 224, 3, device="cuda")
+    x = torch.randn((a.batch,) + tuple(g.layers[g.input].out_shape), device="cuda")
     ex.input_buf(g.input).copy_(x)
     # per-step eager timing
     total_flop = 0
