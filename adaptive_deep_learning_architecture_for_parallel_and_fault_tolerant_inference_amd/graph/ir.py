@@ -345,6 +345,24 @@ class Graph:
         g.output_names = list(d["outputs"])
         return g
 
+    def to_dot(self, show_shapes: bool = True) -> str:
+        """Graphviz DOT of the layer DAG (the reference renders each slice with
+        `tf.keras.utils.plot_model`, `src/node.py:49`); slice inputs that stand for
+        another slice's tensors are drawn dashed."""
+        def q(s: str) -> str:
+            return '"' + s.replace('"', r'\"') + '"'
+        lines = [f"digraph {q(self.name)} {{", "  rankdir=TB;", '  node [shape=record, fontsize=10];']
+        for n in self.order:
+            L = self.layers[n]
+            label = f"{n}|{L.op}" + (f"|{tuple(L.out_shape)}" if show_shapes else "")
+            style = ", style=dashed" if L.op == "input" and L.attrs.get("stands_for", "input") != "input" else ""
+            lines.append(f"  {q(n)} [label={q('{' + label + '}')}{style}];")
+        for n in self.order:
+            for i in self.layers[n].inputs:
+                lines.append(f"  {q(i)} -> {q(n)};")
+        lines.append("}")
+        return "\n".join(lines)
+
     def summary(self) -> str:
         lines = [f"Model: {self.name}", f"{'Layer':40s} {'Op':8s} {'Output':>18s} {'Params':>10s}"]
         for n in self.order:

@@ -66,6 +66,11 @@ class Model:
             w = set_weights(g, list(weights))
         return Model(g, w)
 
+    def plot_model(self, to_file: str = "model.png", show_shapes: bool = True) -> str:
+        """`tf.keras.utils.plot_model` analogue (`src/node.py:49`): DOT source, rendered when Graphviz is present."""
+        from ..utils.plot import plot_model
+        return plot_model(self, to_file, show_shapes)
+
     def summary(self, print_fn=print) -> str:
         s = self.graph.summary()
         if print_fn:

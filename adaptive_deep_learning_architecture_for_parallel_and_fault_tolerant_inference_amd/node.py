@@ -76,6 +76,10 @@ class StageRuntime:
         self.codec = cfg.get("codec", "lz4")
         self.manifest = manifest
         g = manifest.graph()
+        plot_dir = os.environ.get("ADAPT_PLOT_DIR")
+        if plot_dir:                          # the reference's per-worker plot_model (src/node.py:49)
+            from .utils.plot import plot_model, slice_plot_name
+            plot_model(g, slice_plot_name(plot_dir, node.node_id, self.epoch))
         # GPU stages with a GPU codec compress frontier tensors on a side HIP stream
         # while the next micro-batch computes (two buffer sets ping-pong)
         self.gpu_codec = self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")

@@ -340,3 +340,31 @@ def test_inception_v3_keras_auto_names_and_bn_without_scale():
     assert [n for n, _ in m.graph.weight_specs(["dw_bn"])] == ["dw_bn/moving_mean", "dw_bn/moving_variance"]
     y = m.predict(np.zeros((1, 16, 16, 3), np.float32), device="cpu")
     assert np.isfinite(y).all()
+
+
+def test_plot_model_and_per_slice_plots(tmp_path, monkeypatch):
+    """plot_model analogue (`src/node.py:49`): DOT of the DAG; Nodes write one per configured slice."""
+    m = Model.from_keras_json(_small_keras(2), seed=1)
+    path = m.plot_model(str(tmp_path / "small.png"))
+    dot = open(path if path.endswith(".dot") else str(tmp_path / "small.dot")).read()
+    assert dot.startswith('digraph "small"') and '"cat" -> "mp"' in dot and dot.count("->") == 19
+    monkeypatch.setenv("ADAPT_PLOT_DIR", str(tmp_path / "plots"))
+    d = DEFER(membership_port=0, result_port=0, worker_wait=10, ordered=True, batch=2)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu", node_id=f"p{i}",
+                  heartbeat_ttl=0.5) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["branch"], inq, outq), daemon=True).start()
+        inq.put(np.zeros((2, 16, 16, 3), np.float32))
+        outq.get(timeout=60)
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
+    plots = sorted(p.name for p in (tmp_path / "plots").iterdir())
+    assert len(plots) == 2 and all(p.startswith("model_p") and p.endswith(".dot") for p in plots)
+    txt = "".join(open(tmp_path / "plots" / p).read() for p in plots)
+    assert "style=dashed" in txt                     # the second slice's frontier inputs
