@@ -142,7 +142,7 @@ class SliceExecutor:
                 kf, bf = conv_ops.fold_bn(k, weights.get(f"{p['conv']}/bias"), bn, eps)
                 self.packed[i] = conv_ops.pack_stem(kf, bf, p["pads"], dev)
             elif st.kind == "dense":
-                name = st.out
+                name = st.p.get("layer", st.out)
                 k = weights[f"{name}/kernel"]                     # (in, out)
                 b = weights.get(f"{name}/bias", np.zeros(k.shape[1], np.float32))
                 self.packed[i] = conv_ops.pack_conv(k.reshape(1, 1, k.shape[0], k.shape[1]), b, 1,
@@ -249,7 +249,8 @@ class SliceExecutor:
         self._logits: Dict[int, torch.Tensor] = {}
         self._dense_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
-            if st.kind == "dense" and self.batch <= 32 and not st.p.get("relu"):
+            if (st.kind == "dense" and self.batch <= 32 and not st.p.get("relu")
+                    and self.dtype_of(st.out) == torch.float32):          # head.hip writes fp32 logits / probs
                 # small-M head GEMM (csrc/kernels/head.hip): split-K scratch
                 pc = self.packed[i]
                 n = E.dense_small_scratch(self.batch, pc.cout, pc.K)

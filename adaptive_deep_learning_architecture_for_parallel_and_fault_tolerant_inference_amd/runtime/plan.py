@@ -75,7 +75,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
         produced.add(n)
         done.add(n)
         c = L.out_shape[-1] if L.out_shape else 0
-        if len(L.out_shape) == 3 and c % 8 and L.attrs.get("stands_for", "input") == "input":
+        # the user's fp32 image becomes bf16 NHWC with channels padded to 8 (a pure cast when C % 8 == 0)
+        if len(L.out_shape) == 3 and L.attrs.get("stands_for", "input") == "input":
             packed.add(n)
             steps.append(Step("pack", n + "#packed", [n], [], {"cin": c, "cpad": ((c + 7) // 8) * 8}))
 
@@ -296,11 +297,11 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
             mode = 0 if act == "softmax" else own_act(n, L)
             if mode > 2:                        # not an MFMA-epilogue activation: its own step
                 steps.append(Step("dense", n + "#preact", [R(L.inputs[0])], [n],
-                                  {"units": a["units"], "softmax": False, "relu": 0}))
+                                  {"units": a["units"], "softmax": False, "relu": 0, "layer": n}))
                 steps.append(Step("act", n, [n + "#preact"], [], {"mode": mode, "alpha": 0.3}))
             else:
                 steps.append(Step("dense", n, [R(L.inputs[0])], [n],
-                                  {"units": a["units"], "softmax": act == "softmax", "relu": mode}))
+                                  {"units": a["units"], "softmax": act == "softmax", "relu": mode, "layer": n}))
             done.add(n)
         elif L.op == "softmax":
             steps.append(Step("softmax", n, [R(L.inputs[0])], [n]))

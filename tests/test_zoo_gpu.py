@@ -193,3 +193,24 @@ def test_gap_large_and_small_maps(ops, B, H, W, C):
     E.gap(x, out=out, scratch=scratch)
     torch.testing.assert_close(out.float(), x.float().mean(dim=(1, 2)), rtol=1e-2, atol=1e-2)
     assert (need > 0) == (H * W >= E.GAP_LARGE_HW)
+
+
+def test_dense_with_non_relu_activation_chain():
+    """Dense(swish) -> Dense(sigmoid) -> Dense(softmax) (bf16 hidden activations, post-activation steps)."""
+    kj = importlib.import_module(f"{PKG}.graph.keras_json")
+    res = importlib.import_module(f"{PKG}.models.resnet")
+
+    def L(cls, name, inbound, **cfg):
+        cfg["name"] = name
+        return {"class_name": cls, "config": cfg, "name": name,
+                "inbound_nodes": [[[i, 0, 0, {}] for i in inbound]] if inbound else []}
+    layers = [L("InputLayer", "img", [], batch_input_shape=[None, 4, 4, 8]),
+              L("Flatten", "fl", ["img"]),
+              L("Dense", "h1", ["fl"], units=64, activation="swish"),
+              L("Dense", "h2", ["h1"], units=32, activation="sigmoid"),
+              L("Dense", "predictions", ["h2"], units=16, activation="softmax")]
+    js = json.dumps({"class_name": "Functional", "config": {"name": "mlp", "layers": layers,
+                                                            "input_layers": [["img", 0, 0]],
+                                                            "output_layers": [["predictions", 0, 0]]}})
+    g = kj.from_keras_json(js)
+    _model_check(g, res.init_weights(g, 5), 4, "h2", (4, 4, 8), rel_tol=5e-2)
