@@ -192,6 +192,7 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
 // tiles of a two-row step, two per wave.
 namespace {
 constexpr int S2_SP = 7;                                   // pool rows per block
+constexpr int ST_V1_MAX_BLOCKS = 448;                      // auto: v1 up to this many pool-row blocks (B<=8 at 224)
 constexpr int S2_WAVES = 7;
 constexpr int S2_NT = S2_WAVES * 64;
 constexpr int S2_PROWS = 4 * S2_SP + 7;                    // input rows of a block's patch (35)
@@ -352,9 +353,13 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
   if (pool) {
     if (PH < 1 || PW < 1 || PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1)
       return hipErrorInvalidValue;
-    const char* v1 = getenv("ADAPT_STEM_V1");           // A/B switch to the v1 kernel
-    if (!(v1 && v1[0] == '1')) {
-      const int groups = (PH + S2_SP - 1) / S2_SP;
+    // v2 walks S2_SP pool rows per block, so a small batch launches only a few
+    // dozen blocks (8 at B=1): there the one-pool-row-per-block v1 grid fills more
+    // CUs and wins.  ADAPT_STEM_V1=1 / =0 forces v1 / v2 (A/B switch).
+    const int groups = (PH + S2_SP - 1) / S2_SP;
+    const char* v1 = getenv("ADAPT_STEM_V1");
+    const bool use_v1 = v1 && v1[0] ? v1[0] == '1' : PH * B <= ST_V1_MAX_BLOCKS;
+    if (!use_v1) {
       hipLaunchKernelGGL(stem_pool_v2_kernel, dim3(groups * B), dim3(S2_NT), 0, s, x, w, bias, out, H, W, C, OH, OW,
                          pad_t, pad_l, PH, PW, pool_pad, groups);
       return hipGetLastError();

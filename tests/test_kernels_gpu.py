@@ -96,10 +96,7 @@ def test_conv_vs_torch(ops, case, cfg):
 def test_stem_vs_torch(ops, B, H, W, pool, version, monkeypatch):
     """Fused fp32-image -> conv1(7x7/s2)+BN+ReLU [-> 3x3/s2 max-pool] vs F.conv2d/F.max_pool2d
     (v2 = row-group kernel with the conv-row ring; v1 = one pool row per block)."""
-    if version == "v1":
-        monkeypatch.setenv("ADAPT_STEM_V1", "1")
-    else:
-        monkeypatch.delenv("ADAPT_STEM_V1", raising=False)
+    monkeypatch.setenv("ADAPT_STEM_V1", "1" if version == "v1" else "0")
     conv, _ = ops
     dev = "cuda"
     torch.manual_seed(1)

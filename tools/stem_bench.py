@@ -47,6 +47,8 @@ def main():
     pooled = torch.empty(B, 56, 56, 64, device=dev, dtype=torch.bfloat16)
     res = {}
     if a.only in ("", "fused"):
+        res["fused stem auto"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
+        os.environ["ADAPT_STEM_V1"] = "0"
         res["fused stem v2 (conv+pool, row groups)"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
         ref = pooled.clone()
         os.environ["ADAPT_STEM_V1"] = "1"
