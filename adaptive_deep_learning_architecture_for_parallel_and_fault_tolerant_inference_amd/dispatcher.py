@@ -104,6 +104,9 @@ class DEFER:
         self.ordered = ordered
         self.device_graph = device_graph
         self.min_workers = min_workers
+        # a worker whose config port does not answer within this many seconds is left
+        # out of the next epoch even while its membership lease is still alive
+        self.probe_timeout = 0.5
         # gen-2 attributes the reference uses but never initialises
         self.worker_lock = threading.Lock()
         self.inflight_lock = threading.Lock()
@@ -264,7 +267,7 @@ class DEFER:
         """(Re)build the pipeline for the current live worker set; new epoch."""
         with self._reconf_lock:
             t0 = time.time()
-            live = self._get_available_workers()
+            live = self._probe_live(self._get_available_workers())
             if not live:
                 self._log(f"no workers available ({len(live)})")
                 return False
@@ -329,6 +332,42 @@ class DEFER:
                 s.close()
         except OSError:
             return False
+
+    def _probe_live(self, wids: Sequence[str]) -> List[str]:
+        """Keep the workers whose config server answers a ``status`` command.
+
+        A SIGKILLed worker keeps its membership record until the lease expires
+        (TTL), so a re-plan triggered by a socket error would otherwise place a
+        stage on it, fail mid-push and start over.  The probes run in parallel:
+        a dead local process refuses the connect at once, an unreachable host
+        costs at most `probe_timeout`."""
+        if len(wids) == 0:
+            return []
+        ok: Dict[str, bool] = {}
+
+        def probe(wid: str) -> None:
+            with self.worker_lock:
+                rec = self.workers.get(wid)
+            if rec is None:
+                ok[wid] = False
+                return
+            try:
+                with socket.create_connection((rec["host"], int(rec["config_port"])), timeout=self.probe_timeout) as s:
+                    s.settimeout(self.probe_timeout)
+                    socket_send(json.dumps({"cmd": "status"}).encode(), s, CTRL_CHUNK)
+                    ok[wid] = s.recv(1) == ACK
+            except OSError:
+                ok[wid] = False
+
+        ts = [threading.Thread(target=probe, args=(w,), daemon=True) for w in wids]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        dead = [w for w in wids if not ok.get(w)]
+        if dead:
+            self._log(f"unresponsive (lease still alive): {dead}")
+        return [w for w in wids if ok.get(w)]
 
     def _result_host(self, rec: dict) -> str:
         return "127.0.0.1" if rec.get("host") in ("127.0.0.1", "localhost") else self.dispatchIP
@@ -526,7 +565,7 @@ class DEFER:
                 ok = False
             if ok:
                 break
-            time.sleep(0.2)
+            time.sleep(0.1)
         if not ok:
             self._log("recovery failed: no usable workers")
             return
