@@ -193,6 +193,10 @@ class DEFER:
             if ev.type == "DELETE" and p is not None and wid in p.workers:
                 self._log(f"worker {wid} left (lease expired or revoked)")
                 self._reconf_needed.set()
+            elif (ev.type == "PUT" and p is not None and wid in p.workers and rec.get("state") == "LINK_ERROR"
+                  and rec.get("epoch") == p.epoch):
+                self._log(f"worker {wid} reports a broken hop: {rec.get('error')}")
+                self._reconf_needed.set()
             elif ev.type == "PUT" and new and self.elastic and p is not None:
                 self._log(f"worker {wid} joined")
                 self._reconf_needed.set()

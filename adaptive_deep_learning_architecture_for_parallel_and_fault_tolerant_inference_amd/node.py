@@ -125,9 +125,14 @@ class StageRuntime:
             self.threads.append(t)
 
     def _fail(self, where: str, e: BaseException) -> None:
-        if not self.stop.is_set():
+        report = not self.stop.is_set()
+        if report:
             self.error = f"{where}: {type(e).__name__}: {e}"
         self.abort()
+        if report:
+            # a broken hop (neighbour SIGKILLed) is published at once, so the
+            # dispatcher re-plans without waiting for the dead worker's lease TTL
+            self.node._publish(state="LINK_ERROR", epoch=self.epoch, error=self.error)
 
     def _recv_loop(self) -> None:
         try:
