@@ -4,7 +4,9 @@ pipeline micro-batch, synthetic 224x224x3 input, random-init weights
 (BASELINE.json: "images/sec (whole node) ResNet-50 bs=32 at 1/2/4/8 MI355X").
 
 Single GPU:    python bench.py --steps 50 --warmup 10
-N GPUs:        python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+N GPUs:        python bench.py --gpus N           (starts N rank processes itself,
+                   parallel/launch.py), or under torchrun:
+               python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
                    --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
 Parallelism (``--mode``):
@@ -21,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -32,7 +35,8 @@ PKG = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_infer
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="ranks (one per GPU); without torchrun the script launches them itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet50")
@@ -60,21 +64,33 @@ MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": 
 
 def main():
     args = parse()
+    from importlib import import_module
+    launch = import_module(f"{PKG}.parallel.launch")
+    if args.gpus > 1 and not launch.launched_by_torchrun():
+        # no torchrun: become the launcher (before any HIP call in this process)
+        sys.exit(launch.launch_local(sys.argv[1:], args.gpus, script=os.path.abspath(__file__)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using the launched world", file=sys.stderr)
     ndev = torch.cuda.device_count()
     dev_idx = local % max(1, ndev)
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
     backend = args.backend
+    if world > 1 and backend == "nccl" and world > ndev:
+        # RCCL refuses two ranks on one device: rehearse the schedule host-staged
+        if rank == 0:
+            print(f"bench: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank, using gloo "
+                  f"(host-staged rehearsal)", file=sys.stderr)
+        backend = "gloo"
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
 
-    from importlib import import_module
     resnet = import_module(f"{PKG}.models.resnet")
     zoo = import_module(f"{PKG}.models.zoo")
     runner = import_module(f"{PKG}.parallel.runner")
@@ -115,12 +131,18 @@ def main():
         elapsed = t.item()
     images = job.images_per_step * args.steps
     value = images / elapsed
+    n_gpus = 1
+    if world > 1:
+        # distinct physical devices: ranks rehearsing on one GPU count once
+        devs = [None] * world
+        dist.all_gather_object(devs, (socket.gethostname(), dev_idx))
+        n_gpus = launch.distinct_devices(devs)
     if rank == 0:
         rec = {
             "metric": (f"images/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} bs={args.batch}"),
             "value": round(value, 2),
             "unit": "images/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -131,7 +153,8 @@ def main():
             "data": f"synthetic {'x'.join(map(str, image))} NHWC fp32 input, random-init weights (seeded)",
             "config": {"model": args.model, "global_batch": job.global_batch, "seq_len": None,
                        "image": list(image), "parallelism": job.parallelism, "part_at": job.part_at,
-                       "micro_batch": args.batch, "hipgraph": not args.no_graph},
+                       "micro_batch": args.batch, "hipgraph": not args.no_graph,
+                       "ranks": world, "backend": backend if world > 1 else None},
         }
         link = getattr(job, "link", None)
         if args.codec != "none" and link is not None:
