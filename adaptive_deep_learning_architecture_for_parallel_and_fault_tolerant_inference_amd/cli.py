@@ -86,15 +86,17 @@ def cmd_serve(argv):
     ap.add_argument("--device", default=None, help="device for spawned workers (cpu, cuda, cuda:i)")
     ap.add_argument("--transport", default=None)
     ap.add_argument("--codec", default=None)
+    ap.add_argument("--replicas", default=None, help="pipeline replicas: auto (live // stages) or N")
     a = ap.parse_args(argv)
-    cfg = _cfg(a, transport=a.transport, codec=a.codec)
+    cfg = _cfg(a, transport=a.transport, codec=a.codec, replicas=a.replicas)
     from .dispatcher import DEFER
     m = _model(cfg)
     cuts = cfg.cuts(m.graph)
     d = DEFER(membership_port=cfg.membership_port, result_port=cfg.result_port, chunk_size=cfg.chunk_size,
               batch=cfg.batch, codec=cfg.codec, weight_codec=cfg.weight_codec, max_inflight=cfg.max_inflight,
               task_timeout=cfg.task_timeout, worker_wait=max(cfg.worker_wait, 60 if a.spawn else 0),
-              elastic=cfg.elastic, ordered=cfg.ordered, transport=cfg.transport, min_workers=max(1, a.spawn))
+              elastic=cfg.elastic, ordered=cfg.ordered, transport=cfg.transport, min_workers=max(1, a.spawn),
+              replicas=cfg.replicas)
     d.membership_server.start()
     procs = []
     for i in range(a.spawn):

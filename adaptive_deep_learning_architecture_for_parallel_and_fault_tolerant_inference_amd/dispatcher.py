@@ -13,20 +13,30 @@ references five undefined methods and five undefined attributes (SURVEY
   ``part1..partN`` (multi-tensor frontiers allowed), or with the balanced
   planner when the worker count changes;
 * `_get_available_workers` / `_acquire_and_configure_worker` — choose live
-  workers and push each its slice (manifest + index + weights, ACK 0x06) for
-  the current *epoch*;
+  workers and configure each for the current *epoch*: the first time a
+  worker gets a model it receives its slice (manifest + index + weights, ACK
+  0x06); afterwards the whole model is pushed to it once in the background
+  and every later configuration is local slicing on the worker (no push);
+* **PP x DP**: ``replicas="auto"`` forms R = live // k replicas of the k-stage
+  pipeline (the reference lets any idle worker take any partition,
+  `src/dispatcher.py:176-194`); requests are spread round-robin, a stage
+  failure re-forms only its replica, a join adds a replica;
 * `_startDistEdgeInference` — assigns request ids, keeps every in-flight
-  input (`inflight_tasks`), bounded by `concurrency_sem`, and streams it to
-  stage 0;
+  input (`inflight_tasks`), bounded by `concurrency_sem` (max_inflight per
+  replica), and streams it to a replica's stage 0;
 * `_intermediate_result_server` — accepts the last stages' connections,
   de-duplicates results by request id, emits them in completion order (or
   request order with ``ordered=True``) and releases credits;
 * `_task_watchdog` — a request older than `task_timeout` means its pipeline
-  is stuck: re-form it and replay;
-* repartition on worker leave (lease expiry / DELETE event) and, with
-  ``elastic=True``, on join: bump the epoch, re-plan cuts for the live set,
-  reconfigure survivors, replay every unfinished request from its retained
-  input.  Recovery-to-steady time is recorded per event in `recoveries`.
+  is stuck: re-form that replica and replay;
+* failure detection, fastest first: the per-worker *session* connection
+  (EOF the moment a worker process dies), a stage's LINK_ERROR report (broken
+  hop), the result link's EOF, the membership lease (host death), the task
+  watchdog.  Re-forming bumps the replica's epoch, re-plans cuts for its
+  survivors (plus spare workers), reconfigures them and replays every
+  unfinished request of the failed epoch from its retained input.  Workers
+  are told the likely next plans (`prepare`) so a re-plan finds its slices
+  built.  Recovery-to-steady time is recorded per event in `recoveries`.
 
 The data plane between stages is the workers' business (TCP links, or RCCL
 p2p over xGMI between GPU stages); the dispatcher only feeds stage 0 and
@@ -40,13 +50,13 @@ import socket
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
 from .graph.manifest import ACK, SliceManifest, build_manifest, send_slice
 from .graph.planner import plan_cuts
-from .graph.slicer import Slice, partition, validate_slices
+from .graph.slicer import partition, validate_slices
 from .membership.client import MembershipClient, live_workers
 from .membership.server import MembershipServer
 from .membership.store import KVStore
@@ -69,19 +79,67 @@ class Pipeline:
     records: List[dict]
     stage0: Optional[socket.socket] = None
     lock: threading.Lock = field(default_factory=threading.Lock)
+    replica: int = 0
+
+
+class RequestFailed:
+    """Put on the output stream in place of a prediction when a request failed
+    `max_replays` recoveries in a row (a deterministic stage fault): the caller
+    gets an answer for every request instead of waiting forever."""
+
+    def __init__(self, req_id: int, reason: str):
+        self.req_id, self.reason = req_id, reason
+
+    def __repr__(self) -> str:
+        return f"RequestFailed({self.req_id}, {self.reason!r})"
+
+
+class Credits:
+    """`concurrency_sem` (`src/dispatcher.py:151,183`) with a resizable limit:
+    `per_replica` requests in flight per serving replica."""
+
+    def __init__(self, per_replica: int):
+        self.per = max(1, int(per_replica))
+        self.limit = self.per
+        self.used = 0
+        self.cv = threading.Condition()
+
+    def acquire(self, timeout: Optional[float] = None) -> bool:
+        with self.cv:
+            if not self.cv.wait_for(lambda: self.used < self.limit, timeout):
+                return False
+            self.used += 1
+            return True
+
+    def release(self) -> None:
+        with self.cv:
+            self.used = max(0, self.used - 1)
+            self.cv.notify()
+
+    def set_replicas(self, r: int) -> None:
+        with self.cv:
+            self.limit = self.per * max(1, r)
+            self.cv.notify_all()
 
 
 class DEFER:
     def __init__(self, computeNodes: Optional[Sequence[str]] = None, *, membership: Optional[Tuple[str, int]] = None,
                  membership_port: int = 2379, result_port: int = RESULT_PORT, chunk_size: int = 512 * 1000,
-                 batch: int = 1, codec: str = "lz4", weight_codec: str = "zfp+lz4", max_inflight: int = 8,
+                 batch: int = 1, codec: str = "none", weight_codec: str = "zfp+lz4", max_inflight: int = 8,
                  task_timeout: float = 30.0, worker_wait: float = 5.0, elastic: bool = False,
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
-                 transport: str = "tcp", link_codec: str = "none") -> None:
-        """link_codec: compression of the collective stage-to-stage links ("none",
-        "lz4", "zvc"; codec/wire.py, on a side stream); `codec` applies to TCP hops.
-        transport: stage-to-stage links — "tcp" (framed, codec; any host),
-        "rccl" (RCCL p2p over xGMI between GPU workers), "gloo" (CPU workers)."""
+                 transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
+                 resident: bool = True, prepare: bool = True, max_replays: int = 3,
+                 quarantine_s: float = 30.0) -> None:
+        """codec: compression of the TCP hops ("none" default: on a local network
+        the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
+        ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
+        the collective stage-to-stage links ("none", "lz4", "zvc"; codec/wire.py,
+        on a side stream).  transport: stage-to-stage links — "tcp" (framed,
+        codec; any host), "rccl" (RCCL p2p over xGMI between GPU workers),
+        "gloo" (CPU workers).  replicas: "auto" = as many k-stage pipelines as
+        the live workers fill, or a maximum count.  resident: keep the whole
+        model on every worker after its first slice so re-plans push nothing."""
         if transport not in ("tcp", "rccl", "gloo"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
@@ -104,6 +162,11 @@ class DEFER:
         self.ordered = ordered
         self.device_graph = device_graph
         self.min_workers = min_workers
+        self.max_replicas = None if replicas == "auto" else max(1, int(replicas))
+        self.resident = resident
+        self.prepare = prepare
+        self.max_replays = max_replays
+        self.quarantine_s = quarantine_s
         # a worker whose config port does not answer within this many seconds is left
         # out of the next epoch even while its membership lease is still alive
         self.probe_timeout = 0.5
@@ -111,7 +174,7 @@ class DEFER:
         self.worker_lock = threading.Lock()
         self.inflight_lock = threading.Lock()
         self.inflight_tasks: Dict[int, dict] = {}
-        self.concurrency_sem = threading.BoundedSemaphore(max_inflight)
+        self.concurrency_sem = Credits(max_inflight)
         self._shutdown_event = threading.Event()
         self.models_to_dispatch: List[Tuple[SliceManifest, list]] = []
         # membership: external service, or an in-process store + TCP front-end
@@ -128,21 +191,37 @@ class DEFER:
         self.result_sock = listen("0.0.0.0", result_port)
         self.result_port = self.result_sock.getsockname()[1]
         self.workers: Dict[str, dict] = {}
-        self.pipeline: Optional[Pipeline] = None
+        self.replicas: Dict[int, Pipeline] = {}
+        self._rep_lock = threading.Lock()
+        self._next_rid = 0
+        self._rr = 0
         self._epoch = 0
         self._reconf_lock = threading.Lock()
         self._reconf_needed = threading.Event()
+        self._dirty: Dict[int, float] = {}          # replica id -> detection time
+        self._retired: set = set()                  # epochs a re-form has replaced
+        self._excluded: set = set()                 # workers a re-form left out (dead)
+        self._join_pending = False
+        self._lost: Dict[str, object] = {}          # worker id -> pid whose session ended
+        self._quarantine: Dict[str, float] = {}     # worker id -> until (STAGE_ERROR)
+        self._sessions: Dict[str, socket.socket] = {}
+        self._resident: Dict[str, set] = {}         # worker id -> model keys resident there
+        self._slices_by_cuts: Dict[Tuple[str, ...], List[Tuple[SliceManifest, list]]] = {}
+        self._sent_slices: Dict[str, set] = {}
         self._next_req = 0
         self._completed = 0
         self.completion_times: List[float] = []
         self.recoveries: List[dict] = []
         self.events: List[Tuple[float, str]] = []
         self._model: Optional[Model] = None
+        self._model_key = ""
         self._user_cuts: List[str] = []
-        self._order_buf: Dict[int, np.ndarray] = {}
+        self._cur_cuts: List[str] = []
+        self._order_buf: Dict[int, object] = {}
         self._next_emit = 0
         self._output: Optional[queue.Queue] = None
         self._result_conns: set = set()
+        self._bg: List[threading.Thread] = []      # model pushes / prepare hints
 
     # ------------------------------------------------------------ helpers
     @staticmethod
@@ -164,6 +243,32 @@ class DEFER:
     def membership_port(self) -> int:
         return self.membership_addr[1]
 
+    @property
+    def pipeline(self) -> Optional[Pipeline]:
+        """The first serving replica (the single pipeline when replicas=1)."""
+        with self._rep_lock:
+            if not self.replicas:
+                return None
+            return self.replicas[min(self.replicas)]
+
+    def _replica_of(self, wid: str) -> Optional[Pipeline]:
+        with self._rep_lock:
+            for p in self.replicas.values():
+                if wid in p.workers:
+                    return p
+        return None
+
+    def _mark_dirty(self, rid: int, why: str, epoch: Optional[int] = None, wid: Optional[str] = None) -> None:
+        """Schedule replica `rid` for re-forming.  Reports about an epoch that a
+        re-form already retired, or about a worker it already left out, are
+        echoes of the failure being handled (the torn-down links of the old
+        epoch close one after another) and are dropped."""
+        if (epoch is not None and epoch in self._retired) or (wid is not None and wid in self._excluded):
+            return
+        self._log(why)
+        self._dirty.setdefault(rid, time.time())
+        self._reconf_needed.set()
+
     # ---------------------------------------------------------- partition
     def _partition(self, model: Model, layer_parts: Sequence[str]) -> List[Tuple[SliceManifest, list]]:
         """Cut into part1..partN (`src/dispatcher.py:39-53`) -> [(manifest, arrays)]."""
@@ -172,10 +277,22 @@ class DEFER:
         validate_slices(g, slices)
         return [build_manifest(g, s, model.weights) for s in slices]
 
+    def _slices_for(self, cuts: Sequence[str]) -> List[Tuple[SliceManifest, list]]:
+        key = tuple(cuts)
+        if key not in self._slices_by_cuts:
+            self._slices_by_cuts[key] = self._partition(self._model, cuts)
+        return self._slices_by_cuts[key]
+
+    def _plan(self, k: int) -> List[str]:
+        want = len(self._user_cuts) + 1
+        if k == want:
+            return list(self._user_cuts)
+        return plan_cuts(self._model.graph, k, batch=self.batch)[0]
+
     # --------------------------------------------------------- membership
     def _worker_monitor(self) -> None:
-        """Watch /workers/ and keep `self.workers` current; losing a worker of
-        the active pipeline (or gaining one when elastic) triggers repartition."""
+        """Watch /workers/ and keep `self.workers` current; losing a worker of a
+        serving replica (or gaining one) triggers re-forming."""
         def on_event(ev):
             wid = ev.kv.key[len("/workers/"):]
             with self.worker_lock:
@@ -186,19 +303,29 @@ class DEFER:
                         return
                     new = wid not in self.workers
                     self.workers[wid] = rec
+                    if wid in self._lost and rec.get("pid") != self._lost[wid]:
+                        self._lost.pop(wid, None)      # a restarted worker under the same id
+                        self._excluded.discard(wid)
+                        new = True
                 else:
                     new = False
                     self.workers.pop(wid, None)
-            p = self.pipeline
-            if ev.type == "DELETE" and p is not None and wid in p.workers:
-                self._log(f"worker {wid} left (lease expired or revoked)")
-                self._reconf_needed.set()
-            elif (ev.type == "PUT" and p is not None and wid in p.workers and rec.get("state") == "LINK_ERROR"
-                  and rec.get("epoch") == p.epoch):
-                self._log(f"worker {wid} reports a broken hop: {rec.get('error')}")
-                self._reconf_needed.set()
-            elif ev.type == "PUT" and new and self.elastic and p is not None:
+            p = self._replica_of(wid)
+            if ev.type == "DELETE" and p is not None:
+                self._mark_dirty(p.replica, f"worker {wid} left (lease expired or revoked)", wid=wid)
+            elif ev.type == "PUT" and p is not None and rec.get("epoch") == p.epoch and \
+                    rec.get("state") in ("LINK_ERROR", "STAGE_ERROR"):
+                if rec["state"] == "STAGE_ERROR":
+                    # the stage's own compute failed: do not place a stage there again for a while
+                    self._quarantine[wid] = time.time() + self.quarantine_s
+                    self._mark_dirty(p.replica, f"worker {wid} stage error (quarantined): {rec.get('error')}",
+                                     epoch=p.epoch)
+                else:
+                    self._mark_dirty(p.replica, f"worker {wid} reports a broken hop: {rec.get('error')}",
+                                     epoch=p.epoch)
+            elif ev.type == "PUT" and new and self._model is not None and (self.elastic or self.max_replicas != 1):
                 self._log(f"worker {wid} joined")
+                self._join_pending = True
                 self._reconf_needed.set()
 
         with self.worker_lock:
@@ -218,24 +345,71 @@ class DEFER:
     def _get_available_workers(self) -> List[str]:
         with self.worker_lock:
             ws = dict(self.workers)
+            lost = set(self._lost)
         if self.computeNodes:
             allowed = set(self.computeNodes)
             ws = {k: v for k, v in ws.items() if k in allowed or v.get("host") in allowed or "0.0.0.0" in allowed}
-        # workers that failed to load a slice (StateEnum.PARSE_ERROR) are not offered again
-        ws = {k: v for k, v in ws.items() if v.get("state") != "PARSE_ERROR"}
+        now = time.time()
+        # workers that failed to load a slice (StateEnum.PARSE_ERROR), whose session
+        # ended (dead process) or that are quarantined after a STAGE_ERROR are not offered
+        ws = {k: v for k, v in ws.items() if v.get("state") != "PARSE_ERROR" and k not in lost
+              and self._quarantine.get(k, 0) <= now}
         # deterministic order (host, device) keeps stage placement - and each worker's
         # cached slices - stable across epochs; consecutive GPUs of a host become
         # consecutive stages (neighbouring xGMI peers)
         return sorted(ws, key=lambda k: (ws[k].get("host", ""), ws[k].get("device", ""), k))
 
+    # ------------------------------------------------------------ sessions
+    def _ensure_session(self, wid: str) -> None:
+        """Hold one liveness connection per worker: its EOF is the fastest
+        detector of a dead worker process (the kernel closes the socket at once;
+        the lease only expires after its TTL)."""
+        if wid in self._sessions:
+            return
+        with self.worker_lock:
+            rec = self.workers.get(wid)
+        if rec is None:
+            return
+        try:
+            s = socket.create_connection((rec["host"], int(rec["config_port"])), timeout=2)
+            socket_send(json.dumps({"cmd": "session"}).encode(), s, CTRL_CHUNK)
+            if s.recv(1) != ACK:
+                s.close()
+                return
+            s.settimeout(None)
+        except OSError:
+            return
+        self._sessions[wid] = s
+        pid = rec.get("pid")
+
+        def watch():
+            try:
+                while not self._shutdown_event.is_set():
+                    if not s.recv(64):
+                        break
+            except OSError:
+                pass
+            if self._sessions.get(wid) is s:
+                self._sessions.pop(wid, None)
+            if self._shutdown_event.is_set():
+                return
+            with self.worker_lock:
+                self._lost[wid] = pid
+            p = self._replica_of(wid)
+            if p is not None:
+                self._mark_dirty(p.replica, f"worker {wid} connection lost", wid=wid)
+
+        threading.Thread(target=watch, daemon=True, name=f"defer-session-{wid}").start()
+
     # ---------------------------------------------------------- configure
-    def _send_full_configuration(self, rec: dict, manifest: SliceManifest, arrays: list, cfg: dict) -> None:
+    def _send_full_configuration(self, rec: dict, manifest: Optional[SliceManifest], arrays: Optional[list],
+                                 cfg: dict) -> None:
         """Config push + ACK (`src/dispatcher.py:223-264`)."""
         s = socket.create_connection((rec["host"], int(rec["config_port"])), timeout=5)
         try:
             s.settimeout(120)
             socket_send(json.dumps(cfg).encode(), s, CTRL_CHUNK)
-            if not cfg.get("cached"):
+            if manifest is not None:
                 send_slice(s, manifest, arrays, self.chunk_size, self.weight_codec)
             ack = s.recv(1)
             if ack != ACK:
@@ -244,21 +418,38 @@ class DEFER:
         finally:
             s.close()
 
+    def _slice_key(self, cuts: Sequence[str], partition_index: int) -> str:
+        return f"{self._model_key}|{','.join(cuts)}|{partition_index}|b{self.batch}"
+
     def _acquire_and_configure_worker(self, partition_index: int, wid: str, cfg: dict) -> Optional[str]:
-        """Configure worker `wid` with slice `partition_index` (1-based); returns its id or None."""
+        """Configure worker `wid` with slice `partition_index` (1-based) of
+        cfg["part_at"]; returns its id or None.  Resident model: the worker cuts
+        its own slice (no weights move).  Else a slice it already holds is
+        selected by key, and only a new slice is pushed."""
         with self.worker_lock:
             rec = self.workers.get(wid)
         if rec is None:
             return None
-        m, arrays = self.models_to_dispatch[partition_index - 1]
-        key = f"{self._model.name}|{','.join(self._cur_cuts)}|{partition_index}|b{self.batch}"
+        cuts = list(cfg["part_at"])
+        key = self._slice_key(cuts, partition_index)
         cfg = dict(cfg)
         cfg["cache_key"] = key
+        if self._model_key in self._resident.get(wid, ()):
+            cfg["model_key"] = self._model_key
+            try:
+                self._send_full_configuration(rec, None, None, cfg)
+                return wid
+            except RuntimeError as e:
+                if "not resident" not in str(e):
+                    raise
+                self._resident.get(wid, set()).discard(self._model_key)
+                cfg.pop("model_key")
+        m, arrays = self._slices_for(cuts)[partition_index - 1]
         # a worker keeps every slice it was ever sent resident, so a repartition
         # back to known cuts is a pointer swap instead of a weight push
         cfg["cached"] = key in self._sent_slices.get(wid, set())
         try:
-            self._send_full_configuration(rec, m, arrays, cfg)
+            self._send_full_configuration(rec, None if cfg["cached"] else m, arrays, cfg)
         except RuntimeError as e:
             if not (cfg["cached"] and "not cached" in str(e)):
                 raise
@@ -267,60 +458,227 @@ class DEFER:
         self._sent_slices.setdefault(wid, set()).add(key)
         return wid
 
+    def _stage_cfg(self, epoch: int, st: int, k: int, cuts: List[str], recs: List[dict], rid: int) -> dict:
+        rec = recs[st]
+        nxt = None
+        if st < k - 1:
+            nxt = {"host": recs[st + 1]["host"], "port": int(recs[st + 1]["data_port"])}
+        cfg = {"cmd": "configure", "epoch": epoch, "stage": st, "stages": k, "batch": self.batch,
+               "next": nxt, "result_addr": [self._result_host(rec), self.result_port], "part_at": list(cuts),
+               "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid}
+        if self.transport != "tcp":
+            cfg["link_codec"] = self.link_codec
+            cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
+                                 "store_host": self._result_host(rec), "store_port": self._store_port,
+                                 "timeout": 30}
+        return cfg
+
+    def _configure_replica(self, rid: int, members: List[str], cuts: List[str]) -> Optional[Pipeline]:
+        """Configure `members` as the stages of one replica (new epoch) and open
+        its input link.  The k configure pushes run in parallel."""
+        t0 = time.time()
+        k = len(members)
+        self._epoch += 1
+        epoch = self._epoch
+        with self.worker_lock:
+            if any(w not in self.workers for w in members):
+                return None
+            recs = [dict(self.workers[w]) for w in members]
+        errs: List[BaseException] = []
+        ok = [False] * k
+
+        def one(st):
+            try:
+                cfg = self._stage_cfg(epoch, st, k, cuts, recs, rid)
+                ok[st] = self._acquire_and_configure_worker(st + 1, members[st], cfg) is not None
+            except BaseException as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+
+        ts = [threading.Thread(target=one, args=(st,), daemon=True) for st in range(k)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        if not all(ok):
+            self._log(f"replica {rid}: a worker vanished during configuration")
+            return None
+        hello = json.dumps({"epoch": epoch, "from_stage": -1}).encode()
+        s0 = connect(recs[0]["host"], int(recs[0]["data_port"]), hello=hello)
+        for w in members:
+            self._ensure_session(w)
+        p = Pipeline(epoch, list(cuts), list(members), recs, s0, replica=rid)
+        self._log(f"epoch {epoch}: replica {rid}, {k} stages on {members} cuts={cuts} "
+                  f"({(time.time() - t0) * 1e3:.0f} ms)")
+        return p
+
+    def _install(self, p: Pipeline) -> None:
+        with self._rep_lock:
+            old = self.replicas.get(p.replica)
+            self.replicas[p.replica] = p
+            n = len(self.replicas)
+        self._cur_cuts = list(p.part_at)
+        self.models_to_dispatch = self._slices_for(p.part_at)
+        self.concurrency_sem.set_replicas(n)
+        if old is not None and old.stage0 is not None:
+            try:
+                old.stage0.close()
+            except OSError:
+                pass
+        if self.resident or self.prepare:
+            t = threading.Thread(target=self._after_epoch, args=(p,), daemon=True, name="defer-after-epoch")
+            t.start()
+            self._bg.append(t)
+
+    def _drop_replica(self, rid: int) -> None:
+        with self._rep_lock:
+            old = self.replicas.pop(rid, None)
+            n = len(self.replicas)
+        self.concurrency_sem.set_replicas(n)
+        if old is not None and old.stage0 is not None:
+            try:
+                old.stage0.close()
+            except OSError:
+                pass
+
+    def _assigned(self, exclude: Optional[int] = None) -> set:
+        with self._rep_lock:
+            return {w for r, p in self.replicas.items() if r != exclude for w in p.workers}
+
     def _form_pipeline(self) -> bool:
-        """(Re)build the pipeline for the current live worker set; new epoch."""
+        """(Re)build every replica for the current live worker set (new epochs)."""
         with self._reconf_lock:
-            t0 = time.time()
             live = self._probe_live(self._get_available_workers())
             if not live:
                 self._log(f"no workers available ({len(live)})")
                 return False
-            g = self._model.graph
+            with self._rep_lock:
+                old = dict(self.replicas)
+            for rid in old:
+                self._drop_replica(rid)
             want = len(self._user_cuts) + 1
-            k = min(want, len(live)) if not self.elastic else len(live)
-            if k == want:
-                cuts = list(self._user_cuts)
+            if len(live) < want or (self.elastic and self.max_replicas == 1):
+                groups = [live]                               # one pipeline over every live worker
             else:
-                cuts, _ = plan_cuts(g, k, batch=self.batch)
-            self._cur_cuts = cuts
-            self.models_to_dispatch = self._partition(self._model, cuts)
-            members = live[:k]
-            self._epoch += 1
-            epoch = self._epoch
-            old = self.pipeline
-            self.pipeline = None
-            if old is not None and old.stage0 is not None:
+                r = len(live) // want
+                if self.max_replicas is not None:
+                    r = min(r, self.max_replicas)
+                if self.elastic and r == 1:
+                    groups = [live]
+                else:
+                    groups = [live[i * want:(i + 1) * want] for i in range(r)]
+            formed = 0
+            for members in groups:
+                rid = self._next_rid
+                self._next_rid += 1
+                p = self._configure_replica(rid, members, self._plan(len(members)))
+                if p is None:
+                    continue
+                self._install(p)
+                formed += 1
+            used = self._assigned()
+            for wid in live:
+                if wid not in used:
+                    self._send_ctrl(wid, {"cmd": "stop_epoch"})   # spares drop any old data plane
+            return formed > 0
+
+    def _reform(self, rid: int) -> Optional[Pipeline]:
+        """Re-form replica `rid` from its surviving workers plus spares.  Enough
+        workers for the target stage count: survivors keep their stages (their
+        slices are already built) and spares fill the holes; fewer: re-plan
+        balanced cuts over what is left."""
+        with self._reconf_lock:
+            with self._rep_lock:
+                cur = self.replicas.get(rid)
+            old_members = list(cur.workers) if cur else []
+            avail = self._probe_live(self._get_available_workers())
+            others = self._assigned(exclude=rid)
+            survivors = [w for w in old_members if w in avail]
+            spares = [w for w in avail if w not in others and w not in old_members]
+            want = len(self._user_cuts) + 1
+            single = len(self.replicas) <= 1
+            if self.elastic and single:
+                members = survivors + spares                    # elastic single pipeline: use everyone
+            elif len(survivors) + len(spares) >= want:
+                members, it = [], iter(spares)
+                for w in old_members[:want] if len(old_members) >= want else old_members:
+                    members.append(w if w in survivors else next(it))
+                while len(members) < want:
+                    members.append(next(it))
+            else:
+                members = survivors + spares
+            if cur is not None:
+                self._retired.add(cur.epoch)
+            self._excluded.update(w for w in old_members if w not in members)
+            if not members:
+                self._log(f"replica {rid}: no workers left")
+                return None
+            p = self._configure_replica(rid, members, self._plan(len(members)))
+            if p is None:
+                return None
+            self._install(p)
+            for w in old_members:
+                if w not in members and w in avail:
+                    self._send_ctrl(w, {"cmd": "stop_epoch"})
+            return p
+
+    def _after_epoch(self, p: Pipeline) -> None:
+        """Background work after an epoch forms: push the whole model once to
+        every worker that lacks it (so later re-plans are local slicing), then
+        tell each member which slices the likely next plans need (`prepare`)."""
+        g = self._model.graph if self._model else None
+        if g is None:
+            return
+        with self.worker_lock:
+            live = [w for w in self.workers if w not in self._lost]
+        if self.resident:
+            for wid in live:
+                if self._shutdown_event.is_set():
+                    return
+                if self._model_key in self._resident.get(wid, ()):
+                    continue
+                with self.worker_lock:
+                    rec = self.workers.get(wid)
+                if rec is None:
+                    continue
                 try:
-                    old.stage0.close()
-                except OSError:
-                    pass
-            with self.worker_lock:
-                recs = [dict(self.workers[w]) for w in members]
-            # configure last stage first so downstream listeners exist early
-            for st in reversed(range(k)):
-                rec = recs[st]
-                nxt = None
-                if st < k - 1:
-                    nxt = {"host": recs[st + 1]["host"], "port": int(recs[st + 1]["data_port"])}
-                cfg = {"cmd": "configure", "epoch": epoch, "stage": st, "stages": k, "batch": self.batch,
-                       "next": nxt, "result_addr": [self._result_host(rec), self.result_port],
-                       "codec": self.codec, "graph": self.device_graph, "transport": self.transport}
-                if self.transport != "tcp":
-                    cfg["link_codec"] = self.link_codec
-                    cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
-                                         "store_host": self._result_host(rec), "store_port": self._store_port,
-                                         "timeout": 30}
-                if self._acquire_and_configure_worker(st + 1, members[st], cfg) is None:
-                    self._log(f"worker {members[st]} vanished during configuration")
-                    return False
-            # live workers left out of this epoch drop their old data plane
-            for wid in live[k:]:
-                self._send_ctrl(wid, {"cmd": "stop_epoch"})
-            hello = json.dumps({"epoch": epoch, "from_stage": -1}).encode()
-            s0 = connect(recs[0]["host"], int(recs[0]["data_port"]), hello=hello)
-            self.pipeline = Pipeline(epoch, cuts, members, recs, s0)
-            self._log(f"epoch {epoch}: {k} stages on {members} cuts={cuts} ({(time.time() - t0) * 1e3:.0f} ms)")
-            return True
+                    m, arrays = self._whole_model()
+                    self._send_full_configuration(rec, m, arrays, {"cmd": "load_model", "key": self._model_key})
+                    self._resident.setdefault(wid, set()).add(self._model_key)
+                except (OSError, RuntimeError) as e:
+                    self._log(f"model push to {wid} failed: {type(e).__name__}: {e}")
+        if not self.prepare or not any(self._model_key in v for v in self._resident.values()):
+            return
+        k = len(p.workers)
+        spares = [w for w in live if w not in self._assigned()]
+        want = len(self._user_cuts) + 1
+        hints: Dict[str, List[dict]] = {}
+        recs = p.records
+        if spares and k == want:
+            # a spare takes a dead worker's place: it needs any stage of these cuts
+            for w in spares:
+                hints[w] = [self._stage_cfg(0, st, k, p.part_at, recs, p.replica) for st in range(k)]
+        elif k >= 2:
+            cuts = self._plan(k - 1)
+            fake = recs[:k - 1]
+            for pos, w in enumerate(p.workers):
+                # the survivor at position pos becomes stage pos-1 (a worker before it
+                # died) or stays stage pos (one after it died)
+                hints[w] = [self._stage_cfg(0, st, k - 1, cuts, fake, p.replica)
+                            for st in (pos - 1, pos) if 0 <= st < k - 1]
+        for w, cfgs in hints.items():
+            if self._model_key not in self._resident.get(w, ()):
+                continue
+            for c in cfgs:
+                c["cache_key"] = self._slice_key(c["part_at"], c["stage"] + 1)
+                c["model_key"] = self._model_key
+            self._send_ctrl(w, {"cmd": "prepare", "configs": cfgs})
+
+    def _whole_model(self) -> Tuple[SliceManifest, list]:
+        if not hasattr(self, "_whole"):
+            self._whole = self._partition(self._model, [])[0]
+        return self._whole
 
     def _send_ctrl(self, wid: str, cmd: dict) -> bool:
         with self.worker_lock:
@@ -378,20 +736,31 @@ class DEFER:
 
     # ------------------------------------------------------- data: input
     def _send_to_stage0(self, rid: int, x: np.ndarray) -> bool:
-        p = self.pipeline
-        if p is None or p.stage0 is None:
+        """Send request `rid` to the next serving replica (round-robin)."""
+        with self._rep_lock:
+            reps = [self.replicas[r] for r in sorted(self.replicas)]
+        if not reps:
             return False
-        m = Message(1, rid, p.epoch, int(x.shape[0]), [x], [False])
-        try:
-            with p.lock:
-                send_message(p.stage0, m, self.codec, self.chunk_size, timeout_ms=10000)
+        for i in range(len(reps)):
+            p = reps[(self._rr + i) % len(reps)]
+            if p.stage0 is None or p.replica in self._dirty:
+                continue
+            m = Message(1, rid, p.epoch, int(x.shape[0]), [x], [False])
             with self.inflight_lock:
                 if rid in self.inflight_tasks:
                     self.inflight_tasks[rid]["epoch"] = p.epoch
-            return True
-        except (OSError, RuntimeError):
-            self._reconf_needed.set()
-            return False
+                    self.inflight_tasks[rid]["replica"] = p.replica
+            try:
+                with p.lock:
+                    send_message(p.stage0, m, self.codec, self.chunk_size, timeout_ms=10000)
+                self._rr = (self._rr + i + 1) % len(reps)
+                return True
+            except (OSError, RuntimeError):
+                self._mark_dirty(p.replica, f"replica {p.replica}: input link failed", epoch=p.epoch)
+        with self.inflight_lock:
+            if rid in self.inflight_tasks:
+                self.inflight_tasks[rid]["epoch"] = None          # unsent: replayed after recovery
+        return False
 
     def _startDistEdgeInference(self, input_stream: "queue.Queue") -> None:
         """Input pump (`src/dispatcher.py:99-107`): request ids, credits, retention."""
@@ -402,7 +771,9 @@ class DEFER:
                 continue
             if x is None:
                 continue
-            x = np.asarray(x, np.float32)
+            x = np.asarray(x)
+            if x.dtype != np.uint8:
+                x = np.asarray(x, np.float32)
             if x.ndim == 3:
                 x = x[None]
             for i in range(0, x.shape[0], self.batch):
@@ -425,7 +796,7 @@ class DEFER:
         self._next_req += 1
         with self.inflight_lock:
             self.inflight_tasks[rid] = {"partition": partition_index, "data": data, "start_time": time.time(),
-                                        "epoch": None}
+                                        "epoch": None, "replica": None, "replays": 0}
         self._forward_data_to_worker(rid, data)
         return rid
 
@@ -497,10 +868,15 @@ class DEFER:
             threading.Thread(target=self._result_conn, args=(conn, output_stream), daemon=True).start()
 
     def _result_conn(self, conn: socket.socket, output_stream: "queue.Queue") -> None:
+        epoch = None
         try:
             hello = socket_recv(conn, CTRL_CHUNK)
             if not hello:
                 return
+            try:
+                epoch = json.loads(hello).get("epoch")
+            except ValueError:
+                epoch = None
             while not self._shutdown_event.is_set():
                 m = recv_message(conn, self.chunk_size)
                 if m is None:
@@ -511,6 +887,25 @@ class DEFER:
         finally:
             self._result_conns.discard(conn)
             conn.close()
+        if not self._shutdown_event.is_set() and epoch is not None:
+            # the last stage of a serving epoch hung up: that replica is broken
+            with self._rep_lock:
+                hit = [p for p in self.replicas.values() if p.epoch == epoch]
+            for p in hit:
+                self._mark_dirty(p.replica, f"replica {p.replica}: result link of epoch {epoch} closed", epoch=epoch)
+
+    def _emit(self, rid: int, item, output_stream: "queue.Queue") -> None:
+        self._completed += 1
+        self.completion_times.append(time.time())
+        if self.ordered:
+            with self.inflight_lock:
+                self._order_buf[rid] = item
+                while self._next_emit in self._order_buf:
+                    output_stream.put(self._order_buf.pop(self._next_emit))
+                    self._next_emit += 1
+        else:
+            output_stream.put(item)
+        self.concurrency_sem.release()
 
     def _complete(self, m: Message, output_stream: "queue.Queue") -> None:
         with self.inflight_lock:
@@ -525,65 +920,126 @@ class DEFER:
         if m.bf16 and m.bf16[0]:
             pred = (pred.astype(np.uint32) << 16).view(np.float32)
         pred = np.array(pred[: m.count])             # own, writable copy for the caller
-        self._completed += 1
-        self.completion_times.append(time.time())
-        if self.ordered:
-            with self.inflight_lock:
-                self._order_buf[m.req_id] = pred
-                while self._next_emit in self._order_buf:
-                    output_stream.put(self._order_buf.pop(self._next_emit))
-                    self._next_emit += 1
-        else:
-            output_stream.put(pred)
-        self.concurrency_sem.release()
+        self._emit(m.req_id, pred, output_stream)
+
+    @property
+    def duplicates_dropped(self) -> int:
+        return int(METRICS.counters.get("results_duplicate_dropped", 0))
 
     # ----------------------------------------------------- fault handling
     def _task_watchdog(self) -> None:
-        while not self._shutdown_event.wait(0.05):
+        while not self._shutdown_event.wait(0.02):
             now = time.time()
-            stale = False
             with self.inflight_lock:
-                for t in self.inflight_tasks.values():
-                    if now - t["start_time"] > self.task_timeout:
-                        stale = True
-                        break
-            if stale and self.pipeline is not None:
-                self._log("watchdog: stale in-flight task")
-                self._reconf_needed.set()
+                stale = {t["replica"] for t in self.inflight_tasks.values()
+                         if now - t["start_time"] > self.task_timeout and t["replica"] is not None}
+                unsent = any(t["epoch"] is None for t in self.inflight_tasks.values()
+                             if now - t["start_time"] > 0.5)
+            for rid in stale:
+                if rid not in self._dirty:
+                    self._mark_dirty(rid, f"watchdog: stale in-flight task on replica {rid}")
+            if unsent and not self._dirty:
+                self._reconf_needed.set()                # requests that found no replica
             if self._reconf_needed.is_set():
                 self._reconf_needed.clear()
-                self._recover()
+                for rid in sorted(self._dirty):
+                    self._recover(rid)
+                if self._join_pending:
+                    self._join_pending = False
+                    self._handle_join()
+                if not self._dirty:
+                    self._replay_unsent()
 
-    def _recover(self) -> None:
-        t_fail = time.time()
+    def _handle_join(self) -> None:
+        """A new worker: complete a degraded replica, add a replica, or (elastic,
+        single pipeline) deepen the pipeline over every live worker."""
+        want = len(self._user_cuts) + 1
+        with self._rep_lock:
+            reps = dict(self.replicas)
+        if not reps:
+            if self._form_pipeline():
+                self._log("pipeline formed after join")
+            return
+        degraded = [r for r, p in reps.items() if len(p.workers) < want]
+        if degraded:
+            self._recover(degraded[0], cause="join")
+            return
+        spares = [w for w in self._get_available_workers() if w not in self._assigned()]
+        if self.elastic and len(reps) == 1 and (self.max_replicas == 1 or len(spares) < want):
+            self._recover(next(iter(reps)), cause="join")
+            return
+        if self.max_replicas is not None and len(reps) >= self.max_replicas:
+            return
+        spares = self._probe_live(spares)
+        if len(spares) >= want:
+            with self._reconf_lock:
+                rid = self._next_rid
+                self._next_rid += 1
+                p = self._configure_replica(rid, spares[:want], self._plan(want))
+                if p is not None:
+                    self._install(p)
+                    self._log(f"join: replica {rid} added")
+
+    def _replay(self, tasks: List[Tuple[int, dict]]) -> None:
+        for rid, t in tasks:
+            t["replays"] = t.get("replays", 0) + 1
+            if t["replays"] > self.max_replays:
+                with self.inflight_lock:
+                    if self.inflight_tasks.pop(rid, None) is None:
+                        continue
+                METRICS.inc("requests_failed")
+                self._log(f"request {rid} failed {t['replays'] - 1} recoveries: giving up")
+                if self._output is not None:
+                    self._emit(rid, RequestFailed(rid, "replayed too often"), self._output)
+                continue
+            t["start_time"] = time.time()
+            self._send_to_stage0(rid, t["data"])
+
+    def _replay_unsent(self) -> None:
+        with self.inflight_lock:
+            todo = sorted((r, t) for r, t in self.inflight_tasks.items() if t["epoch"] is None)
+        for rid, t in todo:
+            t["start_time"] = time.time()
+            self._send_to_stage0(rid, t["data"])
+
+    def _recover(self, rid: int, cause: str = "failure") -> None:
+        # taken off the dirty list first: a failure during the re-form marks it again
+        t_fail = self._dirty.pop(rid, time.time())
         done_before = self._completed
-        ok = False
-        deadline = t_fail + max(self.worker_wait, 10.0)
+        with self._rep_lock:
+            old = self.replicas.get(rid)
+        old_epoch = old.epoch if old else None
+        p = None
+        deadline = time.time() + max(self.worker_wait, 10.0)
         while not self._shutdown_event.is_set() and time.time() < deadline:
-            # let expired leases drain so the live set is accurate
-            time.sleep(0.05)
             try:
-                ok = self._form_pipeline()
+                p = self._reform(rid)
             except Exception as e:  # noqa: BLE001 - a member died during configuration; retry
                 self._log(f"reconfigure failed: {type(e).__name__}: {e}")
-                ok = False
-            if ok:
+                p = None
+            if p is not None:
+                break
+            with self._rep_lock:
+                others = [r for r in self.replicas if r != rid]
+            if others:                                   # other replicas keep serving: drop this one
+                self._drop_replica(rid)
+                self._log(f"replica {rid} dropped (no workers to re-form it)")
                 break
             time.sleep(0.1)
-        if not ok:
+        if p is None and rid in self.replicas:
             self._log("recovery failed: no usable workers")
             return
         t_ready = time.time()
         with self.inflight_lock:
-            replay = sorted(self.inflight_tasks.items())
-            for _, t in replay:
-                t["start_time"] = time.time()
-        for rid, t in replay:
-            self._send_to_stage0(rid, t["data"])
+            replay = sorted((r, t) for r, t in self.inflight_tasks.items()
+                            if (t["replica"] == rid and t["epoch"] == old_epoch) or t["epoch"] is None)
+        if cause == "failure" or replay:
+            self._replay(replay)
         self.recoveries.append({"t_fail": t_fail, "t_ready": t_ready, "replayed": len(replay),
-                                "epoch": self._epoch, "reconfig_ms": (t_ready - t_fail) * 1e3,
-                                "completed_before": done_before})
-        self._log(f"recovered in {(t_ready - t_fail) * 1e3:.0f} ms, replayed {len(replay)} requests")
+                                "epoch": p.epoch if p else None, "replica": rid, "cause": cause,
+                                "reconfig_ms": (t_ready - t_fail) * 1e3, "completed_before": done_before})
+        self._log(f"replica {rid} recovered ({cause}) in {(t_ready - t_fail) * 1e3:.0f} ms, "
+                  f"replayed {len(replay)} requests")
 
     # --------------------------------------------------------------- main
     def run_defer(self, model: Model, partition_layers: Sequence[str], input_stream: "queue.Queue",
@@ -592,13 +1048,14 @@ class DEFER:
         if self.membership_server is not None and not self.membership_server._thread.is_alive():
             self.membership_server.start()
         self._model = model
+        self._model_key = f"{model.name}@{id(model):x}"
         self._user_cuts = list(partition_layers)
         self._cur_cuts = list(partition_layers)
-        self._sent_slices: Dict[str, set] = {}
+        self._output = output_stream
         # 1. worker monitor
         threading.Thread(target=self._worker_monitor, daemon=True, name="defer-monitor").start()
         # 2. partition (validates the cut list up front)
-        self.models_to_dispatch = self._partition(model, partition_layers)
+        self.models_to_dispatch = self._slices_for(partition_layers)
         # 3. wait for workers
         deadline = time.time() + self.worker_wait
         while time.time() < deadline:
@@ -614,7 +1071,7 @@ class DEFER:
         # 4. result server
         threading.Thread(target=self._intermediate_result_server, args=(output_stream,), daemon=True,
                          name="defer-results").start()
-        # place the pipeline (retry while members come up)
+        # place the pipeline replicas
         if not self._form_pipeline():
             self._shutdown_event.set()
             return
@@ -633,6 +1090,7 @@ class DEFER:
             self._shutdown_event.set()
 
     def shutdown(self, stop_workers: bool = False) -> None:
+        self._shutdown_event.set()
         if stop_workers:
             for rec in list(self.workers.values()):
                 try:
@@ -642,8 +1100,7 @@ class DEFER:
                     s.close()
                 except OSError:
                     pass
-        self._shutdown_event.set()
-        for c in [self.result_sock] + list(self._result_conns):
+        for c in [self.result_sock] + list(self._result_conns) + list(self._sessions.values()):
             try:
                 c.shutdown(socket.SHUT_RDWR)
             except OSError:
@@ -652,12 +1109,17 @@ class DEFER:
                 c.close()
             except OSError:
                 pass
-        p = self.pipeline
-        if p is not None and p.stage0 is not None:
-            try:
-                p.stage0.close()
-            except OSError:
-                pass
+        with self._rep_lock:
+            reps = list(self.replicas.values())
+        for p in reps:
+            if p.stage0 is not None:
+                try:
+                    p.stage0.close()
+                except OSError:
+                    pass
+        for t in self._bg:
+            if t is not threading.current_thread():
+                t.join(timeout=30)
         if self.membership_server is not None:
             self.membership_server.stop()
 

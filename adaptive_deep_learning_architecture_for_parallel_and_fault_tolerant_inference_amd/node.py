@@ -83,9 +83,7 @@ class StageRuntime:
         # GPU stages with a GPU codec compress frontier tensors on a side HIP stream
         # while the next micro-batch computes (two buffer sets ping-pong)
         self.gpu_codec = self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")
-        self.compute = StageCompute(g, weights, int(cfg["batch"]), node.device,
-                                    graph_capture=cfg.get("graph", True), num_sets=2 if self.gpu_codec else 1,
-                                    host_ring=int(cfg.get("queue", 4)) + 4)
+        self.compute = node.stage_compute(cfg, g, weights)
         if self.gpu_codec:
             self._init_gpu_codec()
         self.inq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
@@ -96,6 +94,12 @@ class StageRuntime:
         self.processed = 0
         self.threads = []
         self.error: Optional[str] = None
+        # held while a micro-batch runs on `compute`: abort() waits on it, so a
+        # cached StageCompute is never driven by two epochs' threads at once
+        self._busy = threading.Lock()
+
+    def quiesced(self) -> bool:
+        return True          # abort() waits for the running micro-batch (`_busy`)
 
     # downstream = next stage's data port, or the dispatcher result port
     def _connect_downstream(self) -> socket.socket:
@@ -131,8 +135,10 @@ class StageRuntime:
         self.abort()
         if report:
             # a broken hop (neighbour SIGKILLed) is published at once, so the
-            # dispatcher re-plans without waiting for the dead worker's lease TTL
-            self.node._publish(state="LINK_ERROR", epoch=self.epoch, error=self.error)
+            # dispatcher re-plans without waiting for the dead worker's lease TTL;
+            # a failure of this stage's own compute is a STAGE_ERROR (the
+            # dispatcher quarantines the worker instead of re-placing onto it)
+            self.node.report_failure(self, "LINK_ERROR" if where in ("recv", "send") else "STAGE_ERROR")
 
     def _recv_loop(self) -> None:
         try:
@@ -140,6 +146,10 @@ class StageRuntime:
                 m = recv_message(self.upstream, self.node.state.chunk_size,
                                  keep_encoded=("zvc", "lz4") if self.gpu_codec else ())
                 if m is None:
+                    if not self.stop.is_set():
+                        # clean EOF inside a live epoch: the upstream process died
+                        # (the kernel closed its socket) or its epoch was torn down
+                        raise ConnectionError("upstream closed the link")
                     break
                 if m.epoch != self.epoch:
                     continue                     # stale micro-batch from an older epoch
@@ -268,11 +278,14 @@ class StageRuntime:
                 except queue.Empty:
                     continue
                 self.node.state.state = StateEnum.BUSY
-                if self.gpu_codec:
-                    out = self._compute_gpu(m)
-                else:
-                    outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
-                    out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
+                with self._busy:
+                    if self.stop.is_set():
+                        break
+                    if self.gpu_codec:
+                        out = self._compute_gpu(m)
+                    else:
+                        outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
+                        out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
                 self.processed += 1
                 while not self.stop.is_set():
                     try:
@@ -310,6 +323,10 @@ class StageRuntime:
                     s.close()
                 except OSError:
                     pass
+        # the micro-batch in flight (if any) has left `compute`; every loop raises
+        # out of its `with self._busy` block before it calls _fail -> abort
+        with self._busy:
+            pass
 
 
 class Node:
@@ -340,6 +357,16 @@ class Node:
         self._rt_lock = threading.Lock()
         self._pending_upstream: Dict[int, list] = {}
         self._slice_cache: Dict[str, Tuple[SliceManifest, Dict[str, np.ndarray]]] = {}
+        # resident whole models (graph, weights) by model key: a re-plan to new cuts
+        # is local slicing, with no weight push
+        self._models: Dict[str, Tuple[object, Dict[str, np.ndarray]]] = {}
+        # built stage computes (packed weights + buffers + captured hipGraphs) by
+        # slice key and runtime shape; `prepare` fills it ahead of a failure
+        self._computes: Dict[tuple, object] = {}
+        self._computes_lock = threading.Lock()
+        self._building: Dict[tuple, threading.Event] = {}
+        self._pub_lock = threading.Lock()
+        self._sessions = 0
         self._stop = threading.Event()
         self.threads = []
 
@@ -415,6 +442,11 @@ class Node:
                 s.close()
             except OSError:
                 pass
+        # background builds (prepare) stop between slices: let the one in progress
+        # finish so no thread is inside native code when the interpreter exits
+        for t in list(self.threads):
+            if t.name == "node-prepare" and t is not threading.current_thread():
+                t.join(timeout=60)
 
     def _publish(self, **kw) -> None:
         if self.registration is not None:
@@ -422,6 +454,97 @@ class Node:
                 self.registration.put(**kw)
             except (OSError, ConnectionError, RuntimeError):
                 pass
+
+    def report_failure(self, rt, state: str) -> None:
+        """Publish a failed epoch (LINK_ERROR / STAGE_ERROR) unless a newer epoch
+        has replaced it: the check and the put happen under the lock that also
+        orders the BUSY put of `_start_epoch`, so a late report can never
+        overwrite the record of the epoch that follows."""
+        with self._pub_lock:
+            if self.runtime is not rt or self.state.epoch != rt.epoch:
+                return
+            self._publish(state=state, epoch=rt.epoch, error=rt.error)
+
+    # -------------------------------------------------- stage computes
+    @staticmethod
+    def compute_shape(cfg: Dict, device: str) -> Tuple[int, int, bool]:
+        """(num_sets, host_ring, graph) the epoch runtime for `cfg` builds its
+        StageCompute with: one definition for configure and prepare."""
+        graph = bool(cfg.get("graph", True))
+        if cfg.get("transport", "tcp") == "tcp":
+            gpu_codec = cfg.get("codec", "lz4") in ("zvc", "lz4") and str(device).startswith("cuda")
+            return (2 if gpu_codec else 1), int(cfg.get("queue", 4)) + 4, graph
+        return int(cfg.get("nsets", 2)), 8, graph
+
+    def _compute_key(self, cfg: Dict) -> Optional[tuple]:
+        key = cfg.get("cache_key")
+        if not key:
+            return None
+        return (key, int(cfg["batch"])) + self.compute_shape(cfg, self.device)
+
+    def stage_compute(self, cfg: Dict, g, weights: Dict[str, np.ndarray], capture_mode: str = "global"):
+        """The StageCompute of a slice: reused from the cache (built by an earlier
+        epoch or by `prepare`), else built now and cached."""
+        from .runtime.stage import StageCompute
+        key = self._compute_key(cfg)
+        num_sets, host_ring, graph = self.compute_shape(cfg, self.device)
+        while key is not None:
+            with self._computes_lock:
+                c = self._computes.get(key)
+                if c is not None:
+                    return c
+                ev = self._building.get(key)
+                if ev is None:
+                    ev = self._building[key] = threading.Event()
+                    break
+            ev.wait(60)                             # a prepare is building this one right now
+        try:
+            c = StageCompute(g, weights, int(cfg["batch"]), self.device, graph_capture=graph, num_sets=num_sets,
+                             host_ring=host_ring, capture_mode=capture_mode)
+        finally:
+            if key is not None:
+                with self._computes_lock:
+                    self._building.pop(key).set()
+        if key is not None:
+            with self._computes_lock:
+                self._computes[key] = c
+        return c
+
+    def _evict_compute(self, cfg: Dict) -> None:
+        key = self._compute_key(cfg)
+        if key is not None:
+            with self._computes_lock:
+                self._computes.pop(key, None)
+
+    def _local_slice(self, cfg: Dict):
+        """Slice a resident model locally: (manifest, weights) for cfg's stage."""
+        from .graph.slicer import partition, subgraph
+        g, w = self._models[cfg["model_key"]]
+        sl = partition(g, list(cfg["part_at"]))[int(cfg["stage"])]
+        m = SliceManifest(g.name, sl.index + 1, sl.name, subgraph(g, sl).to_json(),
+                          [{"name": t} for t in sl.inputs], [{"name": t} for t in sl.outputs], [], sl.start, sl.end)
+        return m, w
+
+    def _prepare(self, cfgs) -> None:
+        """Build (and capture) the StageComputes of likely next epochs in the
+        background, so that a re-plan after a failure is a pointer swap.  Capture
+        runs in thread-local mode: the serving threads keep launching meanwhile."""
+        for cfg in cfgs:
+            if self._stop.is_set():
+                return
+            key = self._compute_key(cfg)
+            if key is None or key in self._computes:
+                continue
+            try:
+                if cfg.get("model_key") in self._models:
+                    m, w = self._local_slice(cfg)
+                elif cfg["cache_key"] in self._slice_cache:
+                    m, w = self._slice_cache[cfg["cache_key"]]
+                else:
+                    continue
+                self.stage_compute(cfg, m.graph(), w, capture_mode="thread_local")
+            except Exception:  # noqa: BLE001 - a prepare is an optimisation only
+                traceback.print_exc()
 
     # ------------------------------------------- reference-named helpers
     @staticmethod
@@ -470,7 +593,39 @@ class Node:
                 return
             cmd = json.loads(raw)
             op = cmd.get("cmd")
-            if op == "configure":
+            if op == "configure" and cmd.get("model_key") in self._models:
+                m, w = self._local_slice(cmd)          # resident model: local slicing, no push
+                self.weights_ready_event.set()
+                self._start_epoch(cmd, m, w)
+                conn.sendall(ACK)
+            elif op == "configure" and cmd.get("model_key"):
+                conn.sendall(NAK)
+                socket_send(b"model not resident", conn, CTRL_CHUNK)
+            elif op == "load_model":
+                m, arrays = recv_slice(conn, self.state.chunk_size)
+                self._models[cmd["key"]] = (m.graph(), arrays_to_dict(m, arrays))
+                conn.sendall(ACK)
+            elif op == "prepare":
+                conn.sendall(ACK)
+                t = threading.Thread(target=self._prepare, args=(cmd.get("configs", []),), daemon=True,
+                                     name="node-prepare")
+                t.start()
+                self.threads.append(t)
+            elif op == "session":
+                # liveness channel: the dispatcher holds this connection open and
+                # sees EOF the moment this process dies (no lease TTL to wait for)
+                conn.sendall(ACK)
+                self._sessions += 1
+                conn.settimeout(0.5)
+                while not self._stop.is_set():
+                    try:
+                        if not conn.recv(64):
+                            break
+                    except socket.timeout:
+                        continue
+                    except OSError:
+                        break
+            elif op == "configure":
                 if cmd.get("cached"):
                     key = cmd["cache_key"]
                     if key not in self._slice_cache:
@@ -526,6 +681,8 @@ class Node:
             old = self.runtime
             if old is not None:
                 old.abort()
+                if not old.quiesced():            # a thread still inside the old compute: do not reuse it
+                    self._evict_compute(old.cfg)
             if cfg.get("transport", "tcp") == "tcp":
                 rt = StageRuntime(self, cfg, m, w)
             else:                                   # RCCL (xGMI) / gloo stage-to-stage links
@@ -543,7 +700,8 @@ class Node:
                 for s in self._pending_upstream.pop(e):
                     s.close()
         self.state.state = StateEnum.BUSY
-        self._publish(state="BUSY", epoch=rt.epoch, partition=m.part_index)
+        with self._pub_lock:
+            self._publish(state="BUSY", epoch=rt.epoch, partition=m.part_index, error=None)
 
     # --------------------------------------------------------- data plane
     def _data_server(self) -> None:
@@ -570,6 +728,9 @@ class Node:
 
 
 def main(argv=None):
+    # epoch communicators are aborted by this runtime (re-plan, stall watch): the
+    # NCCL watchdog must not kill the worker over receives an idle pipeline keeps posted
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
     ap = argparse.ArgumentParser(description="ADAPT worker node (one per GPU)")
     ap.add_argument("--dispatcher", default="127.0.0.1", help="dispatcher / membership host")
     ap.add_argument("--membership-port", type=int, default=2379)

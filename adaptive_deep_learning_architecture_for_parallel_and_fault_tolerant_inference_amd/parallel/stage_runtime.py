@@ -34,7 +34,6 @@ from .epoch_group import Aborted, EpochGroup
 
 class CollectiveStageRuntime:
     def __init__(self, node, cfg: Dict, manifest: SliceManifest, weights: Dict[str, np.ndarray]):
-        from ..runtime.stage import StageCompute
         self.node = node
         self.cfg = cfg
         self.epoch = int(cfg["epoch"])
@@ -46,8 +45,7 @@ class CollectiveStageRuntime:
         self.manifest = manifest
         self.nsets = int(cfg.get("nsets", 2))
         g = manifest.graph()
-        self.compute = StageCompute(g, weights, self.batch, node.device, graph_capture=cfg.get("graph", True),
-                                    num_sets=self.nsets)
+        self.compute = node.stage_compute(cfg, g, weights)
         self.gpu = self.compute.gpu
         self.dev = self.compute.device
         self.group: Optional[EpochGroup] = None     # rendezvous happens on the data thread (after ACK)
@@ -110,9 +108,19 @@ class CollectiveStageRuntime:
             self.threads.append(t)
 
     def _fail(self, where: str, e: BaseException) -> None:
-        if not self.stop.is_set() and not isinstance(e, Aborted):
+        report = not self.stop.is_set() and not isinstance(e, Aborted)
+        if report:
             self.error = f"{where}: {type(e).__name__}: {e}"
         self.abort()
+        if report:
+            # same contract as the TCP runtime (node.py): a broken link is
+            # published at once so the dispatcher re-plans without the lease TTL
+            self.node.report_failure(self, "STAGE_ERROR" if where == "compute" else "LINK_ERROR")
+
+    def quiesced(self) -> bool:
+        """No thread of this epoch is still running (safe to reuse its compute)."""
+        me = threading.current_thread()
+        return not any(t.is_alive() for t in self.threads if t is not me)
 
     def abort(self) -> None:
         if self.stop.is_set():
@@ -145,6 +153,8 @@ class CollectiveStageRuntime:
             while not self.stop.is_set():
                 m = recv_message(self.upstream, self.node.state.chunk_size)
                 if m is None:
+                    if not self.stop.is_set():
+                        raise ConnectionError("dispatcher closed the input link")
                     break
                 if m.epoch != self.epoch:
                     continue
@@ -224,12 +234,31 @@ class CollectiveStageRuntime:
             except queue.Full:
                 continue
 
+    def _handshake(self, G: EpochGroup) -> None:
+        """Connect this epoch's p2p links at formation: RCCL builds a pair's
+        communicator on its first send/recv, so without this the first
+        micro-batch after every re-plan would pay the communicator setup."""
+        dev = self.dev if self.gpu else torch.device("cpu")
+        out, inp = torch.ones(1, device=dev), torch.zeros(1, device=dev)
+        works = []
+        if self.next is not None:
+            works.append(G.isend(out, self.next, 99))
+        if self.prev is not None:
+            works.append(G.irecv(inp, self.prev, 99))
+        for w in works:
+            G.wait(w)
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            G.wait_event(ev, timeout_s=float(self.cfg["collective"].get("timeout", 30)))
+
     def _data_loop(self) -> None:
         cc = self.cfg["collective"]
         try:
             self.group = EpochGroup(cc["backend"], cc["store_host"], int(cc["store_port"]), self.epoch, self.stage,
                                     self.stages, self.dev if self.gpu else None, float(cc.get("timeout", 30)),
-                                    ctl=self.link_codec != "none")
+                                    ctl=self.link_codec != "none", stall_s=float(cc.get("stall_s", 10.0)))
+            self._handshake(self.group)
         except Exception as e:  # noqa: BLE001 - rendezvous failed (a member died): epoch is dead
             self._fail("rendezvous", e)
             return

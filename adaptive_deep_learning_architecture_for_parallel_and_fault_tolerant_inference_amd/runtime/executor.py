@@ -629,8 +629,11 @@ class SliceExecutor:
             st = self.steps[i]
             raise RuntimeError(f"step {i} ({st.kind} -> {st.out}, cfg {self.cfg.get(i)}) failed: {e}") from e
 
-    def capture(self) -> None:
-        """Record the step list of every buffer set into its own hipGraph."""
+    def capture(self, mode: str = "global") -> None:
+        """Record the step list of every buffer set into its own hipGraph.
+        mode="thread_local" lets other threads keep launching and synchronising
+        while this one captures (a worker preparing its next slice in the
+        background of a serving epoch)."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -640,7 +643,7 @@ class SliceExecutor:
         torch.cuda.synchronize(self.device)
         for j in range(self.num_sets):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=mode):
                 self._launch(j)
             self._graphs[j] = g
         torch.cuda.synchronize(self.device)

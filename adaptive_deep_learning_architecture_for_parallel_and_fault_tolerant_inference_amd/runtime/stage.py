@@ -50,7 +50,7 @@ def to_numpy(t: torch.Tensor) -> Tuple[np.ndarray, bool]:
 class StageCompute:
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device: str = "cpu",
                  outputs: Optional[Sequence[str]] = None, graph_capture: bool = True, num_sets: int = 1,
-                 host_ring: int = 8):
+                 host_ring: int = 8, capture_mode: str = "global"):
         self.g = g
         self.batch = batch
         self.device = torch.device(device)
@@ -64,7 +64,7 @@ class StageCompute:
             from .executor import SliceExecutor
             self.ex = SliceExecutor(g, weights, batch, device=self.device, outputs=self.outputs, num_sets=num_sets)
             if graph_capture:
-                self.ex.capture()
+                self.ex.capture(mode=capture_mode)
         else:
             from ..ops.reference import ReferenceExecutor
             self.ex = ReferenceExecutor(g, weights, device="cpu")

@@ -31,9 +31,11 @@ class AdaptConfig:
     part_at: Union[List[str], str] = field(default_factory=list)
     batch: int = 1                           # micro-batch size per pipeline message
     elastic: bool = False                    # rebalance on worker join, not only on leave
+    replicas: Union[int, str] = "auto"       # PP x DP: pipeline replicas ("auto" = live // stages)
     # data plane
     transport: str = "tcp"                   # tcp | rccl | gloo
-    codec: str = "lz4"                       # activations on TCP links: none|lz4|zvc|zfp+lz4
+    codec: str = "none"                      # activations on TCP links: none|lz4|zvc|zfp+lz4 (host LZ4 of
+                                             # activations: ratio ~1.02 at 0.2 GB/s, so off by default)
     weight_codec: str = "zfp+lz4"            # slice push (reference: zfp+lz4)
     chunk_size: int = 512 * 1000             # socket chunk (src/dispatcher.py:24)
     # control plane

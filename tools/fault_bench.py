@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--transport", default="tcp")
-    ap.add_argument("--codec", default="lz4")
+    ap.add_argument("--codec", default="none")
+    ap.add_argument("--replicas", default="1", help="pipeline replicas (auto or N)")
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--duration", type=float, default=12.0)
     ap.add_argument("--kill-at", type=float, default=5.0)
@@ -52,7 +53,8 @@ def main():
     m = resnet(a.model, seed=0, input_shape=(a.image, a.image, 3))
     cuts, _ = plan_cuts(m.graph, a.workers, batch=a.batch)
     d = DEFER(membership_port=0, result_port=0, worker_wait=120, batch=a.batch, codec=a.codec, weight_codec="lz4",
-              max_inflight=a.inflight, task_timeout=30, min_workers=a.workers, transport=a.transport)
+              max_inflight=a.inflight, task_timeout=30, min_workers=a.workers, transport=a.transport,
+              replicas=a.replicas)
     d.membership_server.start()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     procs = {}
@@ -76,9 +78,14 @@ def main():
             except queue.Full:
                 continue
 
-    # wait for the pipeline to come up before the clock starts
+    # wait for the pipeline to come up, and for the whole model to be resident on
+    # every worker (background push after the first epoch), before the clock starts
     while d.pipeline is None:
         time.sleep(0.05)
+    deadline = time.time() + 120
+    while time.time() < deadline and sum(1 for v in d._resident.values() if v) < a.workers:
+        time.sleep(0.1)
+    time.sleep(1.0)                  # prepare hints: next plans' slices built in the background
     threading.Thread(target=feeder, daemon=True).start()
     got = 0
     t0 = time.time()
@@ -129,7 +136,9 @@ def main():
         "reconfigure_ms": round(rec["reconfig_ms"], 1) if rec else None,
         "replayed": rec["replayed"] if rec else None,
         "throughput_before_img_s": rate_pre, "throughput_after_img_s": rate_post,
-        "requests_sent": sent[0], "results": got, "duplicates_dropped": None,
+        "requests_sent": sent[0], "results": got, "duplicates_dropped": d.duplicates_dropped,
+        "exactly_once": got == sent[0] - inq.qsize(),
+        "detected_by": next((e for _, e in d.events if t_kill and _ > t_kill), None),
         "events": [(round(t - t0, 3), e) for t, e in d.events],
     }
     print(json.dumps(out, indent=1))
