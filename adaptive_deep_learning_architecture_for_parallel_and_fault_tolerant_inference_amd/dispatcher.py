@@ -130,7 +130,7 @@ class DEFER:
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
                  transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
-                 quarantine_s: float = 30.0) -> None:
+                 quarantine_s: float = 30.0, hb_timeout: float = 0.06) -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
         the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
         ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
@@ -205,6 +205,19 @@ class DEFER:
         self._lost: Dict[str, object] = {}          # worker id -> pid whose session ended
         self._quarantine: Dict[str, float] = {}     # worker id -> until (STAGE_ERROR)
         self._sessions: Dict[str, socket.socket] = {}
+        # native UDP heartbeat monitor (csrc/runtime/heartbeat.cpp): a worker silent
+        # for `hb_timeout` has stopped running, however long its process takes to exit
+        self.hb_period_us = 5000
+        self.hb_timeout = hb_timeout
+        self._hb = None
+        self._hb_port = 0
+        self._hb_suspects: set = set()
+        try:
+            from .native import runtime
+            self._hb = runtime().hb_monitor_start(0)
+            self._hb_port = runtime().hb_monitor_port(self._hb)
+        except Exception:  # noqa: BLE001 - heartbeats are an optimisation over session EOF / leases
+            self._hb = None
         self._resident: Dict[str, set] = {}         # worker id -> model keys resident there
         self._slices_by_cuts: Dict[Tuple[str, ...], List[Tuple[SliceManifest, list]]] = {}
         self._sent_slices: Dict[str, set] = {}
@@ -372,7 +385,8 @@ class DEFER:
             return
         try:
             s = socket.create_connection((rec["host"], int(rec["config_port"])), timeout=2)
-            socket_send(json.dumps({"cmd": "session"}).encode(), s, CTRL_CHUNK)
+            socket_send(json.dumps({"cmd": "session", "hb_port": self._hb_port,
+                                    "hb_period_us": self.hb_period_us}).encode(), s, CTRL_CHUNK)
             if s.recv(1) != ACK:
                 s.close()
                 return
@@ -393,13 +407,42 @@ class DEFER:
                 self._sessions.pop(wid, None)
             if self._shutdown_event.is_set():
                 return
-            with self.worker_lock:
-                self._lost[wid] = pid
-            p = self._replica_of(wid)
-            if p is not None:
-                self._mark_dirty(p.replica, f"worker {wid} connection lost", wid=wid)
+            self._worker_dead(wid, pid, "connection lost")
 
         threading.Thread(target=watch, daemon=True, name=f"defer-session-{wid}").start()
+
+    def _worker_dead(self, wid: str, pid, why: str) -> None:
+        with self.worker_lock:
+            if wid in self._lost:
+                return
+            self._lost[wid] = pid
+        p = self._replica_of(wid)
+        if p is not None:
+            self._mark_dirty(p.replica, f"worker {wid} {why}", wid=wid)
+
+    def _hb_watch(self) -> None:
+        """Poll the native heartbeat monitor: a member silent for `hb_timeout`
+        is dead for placement purposes.  A suspect that beats again (a stall,
+        not a death) is released and offered like a joining worker."""
+        from .native import runtime
+        rt = runtime()
+        while not self._shutdown_event.wait(0.005):
+            ages = dict(rt.hb_monitor_ages(self._hb))
+            members = self._assigned()
+            for wid, age in ages.items():
+                if age > self.hb_timeout and wid in members and wid not in self._lost:
+                    with self.worker_lock:
+                        pid = (self.workers.get(wid) or {}).get("pid")
+                    self._hb_suspects.add(wid)
+                    self._worker_dead(wid, pid, f"heartbeat silent for {age * 1e3:.0f} ms")
+                elif age < self.hb_timeout / 2 and wid in self._hb_suspects and wid in self._sessions:
+                    self._hb_suspects.discard(wid)
+                    with self.worker_lock:
+                        self._lost.pop(wid, None)
+                    self._excluded.discard(wid)
+                    self._log(f"worker {wid} beats again: offered as a spare")
+                    self._join_pending = True
+                    self._reconf_needed.set()
 
     # ---------------------------------------------------------- configure
     def _send_full_configuration(self, rec: dict, manifest: Optional[SliceManifest], arrays: Optional[list],
@@ -1075,8 +1118,10 @@ class DEFER:
         if not self._form_pipeline():
             self._shutdown_event.set()
             return
-        # 5. watchdog (also runs recoveries)
+        # 5. watchdog (also runs recoveries) and the heartbeat watch
         threading.Thread(target=self._task_watchdog, daemon=True, name="defer-watchdog").start()
+        if self._hb is not None:
+            threading.Thread(target=self._hb_watch, daemon=True, name="defer-heartbeats").start()
         # 6. input pump
         threading.Thread(target=self._startDistEdgeInference, args=(input_stream,), daemon=True,
                          name="defer-input").start()
@@ -1120,6 +1165,11 @@ class DEFER:
         for t in self._bg:
             if t is not threading.current_thread():
                 t.join(timeout=30)
+        if self._hb is not None:
+            from .native import runtime
+            time.sleep(0.02)                           # the heartbeat watch has seen the shutdown flag
+            runtime().hb_monitor_stop(self._hb)
+            self._hb = None
         if self.membership_server is not None:
             self.membership_server.stop()
 

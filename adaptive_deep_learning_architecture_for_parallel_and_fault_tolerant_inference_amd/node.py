@@ -616,15 +616,30 @@ class Node:
                 # sees EOF the moment this process dies (no lease TTL to wait for)
                 conn.sendall(ACK)
                 self._sessions += 1
-                conn.settimeout(0.5)
-                while not self._stop.is_set():
+                hb = None
+                if cmd.get("hb_port"):
+                    # GIL-free UDP heartbeat to the dispatcher (csrc/runtime/heartbeat.cpp): it
+                    # stops the instant this process is killed, long before the socket closes
+                    from .native import runtime
                     try:
-                        if not conn.recv(64):
+                        hb = runtime().hb_sender_start(conn.getpeername()[0], int(cmd["hb_port"]), self.node_id,
+                                                       int(cmd.get("hb_period_us", 5000)))
+                    except RuntimeError:
+                        hb = None
+                conn.settimeout(0.5)
+                try:
+                    while not self._stop.is_set():
+                        try:
+                            if not conn.recv(64):
+                                break
+                        except socket.timeout:
+                            continue
+                        except OSError:
                             break
-                    except socket.timeout:
-                        continue
-                    except OSError:
-                        break
+                finally:
+                    if hb is not None:
+                        from .native import runtime
+                        runtime().hb_sender_stop(hb)
             elif op == "configure":
                 if cmd.get("cached"):
                     key = cmd["cache_key"]

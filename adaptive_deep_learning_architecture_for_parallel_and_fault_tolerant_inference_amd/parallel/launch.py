@@ -59,18 +59,19 @@ def rank_envs(nprocs: int, port: int, base: Optional[Dict[str, str]] = None,
 
 
 def launch_local(argv: Sequence[str], nprocs: int, script: Optional[str] = None, timeout_s: Optional[float] = None,
-                 port: Optional[int] = None, poll_s: float = 0.05) -> int:
-    """Run `python <script> <argv>` as `nprocs` ranks; returns the job's exit code.
+                 port: Optional[int] = None, poll_s: float = 0.05, module: Optional[str] = None) -> int:
+    """Run `python <script> <argv>` (or `python -m <module> <argv>`) as `nprocs`
+    ranks; returns the job's exit code.
 
     Ranks inherit stdout/stderr (rank 0 prints the bench line).  When any rank
     exits non-zero, or `timeout_s` passes, the rest of the job is terminated."""
-    script = script or sys.argv[0]
+    target = ["-m", module] if module else [script or sys.argv[0]]
     port = port or free_port()
     envs = rank_envs(nprocs, port)
     procs: List[subprocess.Popen] = []
     for e in envs:
         # each rank leads its own process group so a kill reaches its helpers too
-        procs.append(subprocess.Popen([sys.executable, script, *argv], env=e, start_new_session=True))
+        procs.append(subprocess.Popen([sys.executable, *target, *argv], env=e, start_new_session=True))
     t0 = time.monotonic()
     rc = 0
     try:

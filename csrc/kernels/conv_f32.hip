@@ -1,0 +1,378 @@
+// fp32 execution path: implicit-GEMM convolution / GEMM on the fp32 matrix
+// cores (v_mfma_f32_16x16x4_f32) plus the fp32 pooling / element-wise kernels
+// a ResNet slice needs.  This is the reference's precision: Keras runs the
+// whole model in float32 (`src/node.py:177`, `test/local_infer.py:22`).
+//
+//   out[m][n] = act( sum_k X[m][k] * W[n][k] + bias[n] (+ res[m][n]) )
+//
+// m = (img, oh, ow) over the NHWC output, n = output channel, k = (kh, kw, ci)
+// with ci innermost; weights packed [Npad][Kpad] fp32 (BN folded on the host).
+//
+// Tiling (BM x BN x 16 per block, 4 waves on a WM x WN grid, wave tile TM x TN):
+// * the K permutation trick: an MFMA 16x16x4 takes k-slot q (q = lane / 16)
+//   from every lane group; over the 4 MFMAs of one 16-wide K tile, lane group q
+//   supplies k = 4q + s at step s.  A and B use the same permutation, so the
+//   sum is the plain dot product and each lane fetches ONE float4 per fragment
+//   row per K tile (ds_read_b128) instead of four scalar reads;
+// * LDS rows of 16 floats, float4 chunk index XOR-swizzled with (row >> 2) & 3:
+//   the 16 rows a 16-lane group reads land on 16 distinct 4-bank groups;
+// * register-prefetch double buffer: the next K tile is loaded from global
+//   while the MFMAs of this one run, one barrier per K tile;
+// * epilogue straight from the accumulators: for each of its 4 rows a 16-lane
+//   group writes 16 consecutive floats (64 B) of the output row;
+// * split-K: fp32 partial slabs + a reduce launch that applies the epilogue.
+#include "kernels.h"
+
+namespace adapt {
+
+struct ConvF32Params {
+  const float* x;
+  const float* w;
+  const float* bias;
+  const float* res;
+  float* out;
+  float* ws;
+  int B, H, W, Cin;
+  int OH, OW, N;
+  int KH, KW, stride, pad_t, pad_l;
+  int M, K, Kpad;
+  int relu;
+  int ksplit;
+};
+
+namespace {
+
+constexpr int FBK = 16;          // fp32 elements per K tile (4 float4 chunks)
+constexpr int FNT = 256;
+
+__device__ __forceinline__ int fswz(int r, int c) { return r * FBK + ((c ^ ((r >> 2) & 3)) << 2); }
+
+template <int BM, int BN, int WM, int WN, bool PURE, bool VEC>
+__global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int ACH = BM * 4 / FNT, BCH = BN * 4 / FNT;      // float4 chunks per thread per K tile
+  static_assert(WM * WN == 4 && ACH >= 1 && BCH >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) float sa[2][BM * FBK];
+  __shared__ __attribute__((aligned(16))) float sb[2][BN * FBK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tilesN = (p.N + BN - 1) / BN, tilesM = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
+  const int ktiles = p.Kpad / FBK;
+  const int kper = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = blockIdx.y * kper, kt1 = min(ktiles, kt0 + kper);
+
+  // per-thread A rows: chunk c of the tile = (row c / 4, float4 c % 4)
+  int a_base[ACH], a_ih0[ACH], a_iw0[ACH];
+  const int ohw = p.OH * p.OW;
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int m = m0 + (tid + i * FNT) / 4;
+    if (m < p.M) {
+      if (PURE) {
+        a_base[i] = m * p.Cin;
+        a_ih0[i] = a_iw0[i] = 0;
+      } else {
+        const int img = m / ohw, r = m - img * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+        a_base[i] = img * p.H * p.W * p.Cin;
+        a_ih0[i] = oh * p.stride - p.pad_t;
+        a_iw0[i] = ow * p.stride - p.pad_l;
+      }
+    } else {
+      a_base[i] = -1;
+      a_ih0[i] = -(1 << 28);
+      a_iw0[i] = 0;
+    }
+  }
+  f32x4 ra[ACH], rb[BCH];
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = (tid + i * FNT) & 3;
+      const int k = kt * FBK + c * 4;
+      if (a_base[i] < 0 || k >= p.K) { ra[i] = z4; continue; }
+      if (PURE) {
+        ra[i] = *(const f32x4*)(p.x + a_base[i] + k);
+      } else if (VEC) {                       // Cin % 4 == 0: 4 consecutive k share one tap
+        const int tap = k / p.Cin, ci = k - tap * p.Cin, kh = tap / p.KW, kw = tap - kh * p.KW;
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        ra[i] = ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+                    ? *(const f32x4*)(p.x + a_base[i] + (ih * p.W + iw) * p.Cin + ci) : z4;
+      } else {                                // small Cin (the 3-channel image): element-wise gather
+        f32x4 v = z4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = k + e;
+          if (kk < p.K) {
+            const int tap = kk / p.Cin, ci = kk - tap * p.Cin, kh = tap / p.KW, kw = tap - kh * p.KW;
+            const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+              v[e] = p.x[a_base[i] + (ih * p.W + iw) * p.Cin + ci];
+          }
+        }
+        ra[i] = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * FNT, row = c >> 2, ch = c & 3;
+      rb[i] = *(const f32x4*)(p.w + (size_t)(n0 + row) * p.Kpad + kt * FBK + ch * 4);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * FNT;
+      *(f32x4*)(&sa[buf][fswz(c >> 2, c & 3)]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * FNT;
+      *(f32x4*)(&sb[buf][fswz(c >> 2, c & 3)]) = rb[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = z4;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  if (kt0 < kt1) {
+    load(kt0);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load(kt + 1);
+      f32x4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *(const f32x4*)(&sa[buf][fswz(wm * TM + i * 16 + fr, fq)]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *(const f32x4*)(&sb[buf][fswz(wn * TN + j * 16 + fr, fq)]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      if (more) store(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // epilogue from registers: acc[i][j][r] = C[row = wm*TM + i*16 + fq*4 + r][col = wn*TN + j*16 + fr]
+  float* slab = p.ksplit > 1 ? p.ws + (size_t)blockIdx.y * p.M * p.N : nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * TN + j * 16 + fr;
+    if (n >= p.N) continue;
+    const float b = (slab == nullptr && p.bias) ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * TM + i * 16 + fq * 4 + r;
+        if (m >= p.M) continue;
+        const size_t o = (size_t)m * p.N + n;
+        float v = acc[i][j][r];
+        if (slab) {
+          slab[o] = v;
+          continue;
+        }
+        v += b;
+        if (p.res) v += p.res[o];
+        p.out[o] = act_relu(v, p.relu);
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_f32(ConvF32Params p) {
+  const size_t total = (size_t)p.M * p.N;
+  for (size_t o = blockIdx.x * (size_t)blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int s = 0; s < p.ksplit; ++s) v += p.ws[(size_t)s * total + o];
+    const int n = (int)(o % p.N);
+    if (p.bias) v += p.bias[n];
+    if (p.res) v += p.res[o];
+    p.out[o] = act_relu(v, p.relu);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+hipError_t launch_f32(const ConvF32Params& p, bool pure, bool vec, hipStream_t s) {
+  dim3 grid(((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN), p.ksplit), block(FNT);
+  if (pure) hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, true, true>), grid, block, 0, s, p);
+  else if (vec) hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, true>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, false>), grid, block, 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// fp32 tile configs (index -> BM, BN, WM, WN); ops/conv.py F32_TILES mirrors this
+#define ADAPT_F32_CFGS(X) \
+  X(0, 128, 128, 2, 2)    \
+  X(1, 128, 64, 2, 2)     \
+  X(2, 64, 128, 2, 2)     \
+  X(3, 64, 64, 2, 2)
+
+hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
+                            float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
+                            int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,
+                            hipStream_t s) {
+  ConvF32Params p{x, w, bias, res, out, ws, B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
+                  B * OH * OW, K, Kpad, relu, ksplit < 1 ? 1 : ksplit};
+  if (Kpad % FBK || (p.ksplit > 1 && ws == nullptr)) return hipErrorInvalidValue;
+  const bool pure = KH == 1 && KW == 1 && stride == 1 && pad_t == 0 && pad_l == 0 && H == OH && W == OW &&
+                    Cin % 4 == 0;
+  const bool vec = Cin % 4 == 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (cfg) {
+#define X(id, BM_, BN_, WM_, WN_) case id: e = launch_f32<BM_, BN_, WM_, WN_>(p, pure, vec, s); break;
+    ADAPT_F32_CFGS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess || p.ksplit <= 1) return e;
+  size_t total = (size_t)p.M * p.N;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(splitk_reduce_f32, dim3(blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- fp32 layers
+namespace {
+
+__global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                          int H, int W, int C, int OH, int OW, int K, int S,
+                                                          int pad_t, int pad_l, int pad_zero) {
+  const int C4 = C / 4;
+  const size_t total = (size_t)B * OH * OW * C4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    size_t r = i / C4;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    bool padded = false;
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * S - pad_t + kh;
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = ow * S - pad_l + kw;
+        if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) {
+          padded = true;
+          continue;
+        }
+        const f32x4 v = *(const f32x4*)(x + (((size_t)b * H + ih) * W + iw) * C + c4 * 4);
+        m[0] = fmaxf(m[0], v[0]); m[1] = fmaxf(m[1], v[1]); m[2] = fmaxf(m[2], v[2]); m[3] = fmaxf(m[3], v[3]);
+      }
+    }
+    if (padded && pad_zero) {               // a ZeroPadding2D before the pool: the zeros take part
+      m[0] = fmaxf(m[0], 0.f); m[1] = fmaxf(m[1], 0.f); m[2] = fmaxf(m[2], 0.f); m[3] = fmaxf(m[3], 0.f);
+    }
+    *(f32x4*)(y + i * 4) = m;
+  }
+}
+
+// y[b][c] = mean over HW of x[b][hw][c]; one thread per (b, 4 channels)
+__global__ __launch_bounds__(256) void gap_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                      int HW, int C) {
+  const int C4 = C / 4;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C4) return;
+  const int b = i / C4, c4 = i - b * C4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  const float* p = x + (size_t)b * HW * C + c4 * 4;
+  for (int t = 0; t < HW; ++t) s += *(const f32x4*)(p + (size_t)t * C);
+  const float inv = 1.f / (float)HW;
+  *(f32x4*)(y + (size_t)b * C + c4 * 4) = s * inv;
+}
+
+// elementwise fp32: mode 0 add(+act) a+b, 1 bn affine y = x*scale[c]+shift[c] (+act), 2 act only
+__global__ __launch_bounds__(256) void eltwise_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float* __restrict__ y,
+                                                          size_t n4, int C, int op, int relu) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    f32x4 v = *(const f32x4*)(a + i * 4);
+    if (op == 0) {
+      v += *(const f32x4*)(b + i * 4);
+    } else if (op == 1) {
+      const int c = (int)((i * 4) % C);
+      v[0] = v[0] * scale[c] + shift[c];
+      v[1] = v[1] * scale[c + 1] + shift[c + 1];
+      v[2] = v[2] * scale[c + 2] + shift[c + 2];
+      v[3] = v[3] * scale[c + 3] + shift[c + 3];
+    }
+    v[0] = act_relu(v[0], relu); v[1] = act_relu(v[1], relu);
+    v[2] = act_relu(v[2], relu); v[3] = act_relu(v[3], relu);
+    *(f32x4*)(y + i * 4) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void pad_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H,
+                                                      int W, int C, int OH, int OW, int pad_t, int pad_l) {
+  const size_t total = (size_t)B * OH * OW * C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    size_t r = i / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    const int ih = oh - pad_t, iw = ow - pad_l;
+    y[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? x[(((size_t)b * H + ih) * W + iw) * C + c]
+                                                                       : 0.f;
+  }
+}
+
+int grid_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
+}  // namespace
+
+hipError_t maxpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
+                       int pad_l, int pad_zero, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C / 4)), dim3(256), 0, s, x, y, B, H, W,
+                     C, OH, OW, K, S, pad_t, pad_l, pad_zero);
+  return hipGetLastError();
+}
+
+hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gap_f32_kernel, dim3((B * C / 4 + 255) / 256), dim3(256), 0, s, x, y, B, HW, C);
+  return hipGetLastError();
+}
+
+hipError_t eltwise_f32(const float* a, const float* b, const float* scale, const float* shift, float* y, size_t n,
+                       int C, int op, int relu, hipStream_t s) {
+  if (n % 4 || C % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(eltwise_f32_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, a, b, scale, shift, y, n / 4, C, op,
+                     relu);
+  return hipGetLastError();
+}
+
+hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(pad_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C)), dim3(256), 0, s, x, y, B, H, W, C, OH,
+                     OW, pad_t, pad_l);
+  return hipGetLastError();
+}
+
+}  // namespace adapt

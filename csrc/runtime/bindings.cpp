@@ -42,6 +42,25 @@ static std::pair<const uint8_t*, size_t> view(const py::buffer& b, py::buffer_in
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "ADAPT host runtime: framing transport, LZ4 frame codec, reversible zfp-style codec";
 
+  // ---------------------------------------------------------- heartbeats
+  m.def("hb_sender_start", [](const std::string& host, int port, const std::string& id, int period_us) {
+    return reinterpret_cast<uintptr_t>(hb_sender_start(host, port, id, period_us));
+  });
+  m.def("hb_sender_stop", [](uintptr_t h) {
+    NoGil nogil;
+    hb_sender_stop(reinterpret_cast<void*>(h));
+  });
+  m.def("hb_monitor_start", [](int port) { return reinterpret_cast<uintptr_t>(hb_monitor_start(port)); });
+  m.def("hb_monitor_port", [](uintptr_t h) { return hb_monitor_port(reinterpret_cast<void*>(h)); });
+  m.def("hb_monitor_ages", [](uintptr_t h) { return hb_monitor_ages(reinterpret_cast<void*>(h)); });
+  m.def("hb_monitor_forget", [](uintptr_t h, const std::string& id) {
+    hb_monitor_forget(reinterpret_cast<void*>(h), id);
+  });
+  m.def("hb_monitor_stop", [](uintptr_t h) {
+    NoGil nogil;
+    hb_monitor_stop(reinterpret_cast<void*>(h));
+  });
+
   // ------------------------------------------------------------- framing
   m.def("send_frame", [](int fd, py::buffer data, size_t chunk, int timeout_ms) {
     py::buffer_info info;

@@ -3,6 +3,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace adapt_rt {
@@ -54,5 +55,14 @@ void send_frame_parts(int fd, const std::vector<std::pair<const uint8_t*, size_t
                       int timeout_ms);
 bool recv_exact(int fd, uint8_t* p, size_t n, size_t chunk, int timeout_ms, bool eof_ok_at_start);
 bool recv_frame(int fd, std::vector<uint8_t>& out, size_t chunk, int timeout_ms, size_t max_len);
+
+// ---- liveness heartbeats over UDP (heartbeat.cpp): GIL-free sender / monitor threads
+void* hb_sender_start(const std::string& host, int port, const std::string& id, int period_us);
+void hb_sender_stop(void* h);
+void* hb_monitor_start(int port);
+int hb_monitor_port(void* h);
+std::vector<std::pair<std::string, double>> hb_monitor_ages(void* h);   // id -> seconds since its last beat
+void hb_monitor_forget(void* h, const std::string& id);
+void hb_monitor_stop(void* h);
 
 }  // namespace adapt_rt
