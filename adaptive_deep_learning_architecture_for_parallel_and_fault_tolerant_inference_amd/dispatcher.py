@@ -130,7 +130,7 @@ class DEFER:
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
                  transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
-                 quarantine_s: float = 30.0, hb_timeout: float = 0.06) -> None:
+                 quarantine_s: float = 30.0, hb_timeout: float = 0.06, precision: str = "bf16") -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
         the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
         ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
@@ -166,6 +166,8 @@ class DEFER:
         self.resident = resident
         self.prepare = prepare
         self.max_replays = max_replays
+        self.precision = precision                  # worker compute: "bf16" or "fp32" (reference float32)
+        self.prepare_delay = 1.0                    # s after an epoch forms before `prepare` hints go out
         self.quarantine_s = quarantine_s
         # a worker whose config port does not answer within this many seconds is left
         # out of the next epoch even while its membership lease is still alive
@@ -508,7 +510,8 @@ class DEFER:
             nxt = {"host": recs[st + 1]["host"], "port": int(recs[st + 1]["data_port"])}
         cfg = {"cmd": "configure", "epoch": epoch, "stage": st, "stages": k, "batch": self.batch,
                "next": nxt, "result_addr": [self._result_host(rec), self.result_port], "part_at": list(cuts),
-               "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid}
+               "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid,
+               "precision": self.precision}
         if self.transport != "tcp":
             cfg["link_codec"] = self.link_codec
             cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
@@ -692,6 +695,10 @@ class DEFER:
                 except (OSError, RuntimeError) as e:
                     self._log(f"model push to {wid} failed: {type(e).__name__}: {e}")
         if not self.prepare or not any(self._model_key in v for v in self._resident.values()):
+            return
+        # building the next plans' slices competes with the serving threads for CPU
+        # and the GPU: let a freshly formed epoch reach its steady state first
+        if self._shutdown_event.wait(self.prepare_delay):
             return
         k = len(p.workers)
         spares = [w for w in live if w not in self._assigned()]

@@ -81,9 +81,11 @@ class Model:
         return self.graph.count_params()
 
     # ------------------------------------------------------------ compute
-    def predict(self, x: np.ndarray, device: Optional[str] = None, batch: Optional[int] = None) -> np.ndarray:
+    def predict(self, x: np.ndarray, device: Optional[str] = None, batch: Optional[int] = None,
+                precision: str = "bf16") -> np.ndarray:
         """Single-device inference (`test/local_infer.py:22`): our HIP runtime on
-        a GPU, the fp32 oracle on CPU.  Inputs are NHWC float32 images."""
+        a GPU (precision "bf16" or "fp32", the reference's Keras float32), the
+        fp32 oracle on CPU.  Inputs are NHWC float32 images."""
         import torch
         x = np.asarray(x, np.float32)
         if device is None:
@@ -96,13 +98,13 @@ class Model:
             return ex(torch.from_numpy(x)).numpy()
         from ..runtime.executor import SliceExecutor
         b = batch or x.shape[0]
-        key = (device, b)
+        key = (device, b, precision)
         ent = self._executors.get(key)
         if ent is None:
             # one hipGraph per (device, batch) and a pinned result buffer: a request is
             # H2D -> graph replay -> async D2H -> one sync (the reference re-enters TF's
             # per-layer dispatch on every `model.predict`, test/local_infer.py:22)
-            ex = SliceExecutor(self.graph, self.weights, b, device=device)
+            ex = SliceExecutor(self.graph, self.weights, b, device=device, precision=precision)
             ex.capture()
             yout = ex.output_buf(ex.outputs[0])
             ent = self._executors[key] = (ex, torch.empty(yout.shape, dtype=yout.dtype, pin_memory=True))

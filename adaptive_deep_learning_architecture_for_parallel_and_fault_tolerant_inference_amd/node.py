@@ -480,7 +480,7 @@ class Node:
         key = cfg.get("cache_key")
         if not key:
             return None
-        return (key, int(cfg["batch"])) + self.compute_shape(cfg, self.device)
+        return (key, int(cfg["batch"]), cfg.get("precision", "bf16")) + self.compute_shape(cfg, self.device)
 
     def stage_compute(self, cfg: Dict, g, weights: Dict[str, np.ndarray], capture_mode: str = "global"):
         """The StageCompute of a slice: reused from the cache (built by an earlier
@@ -500,7 +500,8 @@ class Node:
             ev.wait(60)                             # a prepare is building this one right now
         try:
             c = StageCompute(g, weights, int(cfg["batch"]), self.device, graph_capture=graph, num_sets=num_sets,
-                             host_ring=host_ring, capture_mode=capture_mode)
+                             host_ring=host_ring, capture_mode=capture_mode,
+                             precision=cfg.get("precision", "bf16"))
         finally:
             if key is not None:
                 with self._computes_lock:

@@ -304,3 +304,96 @@ def stem_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool: bool 
     kernels().stem_forward(ptr(x), ptr(ps.w), ptr(ps.bias), ptr(out), B, H, W, C, OH, OW, ps.pad_t, ps.pad_l,
                            int(pool), PH, PW, pool_pad, stream_handle(stream))
     return out
+
+
+# ------------------------------------------------------------------ fp32 path
+# The reference's precision (Keras float32, `src/node.py:177`): conv / GEMM on
+# the fp32 matrix cores, csrc/kernels/conv_f32.hip.  Tiles (BM, BN) per cfg id
+# mirror ADAPT_F32_CFGS there; K tiles are 16 floats.
+F32_BK = 16
+F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+
+
+def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, device,
+                  row_align: int = 128) -> PackedConv:
+    """[Npad][Kpad] fp32 weights, k = (kh, kw, ci) with ci innermost; no channel padding."""
+    kh, kw, cin, cout = kernel_hwio.shape
+    K = kh * kw * cin
+    Kpad = int(math.ceil(K / F32_BK) * F32_BK)
+    Npad = int(math.ceil(cout / row_align) * row_align)
+    wt = np.zeros((Npad, Kpad), np.float32)
+    wt[:cout, :K] = np.asarray(kernel_hwio, np.float32).transpose(3, 0, 1, 2).reshape(cout, K)
+    (pt, pb), (pl, pr) = pads
+    return PackedConv(w=torch.from_numpy(wt).to(device=device).contiguous(),
+                      bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),
+                      kh=kh, kw=kw, cin=cin, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
+
+
+def choose_cfg_f32(M: int, N: int, Kpad: int, occupancy: int = 2):
+    """(cfg, ksplit) for the fp32 kernel: the fp32 matrix rate is 1/16 of bf16,
+    so every conv is compute-bound; fill the CUs first, then prefer big tiles."""
+    best = None
+    ktiles = Kpad // F32_BK
+    for cfg, (bm, bn) in F32_TILES.items():
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        for ks in (1, 2, 4, 8, 16):
+            if ks > 1 and ktiles // ks < 8:
+                continue
+            blocks = tiles * ks
+            waves = math.ceil(blocks / (NUM_CUS * occupancy))
+            eff = {0: 1.0, 1: 0.93, 2: 0.93, 3: 0.8}[cfg]
+            t = waves * bm * bn * (Kpad / ks) / eff
+            if ks > 1:
+                t += M * N * (ks + 1) * 2.0          # slab write + reduce read (fp32), arbitrary units
+            if blocks < NUM_CUS:
+                t *= 1.0 + 0.5 * (NUM_CUS - blocks) / NUM_CUS
+            cand = (t, cfg, ks)
+            if best is None or cand < best:
+                best = cand
+    return best[1], best[2]
+
+
+def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                     relu: int = 0, cfg: Optional[int] = None, ksplit: int = 1,
+                     workspace: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """fp32 conv / GEMM: x [B,H,W,Cin] (or [M,K]) fp32 -> out [B,OH,OW,Cout] fp32, with
+    act(conv + bias (+ residual)) fused.  ksplit > 1 needs `workspace` (ksplit*M*N fp32)."""
+    if x.dim() == 2:
+        B, H, W, C = x.shape[0], 1, 1, x.shape[1]
+    else:
+        B, H, W, C = x.shape
+    if C != pc.cin:
+        raise ValueError(f"conv expects {pc.cin} input channels, got {C}")
+    for t, nm in ((x, "x"), (out, "out")):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"fp32 conv: {nm} must be contiguous fp32")
+    if pc.w.dtype != torch.float32:
+        raise ValueError("fp32 conv needs weights packed by pack_conv_f32")
+    OH, OW = pc.out_hw(H, W)
+    M, N = B * OH * OW, pc.cout
+    if out.numel() != M * N:
+        raise ValueError(f"conv output buffer has {out.numel()} elements, need {M * N}")
+    if residual is not None and (residual.numel() != M * N or residual.dtype != torch.float32
+                                 or not residual.is_contiguous()):
+        raise ValueError("residual must be contiguous fp32 with the output's shape")
+    if int(relu) not in (0, 1, 2):
+        raise ValueError("conv epilogue activation must be 0 (none), 1 (ReLU) or 2 (ReLU6)")
+    if cfg is None:
+        cfg, ksplit = choose_cfg_f32(M, N, pc.Kpad)
+    if cfg not in F32_TILES:
+        raise ValueError(f"unknown fp32 tile config {cfg}")
+    bm, bn = F32_TILES[cfg]
+    if pc.w.shape[0] < math.ceil(N / bn) * bn or pc.Kpad % F32_BK:
+        raise ValueError("packed fp32 weights not padded to the tile")
+    ws_ptr = 0
+    if ksplit > 1:
+        need = ksplit * M * N
+        if workspace is None:
+            workspace = torch.empty(need, dtype=torch.float32, device=x.device)
+        if workspace.numel() < need or workspace.dtype != torch.float32:
+            raise ValueError(f"ksplit {ksplit} needs an fp32 workspace of {need} elements")
+        ws_ptr = ptr(workspace)
+    kernels().conv_f32_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C, OH, OW,
+                               N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.K, pc.Kpad, int(relu),
+                               max(1, int(ksplit)), int(cfg), stream_handle(stream))
+    return out

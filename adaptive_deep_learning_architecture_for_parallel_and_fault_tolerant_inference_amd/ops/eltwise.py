@@ -262,3 +262,60 @@ def gmp(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
         raise ValueError("gmp: bad shapes")
     kernels().gmp(ptr(x), ptr(out), B, H * W, Cp, stream_handle(stream))
     return out
+
+
+# ------------------------------------------------------------------ fp32 path
+def maxpool_f32(x: torch.Tensor, out: torch.Tensor, k: int, s: int, pad_t: int = 0, pad_l: int = 0,
+                pad_zero: bool = True, stream=None) -> torch.Tensor:
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    B, H, W, C = x.shape
+    _, OH, OW, C2 = out.shape
+    k = k[0] if isinstance(k, (tuple, list)) else k
+    s = s[0] if isinstance(s, (tuple, list)) else s
+    if C2 != C or C % 4:
+        raise ValueError("fp32 maxpool needs matching channels, a multiple of 4")
+    kernels().maxpool_f32(ptr(x), ptr(out), B, H, W, C, OH, OW, int(k), int(s), int(pad_t), int(pad_l),
+                          int(bool(pad_zero)), stream_handle(stream))
+    return out
+
+
+def gap_f32(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    B, H, W, C = x.shape
+    if out.numel() != B * C or C % 4:
+        raise ValueError("fp32 GAP: out must be [B][C], C a multiple of 4")
+    kernels().gap_f32(ptr(x), ptr(out), B, H * W, C, stream_handle(stream))
+    return out
+
+
+def eltwise_f32(a: torch.Tensor, out: torch.Tensor, b: Optional[torch.Tensor] = None,
+                scale: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None, relu: int = 0,
+                stream=None) -> torch.Tensor:
+    """out = act(a + b) | act(a * scale[c] + shift[c]) | act(a), all fp32."""
+    _chk(a, torch.float32, "a"); _chk(out, torch.float32, "out")
+    if out.numel() != a.numel():
+        raise ValueError("eltwise: element counts differ")
+    C = a.shape[-1]
+    op = 2
+    if b is not None:
+        _chk(b, torch.float32, "b")
+        if b.numel() != a.numel():
+            raise ValueError("eltwise add: element counts differ")
+        op = 0
+    elif scale is not None:
+        if scale.numel() != C or shift is None or shift.numel() != C:
+            raise ValueError("eltwise bn: scale/shift need one value per channel")
+        op = 1
+    kernels().eltwise_f32(ptr(a), ptr(b), ptr(scale), ptr(shift), ptr(out), a.numel(), C, op, int(relu),
+                          stream_handle(stream))
+    return out
+
+
+def pad_f32(x: torch.Tensor, out: torch.Tensor, pad_t: int, pad_l: int, stream=None) -> torch.Tensor:
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    B, H, W, C = x.shape
+    _, OH, OW, C2 = out.shape
+    if C2 != C or OH < H + pad_t or OW < W + pad_l:
+        raise ValueError("pad: output too small")
+    kernels().pad_f32(ptr(x), ptr(out), B, H, W, C, OH, OW, int(pad_t), int(pad_l), stream_handle(stream))
+    return out

@@ -33,9 +33,10 @@ class DPJob:
     per-layer GEMMs of different micro-batches fill CUs the other leaves idle."""
 
     def __init__(self, g, weights, world: int, rank: int, device, batch: int, graph: bool = True, tune: bool = False,
-                 streams: int = 1):
+                 streams: int = 1, precision: str = "bf16"):
         self.device = torch.device(device)
-        self.exs = [SliceExecutor(g, weights, batch, device=device, tune=tune and i == 0) for i in range(streams)]
+        self.exs = [SliceExecutor(g, weights, batch, device=device, tune=tune and i == 0, precision=precision)
+                    for i in range(streams)]
         for ex in self.exs[1:]:           # share packed weights with the first executor
             ex.packed = self.exs[0].packed
             ex.cfg = dict(self.exs[0].cfg)
@@ -80,7 +81,7 @@ class PipelineJob:
 
     def __init__(self, g, weights, world: int, rank: int, device, batch: int, stages: int,
                  part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False, nsets: int = 2,
-                 host_staged: bool = False, codec: str = "none"):
+                 host_staged: bool = False, codec: str = "none", precision: str = "bf16"):
         if world % stages:
             raise ValueError(f"world {world} not divisible by stages {stages}")
         self.stages = stages
@@ -97,7 +98,7 @@ class PipelineJob:
         self.slice = sl
         sg = subgraph(g, sl)
         self.ex = SliceExecutor(sg, {k: v for k, v in weights.items()}, batch, device=device, tune=tune,
-                                num_sets=nsets)
+                                num_sets=nsets, precision=precision)
         if graph:
             self.ex.capture()
         rk = stage_ranks(self.stage, stages, self.replica)
@@ -144,17 +145,18 @@ class PipelineJob:
 
 def build_job(g, weights, mode: str, world: int, rank: int, device, batch: int = 32, stages: int = 0,
               part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False,
-              host_staged: bool = False, streams: int = 1, codec: str = "none"):
+              host_staged: bool = False, streams: int = 1, codec: str = "none", precision: str = "bf16"):
     if mode == "dp" or world == 1 and not part_at:
-        return DPJob(g, weights, world, rank, device, batch, graph=graph, tune=tune, streams=streams)
+        return DPJob(g, weights, world, rank, device, batch, graph=graph, tune=tune, streams=streams,
+                     precision=precision)
     if mode == "pp":
         k = len(part_at) + 1 if part_at else world
         if k != world:
             raise ValueError(f"pp mode: {k} stages for {world} ranks")
         return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune,
-                           host_staged=host_staged, codec=codec)
+                           host_staged=host_staged, codec=codec, precision=precision)
     if mode == "ppdp":
         k = stages or (len(part_at) + 1 if part_at else 2)
         return PipelineJob(g, weights, world, rank, device, batch, k, part_at, graph=graph, tune=tune,
-                           host_staged=host_staged, codec=codec)
+                           host_staged=host_staged, codec=codec, precision=precision)
     raise ValueError(f"unknown mode {mode}")

@@ -75,14 +75,28 @@ def _nbytes(shape, dtype) -> int:
 class SliceExecutor:
     """Runs one (sub)graph for a fixed batch on one device with our HIP kernels."""
 
+    FP32_KINDS = ("conv", "dense", "maxpool", "gap", "softmax", "add", "bn", "relu", "pad", "copy")
+
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device="cuda",
-                 outputs: Optional[Sequence[str]] = None, tune: bool = False, num_sets: int = 1):
+                 outputs: Optional[Sequence[str]] = None, tune: bool = False, num_sets: int = 1,
+                 precision: str = "bf16"):
+        """precision: "bf16" (bf16 activations / weights, fp32 accumulation: the
+        fast path) or "fp32" (fp32 activations and weights on the fp32 matrix
+        cores: the reference's Keras float32 numerics, csrc/kernels/conv_f32.hip)."""
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be bf16 or fp32, got {precision!r}")
         self.g = g
         self.batch = batch
         self.device = torch.device(device)
         self.outputs = list(outputs or g.output_names)
         self.num_sets = num_sets
-        self.steps: List[Step] = compile_plan(g, self.outputs)
+        self.precision = precision
+        self.fp32 = precision == "fp32"
+        self.steps: List[Step] = compile_plan(g, self.outputs, fp32=self.fp32)
+        if self.fp32:
+            bad = sorted({st.kind for st in self.steps if st.kind not in self.FP32_KINDS})
+            if bad:
+                raise NotImplementedError(f"fp32 execution has no kernels for {bad} (model {g.name})")
         self._graphs: List[Optional[torch.cuda.CUDAGraph]] = [None] * num_sets
         self._pack_weights(weights)
         self._alloc()
@@ -94,11 +108,13 @@ class SliceExecutor:
         shp = tuple(self.g.layers[base].out_shape)
         # activations are stored with channels padded to a multiple of 8 (16-byte
         # vectors); only the user's fp32 image keeps its true channel count
-        if len(shp) == 3 and shp[-1] % 8 and self.dtype_of(name) != torch.float32:
+        if len(shp) == 3 and shp[-1] % 8 and self.dtype_of(name) != torch.float32 and not self.fp32:
             shp = shp[:-1] + (((shp[-1] + 7) // 8) * 8,)
         return (self.batch,) + shp
 
     def dtype_of(self, name: str):
+        if self.fp32:
+            return torch.float32
         base = name.split("#")[0]
         L = self.g.layers[base]
         if (L.op == "input" and base == name and len(L.out_shape) == 3
@@ -112,6 +128,9 @@ class SliceExecutor:
     def _pack_weights(self, weights: Dict[str, np.ndarray]) -> None:
         self.packed: Dict[int, object] = {}
         dev = self.device
+        if self.fp32:
+            self._pack_weights_f32(weights)
+            return
         for i, st in enumerate(self.steps):
             if st.kind == "conv":
                 p = st.p
@@ -188,6 +207,27 @@ class SliceExecutor:
                 self.packed[i] = (torch.tensor(s, dtype=torch.float32, device=dev),
                                   torch.tensor(bt - mu * s, dtype=torch.float32, device=dev))
 
+    def _pack_weights_f32(self, weights: Dict[str, np.ndarray]) -> None:
+        dev = self.device
+        for i, st in enumerate(self.steps):
+            if st.kind == "conv":
+                kf, bf = self._folded(weights, st.p)
+                self.packed[i] = conv_ops.pack_conv_f32(kf, bf, st.p["stride"], st.p["pads"], dev)
+            elif st.kind == "dense":
+                name = st.p.get("layer", st.out)
+                k = weights[f"{name}/kernel"]
+                b = weights.get(f"{name}/bias", np.zeros(k.shape[1], np.float32))
+                self.packed[i] = conv_ops.pack_conv_f32(k.reshape(1, 1, k.shape[0], k.shape[1]), b, 1,
+                                                        ((0, 0), (0, 0)), dev)
+            elif st.kind == "bn":
+                bp_ = bn_params(weights, st.p["bn"])
+                gm, bt, mu, var = (np.asarray(bp_[n], np.float64) for n in
+                                   ("gamma", "beta", "moving_mean", "moving_variance"))
+                eps = self.g.layers[st.p["bn"]].attrs.get("epsilon", 1e-3)
+                sc = gm / np.sqrt(var + eps)
+                self.packed[i] = (torch.tensor(sc, dtype=torch.float32, device=dev),
+                                  torch.tensor(bt - mu * sc, dtype=torch.float32, device=dev))
+
     def _folded(self, weights: Dict[str, np.ndarray], p: Dict):
         """BN-folded (kernel HWIO, bias) of a conv step's parameters."""
         cname = p["conv"]
@@ -249,17 +289,18 @@ class SliceExecutor:
         self._logits: Dict[int, torch.Tensor] = {}
         self._dense_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
-            if (st.kind == "dense" and self.batch <= 32 and not st.p.get("relu")
+            if (st.kind == "dense" and self.batch <= 32 and not st.p.get("relu") and not self.fp32
                     and self.dtype_of(st.out) == torch.float32):          # head.hip writes fp32 logits / probs
                 # small-M head GEMM (csrc/kernels/head.hip): split-K scratch
                 pc = self.packed[i]
                 n = E.dense_small_scratch(self.batch, pc.cout, pc.K)
                 self._dense_part[i] = torch.empty(n, dtype=torch.float32, device=dev)
-            elif st.kind == "dense" and st.p["softmax"]:
+            if st.kind == "dense" and st.p["softmax"]:
+                # pre-softmax logits stay readable (`logits()`): numerics checks compare them
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
         self._gap_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
-            if st.kind == "gap" and self.device.type == "cuda":
+            if st.kind == "gap" and self.device.type == "cuda" and not self.fp32:
                 shp = self.shape_of(st.ins[0])
                 if len(shp) == 4:
                     need = E.gap_scratch_elems(shp[0], shp[1] * shp[2], shp[3])
@@ -334,6 +375,11 @@ class SliceExecutor:
     def _ensure_ws(self) -> None:
         need = ctr = 0
         for i, (cfg, ks) in self.cfg.items():
+            if self.fp32:
+                if ks > 1:
+                    B, H, W, C, OH, OW, pc = self._conv_geom(i)
+                    need = max(need, ks * B * OH * OW * pc.cout)
+                continue
             if ks != 1:
                 B, H, W, C, OH, OW, pc = self._conv_geom(i)
                 need = max(need, conv_ops.workspace_elems(B * OH * OW, pc.cout, pc.Kpad, cfg, ks))
@@ -356,6 +402,11 @@ class SliceExecutor:
             if st.kind not in ("conv", "dense") or i in self._dense_part:    # small-M heads: head.hip
                 continue
             B, H, W, C, OH, OW, pc = self._conv_geom(i)
+            if self.fp32:
+                key = "f32|" + conv_key(B, H, W, C, pc)
+                cfg, ks = table[key][:2] if key in table else conv_ops.choose_cfg_f32(B * OH * OW, pc.cout, pc.Kpad)
+                self.cfg[i] = (int(cfg), int(ks))
+                continue
             if pc.cout % 8:
                 raise NotImplementedError(f"{st.kind} {st.out}: {pc.cout} output channels (the MFMA GEMM path "
                                           f"needs a multiple of 8)")
@@ -366,7 +417,7 @@ class SliceExecutor:
                 cfg, ks = conv_ops.choose_cfg(B * OH * OW, pc.cout, pc.Kpad)
             self.cfg[i] = (int(cfg), int(ks))
         self._ensure_ws()
-        if tune:
+        if tune and not self.fp32:
             self.autotune()
 
     def autotune(self, reps: int = 20, persist: bool = True, refine: int = 3) -> Dict[str, List]:
@@ -530,7 +581,9 @@ class SliceExecutor:
                 self._side_stream.wait_event(fork)
                 stream, ws, ctr = self._side_stream, self._ws_side, self._ctr_side
             k = st.kind
-            if k == "pack":
+            if self.fp32:
+                self._launch_f32(i, st, b, stream, ws)
+            elif k == "pack":
                 E.input_pack(b[st.ins[0]], b[st.out], stream=stream)
             elif k == "stem":
                 conv_ops.stem_forward(b[st.ins[0]], self.packed[i], b[st.out], pool=st.p["pool"],
@@ -587,7 +640,8 @@ class SliceExecutor:
             elif k == "dense" and i in self._dense_part:
                 x = b[st.ins[0]].reshape(self.batch, -1)
                 if st.p["softmax"]:
-                    E.dense_small(x, self.packed[i], self._dense_part[i], probs=b[st.out], stream=stream)
+                    E.dense_small(x, self.packed[i], self._dense_part[i], logits=self._logits[i], probs=b[st.out],
+                                  stream=stream)
                 else:
                     E.dense_small(x, self.packed[i], self._dense_part[i], logits=b[st.out], stream=stream)
             elif k == "dense":
@@ -621,6 +675,50 @@ class SliceExecutor:
                     s[r + "#out"].copy_(s[r], non_blocking=True)
             else:
                 s[r + "#out"].copy_(s[r], non_blocking=True)
+
+    def _launch_f32(self, i: int, st: Step, b, stream, ws) -> None:
+        """One step of the fp32 path (csrc/kernels/conv_f32.hip)."""
+        k = st.kind
+        if k == "conv":
+            cfg, ks = self.cfg[i]
+            res = b[st.ins[1]] if len(st.ins) > 1 else None
+            conv_ops.conv_forward_f32(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
+                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream)
+        elif k == "dense":
+            cfg, ks = self.cfg[i]
+            x = b[st.ins[0]].reshape(self.batch, -1)
+            dst = self._logits[i] if st.p["softmax"] else b[st.out]
+            conv_ops.conv_forward_f32(x, self.packed[i], dst, relu=st.p.get("relu", 0), cfg=cfg, ksplit=ks,
+                                      workspace=ws, stream=stream)
+            if st.p["softmax"]:
+                E.softmax_rows(dst, b[st.out], stream=stream)
+        elif k == "maxpool":
+            (pt, _), (pl, _) = st.p["pads"]
+            E.maxpool_f32(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, st.p.get("pad_zero", True),
+                          stream=stream)
+        elif k == "gap":
+            E.gap_f32(b[st.ins[0]], b[st.out], stream=stream)
+        elif k == "softmax":
+            E.softmax_rows(b[st.ins[0]], b[st.out], stream=stream)
+        elif k == "add":
+            E.eltwise_f32(b[st.ins[0]], b[st.out], b=b[st.ins[1]], relu=st.p["relu"], stream=stream)
+        elif k == "bn":
+            sc, sh = self.packed[i]
+            E.eltwise_f32(b[st.ins[0]], b[st.out], scale=sc, shift=sh, relu=st.p["relu"], stream=stream)
+        elif k == "relu":
+            E.eltwise_f32(b[st.ins[0]], b[st.out], relu=st.p.get("mode", 1) or 1, stream=stream)
+        elif k == "pad":
+            (pt, _), (pl, _) = st.p["pad"]
+            E.pad_f32(b[st.ins[0]], b[st.out], pt, pl, stream=stream)
+        elif k == "copy":
+            src, dst = b[st.ins[0]], b[st.out]
+            if stream is not None:
+                with torch.cuda.stream(stream):
+                    dst.view(-1).copy_(src.view(-1), non_blocking=True)
+            else:
+                dst.view(-1).copy_(src.view(-1), non_blocking=True)
+        else:
+            raise NotImplementedError(f"fp32 {k}")
 
     def _debug_check(self, i: int) -> None:
         try:
@@ -660,6 +758,13 @@ class SliceExecutor:
         else:
             self._launch(set_idx)
         return {o: self.output_buf(o, set_idx) for o in self.outputs}
+
+    def logits(self) -> Optional[torch.Tensor]:
+        """Pre-softmax logits of the last Dense(softmax) step (None if there is none)."""
+        for i in reversed(range(len(self.steps))):
+            if i in self._logits:
+                return self._logits[i]
+        return None
 
     def run(self, inputs: Dict[str, torch.Tensor], set_idx: int = 0) -> Dict[str, torch.Tensor]:
         for n, t in inputs.items():

@@ -51,7 +51,10 @@ def _phys(name: str, packed: Set[str]) -> str:
     return name + "#packed" if name in packed else name
 
 
-def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
+def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = False) -> List[Step]:
+    """fp32=True: the fp32 execution path (csrc/kernels/conv_f32.hip) keeps the
+    image as it is (no bf16 pack, so no stem fusion) and runs sibling convs as
+    separate GEMMs."""
     outputs = list(outputs or g.output_names)
     outset = set(outputs)
     cons = g.consumers()
@@ -76,7 +79,7 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
         done.add(n)
         c = L.out_shape[-1] if L.out_shape else 0
         # the user's fp32 image becomes bf16 NHWC with channels padded to 8 (a pure cast when C % 8 == 0)
-        if len(L.out_shape) == 3 and L.attrs.get("stands_for", "input") == "input":
+        if len(L.out_shape) == 3 and L.attrs.get("stands_for", "input") == "input" and not fp32:
             packed.add(n)
             steps.append(Step("pack", n + "#packed", [n], [], {"cin": c, "cpad": ((c + 7) // 8) * 8}))
 
@@ -312,6 +315,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None) -> List[Step]:
     missing = [o for o in outputs if o not in produced]
     if missing:
         raise RuntimeError(f"plan does not produce outputs {missing}")
+    if fp32:
+        return steps
     if os.environ.get("ADAPT_NO_STEM", "0") != "1":
         steps = _fuse_stem(g, steps, outset)
     if os.environ.get("ADAPT_NO_SIBLINGS", "0") != "1":

@@ -50,7 +50,7 @@ def to_numpy(t: torch.Tensor) -> Tuple[np.ndarray, bool]:
 class StageCompute:
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device: str = "cpu",
                  outputs: Optional[Sequence[str]] = None, graph_capture: bool = True, num_sets: int = 1,
-                 host_ring: int = 8, capture_mode: str = "global"):
+                 host_ring: int = 8, capture_mode: str = "global", precision: str = "bf16"):
         self.g = g
         self.batch = batch
         self.device = torch.device(device)
@@ -62,7 +62,8 @@ class StageCompute:
         self._pin_next = 0
         if self.gpu:
             from .executor import SliceExecutor
-            self.ex = SliceExecutor(g, weights, batch, device=self.device, outputs=self.outputs, num_sets=num_sets)
+            self.ex = SliceExecutor(g, weights, batch, device=self.device, outputs=self.outputs, num_sets=num_sets,
+                                    precision=precision)
             if graph_capture:
                 self.ex.capture(mode=capture_mode)
         else:

@@ -51,6 +51,9 @@ def parse():
                     help="independent bs=--batch micro-batches in flight per GPU (dp mode)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = host-staged rehearsal (several ranks per GPU)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute precision: bf16 (fp32 accumulation) or fp32 end to end (the reference's "
+                         "Keras float32, on the fp32 matrix cores)")
     ap.add_argument("--codec", default="none", choices=["none", "lz4", "zvc"],
                     help="pp/ppdp: compress stage-boundary activations on a side stream (BASELINE config 3)")
     return ap.parse_args()
@@ -100,7 +103,8 @@ def main():
     part_at = [s for s in args.part_at.split(",") if s]
     job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
                            stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune,
-                           host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec)
+                           host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec,
+                           precision=args.dtype)
     # synthetic input, resident on device (data="synthetic")
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     image = tuple(g.layers[g.input].out_shape)          # 224x224x3 (ResNet-50); the model's own size otherwise
@@ -149,7 +153,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_IMG_S, 4) if BASELINE_IMG_S else None),
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": f"synthetic {'x'.join(map(str, image))} NHWC fp32 input, random-init weights (seeded)",
             "config": {"model": args.model, "global_batch": job.global_batch, "seq_len": None,
                        "image": list(image), "parallelism": job.parallelism, "part_at": job.part_at,

@@ -179,6 +179,30 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_bf16_f32", [](u64 x, u64 y, size_t n, u64 s) {
     check(adapt::cast_bf16_f32(P<const bf16>(x), P<float>(y), n, S(s)), "cast_bf16_f32");
   });
+  m.def("conv_f32_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, int B, int H, int W, int Cin,
+                               int OH, int OW, int N, int KH, int KW, int stride, int pad_t, int pad_l, int K,
+                               int Kpad, int relu, int ksplit, int cfg, u64 s) {
+    py::gil_scoped_release nogil;
+    check(adapt::conv_f32_forward(P<const float>(x), P<const float>(w), P<const float>(bias), P<const float>(res),
+                                  P<float>(out), P<float>(ws), B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
+                                  K, Kpad, relu, ksplit, cfg, S(s)),
+          "conv_f32_forward");
+  });
+  m.def("maxpool_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int K, int Sd, int pad_t,
+                          int pad_l, int pad_zero, u64 s) {
+    check(adapt::maxpool_f32(P<const float>(x), P<float>(y), B, H, W, C, OH, OW, K, Sd, pad_t, pad_l, pad_zero,
+                             S(s)), "maxpool_f32");
+  });
+  m.def("gap_f32", [](u64 x, u64 y, int B, int HW, int C, u64 s) {
+    check(adapt::gap_f32(P<const float>(x), P<float>(y), B, HW, C, S(s)), "gap_f32");
+  });
+  m.def("eltwise_f32", [](u64 a, u64 b, u64 scale, u64 shift, u64 y, size_t n, int C, int op, int relu, u64 s) {
+    check(adapt::eltwise_f32(P<const float>(a), P<const float>(b), P<const float>(scale), P<const float>(shift),
+                             P<float>(y), n, C, op, relu, S(s)), "eltwise_f32");
+  });
+  m.def("pad_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int pt, int pl, u64 s) {
+    check(adapt::pad_f32(P<const float>(x), P<float>(y), B, H, W, C, OH, OW, pt, pl, S(s)), "pad_f32");
+  });
   m.def("cast_f32_bf16", [](u64 x, u64 y, size_t n, u64 s) {
     check(adapt::cast_f32_bf16(P<const float>(x), P<bf16>(y), n, S(s)), "cast_f32_bf16");
   });

@@ -98,4 +98,17 @@ hipError_t cast_f32_bf16(const float* x, bf16* y, size_t n, hipStream_t s);
 hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
                         int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
                         hipStream_t s);
+// fp32 path (conv_f32.hip): MFMA f32 implicit-GEMM conv / GEMM and fp32 layers
+hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
+                            float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
+                            int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,
+                            hipStream_t s);
+hipError_t maxpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
+                       int pad_l, int pad_zero, hipStream_t s);
+hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
+// op 0: y = act(a + b); op 1: y = act(a * scale[c] + shift[c]); op 2: y = act(a)
+hipError_t eltwise_f32(const float* a, const float* b, const float* scale, const float* shift, float* y, size_t n,
+                       int C, int op, int relu, hipStream_t s);
+hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
+                   hipStream_t s);
 }  // namespace adapt

@@ -1,0 +1,149 @@
+"""fp32 execution path (csrc/kernels/conv_f32.hip) against fp32/fp64 oracles.
+
+The reference computes in Keras float32 (`src/node.py:177`,
+`test/local_infer.py:22`); `SliceExecutor(precision="fp32")` runs every conv /
+GEMM on the fp32 matrix cores (v_mfma_f32_16x16x4_f32) with fp32 activations.
+Kernel checks compare with a float64 CPU oracle; the model check compares the
+pre-softmax logits of ResNet-50 with the fp32 CPU oracle at rel <= 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import eltwise as E
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_conv(x, k, b, stride, pads, res=None, relu=0):
+    """float64 CPU oracle: NHWC x, HWIO k."""
+    (pt, pb), (pl, pr) = pads
+    xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
+    xt = F.pad(xt, (pl, pr, pt, pb))
+    y = F.conv2d(xt, torch.from_numpy(k).double().permute(3, 2, 0, 1), torch.from_numpy(b).double(), stride=stride)
+    y = y.permute(0, 2, 3, 1)
+    if res is not None:
+        y = y + torch.from_numpy(res).double()
+    if relu == 1:
+        y = y.clamp_min(0)
+    elif relu == 2:
+        y = y.clamp(0, 6)
+    return y.numpy()
+
+
+SHAPES = [  # (B, H, W, Cin, Cout, k, stride, pad, residual, relu)
+    (2, 56, 56, 3, 64, 7, 2, 3, False, 1),          # stem: 3-channel gather path
+    (2, 28, 28, 64, 256, 1, 1, 0, True, 1),         # 1x1 + residual + ReLU (pure GEMM path)
+    (2, 28, 28, 64, 64, 3, 1, 1, False, 1),         # 3x3 halo
+    (2, 28, 28, 128, 256, 1, 2, 0, False, 0),       # strided projection shortcut
+    (4, 7, 7, 512, 2048, 1, 1, 0, True, 1),         # small-M stage-5 shape
+    (3, 14, 14, 256, 96, 3, 1, 1, False, 2),        # ReLU6, N not a tile multiple
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("ksplit", [1, 4])
+def test_conv_f32_matches_fp64(shape, ksplit):
+    B, H, W, Cin, Cout, k, s, pad, has_res, relu = shape
+    rng = np.random.default_rng(hash(shape) % 2**32)
+    x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
+    kern = (rng.standard_normal((k, k, Cin, Cout)) / np.sqrt(k * k * Cin)).astype(np.float32)
+    bias = rng.standard_normal(Cout).astype(np.float32)
+    pads = ((pad, pad), (pad, pad))
+    OH = (H + 2 * pad - k) // s + 1
+    OW = (W + 2 * pad - k) // s + 1
+    res = rng.standard_normal((B, OH, OW, Cout)).astype(np.float32) if has_res else None
+    want = _ref_conv(x, kern, bias, s, pads, res, relu)
+    pc = C.pack_conv_f32(kern, bias, s, pads, "cuda")
+    out = torch.empty((B, OH, OW, Cout), dtype=torch.float32, device="cuda")
+    for cfg in C.F32_TILES:
+        C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out, None if res is None else torch.from_numpy(res).cuda(),
+                           relu=relu, cfg=cfg, ksplit=ksplit)
+        got = out.cpu().numpy()
+        err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
+        assert err < 2e-5, f"cfg {cfg} ksplit {ksplit}: rel err {err}"
+
+
+def test_dense_f32_split_k():
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((32, 2048)).astype(np.float32)
+    w = (rng.standard_normal((2048, 1000)) / 45).astype(np.float32)
+    b = rng.standard_normal(1000).astype(np.float32)
+    pc = C.pack_conv_f32(w.reshape(1, 1, 2048, 1000), b, 1, ((0, 0), (0, 0)), "cuda")
+    out = torch.empty((32, 1000), dtype=torch.float32, device="cuda")
+    C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out, cfg=3, ksplit=16)
+    want = x.astype(np.float64) @ w.astype(np.float64) + b
+    assert np.abs(out.cpu().numpy() - want).max() / np.abs(want).max() < 2e-5
+
+
+def test_f32_layers():
+    rng = np.random.default_rng(1)
+    x = torch.from_numpy(rng.standard_normal((2, 15, 15, 64)).astype(np.float32))
+    y = torch.empty((2, 8, 8, 64), device="cuda")
+    E.maxpool_f32(x.cuda(), y, 3, 2, 1, 1, pad_zero=False)
+    want = F.max_pool2d(F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1), value=float("-inf")), 3, 2).permute(0, 2, 3, 1)
+    assert torch.equal(y.cpu(), want)
+    g = torch.empty((2, 64), device="cuda")
+    E.gap_f32(x.cuda(), g)
+    assert torch.allclose(g.cpu(), x.mean(dim=(1, 2)), rtol=1e-6, atol=1e-6)
+    a, b2 = x.cuda(), torch.from_numpy(rng.standard_normal((2, 15, 15, 64)).astype(np.float32)).cuda()
+    o = torch.empty_like(a)
+    E.eltwise_f32(a, o, b=b2, relu=1)
+    assert torch.allclose(o, (a + b2).clamp_min(0))
+    sc, sh = torch.rand(64, device="cuda"), torch.rand(64, device="cuda")
+    E.eltwise_f32(a, o, scale=sc, shift=sh)
+    assert torch.allclose(o, a * sc + sh, rtol=1e-6, atol=1e-6)
+    p = torch.empty((2, 17, 17, 64), device="cuda")
+    E.pad_f32(a, p, 1, 1)
+    assert torch.equal(p.cpu(), F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1)).permute(0, 2, 3, 1))
+
+
+def _oracle_logits(g, w, x):
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.reference import \
+        ReferenceExecutor
+    feat = ReferenceExecutor(g, w, device="cpu").run({g.input: torch.from_numpy(x)}, outputs=["avg_pool"])["avg_pool"]
+    return feat.double().numpy() @ w["predictions/kernel"].astype(np.float64) + w["predictions/bias"]
+
+
+@pytest.mark.parametrize("depth", ["resnet50", "resnet152"])
+def test_resnet_fp32_logits_match_oracle(depth):
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models import resnet as R
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import \
+        SliceExecutor
+    g = R.build_resnet(depth)
+    w = R.init_weights(g, seed=0)
+    x = np.random.default_rng(2).standard_normal((2, 224, 224, 3)).astype(np.float32)
+    ex = SliceExecutor(g, w, batch=2, device="cuda:0", precision="fp32")
+    ex.capture()
+    probs = ex(torch.from_numpy(x).cuda())
+    logits = ex.logits().double().cpu().numpy()
+    want = _oracle_logits(g, w, x)
+    rel = np.abs(logits - want).max() / np.abs(want).max()
+    assert rel <= 1e-4, f"{depth} fp32 logits rel err {rel}"
+    assert (logits.argmax(-1) == want.argmax(-1)).all()
+    sm = np.exp(want - want.max(-1, keepdims=True))
+    sm /= sm.sum(-1, keepdims=True)
+    assert np.abs(probs.double().cpu().numpy() - sm).max() < 1e-5
+
+
+def test_resnet50_bf16_logits_and_top1():
+    """The bf16 fast path against the same fp32 oracle: logits within a bf16
+    budget, top-1 equal wherever the oracle's top-2 margin exceeds that budget."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models import resnet as R
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import \
+        SliceExecutor
+    g = R.build_resnet("resnet50")
+    w = R.init_weights(g, seed=0)
+    x = np.random.default_rng(3).standard_normal((8, 224, 224, 3)).astype(np.float32)
+    ex = SliceExecutor(g, w, batch=8, device="cuda:0")
+    ex(torch.from_numpy(x).cuda())
+    logits = ex.logits().double().cpu().numpy()
+    want = _oracle_logits(g, w, x)
+    scale = np.abs(want).max()
+    rel = np.abs(logits - want).max() / scale
+    assert rel <= 5e-2, f"bf16 logits rel err {rel}"
+    top2 = np.sort(want, -1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > 2 * rel * scale
+    assert (logits.argmax(-1) == want.argmax(-1))[clear].all()

@@ -85,7 +85,7 @@ def main():
     deadline = time.time() + 120
     while time.time() < deadline and sum(1 for v in d._resident.values() if v) < a.workers:
         time.sleep(0.1)
-    time.sleep(1.0)                  # prepare hints: next plans' slices built in the background
+    time.sleep(d.prepare_delay + 1.5)   # prepare hints: next plans' slices built in the background
     threading.Thread(target=feeder, daemon=True).start()
     got = 0
     t0 = time.time()
