@@ -87,6 +87,12 @@ def cmd_serve(argv):
     ap.add_argument("--transport", default=None)
     ap.add_argument("--codec", default=None)
     ap.add_argument("--replicas", default=None, help="pipeline replicas: auto (live // stages) or N")
+    ap.add_argument("--ingest", default="auto", choices=["auto", "tcp"],
+                    help="auto: same-host shared-memory request slots; tcp: inline on the socket")
+    ap.add_argument("--uint8", action="store_true", help="send uint8 images (4x fewer bytes), preprocessed on the GPU")
+    ap.add_argument("--preprocess", default="none", choices=["none", "caffe", "tf", "torch"],
+                    help="Keras preprocess_input mode applied by stage 0 to uint8 requests")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="worker compute precision")
     a = ap.parse_args(argv)
     cfg = _cfg(a, transport=a.transport, codec=a.codec, replicas=a.replicas)
     from .dispatcher import DEFER
@@ -96,7 +102,7 @@ def cmd_serve(argv):
               batch=cfg.batch, codec=cfg.codec, weight_codec=cfg.weight_codec, max_inflight=cfg.max_inflight,
               task_timeout=cfg.task_timeout, worker_wait=max(cfg.worker_wait, 60 if a.spawn else 0),
               elastic=cfg.elastic, ordered=cfg.ordered, transport=cfg.transport, min_workers=max(1, a.spawn),
-              replicas=cfg.replicas)
+              replicas=cfg.replicas, ingest=a.ingest, preprocess=a.preprocess, precision=a.dtype)
     d.membership_server.start()
     procs = []
     for i in range(a.spawn):
@@ -108,7 +114,11 @@ def cmd_serve(argv):
                                        "--device", dev, "--id", f"local{i}", "--ttl", str(cfg.lease_ttl)],
                                       start_new_session=True))
     inq, outq = queue.Queue(cfg.max_inflight * 2), queue.Queue()
-    x = np.random.default_rng(cfg.seed).standard_normal((cfg.batch,) + tuple(cfg.image)).astype(np.float32)
+    rng = np.random.default_rng(cfg.seed)
+    if a.uint8:
+        x = rng.integers(0, 256, (cfg.batch,) + tuple(cfg.image), dtype=np.uint8)
+    else:
+        x = rng.standard_normal((cfg.batch,) + tuple(cfg.image)).astype(np.float32)
     t = threading.Thread(target=d.run_defer, args=(m, cuts, inq, outq), daemon=True)
     start = time.time()
     t.start()

@@ -26,7 +26,9 @@ import numpy as np
 
 from ..native import runtime
 
-CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3, "zvc": 4}
+# "shm": the payload is a reference (segment name + offset) to a same-host
+# shared-memory slot holding the raw array (transport/shm.py)
+CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3, "zvc": 4, "shm": 5}
 _CODEC_NAMES = {v: k for k, v in CODECS.items()}
 # dtype codes (bf16 travels as raw 16-bit words)
 DTYPES = {0: np.float32, 1: np.float64, 2: np.float16, 3: np.uint16, 4: np.int32, 5: np.int64, 6: np.uint8,
@@ -124,6 +126,13 @@ def decode(buf, threads: int = 4, copy: bool = True) -> np.ndarray:
         return rt.zfp_decompress(body, threads).reshape(shape)
     if codec == 4:
         return _fin(np.frombuffer(rt.zvc_decompress(body), dtype=np_dt))
+    if codec == 5:
+        from ..transport import shm
+        raw = bytes(body)
+        cut = raw.index(b"\0")
+        off = int.from_bytes(raw[cut + 1:cut + 9], "little")
+        a = shm.view(raw[:cut].decode(), off, np_dt, shape, register_device=shm.REGISTER_DEVICE)
+        return a.copy() if copy else a
     raise ValueError(f"unknown codec id {codec}")
 
 

@@ -130,7 +130,8 @@ class DEFER:
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
                  transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
-                 quarantine_s: float = 30.0, hb_timeout: float = 0.06, precision: str = "bf16") -> None:
+                 quarantine_s: float = 30.0, hb_timeout: float = 0.06, precision: str = "bf16",
+                 ingest: str = "auto", preprocess: str = "none") -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
         the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
         ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
@@ -139,7 +140,11 @@ class DEFER:
         codec; any host), "rccl" (RCCL p2p over xGMI between GPU workers),
         "gloo" (CPU workers).  replicas: "auto" = as many k-stage pipelines as
         the live workers fill, or a maximum count.  resident: keep the whole
-        model on every worker after its first slice so re-plans push nothing."""
+        model on every worker after its first slice so re-plans push nothing.
+        ingest: "auto" = requests go through same-host shared memory to a local
+        stage 0 (transport/shm.py; only a descriptor crosses the socket), "tcp" =
+        always inline.  preprocess: Keras preprocess_input mode stage 0 applies on
+        the GPU to uint8 image requests ("none", "caffe", "tf", "torch")."""
         if transport not in ("tcp", "rccl", "gloo"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
@@ -168,6 +173,9 @@ class DEFER:
         self.max_replays = max_replays
         self.precision = precision                  # worker compute: "bf16" or "fp32" (reference float32)
         self.prepare_delay = 1.0                    # s after an epoch forms before `prepare` hints go out
+        self.preprocess = preprocess
+        from .transport import shm as _shm
+        self._shm = _shm.ShmPool() if ingest == "auto" and _shm.available() else None
         self.quarantine_s = quarantine_s
         # a worker whose config port does not answer within this many seconds is left
         # out of the next epoch even while its membership lease is still alive
@@ -511,7 +519,7 @@ class DEFER:
         cfg = {"cmd": "configure", "epoch": epoch, "stage": st, "stages": k, "batch": self.batch,
                "next": nxt, "result_addr": [self._result_host(rec), self.result_port], "part_at": list(cuts),
                "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid,
-               "precision": self.precision}
+               "precision": self.precision, "preprocess": self.preprocess}
         if self.transport != "tcp":
             cfg["link_codec"] = self.link_codec
             cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
@@ -785,8 +793,13 @@ class DEFER:
         return "127.0.0.1" if rec.get("host") in ("127.0.0.1", "localhost") else self.dispatchIP
 
     # ------------------------------------------------------- data: input
-    def _send_to_stage0(self, rid: int, x: np.ndarray) -> bool:
-        """Send request `rid` to the next serving replica (round-robin)."""
+    def _local(self, rec: dict) -> bool:
+        return rec.get("host") in ("127.0.0.1", "localhost", self.dispatchIP)
+
+    def _send_to_stage0(self, rid: int, x) -> bool:
+        """Send request `rid` to the next serving replica (round-robin).  `x` is an
+        array or a shared-memory slot reference (sent as its descriptor to a
+        same-host stage 0, as bytes to a remote one)."""
         with self._rep_lock:
             reps = [self.replicas[r] for r in sorted(self.replicas)]
         if not reps:
@@ -795,7 +808,8 @@ class DEFER:
             p = reps[(self._rr + i) % len(reps)]
             if p.stage0 is None or p.replica in self._dirty:
                 continue
-            m = Message(1, rid, p.epoch, int(x.shape[0]), [x], [False])
+            t = x if not hasattr(x, "container") or self._local(p.records[0]) else x.array
+            m = Message(1, rid, p.epoch, int(x.shape[0]), [t], [False])
             with self.inflight_lock:
                 if rid in self.inflight_tasks:
                     self.inflight_tasks[rid]["epoch"] = p.epoch
@@ -844,6 +858,10 @@ class DEFER:
             raise ValueError("the dispatcher forwards to partition 1; stages feed each other")
         rid = self._next_req
         self._next_req += 1
+        if self._shm is not None:
+            from .transport.shm import ShmRef
+            # the slot is the retained input: a replay re-sends its descriptor
+            data = ShmRef(self._shm.put(data), data.dtype, data.shape)
         with self.inflight_lock:
             self.inflight_tasks[rid] = {"partition": partition_index, "data": data, "start_time": time.time(),
                                         "epoch": None, "replica": None, "replays": 0}
@@ -963,6 +981,7 @@ class DEFER:
         if task is None:
             METRICS.inc("results_duplicate_dropped")
             return                                   # duplicate from a replay: drop
+        self._release_input(task)
         METRICS.observe("request_latency_ms", (time.time() - task["start_time"]) * 1e3)
         METRICS.inc("results")
         TRACER.event("complete", req=m.req_id, epoch=m.epoch, count=m.count)
@@ -971,6 +990,12 @@ class DEFER:
             pred = (pred.astype(np.uint32) << 16).view(np.float32)
         pred = np.array(pred[: m.count])             # own, writable copy for the caller
         self._emit(m.req_id, pred, output_stream)
+
+    @staticmethod
+    def _release_input(task: dict) -> None:
+        d = task.get("data")
+        if hasattr(d, "slot"):
+            d.slot.release()
 
     @property
     def duplicates_dropped(self) -> int:
@@ -1037,6 +1062,7 @@ class DEFER:
                 with self.inflight_lock:
                     if self.inflight_tasks.pop(rid, None) is None:
                         continue
+                self._release_input(t)
                 METRICS.inc("requests_failed")
                 self._log(f"request {rid} failed {t['replays'] - 1} recoveries: giving up")
                 if self._output is not None:
@@ -1179,6 +1205,8 @@ class DEFER:
             self._hb = None
         if self.membership_server is not None:
             self.membership_server.stop()
+        if self._shm is not None:
+            self._shm.close()
 
     # ---------------------------------------------------------- metrics
     def throughput(self, window: float = 1.0, now: Optional[float] = None) -> float:

@@ -15,20 +15,84 @@ ourselves, so this module provides:
 """
 from __future__ import annotations
 
+import json
 from dataclasses import dataclass
+from pathlib import Path
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from .ir import Graph
+
+# measured per-layer costs (tools/profile_r50.py --calib) and link rates
+# (parallel/check.py --p2p-bw) for gfx950; the analytic model is the fallback
+CALIB_FILE = Path(__file__).resolve().parent.parent / "tuning" / "gfx950_layer_costs.json"
+LINK_FILE = Path(__file__).resolve().parent.parent / "tuning" / "gfx950_links.json"
 
 # MI355X ballpark figures (MI355X_MICROARCH.md): dense bf16 MFMA ~2.5 PF,
 # achievable HBM ~6.3 TB/s, one xGMI link ~150 GB/s.
 @dataclass
 class HwModel:
-    mfma_flops: float = 2.5e15 * 0.45     # sustained fraction for implicit-GEMM conv
-    hbm_bw: float = 6.0e12
-    link_bw: float = 150e9
+    # sustained rate of our fused implicit-GEMM convs: per-layer MI355X measurements
+    # at bs=32 run at 0.16-0.55 PF (profiles/r50_bs32_steps_v14.json); 0.35 PF is
+    # their FLOP-weighted mean (the round-1 guess of 1.1 PF made late stages look
+    # twice as cheap as they are)
+    mfma_flops: float = 0.35e15
+    hbm_bw: float = 5.0e12                # measured 1x1-conv streaming rate (3.7-5.5 TB/s)
+    link_bw: float = 150e9                # replaced by the measured RCCL p2p rate when present
     launch_s: float = 1.5e-6              # kernel boundary inside a hipGraph
     act_bytes: int = 2                    # bf16 activations
+
+
+def _calib_key(g: Graph, batch: int, precision: str) -> str:
+    return f"{g.name}|{len(g.order)}|b{batch}|{precision}"
+
+
+def save_calibration(g: Graph, batch: int, precision: str, steps: Sequence[dict],
+                     graph_ms: Optional[float] = None) -> Dict[str, float]:
+    """Store measured per-step times as per-layer seconds: a fused step's time goes
+    to the last layer it covers (cut candidates are fusion-group ends, so a step
+    never straddles one)."""
+    costs: Dict[str, float] = {}
+    for st in steps:
+        covers = [c for c in st.get("covers", []) if c in g.layers] or [st["out"].split("#")[0]]
+        last = max(covers, key=lambda c: g.order.index(c))
+        costs[last] = costs.get(last, 0.0) + float(st["ms"]) * 1e-3
+    try:
+        table = json.loads(CALIB_FILE.read_text())
+    except (OSError, ValueError):
+        table = {}
+    table[_calib_key(g, batch, precision)] = {"costs_s": costs, "graph_ms": graph_ms}
+    CALIB_FILE.parent.mkdir(parents=True, exist_ok=True)
+    CALIB_FILE.write_text(json.dumps(table, indent=1, sort_keys=True))
+    return costs
+
+
+def load_calibration(g: Graph, batch: int, precision: str = "bf16") -> Optional[Dict[str, float]]:
+    """Measured per-layer seconds for (model, batch, precision), if profiled."""
+    try:
+        ent = json.loads(CALIB_FILE.read_text()).get(_calib_key(g, batch, precision))
+    except (OSError, ValueError):
+        return None
+    if not ent:
+        return None
+    costs = {n: 0.0 for n in g.order}
+    costs.update({k: float(v) for k, v in ent["costs_s"].items() if k in costs})
+    return costs
+
+
+def measured_link_bw() -> Optional[float]:
+    """RCCL p2p bytes/s between neighbouring MI355X (parallel/check.py --p2p-bw)."""
+    try:
+        return float(json.loads(LINK_FILE.read_text())["link_bw"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def default_hw() -> HwModel:
+    hw = HwModel()
+    bw = measured_link_bw()
+    if bw:
+        hw.link_bw = bw
+    return hw
 
 
 def layer_costs(g: Graph, batch: int = 32, hw: Optional[HwModel] = None) -> Dict[str, float]:
@@ -112,11 +176,16 @@ def default_candidates(g: Graph) -> List[str]:
 
 def plan_cuts(g: Graph, stages: int, batch: int = 32, hw: Optional[HwModel] = None,
               costs: Optional[Dict[str, float]] = None,
-              candidates: Optional[Sequence[str]] = None) -> Tuple[List[str], List[float]]:
-    """Min-max DP: returns (part_at, per-stage estimated seconds)."""
+              candidates: Optional[Sequence[str]] = None, precision: str = "bf16",
+              calibrated: bool = True) -> Tuple[List[str], List[float]]:
+    """Min-max DP: returns (part_at, per-stage estimated seconds).  Layer costs:
+    `costs` if given, else the measured calibration for (model, batch,
+    precision) when one exists, else the analytic roofline model."""
     if stages < 1:
         raise ValueError("stages must be >= 1")
-    hw = hw or HwModel()
+    hw = hw or default_hw()
+    if costs is None and calibrated:
+        costs = load_calibration(g, batch, precision)
     costs = costs or layer_costs(g, batch, hw)
     if stages == 1:
         return [], [sum(costs.values())]

@@ -283,6 +283,13 @@ class StageRuntime:
                         break
                     if self.gpu_codec:
                         out = self._compute_gpu(m)
+                    elif self.compute.gpu:
+                        # pipelined: H2D, ingest, graph replay and D2H are only enqueued here;
+                        # the send thread waits for the event (micro-batch t computes while
+                        # t+1 is received and t-1 is sent)
+                        ev, res = self.compute.submit(m.tensors, m.bf16, m.count)
+                        out = (ev, Message(self.stage + 2, m.req_id, m.epoch, m.count, [r[0] for r in res],
+                                           [r[1] for r in res]))
                     else:
                         outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
                         out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
@@ -305,7 +312,13 @@ class StageRuntime:
                     m = self.outq.get(timeout=0.1)
                 except queue.Empty:
                     continue
-                if isinstance(m, tuple):                   # GPU-encoded frontier (side stream)
+                if isinstance(m, tuple) and len(m) == 2:   # pipelined GPU micro-batch: outputs on the host at `ev`
+                    ev, m = m
+                    while not ev.query():
+                        if self.stop.is_set():
+                            return
+                        time.sleep(0.0001)
+                elif isinstance(m, tuple):                 # GPU-encoded frontier (side stream)
                     m = self._finish_gpu_message(m)
                 send_message(self.downstream, m, self.codec, self.node.state.chunk_size)
         except Exception as e:  # noqa: BLE001
@@ -339,6 +352,9 @@ class Node:
             import torch
             device = "cuda:0" if torch.cuda.is_available() else "cpu"
         self.device = device
+        if str(device).startswith("cuda"):
+            from .transport import shm
+            shm.REGISTER_DEVICE = True       # same-host ingest slots are page-locked for DMA
         self.host = host
         self.advertise_host = advertise_host or ("127.0.0.1" if dispatcher_ip in ("127.0.0.1", "localhost")
                                                  else get_local_ip())
@@ -472,15 +488,17 @@ class Node:
         StageCompute with: one definition for configure and prepare."""
         graph = bool(cfg.get("graph", True))
         if cfg.get("transport", "tcp") == "tcp":
-            gpu_codec = cfg.get("codec", "lz4") in ("zvc", "lz4") and str(device).startswith("cuda")
-            return (2 if gpu_codec else 1), int(cfg.get("queue", 4)) + 4, graph
+            # GPU stages double-buffer (pipelined submit / GPU codec); the host ring of
+            # output buffers outlives the bounded queues between the stage's threads
+            return (2 if str(device).startswith("cuda") else 1), int(cfg.get("queue", 4)) + 4, graph
         return int(cfg.get("nsets", 2)), 8, graph
 
     def _compute_key(self, cfg: Dict) -> Optional[tuple]:
         key = cfg.get("cache_key")
         if not key:
             return None
-        return (key, int(cfg["batch"]), cfg.get("precision", "bf16")) + self.compute_shape(cfg, self.device)
+        return (key, int(cfg["batch"]), cfg.get("precision", "bf16"), cfg.get("preprocess", "none")) + \
+            self.compute_shape(cfg, self.device)
 
     def stage_compute(self, cfg: Dict, g, weights: Dict[str, np.ndarray], capture_mode: str = "global"):
         """The StageCompute of a slice: reused from the cache (built by an earlier
@@ -501,7 +519,7 @@ class Node:
         try:
             c = StageCompute(g, weights, int(cfg["batch"]), self.device, graph_capture=graph, num_sets=num_sets,
                              host_ring=host_ring, capture_mode=capture_mode,
-                             precision=cfg.get("precision", "bf16"))
+                             precision=cfg.get("precision", "bf16"), preprocess=cfg.get("preprocess", "none"))
         finally:
             if key is not None:
                 with self._computes_lock:

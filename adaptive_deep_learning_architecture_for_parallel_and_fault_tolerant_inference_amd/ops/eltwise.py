@@ -8,6 +8,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import numpy as np
+
 import torch
 
 from ._lib import kernels, ptr, stream_handle
@@ -319,3 +321,44 @@ def pad_f32(x: torch.Tensor, out: torch.Tensor, pad_t: int, pad_l: int, stream=N
         raise ValueError("pad: output too small")
     kernels().pad_f32(ptr(x), ptr(out), B, H, W, C, OH, OW, int(pad_t), int(pad_l), stream_handle(stream))
     return out
+
+
+# ------------------------------------------------------------------ ingest
+# Keras `preprocess_input` modes (keras.applications.imagenet_utils): caffe =
+# RGB -> BGR then minus the ImageNet BGR mean (ResNet / VGG; the reference's
+# `test/test.py:20-23`), tf = x / 127.5 - 1 (MobileNet, Inception), torch =
+# (x / 255 - mean) / std (DenseNet), none = plain cast.
+PREPROCESS = {
+    "none": (False, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0)),
+    "caffe": (True, (1.0, 1.0, 1.0), (-103.939, -116.779, -123.68)),
+    "tf": (False, (1 / 127.5,) * 3, (-1.0, -1.0, -1.0)),
+    "torch": (False, tuple(1 / (255.0 * s) for s in (0.229, 0.224, 0.225)),
+              tuple(-m / s for m, s in zip((0.485, 0.456, 0.406), (0.229, 0.224, 0.225)))),
+}
+
+
+def ingest_u8(x: torch.Tensor, out: torch.Tensor, mode: str = "none", stream=None) -> torch.Tensor:
+    """uint8 NHWC images (device) -> fp32 model input with `mode` preprocessing."""
+    if x.dtype != torch.uint8 or not x.is_contiguous():
+        raise ValueError("ingest: x must be contiguous uint8")
+    _chk(out, torch.float32, "out")
+    if out.numel() < x.numel() or out.shape[-1] != x.shape[-1]:
+        raise ValueError(f"ingest: out {tuple(out.shape)} cannot hold x {tuple(x.shape)}")
+    C = x.shape[-1]
+    rev, sc, sh = PREPROCESS[mode]
+    if C != 3 and mode != "none":
+        raise ValueError(f"preprocess mode {mode!r} needs 3 channels, got {C}")
+    scale = [sc[c] if c < 3 else 1.0 for c in range(C)]
+    shift = [sh[c] if c < 3 else 0.0 for c in range(C)]
+    kernels().ingest_u8(ptr(x), ptr(out), x.numel(), C, int(rev), scale, shift, stream_handle(stream))
+    return out
+
+
+def preprocess_ref(x: np.ndarray, mode: str) -> np.ndarray:
+    """Host reference of `ingest_u8` (float64 math, fp32 result)."""
+    rev, sc, sh = PREPROCESS[mode]
+    y = x.astype(np.float64)
+    if rev:
+        y = y[..., ::-1]
+    C = y.shape[-1]
+    return (y * np.asarray(sc[:C]) + np.asarray(sh[:C])).astype(np.float32)

@@ -7,6 +7,13 @@ BASELINE.json config 1 and of the CPU-only integration tests.
 Host-side arrays in/out are numpy; bfloat16 tensors travel as uint16 bit
 patterns with a flag (numpy has no bf16).  Device-resident paths (RCCL links)
 use `device_inputs()` / `device_outputs()` directly and never touch the host.
+
+`submit()` is the pipelined GPU path of a TCP stage: H2D of micro-batch t
+(straight from a page-locked shared-memory slot when the dispatcher is on
+the same host), the ingest kernel (uint8 images -> preprocessed fp32), the
+graph replay and the D2H of the outputs are all enqueued on the stream and
+only an event comes back, so the host receives t+1 and sends t-1 while t
+computes (two buffer sets alternate).  `run_host()` is its synchronous form.
 """
 from __future__ import annotations
 
@@ -40,6 +47,13 @@ def to_torch(a: np.ndarray, is_bf16: bool, device) -> torch.Tensor:
     return t.to(device, non_blocking=False)
 
 
+def _readonly_tensor(a: np.ndarray) -> torch.Tensor:
+    """A CPU tensor over a read-only array (a received frame or a shm slot), no copy."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        return torch.from_numpy(np.ascontiguousarray(a))
+
+
 def to_numpy(t: torch.Tensor) -> Tuple[np.ndarray, bool]:
     t = t.detach()
     if t.dtype == torch.bfloat16:
@@ -50,8 +64,12 @@ def to_numpy(t: torch.Tensor) -> Tuple[np.ndarray, bool]:
 class StageCompute:
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device: str = "cpu",
                  outputs: Optional[Sequence[str]] = None, graph_capture: bool = True, num_sets: int = 1,
-                 host_ring: int = 8, capture_mode: str = "global", precision: str = "bf16"):
+                 host_ring: int = 8, capture_mode: str = "global", precision: str = "bf16",
+                 preprocess: str = "none"):
         self.g = g
+        self.preprocess = preprocess          # uint8 image inputs: Keras preprocess_input mode (ops/eltwise.py)
+        self._u8: Dict[Tuple[str, int], torch.Tensor] = {}
+        self._tick = 0
         self.batch = batch
         self.device = torch.device(device)
         self.inputs = list(g.input_names)
@@ -76,11 +94,40 @@ class StageCompute:
         pad = torch.zeros((self.batch - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return torch.cat([t, pad])
 
-    def _d2h_pinned(self, outs: Dict[str, torch.Tensor], count: int) -> List[Tuple[np.ndarray, bool]]:
-        """Device outputs -> numpy views of a ring of pinned host buffers (one async
-        DMA per tensor instead of a pageable .cpu() allocation + copy).  A view
-        stays valid for `host_ring` further calls: the caller's queues are bounded
-        below that (node.py sizes it as queue depth + 4)."""
+    def _feed(self, name: str, a: np.ndarray, is_bf16: bool, count: int, j: int) -> None:
+        """Host array -> input buffer `name` of set j, on the current stream."""
+        from ..ops import eltwise as E
+        dst = self.ex.input_buf(name, j)
+        if a.dtype == np.uint8 and dst.dtype == torch.float32 and tuple(a.shape[1:]) == tuple(dst.shape[1:]):
+            key = (name, j)
+            u8 = self._u8.get(key)
+            if u8 is None:
+                u8 = self._u8[key] = torch.zeros(tuple(dst.shape), dtype=torch.uint8, device=self.device)
+            src = _readonly_tensor(a)
+            # async when `a` is page-locked (a registered shm slot); the slot outlives the request
+            u8[: a.shape[0]].copy_(src, non_blocking=src.is_pinned())
+            if a.shape[0] < dst.shape[0]:
+                u8[a.shape[0]:].zero_()
+            E.ingest_u8(u8, dst, self.preprocess)
+            return
+        t = to_torch(a, is_bf16, self.device)
+        if t.dtype != dst.dtype:
+            t = t.to(dst.dtype)
+        if t.shape[-1] != dst.shape[-1]:          # channel padding (e.g. 3 -> 8)
+            t = torch.nn.functional.pad(t, (0, dst.shape[-1] - t.shape[-1]))
+        t = self._pad(t, count)
+        dst.copy_(t)
+
+    def submit(self, arrays: Sequence[np.ndarray], bf16_flags: Sequence[bool], count: int):
+        """Enqueue one micro-batch (GPU): returns (event, [(array, bf16)]) whose host
+        arrays are valid once the event has completed."""
+        if len(arrays) != len(self.inputs):
+            raise ValueError(f"stage expects {len(self.inputs)} inputs, got {len(arrays)}")
+        j = self._tick % self.ex.num_sets
+        self._tick += 1
+        for name, a, b in zip(self.inputs, arrays, bf16_flags):
+            self._feed(name, a, b, count, j)
+        outs = self.ex.forward(j)
         if not self._pinned:
             for _ in range(self.host_ring):
                 self._pinned.append({o: torch.empty(tuple(outs[o].shape), dtype=outs[o].dtype, pin_memory=True)
@@ -89,7 +136,8 @@ class StageCompute:
         self._pin_next = (self._pin_next + 1) % self.host_ring
         for o in self.outputs:
             slot[o].copy_(outs[o], non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
         res = []
         for o in self.outputs:
             h = slot[o][:count]
@@ -97,32 +145,25 @@ class StageCompute:
                 res.append((h.view(torch.int16).numpy().view(np.uint16), True))
             else:
                 res.append((h.numpy(), False))
-        return res
+        return ev, res
 
     def run_host(self, arrays: Sequence[np.ndarray], bf16_flags: Sequence[bool], count: int
                  ) -> Tuple[List[np.ndarray], List[bool]]:
         if len(arrays) != len(self.inputs):
             raise ValueError(f"stage expects {len(self.inputs)} inputs, got {len(arrays)}")
         if self.gpu:
-            for name, a, b in zip(self.inputs, arrays, bf16_flags):
-                dst = self.ex.input_buf(name)
-                t = to_torch(a, b, self.device)
-                if t.dtype != dst.dtype:
-                    t = t.to(dst.dtype)
-                if t.shape[-1] != dst.shape[-1]:          # channel padding (e.g. 3 -> 8)
-                    t = torch.nn.functional.pad(t, (0, dst.shape[-1] - t.shape[-1]))
-                t = self._pad(t, count)
-                dst.copy_(t)
-            outs = self.ex.forward(0)
-            res = self._d2h_pinned(outs, count)
-        else:
-            feed = {}
-            for name, a, b in zip(self.inputs, arrays, bf16_flags):
-                t = to_torch(a, b, "cpu").float()
-                true_c = self.g.layers[name].out_shape[-1] if self.g.layers[name].out_shape else None
-                if true_c and t.dim() == 4 and t.shape[-1] != true_c:
-                    t = t[..., :true_c]
-                feed[name] = t
-            outs = self.ex.run(feed, outputs=self.outputs)
-            res = [(outs[o][:count].float().numpy(), False) for o in self.outputs]
-        return [r[0] for r in res], [r[1] for r in res]
+            ev, res = self.submit(arrays, bf16_flags, count)
+            ev.synchronize()
+            return [r[0] for r in res], [r[1] for r in res]
+        feed = {}
+        for name, a, b in zip(self.inputs, arrays, bf16_flags):
+            if a.dtype == np.uint8 and self.preprocess != "none":
+                from ..ops.eltwise import preprocess_ref
+                a = preprocess_ref(a, self.preprocess)
+            t = to_torch(a, b, "cpu").float()
+            true_c = self.g.layers[name].out_shape[-1] if self.g.layers[name].out_shape else None
+            if true_c and t.dim() == 4 and t.shape[-1] != true_c:
+                t = t[..., :true_c]
+            feed[name] = t
+        outs = self.ex.run(feed, outputs=self.outputs)
+        return [outs[o][:count].float().numpy() for o in self.outputs], [False] * len(self.outputs)

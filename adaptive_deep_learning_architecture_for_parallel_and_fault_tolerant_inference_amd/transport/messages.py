@@ -49,6 +49,9 @@ def send_message(sock: socket.socket, m: Message, codec: str = "lz4", chunk_size
         if isinstance(t, tuple):
             # (container header, payload view) from the GPU side-stream codec
             socket_send_parts(list(t), sock, chunk_size, timeout_ms)
+        elif hasattr(t, "container"):
+            # a same-host shared-memory slot (transport/shm.py): only its descriptor travels
+            socket_send(t.container(), sock, chunk_size, timeout_ms)
         elif isinstance(t, (bytes, bytearray)):
             # a container already encoded elsewhere (GPU side-stream codec)
             socket_send(t, sock, chunk_size, timeout_ms)

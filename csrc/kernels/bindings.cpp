@@ -5,9 +5,11 @@
 // ops/*.py before any launch.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "kernels.h"
 
@@ -202,6 +204,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("pad_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int pt, int pl, u64 s) {
     check(adapt::pad_f32(P<const float>(x), P<float>(y), B, H, W, C, OH, OW, pt, pl, S(s)), "pad_f32");
+  });
+  m.def("ingest_u8", [](u64 x, u64 y, size_t n, int C, int reverse, std::vector<float> scale,
+                        std::vector<float> shift, u64 s) {
+    if ((int)scale.size() < C || (int)shift.size() < C) throw std::runtime_error("ingest_u8: scale/shift per channel");
+    check(adapt::ingest_u8(P<const uint8_t>(x), P<float>(y), n, C, reverse, scale.data(), shift.data(), S(s)),
+          "ingest_u8");
   });
   m.def("cast_f32_bf16", [](u64 x, u64 y, size_t n, u64 s) {
     check(adapt::cast_f32_bf16(P<const float>(x), P<bf16>(y), n, S(s)), "cast_f32_bf16");

@@ -111,4 +111,7 @@ hipError_t eltwise_f32(const float* a, const float* b, const float* scale, const
                        int C, int op, int relu, hipStream_t s);
 hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
                    hipStream_t s);
+// serving ingest (ingest.hip): uint8 NHWC -> fp32, y = x[rev(c)] * scale[c] + shift[c] (host scale/shift, C <= 4)
+hipError_t ingest_u8(const uint8_t* x, float* y, size_t n, int C, int reverse, const float* scale,
+                     const float* shift, hipStream_t s);
 }  // namespace adapt

@@ -168,3 +168,30 @@ def test_probe_live_drops_dead_worker_with_live_lease():
     finally:
         live.close()
         d.shutdown()
+
+
+def test_uint8_ingest_shm_caffe_preprocess(tiny):
+    """uint8 image requests through same-host shared memory, caffe
+    `preprocess_input` applied by stage 0 (`test/test.py:20-23`)."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.eltwise import \
+        preprocess_ref
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, ordered=True, batch=2, weight_codec="lz4",
+              min_workers=2, replicas=1, preprocess="caffe")
+    assert d._shm is not None
+    d.membership_server.start()
+    nodes = _nodes(d, 2, "u")
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, ["conv3_block1_out"], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(5)
+        xs = [rng.integers(0, 256, (3, 32, 32, 3), dtype=np.uint8) for _ in range(3)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=60) for _ in range(6)])
+        want = tiny.predict(preprocess_ref(np.concatenate(xs), "caffe"), device="cpu")
+        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+        assert len(d._shm._all) >= 1 and {s.nbytes for s in d._shm._all} <= {3072, 2 * 3072}
+    finally:
+        d.shutdown(stop_workers=True)
+        for nd in nodes:
+            nd.stop()

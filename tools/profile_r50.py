@@ -41,10 +41,13 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--baseline", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--calib", action="store_true",
+                    help="write the measured per-layer costs into the planner's calibration table")
     a = ap.parse_args()
     g = build_model(a.model)
     w = init_weights(g, 0)
-    ex = SliceExecutor(g, w, a.batch, tune=a.tune)
+    ex = SliceExecutor(g, w, a.batch, tune=a.tune, precision=a.dtype)
     x = torch.randn((a.batch,) + tuple(g.layers[g.input].out_shape), device="cuda")
     ex.input_buf(g.input).copy_(x)
     # per-step eager timing
@@ -91,7 +94,8 @@ def main():
             flop = 2 * o.numel() * st.p["kernel"][0] * st.p["kernel"][1]
         total_flop += flop
         per.append({"i": i, "kind": st.kind, "out": st.out, "ms": round(t, 4),
-                    "tflops": round(flop / t / 1e9, 1) if flop else None, "cfg": ex.cfg.get(i)})
+                    "tflops": round(flop / t / 1e9, 1) if flop else None, "cfg": ex.cfg.get(i),
+                    "flop": flop, "covers": list(st.covers)})
     ex.capture()
     t_graph = time_fn(lambda: ex.forward(0), reps=100, warm=10)
     print(f"{'i':>3} {'kind':8} {'out':28} {'ms':>8} {'TF/s':>7} cfg")
@@ -122,6 +126,11 @@ def main():
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)
+    if a.calib:
+        from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.graph.planner import \
+            save_calibration
+        save_calibration(g, a.batch, a.dtype, per, graph_ms=t_graph)
+        print(f"calibration written for {g.name} b{a.batch} {a.dtype}")
 
 
 if __name__ == "__main__":
