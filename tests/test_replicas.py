@@ -72,6 +72,7 @@ def test_pp_dp_replicas_serve_and_reform_one(tiny):
         assert _wait(lambda: d.replicas.get(ra) is not None and d.replicas[ra].epoch != reps[ra][0])
         assert d.replicas[rb].epoch == reps[rb][0]
         assert victim not in d.replicas[ra].workers
+        assert _wait(lambda: len(d.recoveries) > 0)       # recorded after the replay that follows the re-form
         rec = d.recoveries[0]
         assert rec["replica"] == ra
         assert rec["t_fail"] - t_kill < 1.0          # session EOF, not the 2 s lease
