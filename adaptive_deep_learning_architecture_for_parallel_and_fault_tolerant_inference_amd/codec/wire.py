@@ -12,6 +12,9 @@ ONE contiguous device byte buffer, ``wire``, that travels as a single
            (`lz4_gpu_decompress_dev`) instead of walking the frame on the host.
 * ``zvc``  ``wire = AZVC stream`` (csrc/kernels/zvc_gpu.hip); the stream holds
            its own segment-size table (`zvc_gpu_decompress_dev`).
+* ``zfp``  float32 tensors only (the reference's zfp): ``wire = [u64 word count
+           per 4^d block | payload words]``, i.e. the host zfp container
+           (chunk_blocks = 1) without its fixed header (csrc/kernels/zfp_gpu.hip).
 
 GPU encodes run on a side HIP stream behind an event of the producer stream
 (BASELINE config 3: compression overlapped with the next micro-batch's
@@ -28,7 +31,7 @@ import torch
 
 from ..native import runtime
 
-KINDS = ("lz4", "zvc")
+KINDS = ("lz4", "zvc", "zfp")
 
 
 class WireCodec:
@@ -45,17 +48,31 @@ class WireCodec:
         self.n = self.numel * self.esz
         if kind == "zvc" and self.esz not in (2, 4):
             raise ValueError("zvc needs 2- or 4-byte elements")
+        if kind == "zfp" and like.dtype != torch.float32:
+            raise ValueError("zfp wire codec needs float32 tensors (zfp has no bf16 mode)")
+        self.shape = tuple(like.shape)
         if self.n == 0:
             raise ValueError("empty tensor")
         self._nbytes: Optional[int] = None
         self.head = 0
         if not self.gpu:
-            self.wire = torch.empty(self.n + self.n // 8 + 4096, dtype=torch.uint8)
+            # zfp's worst case on small blocks (1-D/2-D tensors) nearly doubles the bytes
+            cap = 2 * self.n + 8 * self.numel + 4096 if kind == "zfp" else self.n + self.n // 8 + 4096
+            self.wire = torch.empty(cap, dtype=torch.uint8)
             return
         from ..ops._lib import kernels
         K = self.K = kernels()
         self.stream = stream if stream is not None else torch.cuda.Stream(device=self.device)
         dev = self.device
+        if kind == "zfp":
+            from .gpu_zfp import GpuZFP
+            self.zfp = GpuZFP(self.shape, dev)
+            self.zfp.stream = self.stream
+            self.wire = self.zfp.out.view(torch.uint8)
+            self.total_host = self.zfp.total_host
+            self.done = self.zfp.done
+            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+            return
         if kind == "lz4":
             ch = K.lz4_gpu_chunk()
             self.nidx = (self.n + ch - 1) // ch
@@ -88,7 +105,11 @@ class WireCodec:
         if not self.gpu:
             raw = t.view(torch.uint8).reshape(-1).numpy()
             rt = runtime()
-            b = rt.lz4_compress(raw) if self.kind == "lz4" else rt.zvc_compress(raw, self.esz)
+            if self.kind == "zfp":
+                from .gpu_zfp import header, zfp_shape
+                b = rt.zfp_compress(t.numpy().reshape(zfp_shape(self.shape)), 4, 1)[len(header(self.shape)) + 8:]
+            else:
+                b = rt.lz4_compress(raw) if self.kind == "lz4" else rt.zvc_compress(raw, self.esz)
             if len(b) > self.wire.numel():
                 raise RuntimeError("host codec output exceeds the wire buffer")
             self.wire[:len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
@@ -98,6 +119,8 @@ class WireCodec:
         if ev is None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
+        if self.kind == "zfp":
+            return self.zfp.compress(t, after=ev)
         self.stream.wait_event(ev)
         s = int(self.stream.cuda_stream)
         w = self.wire.data_ptr()
@@ -116,7 +139,10 @@ class WireCodec:
         """Message length of the last encode (waits for that encode only)."""
         if self._nbytes is None:
             self.done.synchronize()
-            self._nbytes = self.head + int(self.total_host.item())
+            if self.kind == "zfp":
+                self._nbytes = 8 * (self.zfp.nblocks + int(self.total_host.item()))
+            else:
+                self._nbytes = self.head + int(self.total_host.item())
         return self._nbytes
 
     # ------------------------------------------------------------ decode
@@ -129,14 +155,23 @@ class WireCodec:
         if not self.gpu:
             data = self.wire[:nbytes].numpy().tobytes()
             rt = runtime()
-            raw = rt.lz4_decompress(data) if self.kind == "lz4" else rt.zvc_decompress(data)
+            if self.kind == "zfp":
+                import struct
+                from .gpu_zfp import header, zfp_shape
+                nb = int(np.prod([(v + 3) // 4 for v in zfp_shape(self.shape)]))
+                raw = rt.zfp_decompress(header(self.shape) + struct.pack("<Q", nb) + data, 4).tobytes()
+            else:
+                raw = rt.lz4_decompress(data) if self.kind == "lz4" else rt.zvc_decompress(data)
             if len(raw) != self.n:
                 raise RuntimeError(f"decoded {len(raw)} bytes, expected {self.n}")
             out.view(torch.uint8).reshape(-1).copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8))
             return out
         s = int((stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream)
         w = self.wire.data_ptr()
-        if self.kind == "lz4":
+        if self.kind == "zfp":
+            z = self.zfp
+            self.K.zfp_gpu_decompress(w, z.zshape, z.offs.data_ptr(), z.total.data_ptr(), out.data_ptr(), s)
+        elif self.kind == "lz4":
             self.K.lz4_gpu_decompress_dev(w + self.head, w, self.nidx, self.dec_offs.data_ptr(), out.data_ptr(), self.n,
                                           self.err.data_ptr(), s)
         else:

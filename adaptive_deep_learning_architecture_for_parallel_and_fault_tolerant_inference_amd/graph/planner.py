@@ -147,13 +147,43 @@ def articulation_points(g: Graph) -> List[str]:
     return verified
 
 
-def default_candidates(g: Graph) -> List[str]:
+def prefix_points(g: Graph) -> List[str]:
+    """Layers `c` whose ancestor set is exactly the topological prefix up to c:
+    a cut there makes every stage a contiguous range of the order (so prefix
+    sums give stage costs), but unlike an articulation point more than one
+    tensor may cross it (a residual branch in flight: the multi-tensor frontier
+    of BASELINE config 2)."""
+    order = g.order
+    out = []
+    seen = set()
+    for i, n in enumerate(order):
+        seen.add(n)
+        if g.layers[n].op == "input" or n == g.output:
+            continue
+        anc = g.ancestors(n)
+        if len(anc) == i + 1 and anc == seen:
+            out.append(n)
+    return out
+
+
+def crossing_bytes(g: Graph, cut: str, act_bytes: int = 2) -> int:
+    """Bytes per image of every tensor produced up to `cut` and consumed after it."""
+    idx = {n: i for i, n in enumerate(g.order)}
+    i = idx[cut]
+    cons = g.consumers()
+    return sum(g.tensor_bytes(t, act_bytes) for t in g.order[: i + 1]
+               if any(idx[c] > i for c in cons.get(t, [])))
+
+
+def default_candidates(g: Graph, fine: bool = True) -> List[str]:
     """Articulation points at fusion-group ends: cutting there never splits a
     conv+BN+add+ReLU (or dwconv+BN+ReLU6) epilogue across stages.  ResNet:
     ``pool1_pool`` and the ``*_out`` block outputs; MobileNetV2: the block
     outputs (``*_add`` or ``*_project_BN``); DenseNet: the ``*_concat`` /
     ``pool*_pool`` tensors; VGG: the conv outputs and pools.  A tensor whose
-    only consumer is a ZeroPadding2D is skipped (the pad folds into the next op)."""
+    only consumer is a ZeroPadding2D is skipped (the pad folds into the next op).
+    With `fine`, cuts inside a residual block (after its ``_1_relu`` /
+    ``_2_relu``: the block input crosses too) are candidates as well."""
     cons = g.consumers()
 
     def group_end(n: str) -> bool:
@@ -171,16 +201,23 @@ def default_candidates(g: Graph) -> List[str]:
         if L.op in ("conv", "dwconv"):
             return L.attrs.get("activation") == "relu"
         return False
-    return [n for n in articulation_points(g) if group_end(n)]
+    pts = prefix_points(g) if fine else articulation_points(g)
+    return [n for n in pts if group_end(n)]
 
 
 def plan_cuts(g: Graph, stages: int, batch: int = 32, hw: Optional[HwModel] = None,
               costs: Optional[Dict[str, float]] = None,
               candidates: Optional[Sequence[str]] = None, precision: str = "bf16",
-              calibrated: bool = True) -> Tuple[List[str], List[float]]:
+              calibrated: bool = True, objective: str = "throughput") -> Tuple[List[str], List[float]]:
     """Min-max DP: returns (part_at, per-stage estimated seconds).  Layer costs:
     `costs` if given, else the measured calibration for (model, batch,
-    precision) when one exists, else the analytic roofline model."""
+    precision) when one exists, else the analytic roofline model.
+
+    objective "throughput": a stage's period is max(compute, receive, send) on
+    its link (the three overlap on separate streams); plans whose period is set
+    by a link tie on it and are then ranked by their slowest *compute* stage.
+    objective "compute": links are ignored (one device, or links much faster
+    than the stages)."""
     if stages < 1:
         raise ValueError("stages must be >= 1")
     hw = hw or default_hw()
@@ -201,27 +238,32 @@ def plan_cuts(g: Graph, stages: int, batch: int = 32, hw: Optional[HwModel] = No
     total = prefix[-1]
     # positions: 0 = start, cands..., end
     pos = [-1] + [idx[c] for c in cands] + [len(order) - 1]
-    comm = [0.0] + [g.tensor_bytes(c, hw.act_bytes) * batch / hw.link_bw for c in cands] + [0.0]
+    if objective not in ("throughput", "compute"):
+        raise ValueError(f"objective must be throughput or compute, got {objective!r}")
+    link = objective == "throughput"
+    comm = [0.0] + [crossing_bytes(g, c, hw.act_bytes) * batch / hw.link_bw if link else 0.0 for c in cands] + [0.0]
 
-    def seg(a: int, b: int) -> float:   # stage from after pos[a] to pos[b] inclusive
-        t = prefix[pos[b] + 1] - prefix[pos[a] + 1]
+    def compute(a: int, b: int) -> float:   # stage from after pos[a] to pos[b] inclusive
+        return prefix[pos[b] + 1] - prefix[pos[a] + 1]
+
+    def seg(a: int, b: int) -> float:
         # receive / compute / send run on separate HIP streams over a stream of
         # micro-batches, so a stage's steady-state period is the max of the three.
-        return max(t, comm[a], comm[b])
+        return max(compute(a, b), comm[a], comm[b])
 
     P = len(pos)
-    INF = float("inf")
-    # dp[k][j]: best max cost covering up to pos[j] with k stages
+    INF = (float("inf"), float("inf"))
+    # dp[k][j]: best (max period, max compute) covering up to pos[j] with k stages
     dp = [[INF] * P for _ in range(stages + 1)]
     arg = [[-1] * P for _ in range(stages + 1)]
-    dp[0][0] = 0.0
+    dp[0][0] = (0.0, 0.0)
     for k in range(1, stages + 1):
         for j in range(1, P):
             best, barg = INF, -1
             for i in range(0, j):
                 if dp[k - 1][i] == INF:
                     continue
-                v = max(dp[k - 1][i], seg(i, j))
+                v = (max(dp[k - 1][i][0], seg(i, j)), max(dp[k - 1][i][1], compute(i, j)))
                 if v < best:
                     best, barg = v, i
             dp[k][j] = best

@@ -205,6 +205,21 @@ PYBIND11_MODULE(_C, m) {
   m.def("pad_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int pt, int pl, u64 s) {
     check(adapt::pad_f32(P<const float>(x), P<float>(y), B, H, W, C, OH, OW, pt, pl, S(s)), "pad_f32");
   });
+  m.def("zfp_gpu_maxw", &adapt::zfp_gpu_maxw);
+  m.def("zfp_gpu_nblocks", [](std::vector<int64_t> shape) {
+    return adapt::zfp_gpu_nblocks(shape.data(), (int)shape.size());
+  });
+  m.def("zfp_gpu_compress", [](u64 src, std::vector<int64_t> shape, u64 scratch, u64 offs, u64 out, u64 total,
+                               u64 s) {
+    check(adapt::zfp_gpu_compress(P<const float>(src), shape.data(), (int)shape.size(), P<uint64_t>(scratch),
+                                  P<uint64_t>(offs), P<uint64_t>(out), P<uint64_t>(total), S(s)),
+          "zfp_gpu_compress");
+  });
+  m.def("zfp_gpu_decompress", [](u64 table, std::vector<int64_t> shape, u64 offs, u64 total, u64 dst, u64 s) {
+    check(adapt::zfp_gpu_decompress(P<const uint64_t>(table), shape.data(), (int)shape.size(), P<uint64_t>(offs),
+                                    P<uint64_t>(total), P<float>(dst), S(s)),
+          "zfp_gpu_decompress");
+  });
   m.def("ingest_u8", [](u64 x, u64 y, size_t n, int C, int reverse, std::vector<float> scale,
                         std::vector<float> shift, u64 s) {
     if ((int)scale.size() < C || (int)shift.size() < C) throw std::runtime_error("ingest_u8: scale/shift per channel");

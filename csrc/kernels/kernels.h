@@ -111,6 +111,13 @@ hipError_t eltwise_f32(const float* a, const float* b, const float* scale, const
                        int C, int op, int relu, hipStream_t s);
 hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
                    hipStream_t s);
+// reversible zfp-style float32 codec on the GPU (zfp_gpu.hip), bit-exact with the host v2 container
+uint32_t zfp_gpu_maxw(int nd);
+uint64_t zfp_gpu_nblocks(const int64_t* shape, int nd);
+hipError_t zfp_gpu_compress(const float* src, const int64_t* shape, int nd, uint64_t* scratch, uint64_t* offs,
+                            uint64_t* out, uint64_t* total, hipStream_t s);
+hipError_t zfp_gpu_decompress(const uint64_t* table, const int64_t* shape, int nd, uint64_t* offs, uint64_t* total,
+                              float* dst, hipStream_t s);
 // serving ingest (ingest.hip): uint8 NHWC -> fp32, y = x[rev(c)] * scale[c] + shift[c] (host scale/shift, C <= 4)
 hipError_t ingest_u8(const uint8_t* x, float* y, size_t n, int C, int reverse, const float* scale,
                      const float* shift, hipStream_t s);

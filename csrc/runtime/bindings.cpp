@@ -236,7 +236,7 @@ PYBIND11_MODULE(_runtime, m) {
   });
 
   // ---------------------------------------------------------------- zfp
-  m.def("zfp_compress", [](py::array arr, int threads) {
+  m.def("zfp_compress", [](py::array arr, int threads, size_t chunk_blocks) {
     py::buffer_info info = arr.request();
     int code;
     if (info.format == py::format_descriptor<float>::format() && info.itemsize == 4) code = 0;
@@ -249,10 +249,16 @@ PYBIND11_MODULE(_runtime, m) {
     std::vector<uint8_t> out;
     {
       NoGil nogil;
-      out = zfp_compress(info.ptr, code, shape, threads);
+      out = zfp_compress(info.ptr, code, shape, threads, chunk_blocks);
     }
     return to_bytes(out);
-  }, py::arg("arr"), py::arg("threads") = 4);
+  }, py::arg("arr"), py::arg("threads") = 4, py::arg("chunk_blocks") = 0);
+  m.def("zfp_info", [](py::buffer data) {
+    py::buffer_info info;
+    auto v = view(data, info);
+    ZfpHeader h = zfp_header(v.first, v.second);
+    return py::make_tuple(h.dtype, h.shape, h.payload_off, h.chunk_blocks);
+  });
   m.def("zfp_decompress", [](py::buffer data, int threads) {
     py::buffer_info info;
     auto v = view(data, info);

@@ -40,8 +40,11 @@ struct ZfpHeader {
   int dtype;                  // 0 = float32, 1 = float64
   std::vector<size_t> shape;  // C order
   size_t payload_off;
+  size_t chunk_blocks;        // blocks per independently coded chunk (v1: 4096)
 };
-std::vector<uint8_t> zfp_compress(const void* src, int dtype_code, const std::vector<size_t>& shape, int threads);
+// chunk_blocks 0 / 4096: version-1 container; any other value: version 2 (header carries it)
+std::vector<uint8_t> zfp_compress(const void* src, int dtype_code, const std::vector<size_t>& shape, int threads,
+                                  size_t chunk_blocks = 0);
 ZfpHeader zfp_header(const uint8_t* data, size_t n);
 void zfp_decompress(const uint8_t* data, size_t n, void* dst, int threads);
 

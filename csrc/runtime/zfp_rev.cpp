@@ -277,19 +277,25 @@ template <typename U> void decode_range(U* dst, const Geometry& g, size_t b0, si
 }
 
 static const uint32_t MAGIC = 0x5046'5A41u;   // "AZFP"
-static const size_t CHUNK_BLOCKS = 4096;
+static const size_t CHUNK_BLOCKS = 4096;       // version 1: fixed chunk of blocks
 
+// Version 2 adds a u64 `chunk_blocks` after the shape.  The GPU codec
+// (kernels/zfp_gpu.hip) writes chunk_blocks = 1: every block is its own
+// word-aligned bitstream, so blocks encode and decode in parallel threads;
+// this encoder produces the identical bytes for the same chunk_blocks.
 template <typename U>
-std::vector<uint8_t> compress_t(const U* src, const std::vector<size_t>& shape, int dtype_code, int threads) {
+std::vector<uint8_t> compress_t(const U* src, const std::vector<size_t>& shape, int dtype_code, int threads,
+                                size_t chunk_blocks) {
   Geometry g = make_geom(shape);
-  size_t nchunks = (g.nblocks + CHUNK_BLOCKS - 1) / CHUNK_BLOCKS;
+  const size_t CB = chunk_blocks ? chunk_blocks : CHUNK_BLOCKS;
+  size_t nchunks = (g.nblocks + CB - 1) / CB;
   std::vector<BitWriter> bws(nchunks);
   int nt = std::max(1, std::min<int>(threads, (int)nchunks));
   std::vector<std::thread> pool;
   for (int t = 0; t < nt; ++t) {
     pool.emplace_back([&, t]() {
       for (size_t c = t; c < nchunks; c += nt) {
-        size_t b0 = c * CHUNK_BLOCKS, b1 = std::min(g.nblocks, b0 + CHUNK_BLOCKS);
+        size_t b0 = c * CB, b1 = std::min(g.nblocks, b0 + CB);
         encode_range(src, g, b0, b1, bws[c]);
         bws[c].flush();
       }
@@ -301,11 +307,12 @@ std::vector<uint8_t> compress_t(const U* src, const std::vector<size_t>& shape, 
   auto put = [&](const void* p, size_t n) { const uint8_t* b = (const uint8_t*)p; out.insert(out.end(), b, b + n); };
   uint8_t hdr[8] = {0};
   std::memcpy(hdr, &MAGIC, 4);
-  hdr[4] = 1;
+  hdr[4] = CB == CHUNK_BLOCKS ? 1 : 2;
   hdr[5] = (uint8_t)dtype_code;
   hdr[6] = (uint8_t)shape.size();
   put(hdr, 8);
   for (size_t s : shape) { uint64_t v = s; put(&v, 8); }
+  if (hdr[4] == 2) { uint64_t v = CB; put(&v, 8); }
   uint64_t nc = nchunks;
   put(&nc, 8);
   for (auto& bw : bws) { uint64_t w = bw.words.size(); put(&w, 8); }
@@ -314,13 +321,14 @@ std::vector<uint8_t> compress_t(const U* src, const std::vector<size_t>& shape, 
 }
 
 template <typename U>
-void decompress_t(const uint8_t* data, size_t n, size_t off, const std::vector<size_t>& shape, U* dst, int threads) {
+void decompress_t(const uint8_t* data, size_t n, size_t off, const std::vector<size_t>& shape, U* dst, int threads,
+                  size_t CB) {
   Geometry g = make_geom(shape);
   if (n - off < 8) throw std::runtime_error("zfp: truncated");
   uint64_t nchunks;
   std::memcpy(&nchunks, data + off, 8);
   off += 8;
-  if (nchunks != (g.nblocks + CHUNK_BLOCKS - 1) / CHUNK_BLOCKS) throw std::runtime_error("zfp: chunk count mismatch");
+  if (CB == 0 || nchunks != (g.nblocks + CB - 1) / CB) throw std::runtime_error("zfp: chunk count mismatch");
   if (n - off < nchunks * 8) throw std::runtime_error("zfp: truncated chunk table");
   std::vector<uint64_t> words(nchunks), start(nchunks);
   std::memcpy(words.data(), data + off, nchunks * 8);
@@ -341,7 +349,7 @@ void decompress_t(const uint8_t* data, size_t n, size_t off, const std::vector<s
           std::vector<uint64_t> w(words[c]);
           std::memcpy(w.data(), data + start[c], words[c] * 8);
           BitReader br(w.data(), w.size());
-          size_t b0 = c * CHUNK_BLOCKS, b1 = std::min(g.nblocks, b0 + CHUNK_BLOCKS);
+          size_t b0 = c * CB, b1 = std::min(g.nblocks, b0 + CB);
           decode_range(dst, g, b0, b1, br);
         }
       } catch (const std::exception& e) {
@@ -356,9 +364,10 @@ void decompress_t(const uint8_t* data, size_t n, size_t off, const std::vector<s
 
 }  // namespace
 
-std::vector<uint8_t> zfp_compress(const void* src, int dtype_code, const std::vector<size_t>& shape, int threads) {
-  if (dtype_code == 0) return compress_t<uint32_t>((const uint32_t*)src, shape, 0, threads);
-  if (dtype_code == 1) return compress_t<uint64_t>((const uint64_t*)src, shape, 1, threads);
+std::vector<uint8_t> zfp_compress(const void* src, int dtype_code, const std::vector<size_t>& shape, int threads,
+                                  size_t chunk_blocks) {
+  if (dtype_code == 0) return compress_t<uint32_t>((const uint32_t*)src, shape, 0, threads, chunk_blocks);
+  if (dtype_code == 1) return compress_t<uint64_t>((const uint64_t*)src, shape, 1, threads, chunk_blocks);
   throw std::runtime_error("zfp: dtype must be float32 (0) or float64 (1)");
 }
 
@@ -377,13 +386,24 @@ ZfpHeader zfp_header(const uint8_t* data, size_t n) {
     h.shape.push_back((size_t)v);
   }
   h.payload_off = 8 + (size_t)nd * 8;
+  h.chunk_blocks = CHUNK_BLOCKS;
+  if (data[4] == 2) {
+    if (n < h.payload_off + 8) throw std::runtime_error("zfp: bad header");
+    uint64_t v;
+    std::memcpy(&v, data + h.payload_off, 8);
+    h.chunk_blocks = (size_t)v;
+    h.payload_off += 8;
+  } else if (data[4] != 1) {
+    throw std::runtime_error("zfp: unknown container version");
+  }
   return h;
 }
 
 void zfp_decompress(const uint8_t* data, size_t n, void* dst, int threads) {
   ZfpHeader h = zfp_header(data, n);
-  if (h.dtype == 0) decompress_t<uint32_t>(data, n, h.payload_off, h.shape, (uint32_t*)dst, threads);
-  else if (h.dtype == 1) decompress_t<uint64_t>(data, n, h.payload_off, h.shape, (uint64_t*)dst, threads);
+  if (h.dtype == 0) decompress_t<uint32_t>(data, n, h.payload_off, h.shape, (uint32_t*)dst, threads, h.chunk_blocks);
+  else if (h.dtype == 1)
+    decompress_t<uint64_t>(data, n, h.payload_off, h.shape, (uint64_t*)dst, threads, h.chunk_blocks);
   else throw std::runtime_error("zfp: bad dtype");
 }
 

@@ -70,3 +70,46 @@ def test_gpu_lz4_decoder_reads_host_frames_with_gpu_blocks(mods):
         c.decompress(frame, y)
         torch.cuda.synchronize()
         assert torch.equal(y.view(torch.int16), x.view(torch.int16)), name
+
+
+@pytest.mark.parametrize("shape", [(13,), (6, 10), (3, 9, 10), (4, 7, 7, 64), (2, 3, 5, 6, 8)])
+def test_gpu_zfp_bitexact_with_host_and_lossless(shape):
+    """GPU zfp (csrc/kernels/zfp_gpu.hip) writes the host codec's v2 container
+    byte for byte (chunk_blocks=1) and decodes losslessly, specials included."""
+    import numpy as np
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.gpu_zfp import GpuZFP
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.native import runtime
+    rng = np.random.default_rng(len(shape))
+    a = rng.standard_normal(shape).astype(np.float32).reshape(-1)
+    a[:5] = [np.inf, -np.inf, -0.0, 1e-42, np.nan]
+    a[5:50] = np.maximum(a[5:50], 0)
+    a = a.reshape(shape)
+    t = torch.from_numpy(a).cuda()
+    z = GpuZFP(shape)
+    z.compress(t)
+    c = z.container()
+    host = runtime().zfp_compress(a.reshape(-1 if a.ndim == 0 else a.shape) if a.ndim <= 4
+                                  else a.reshape((-1,) + shape[-3:]), 4, 1)
+    assert c == host
+    out = torch.empty_like(t)
+    z.decompress(c, out)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == a.tobytes()
+
+
+def test_gpu_zfp_wire_codec_round_trip_and_host_interop(mods):
+    wire, rt = mods
+    t = torch.randn(8, 14, 14, 32, device="cuda").relu()
+    enc, dec = wire.WireCodec("zfp", t), wire.WireCodec("zfp", t)
+    enc.encode(t)
+    n = enc.nbytes()
+    dec.wire[:n].copy_(enc.wire[:n])
+    out = torch.empty_like(t)
+    dec.decode(n, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, t)
+    host = wire.WireCodec("zfp", t.cpu())
+    host.wire[:n].copy_(enc.wire[:n].cpu())
+    o2 = torch.empty_like(t.cpu())
+    host.decode(n, o2)
+    assert torch.equal(o2, t.cpu())

@@ -140,3 +140,38 @@ def test_node_state_api():
     assert [e.value for e in StateEnum] == [0, 1, 2, 3]
     ns.state = StateEnum.BUSY
     assert ns.record()["state"] == "BUSY"
+
+
+@pytest.mark.parametrize("chunk_blocks", [0, 1, 5])
+@pytest.mark.parametrize("shape", [(7,), (5, 9), (3, 6, 10), (2, 5, 7, 9), (2, 2, 3, 5, 4)])
+def test_zfp_container_versions_round_trip(shape, chunk_blocks):
+    """zfp v1 (4096-block chunks) and v2 (chunk_blocks in the header, the GPU
+    codec's layout with chunk_blocks=1) are lossless on any float32 data,
+    including inf / nan / -0 / denormals."""
+    rng = np.random.default_rng(len(shape) * 7 + chunk_blocks)
+    a = rng.standard_normal(shape).astype(np.float32).reshape(-1)
+    a[:4] = [np.inf, -np.inf, -0.0, 1e-42][: min(4, a.size)]
+    if a.size > 5:
+        a[5] = np.nan
+    a = a.reshape(shape)
+    if a.ndim > 4:
+        a = a.reshape((-1,) + shape[-3:])
+    rt = runtime()
+    c = rt.zfp_compress(a, 4, chunk_blocks)
+    dt, shp, off, cb = rt.zfp_info(c)
+    assert tuple(shp) == a.shape and cb == (chunk_blocks or 4096)
+    b = rt.zfp_decompress(c, 4)
+    assert b.tobytes() == a.tobytes()
+
+
+def test_zfp_wire_codec_cpu_round_trip():
+    import torch
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.wire import WireCodec
+    t = torch.randn(2, 6, 5, 8)
+    enc, dec = WireCodec("zfp", t), WireCodec("zfp", t)
+    enc.encode(t)
+    n = enc.nbytes()
+    dec.wire[:n].copy_(enc.wire[:n])
+    out = torch.empty_like(t)
+    dec.decode(n, out)
+    assert torch.equal(out, t)

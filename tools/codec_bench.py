@@ -18,6 +18,7 @@ import torch  # noqa: E402
 
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd import codec as C  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.gpu_lz4 import GpuLZ4  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.gpu_zfp import GpuZFP  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.codec.gpu_zvc import GpuZVC  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet, init_weights  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.native import runtime  # noqa: E402
@@ -67,6 +68,20 @@ def main():
         t0 = time.perf_counter()
         zf = C.encode(f32, "zfp+lz4")
         t_zfp = time.perf_counter() - t0
+        # the reference's zfp (reversible) on the GPU side stream, fp32 activations
+        t32 = t.float().contiguous()
+        gz = GpuZFP(tuple(t32.shape))
+        gz.compress(t32)
+        zc_bytes = gz.container()
+        exact = zc_bytes == rt.zfp_compress(f32, 8, 1)
+        t_gzfp = gpu_time(lambda: (gz.compress(t32), gz.done.synchronize()), reps=5)
+        back = torch.empty_like(t32)
+        t_gzfp_dec = gpu_time(lambda: gz.decompress(zc_bytes, back), reps=3)
+        if not torch.equal(back, t32):
+            raise RuntimeError(f"GPU zfp round trip mismatch on {name}")
+        t0 = time.perf_counter()
+        rt.zfp_compress(f32, 8)
+        t_hzfp = time.perf_counter() - t0
         zc = GpuZVC(t.numel(), 2)
         zc.compress(t)
         zs = zc.stream_bytes()
@@ -84,12 +99,17 @@ def main():
                      "gpu_lz4_ratio": nbytes / len(frame), "gpu_lz4_GBps": nbytes / t_gpu / 1e9,
                      "host_lz4_ratio": nbytes / len(hf), "host_lz4_GBps": nbytes / t_host / 1e9,
                      "zfp_lz4_ratio_vs_bf16": nbytes / len(zf), "zfp_lz4_GBps": f32.nbytes / t_zfp / 1e9,
+                     "gpu_zfp_ratio_fp32": f32.nbytes / len(zc_bytes), "gpu_zfp_GBps": f32.nbytes / t_gzfp / 1e9,
+                     "gpu_zfp_dec_GBps_incl_h2d": f32.nbytes / t_gzfp_dec / 1e9,
+                     "gpu_zfp_bitexact_with_host": bool(exact), "host_zfp_GBps": f32.nbytes / t_hzfp / 1e9,
                      "fwd_ms": t_fwd * 1e3, "fwd_plus_side_encode_ms": t_both * 1e3})
     for r in rows:
         print(f"{r['tensor']:18s} {r['mbytes']:7.1f} MB | GPU zvc x{r['gpu_zvc_ratio']:.2f} {r['gpu_zvc_GBps']:7.1f} GB/s"
               f" | GPU lz4 x{r['gpu_lz4_ratio']:.2f} {r['gpu_lz4_GBps']:7.1f} GB/s"
               f" | host lz4 x{r['host_lz4_ratio']:.2f} {r['host_lz4_GBps']:5.2f} GB/s"
               f" | zfp+lz4 x{r['zfp_lz4_ratio_vs_bf16']:.2f} {r['zfp_lz4_GBps']:5.2f} GB/s"
+              f" | GPU zfp(fp32) x{r['gpu_zfp_ratio_fp32']:.2f} {r['gpu_zfp_GBps']:6.1f} GB/s"
+              f" (host {r['host_zfp_GBps']:.2f}, exact={r['gpu_zfp_bitexact_with_host']})"
               f" | fwd {r['fwd_ms']:.3f} ms, fwd||encode {r['fwd_plus_side_encode_ms']:.3f} ms")
     if a.json:
         with open(a.json, "w") as f:

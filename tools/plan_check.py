@@ -54,16 +54,20 @@ def main():
     ap.add_argument("--stages", default="2,4,8")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--analytic", action="store_true", help="ignore the calibration table")
+    ap.add_argument("--objective", default="compute", choices=["compute", "throughput"],
+                    help="planner objective (compute: balance the per-stage compute this tool measures)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     g = build_model(a.model)
     w = init_weights(g, 0)
     calibrated = (not a.analytic) and load_calibration(g, a.batch, a.dtype) is not None
-    out = {"model": a.model, "batch": a.batch, "dtype": a.dtype, "calibrated": calibrated, "plans": []}
+    out = {"model": a.model, "batch": a.batch, "dtype": a.dtype, "calibrated": calibrated,
+           "objective": a.objective, "plans": []}
     full_ms = time_slice(g, w, a.batch, a.dtype)
     out["unsliced_ms"] = full_ms
     for k in [int(v) for v in a.stages.split(",") if v]:
-        cuts, est = plan_cuts(g, k, batch=a.batch, precision=a.dtype, calibrated=not a.analytic)
+        cuts, est = plan_cuts(g, k, batch=a.batch, precision=a.dtype, calibrated=not a.analytic,
+                              objective=a.objective)
         meas = [time_slice(subgraph(g, s), w, a.batch, a.dtype) for s in partition(g, cuts)]
         ideal = sum(meas) / k
         rec = {"stages": k, "part_at": cuts, "est_ms": [round(t * 1e3, 4) for t in est],
