@@ -56,9 +56,8 @@ def traverse_improved(model, name: str, start: str, part_name: str, inpt: Option
             frontier.append(name)
         tensor_cache[name] = name
         return name
-    stack = []
-    for prev in get_previous(g, name):
-        stack.append(traverse_improved(g, prev, start, part_name, inpt, tensor_cache, strict, frontier))
+    for prev in get_previous(g, name):            # memoised DFS towards `start` (src/dag_util.py:23-40)
+        traverse_improved(g, prev, start, part_name, inpt, tensor_cache, strict, frontier)
     tensor_cache[name] = name
     return name
 
@@ -77,8 +76,6 @@ def construct_model(model, start: str, end: str, part_name: str = "part_begin", 
         for i in g.layers[n].inputs:
             if i not in own and i not in inputs:
                 inputs.append(i)
-    if start == g.input and g.input not in own:
-        pass
     if strict and inputs != [start]:
         raise RuntimeError(f"cut {start!r} -> {end!r} needs frontier {inputs}, not a single tensor")
     if end == start:

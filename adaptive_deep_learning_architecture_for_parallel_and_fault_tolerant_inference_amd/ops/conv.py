@@ -397,3 +397,63 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
                                N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.K, pc.Kpad, int(relu),
                                max(1, int(ksplit)), int(cfg), stream_handle(stream))
     return out
+
+
+# ------------------------------------------------------- fused bottleneck
+# One launch per ResNet bottleneck block of stage 2 (csrc/kernels/bottleneck.hip):
+# 1x1 (CIN -> 64) -> 3x3 (64 -> 64) -> 1x1 (64 -> 256) + identity / projection
+# shortcut, BN folded, over 8x8 output tiles held in LDS.
+def pack_fragments(bm: np.ndarray) -> np.ndarray:
+    """[N][K] fp32 -> bf16-ready fp32 array in MFMA 16x16x32 B-fragment order:
+    (n-frag, k-step, lane = (k-chunk << 4) | row, 8 k values), so each wave
+    loads one fragment as a single coalesced 1 KiB read."""
+    N, K = bm.shape
+    if N % 16 or K % 32:
+        raise ValueError(f"fragment packing needs N % 16 == 0 and K % 32 == 0, got {bm.shape}")
+    return np.ascontiguousarray(bm.reshape(N // 16, 16, K // 32, 4, 8).transpose(0, 2, 3, 1, 4)).reshape(-1)
+
+
+@dataclass
+class PackedBottleneck:
+    w1: torch.Tensor
+    w2: torch.Tensor
+    w3: torch.Tensor
+    b1: torch.Tensor
+    b2: torch.Tensor
+    b3: torch.Tensor
+    cin: int
+    proj: bool
+
+
+def pack_bottleneck(k1, b1, k2, b2, k3, b3, kp=None, bp=None, device="cuda") -> PackedBottleneck:
+    """HWIO kernels (BN folded) of the three convs [+ the projection shortcut]."""
+    cin = k1.shape[2]
+    if k1.shape[:2] != (1, 1) or k1.shape[3] != 64 or k2.shape != (3, 3, 64, 64) or k3.shape != (1, 1, 64, 256):
+        raise ValueError("fused bottleneck: expects 1x1 CIN->64, 3x3 64->64, 1x1 64->256")
+    if (kp is None) != (cin == 256) or (kp is not None and kp.shape != (1, 1, 64, 256)):
+        raise ValueError("fused bottleneck: identity needs CIN 256, projection needs CIN 64 and a 64->256 1x1")
+    w3 = k3[0, 0].T                                       # [256][64]
+    bias3 = np.asarray(b3, np.float64)
+    if kp is not None:
+        w3 = np.concatenate([w3, kp[0, 0].T], axis=1)     # K = [y2 | x]: the projection rides the last GEMM
+        bias3 = bias3 + np.asarray(bp, np.float64)
+
+    def dev(a, dt=torch.bfloat16):
+        return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device=device, dtype=dt).contiguous()
+    return PackedBottleneck(
+        w1=dev(pack_fragments(k1[0, 0].T)), w2=dev(pack_fragments(k2.transpose(3, 0, 1, 2).reshape(64, 576))),
+        w3=dev(pack_fragments(w3)), b1=dev(b1, torch.float32), b2=dev(b2, torch.float32),
+        b3=dev(bias3, torch.float32), cin=cin, proj=kp is not None)
+
+
+def bottleneck_forward(x: torch.Tensor, pb: PackedBottleneck, out: torch.Tensor, stream=None) -> torch.Tensor:
+    if x.dtype != torch.bfloat16 or out.dtype != torch.bfloat16 or not x.is_contiguous() or not out.is_contiguous():
+        raise ValueError("fused bottleneck: contiguous bf16 NHWC in and out")
+    B, H, W, C = x.shape
+    if C != pb.cin or H % 8 or W % 8:
+        raise ValueError(f"fused bottleneck: input {tuple(x.shape)} (needs {pb.cin} channels, H, W multiples of 8)")
+    if tuple(out.shape) != (B, H, W, 256):
+        raise ValueError(f"fused bottleneck: output {tuple(out.shape)} != {(B, H, W, 256)}")
+    kernels().bottleneck_forward(ptr(x), ptr(pb.w1), ptr(pb.w2), ptr(pb.w3), ptr(pb.b1), ptr(pb.b2), ptr(pb.b3),
+                                 ptr(out), B, H, W, pb.cin, bool(pb.proj), stream_handle(stream))
+    return out

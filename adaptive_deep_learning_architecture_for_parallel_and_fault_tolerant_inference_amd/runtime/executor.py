@@ -150,6 +150,15 @@ class SliceExecutor:
                 pc = conv_ops.pack_conv(kf, bf, p["stride"], p["pads"], dev, cin_pad=cin_pad)
                 pc.n_split = n_split
                 self.packed[i] = pc
+            elif st.kind == "bottleneck":
+                p = st.p
+                k1, b1 = self._folded(weights, p["c1"])
+                k2, b2 = self._folded(weights, p["c2"])
+                k3, b3 = self._folded(weights, p["c3"])
+                kp = bp = None
+                if p["proj"] is not None:
+                    kp, bp = self._folded(weights, p["proj"])
+                self.packed[i] = conv_ops.pack_bottleneck(k1, b1, k2, b2, k3, b3, kp, bp, device=dev)
             elif st.kind == "stem":
                 p = st.p
                 k = weights[f"{p['conv']}/kernel"]
@@ -585,6 +594,8 @@ class SliceExecutor:
                 self._launch_f32(i, st, b, stream, ws)
             elif k == "pack":
                 E.input_pack(b[st.ins[0]], b[st.out], stream=stream)
+            elif k == "bottleneck":
+                conv_ops.bottleneck_forward(b[st.ins[0]], self.packed[i], b[st.out], stream=stream)
             elif k == "stem":
                 conv_ops.stem_forward(b[st.ins[0]], self.packed[i], b[st.out], pool=st.p["pool"],
                                       pool_pad=st.p["pool_pad"], stream=stream)

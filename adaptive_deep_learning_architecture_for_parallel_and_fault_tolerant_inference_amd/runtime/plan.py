@@ -317,11 +317,71 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
         raise RuntimeError(f"plan does not produce outputs {missing}")
     if fp32:
         return steps
+    if os.environ.get("ADAPT_FUSED_BOTTLENECK", "1") == "1":
+        steps = fuse_bottlenecks(g, steps, outset)
     if os.environ.get("ADAPT_NO_STEM", "0") != "1":
         steps = _fuse_stem(g, steps, outset)
     if os.environ.get("ADAPT_NO_SIBLINGS", "0") != "1":
         steps = merge_siblings(steps)
     return steps
+
+
+def fuse_bottlenecks(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
+    """1x1 (->64, ReLU) -> 3x3 s1 p1 (64->64, ReLU) -> 1x1 (64->256) + shortcut + ReLU
+    ==> one ``bottleneck`` step (csrc/kernels/bottleneck.hip) when the block's
+    input is H x W x 256 (identity shortcut) or H x W x 64 with a stride-1 1x1
+    projection shortcut, H and W multiples of 8, and no intermediate tensor is
+    needed elsewhere (a cut inside the block keeps it unfused).  ResNet
+    stage 2: three launches and two 51 MB round trips per block become one."""
+    def users(t: str) -> List[int]:
+        return [j for j, st in enumerate(steps) if t in st.ins]
+
+    def conv(j, k, filters, relu, res):
+        st = steps[j]
+        p = st.p
+        return (st.kind == "conv" and p.get("kernel") == k and p.get("stride") == 1 and p.get("filters") == filters
+                and p.get("relu") == relu and bool(p.get("residual")) == res and not p.get("packed_input")
+                and not p.get("sibling"))
+
+    drop: Set[int] = set()
+    repl: Dict[int, Step] = {}
+    for j3, s3 in enumerate(steps):
+        if j3 in drop or not conv(j3, (1, 1), 256, 1, True):
+            continue
+        y2, sc = s3.ins[0], s3.ins[1]
+        u2 = [j for j, st in enumerate(steps) if st.out == y2]
+        if len(u2) != 1 or y2 in outset or users(y2) != [j3] or not conv(u2[0], (3, 3), 64, 1, False):
+            continue
+        j2 = u2[0]
+        if steps[j2].p["pads"] != ((1, 1), (1, 1)):
+            continue
+        y1 = steps[j2].ins[0]
+        u1 = [j for j, st in enumerate(steps) if st.out == y1]
+        if len(u1) != 1 or y1 in outset or users(y1) != [j2] or not conv(u1[0], (1, 1), 64, 1, False):
+            continue
+        j1 = u1[0]
+        x = steps[j1].ins[0]
+        xl = g.layers[x.split("#")[0]]
+        if len(xl.out_shape) != 3 or xl.out_shape[0] % 8 or xl.out_shape[1] % 8:
+            continue
+        proj = None
+        if sc == x and xl.out_shape[2] == 256:
+            pass                                          # identity shortcut
+        elif xl.out_shape[2] == 64:
+            up = [j for j, st in enumerate(steps) if st.out == sc]
+            if (len(up) != 1 or sc in outset or users(sc) != [j3] or not conv(up[0], (1, 1), 256, 0, False)
+                    or steps[up[0]].ins[0] != x):
+                continue
+            proj = up[0]
+        else:
+            continue
+        group = [j1, j2, j3] + ([proj] if proj is not None else [])
+        covers = [c for jj in sorted(group) for c in steps[jj].covers]
+        p = {"c1": steps[j1].p, "c2": steps[j2].p, "c3": steps[j3].p,
+             "proj": steps[proj].p if proj is not None else None, "cin": xl.out_shape[2]}
+        repl[j3] = Step("bottleneck", s3.out, [x], covers, p)
+        drop.update(jj for jj in group if jj != j3)
+    return [repl.get(j, st) for j, st in enumerate(steps) if j not in drop]
 
 
 def merge_siblings(steps: List[Step]) -> List[Step]:

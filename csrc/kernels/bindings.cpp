@@ -220,6 +220,12 @@ PYBIND11_MODULE(_C, m) {
                                     P<uint64_t>(total), P<float>(dst), S(s)),
           "zfp_gpu_decompress");
   });
+  m.def("bottleneck_forward", [](u64 x, u64 w1, u64 w2, u64 w3, u64 b1, u64 b2, u64 b3, u64 out, int B, int H, int W,
+                                 int cin, bool proj, u64 s) {
+    adapt::BottleneckParams p{P<const bf16>(x), P<const bf16>(w1), P<const bf16>(w2), P<const bf16>(w3),
+                              P<const float>(b1), P<const float>(b2), P<const float>(b3), P<bf16>(out), B, H, W};
+    check(adapt::bottleneck_forward(p, cin, proj, S(s)), "bottleneck_forward");
+  });
   m.def("ingest_u8", [](u64 x, u64 y, size_t n, int C, int reverse, std::vector<float> scale,
                         std::vector<float> shift, u64 s) {
     if ((int)scale.size() < C || (int)shift.size() < C) throw std::runtime_error("ingest_u8: scale/shift per channel");

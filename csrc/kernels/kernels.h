@@ -118,6 +118,19 @@ hipError_t zfp_gpu_compress(const float* src, const int64_t* shape, int nd, uint
                             uint64_t* out, uint64_t* total, hipStream_t s);
 hipError_t zfp_gpu_decompress(const uint64_t* table, const int64_t* shape, int nd, uint64_t* offs, uint64_t* total,
                               float* dst, hipStream_t s);
+// fused ResNet bottleneck block (bottleneck.hip): 1x1 -> 3x3 -> 1x1 + shortcut, 8x8 tiles in LDS
+struct BottleneckParams {
+  const bf16* x;
+  const bf16* w1;
+  const bf16* w2;
+  const bf16* w3;
+  const float* b1;
+  const float* b2;
+  const float* b3;
+  bf16* out;
+  int B, H, W;
+};
+hipError_t bottleneck_forward(const BottleneckParams& p, int cin, bool proj, hipStream_t s);
 // serving ingest (ingest.hip): uint8 NHWC -> fp32, y = x[rev(c)] * scale[c] + shift[c] (host scale/shift, C <= 4)
 hipError_t ingest_u8(const uint8_t* x, float* y, size_t n, int C, int reverse, const float* scale,
                      const float* shift, hipStream_t s);

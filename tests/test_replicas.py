@@ -196,3 +196,40 @@ def test_uint8_ingest_shm_caffe_preprocess(tiny):
         d.shutdown(stop_workers=True)
         for nd in nodes:
             nd.stop()
+
+
+def test_link_error_report_triggers_replan_without_a_death(tiny):
+    """A stage that publishes LINK_ERROR for the serving epoch (what a broken hop
+    does, node.py `_fail`) makes the dispatcher re-form that replica at once; no
+    process dies, so neither the session EOF nor the lease can be the trigger."""
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, ordered=True, batch=1, weight_codec="lz4",
+              min_workers=2, replicas=1)
+    d.membership_server.start()
+    nodes = _nodes(d, 2, "l")
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, ["conv3_block1_out"], inq, outq), daemon=True).start()
+        assert _wait(lambda: d.pipeline is not None)
+        e0 = d.pipeline.epoch
+        x = np.random.default_rng(6).standard_normal((1, 32, 32, 3)).astype(np.float32)
+        inq.put(x)
+        outq.get(timeout=60)
+        nd = next(n for n in nodes if n.node_id == d.pipeline.workers[1])
+        rt = nd.runtime
+        rt.error = "recv: injected broken hop"
+        t0 = time.time()
+        nd.report_failure(rt, "LINK_ERROR")
+        assert _wait(lambda: d.pipeline is not None and d.pipeline.epoch > e0, timeout=10)
+        assert time.time() - t0 < 1.5                      # well under the 2 s lease TTL of these nodes
+        assert any("reports a broken hop" in e for _, e in d.events)
+        inq.put(x)
+        np.testing.assert_allclose(outq.get(timeout=60), tiny.predict(x, device="cpu"), rtol=1e-4, atol=1e-5)
+        # a late report about the retired epoch is ignored
+        n_rec = len(d.recoveries)
+        nd.report_failure(rt, "LINK_ERROR")
+        time.sleep(0.3)
+        assert len(d.recoveries) == n_rec
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
