@@ -95,7 +95,8 @@ def test_planner_balanced(r50):
     assert "conv3_block1_1_conv" not in articulation_points(r50)
 
 
-def test_plan_fuses_resnet(r50):
+def test_plan_fuses_resnet(r50, monkeypatch):
+    monkeypatch.setenv("ADAPT_FUSED_BOTTLENECK", "0")      # per-conv plan; the fused blocks are tested below
     steps = compile_plan(r50)
     kinds = [s.kind for s in steps]
     assert kinds.count("bn") == 0 and kinds.count("add") == 0
@@ -133,7 +134,22 @@ def test_plan_stem_respects_cuts(r50, monkeypatch):
     assert [x.kind for x in compile_plan(subgraph(r50, s[0]))] == ["pack", "conv"]
     monkeypatch.setenv("ADAPT_NO_STEM", "1")
     kinds = [x.kind for x in compile_plan(r50)]
-    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds.count("conv") == 49   # 53 convs, 4 sibling pairs merged
+    # 53 convs, 4 sibling pairs merged, the 3 stage-2 blocks (9 conv steps) fused into bottleneck steps
+    assert kinds[:3] == ["pack", "conv", "maxpool"] and kinds.count("conv") == 40 and kinds.count("bottleneck") == 3
+
+
+def test_plan_fused_bottlenecks(r50):
+    steps = compile_plan(r50)
+    kinds = [s.kind for s in steps]
+    assert kinds[:4] == ["stem", "bottleneck", "bottleneck", "bottleneck"] and kinds.count("conv") == 39
+    b = [s for s in steps if s.kind == "bottleneck"]
+    assert [s.out for s in b] == [f"conv2_block{i}_out" for i in (1, 2, 3)]
+    assert b[0].p["proj"] and not b[1].p["proj"] and not b[2].p["proj"]
+    assert b[0].ins == ["pool1_pool"] and b[1].ins == ["conv2_block1_out"]
+    # a cut inside block 2 leaves that block on the per-conv path
+    s = partition(r50, ["conv2_block2_2_relu"])
+    k0 = [x.kind for x in compile_plan(subgraph(r50, s[0]))]
+    assert k0.count("bottleneck") == 1 and k0.count("conv") == 2
 
 
 def test_plan_unfused_at_cut(r50):
