@@ -70,30 +70,47 @@ struct GldsShape {
   static constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32>
+// ABL: ablation switches for tools/conv_ablate.hip (0 in every production
+// instance): 1 = no MFMA, 2 = no LDS-DMA, 4 = every K tile re-fetches the
+// block's first one (L2-hot operands), 8 = no fragment ds_reads, 16 = no K
+// loop at all (launch + prologue + epilogue only).
+//
+// NL > 0: NL dedicated loader waves beside the WM x WN compute waves.  The
+// ablation (tools/conv_ablate.hip, profiles/r2/conv_ablate.txt) showed the
+// LDS-DMA feed and the MFMA work of one K tile SERIALISE when the compute
+// waves issue the pieces themselves (a piece's issue stalls its wave while the
+// CU's address path is busy, and the MFMAs behind it in program order wait):
+// base ~= DMA-only + compute-only.  Loader waves only issue pieces and wait for
+// them (counted vmcnt, then the shared barrier); compute waves only ds_read and
+// MFMA, so the two overlap.
+template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32, int ABL = 0, int NL = 0>
 __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __restrict__ zero, char* smem,
                                           int tile, int kt0, int kt1, int split_idx, const SkSeg& sk) {
   using S = GldsShape<BM, BN, WM, WN, STAGES>;
-  constexpr int NW = S::NW, NT = S::NT;
+  constexpr int NW = S::NW;                  // compute waves
+  constexpr int NT = (NW + NL) * 64;         // all threads of the block
+  constexpr int NWI = NL > 0 ? NL : NW;      // waves that issue the LDS-DMA pieces
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);   // glds instructions per wave per tile
+  constexpr int A_INS = BM / (8 * NWI), B_INS = BN / (8 * NWI);   // glds instructions per issuing wave per tile
   constexpr int LPW = A_INS + B_INS;
   constexpr int TILE_A = BM * 128, STAGE_BYTES = S::STAGE_BYTES;
   constexpr int EPI_LD = BN + 4;
-  static_assert((NW == 4 || NW == 8 || NW == 16) && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN,
+  static_assert((NW == 4 || NW == 8 || NW == 16) && A_INS * 8 * NWI == BM && B_INS * 8 * NWI == BN,
                 "waves / tile split");
   static_assert(STAGES >= 2 && S::LDS_BYTES + 16 <= 160 * 1024, "stages");
   static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
+  const bool loader = NL > 0 && wave >= NW;  // wave-uniform
+  const int iwave = NL > 0 ? (loader ? wave - NW : 0) : wave;   // index among the issuing waves
+  const int wm = (loader ? 0 : wave) / WN, wn = (loader ? 0 : wave) % WN;
 
   const int tilesN = (p.N + BN - 1) / BN;
   const int tm = tile / tilesN, tn = tile % tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = kt1 > kt0 ? kt1 - kt0 : 0;
+  const int nk = (ABL & 16) ? 0 : (kt1 > kt0 ? kt1 - kt0 : 0);
 
   // ---- per-lane source bookkeeping (rows fixed over the K loop)
   //
@@ -111,7 +128,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
   const int ohw = p.OH * p.OW;
 #pragma unroll
   for (int i = 0; i < A_INS; ++i) {
-    const int r = (wave * A_INS + i) * 8 + lrow;        // tile row
+    const int r = (iwave * A_INS + i) * 8 + lrow;       // tile row
     const int m = m0 + r;
     const int c = pchunk ^ ((r >> 1) & 7);              // logical chunk this lane fetches
     a_ih0[i] = a_iw0[i] = 0;
@@ -135,7 +152,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
   const bf16* b_src[B_INS];
 #pragma unroll
   for (int i = 0; i < B_INS; ++i) {
-    const int r = (wave * B_INS + i) * 8 + lrow;
+    const int r = (iwave * B_INS + i) * 8 + lrow;
     b_src[i] = p.w + (size_t)(n0 + r) * p.Kpad + (pchunk ^ ((r >> 1) & 7)) * 8;
   }
   // issue cursor (wave-uniform): tap (kh, kw) and channel slice cc of the next tile to fetch
@@ -168,22 +185,22 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
   auto issue = [&](int slot) {
     char* sa = smem + slot * STAGE_BYTES;
     char* sb = sa + TILE_A;
-    const int kt = ck;
-    const bool live = kt < kt1;
+    const int kt = (ABL & 4) ? kt0 : ck;
+    const bool live = ck < kt1;
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) {
+    for (int i = 0; i < ((ABL & 2) ? 0 : A_INS); ++i) {
       const bf16* src;
       if (PURE) src = (live && a_ptr[i] != nullptr) ? a_ptr[i] + (size_t)kt * BK2 : zero;
       else src = (live && ((a_ok >> i) & 1u)) ? a_ptr[i] + tap_off + c_cc * BK2 : zero;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sa + (wave * A_INS + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sa + (iwave * A_INS + i) * 1024), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < B_INS; ++i) {
+    for (int i = 0; i < ((ABL & 2) ? 0 : B_INS); ++i) {
       const bf16* src = live ? b_src[i] + (size_t)kt * BK2 : zero;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (wave * B_INS + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (iwave * B_INS + i) * 1024), 16, 0, 0);
     }
     ++ck;
-    if (!PURE) {
+    if (!PURE && !(ABL & 4)) {
       const bool roll_c = ++c_cc == cpt;
       const bool roll_w = roll_c && c_kw + 1 == p.KW;
       c_cc = roll_c ? 0 : c_cc;
@@ -205,36 +222,63 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
   EpiRes<BM, BN, NT> rpre;
   const bool use_pre = sk.slot < 0 && p.ksplit == 1 && p.res != nullptr;
   if (use_pre) rpre.prefetch(p, m0, n0, tid, p.M);
+  if (NL == 0 || loader) {
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) issue(s);
+    for (int s = 0; s < STAGES - 1; ++s) issue(s);
+  }
 
   constexpr int MT = 2 * FM * FN;          // MFMAs per wave per K tile
   for (int t = 0; t < nk; ++t) {
-    // tile t must have landed; the STAGES-2 tiles issued after it stay in flight
-    wait_vm<(STAGES - 2) * LPW>();
+    // tile t must have landed (the issuing waves' counted wait + the barrier
+    // orders it for every reader); the STAGES-2 tiles issued after it stay in flight
+    if (NL == 0 || loader) wait_vm<(STAGES - 2) * LPW>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int nslot = (t + STAGES - 1) % STAGES;
-    if constexpr (!ILV) issue(nslot);
+    if constexpr (NL > 0) {
+      if (loader) {
+        issue(nslot);
+        continue;
+      }
+    } else if constexpr (!ILV) {
+      issue(nslot);
+    }
     const char* sa = smem + (t % STAGES) * STAGE_BYTES;
     const char* sb = sa + TILE_A;
     bf16x8 af[2][FM], bfr[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if constexpr (ABL & 8) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[ks][i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, ks * 4 + fq));
+        for (int i = 0; i < FM; ++i) af[ks][i] = (bf16x8){};
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[ks][j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, ks * 4 + fq));
+        for (int j = 0; j < FN; ++j) bfr[ks][j] = (bf16x8){};
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[ks][i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[ks][j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, ks * 4 + fq));
+      }
     }
+    if constexpr (ABL & 1) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[ks][i]));
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
-    if constexpr (ILV) {
+        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(bfr[ks][j]));
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (ILV && NL == 0) {
       // LDS-DMA pieces for tile t+STAGES-1 spread between this tile's MFMAs
       // (one wave per SIMD: a piece costs ~100 issue cycles that otherwise
       // serialise in front of the MFMA block)
@@ -256,14 +300,16 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
 
   // ---- epilogue (as conv_igemm.hip)
   float* epi = (float*)smem;
+  if (!loader) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = wn * TN + j * 16 + fr;
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * TN + j * 16 + fr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) epi[(wm * TM + i * 16 + fq * 4 + r) * EPI_LD + col] = acc[i][j][r];
-    }
+        for (int r = 0; r < 4; ++r) epi[(wm * TM + i * 16 + fq * 4 + r) * EPI_LD + col] = acc[i][j][r];
+      }
+  }
   __syncthreads();
   constexpr int CPR = BN / 8;
   constexpr int NCH = BM * CPR;
@@ -369,8 +415,8 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
 // (b) stream-K (p.ksplit < 0): the tiles x K-tiles iteration space is cut into
 // equal contiguous ranges of p.sk_iters, one per block, so ~200-tile problems
 // keep every CU busy instead of leaving a quarter of the chip idle.
-template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32>
-__global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
+template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32, int ABL = 0, int NL = 0>
+__global__ __launch_bounds__((WM * WN + NL) * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
   using S = GldsShape<BM, BN, WM, WN, STAGES>;
   __shared__ __attribute__((aligned(16))) char smem[S::LDS_BYTES + 16];
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -380,8 +426,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p
     const int kt_per = (kt + p.ksplit - 1) / p.ksplit;
     const int kt0 = blockIdx.y * kt_per;
     const int kt1 = min(kt, kt0 + kt_per);
-    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32>(p, zero, smem, tile, kt0, kt1, blockIdx.y,
-                                                          SkSeg{-1, 1, 0, 0});
+    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32, ABL, NL>(p, zero, smem, tile, kt0, kt1, blockIdx.y,
+                                                                   SkSeg{-1, 1, 0, 0});
     return;
   }
   const int g = blockIdx.x, iters = p.sk_iters;
@@ -397,7 +443,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_glds_kernel(ConvParams p
       const int g_first = (tile * kt) / iters, g_last = ((tile + 1) * kt - 1) / iters;
       sk = SkSeg{sk_slot(g, tile, kt, iters), g_last - g_first + 1, g - g_first, g_first};
     }
-    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32>(p, zero, smem, tile, kbeg, kend, 0, sk);
+    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32, ABL, NL>(p, zero, smem, tile, kbeg, kend, 0, sk);
     it += kend - kbeg;
     __syncthreads();   // the next segment's DMA reuses the epilogue's LDS
   }

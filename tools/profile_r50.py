@@ -5,10 +5,10 @@ and a PyTorch/MIOpen bf16 baseline on the same graph for comparison.
     python tools/profile_r50.py --batch 32 [--tune] [--baseline] [--model resnet50]
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -34,6 +34,32 @@ def time_fn(fn, reps=50, warm=5):
     return s.elapsed_time(e) / reps
 
 
+@contextlib.contextmanager
+def single_step(ex, i):
+    """Temporarily make step `i` the executor's whole plan (same buffers, same
+    packed weights and tuned config), so `ex._launch(0)` runs just that step."""
+    st = ex.steps[i]
+    saved = (ex.steps, ex.packed, ex.cfg, ex._logits, ex._dense_part, ex._gap_part, ex._side, ex.relay)
+    ex.steps = [st]
+    ex.packed = {0: saved[1][i]} if i in saved[1] else {}
+    ex.cfg = {0: saved[2][i]} if i in saved[2] else {}
+    ex._logits = {0: saved[3][i]} if i in saved[3] else {}
+    ex._dense_part = {0: saved[4][i]} if i in saved[4] else {}
+    ex._gap_part = {0: saved[5][i]} if i in saved[5] else {}
+    ex._side = {}
+    ex.relay = []
+    try:
+        yield st
+    finally:
+        ex.steps, ex.packed, ex.cfg, ex._logits, ex._dense_part, ex._gap_part, ex._side, ex.relay = saved
+
+
+def step_flop(g, st, batch):
+    """FLOPs of a plan step: 2 x MACs of every conv / dense layer it covers
+    (a fused bottleneck step covers three or four convs)."""
+    return 2 * batch * sum(g.layer_macs(c) for c in st.covers if g.layers[c].op in ("conv", "dwconv", "dense"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
@@ -55,22 +81,7 @@ def main():
     # time each step alone by swapping in a one-step plan (same buffers)
     per = []
     for i, st in enumerate(ex.steps):
-        saved = ex.steps
-        ex.steps = [st]
-        packed_saved, cfg_saved = ex.packed, ex.cfg
-        ex.packed = {0: packed_saved.get(i)} if i in packed_saved else {}
-        ex.cfg = {0: cfg_saved[i]} if i in cfg_saved else {}
-        logits_saved = ex._logits
-        ex._logits = {0: logits_saved[i]} if i in logits_saved else {}
-        dense_saved = ex._dense_part
-        ex._dense_part = {0: dense_saved[i]} if i in dense_saved else {}
-        gap_saved = ex._gap_part
-        ex._gap_part = {0: gap_saved[i]} if i in gap_saved else {}
-        side_saved = ex._side
-        ex._side = {}
-        relay_saved = ex.relay
-        ex.relay = []
-        try:
+        with single_step(ex, i):
             # capture 20 back-to-back launches of this one step in a hipGraph so the
             # number is device time, not Python launch overhead
             ex._launch(0)
@@ -80,18 +91,7 @@ def main():
                 for _ in range(20):
                     ex._launch(0)
             t = time_fn(lambda: gg.replay(), reps=5, warm=2) / 20
-        finally:
-            ex.steps, ex.packed, ex.cfg, ex._logits, ex.relay = saved, packed_saved, cfg_saved, logits_saved, relay_saved
-            ex._dense_part = dense_saved
-            ex._gap_part = gap_saved
-            ex._side = side_saved
-        flop = 0
-        if st.kind in ("conv", "dense"):
-            B, H, W, C, OH, OW, pc = ex._conv_geom(i)
-            flop = 2 * B * OH * OW * pc.cout * pc.kh * pc.kw * pc.cin
-        elif st.kind == "dwconv":
-            o = ex.bufs(0)[st.out]
-            flop = 2 * o.numel() * st.p["kernel"][0] * st.p["kernel"][1]
+        flop = step_flop(g, st, a.batch)
         total_flop += flop
         per.append({"i": i, "kind": st.kind, "out": st.out, "ms": round(t, 4),
                     "tflops": round(flop / t / 1e9, 1) if flop else None, "cfg": ex.cfg.get(i),
