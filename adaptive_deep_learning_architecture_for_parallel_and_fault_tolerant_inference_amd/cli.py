@@ -89,6 +89,9 @@ def cmd_serve(argv):
     ap.add_argument("--replicas", default=None, help="pipeline replicas: auto (live // stages) or N")
     ap.add_argument("--ingest", default="auto", choices=["auto", "tcp"],
                     help="auto: same-host shared-memory request slots; tcp: inline on the socket")
+    ap.add_argument("--links", default="auto", choices=["auto", "tcp"],
+                    help="auto: stage->stage hops between workers sharing /dev/shm carry shared-memory slots; "
+                         "tcp: inline on the socket")
     ap.add_argument("--uint8", action="store_true", help="send uint8 images (4x fewer bytes), preprocessed on the GPU")
     ap.add_argument("--preprocess", default="none", choices=["none", "caffe", "tf", "torch"],
                     help="Keras preprocess_input mode applied by stage 0 to uint8 requests")
@@ -102,7 +105,8 @@ def cmd_serve(argv):
               batch=cfg.batch, codec=cfg.codec, weight_codec=cfg.weight_codec, max_inflight=cfg.max_inflight,
               task_timeout=cfg.task_timeout, worker_wait=max(cfg.worker_wait, 60 if a.spawn else 0),
               elastic=cfg.elastic, ordered=cfg.ordered, transport=cfg.transport, min_workers=max(1, a.spawn),
-              replicas=cfg.replicas, ingest=a.ingest, preprocess=a.preprocess, precision=a.dtype)
+              replicas=cfg.replicas, ingest=a.ingest, preprocess=a.preprocess, precision=a.dtype,
+              links=a.links)
     d.membership_server.start()
     procs = []
     for i in range(a.spawn):

@@ -20,7 +20,7 @@ the data falls back to ``none`` for that message.
 from __future__ import annotations
 
 import struct
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -134,6 +134,15 @@ def decode(buf, threads: int = 4, copy: bool = True) -> np.ndarray:
         a = shm.view(raw[:cut].decode(), off, np_dt, shape, register_device=shm.REGISTER_DEVICE)
         return a.copy() if copy else a
     raise ValueError(f"unknown codec id {codec}")
+
+
+def shm_name(buf) -> Optional[str]:
+    """Segment name of a "shm" container (None for every other codec)."""
+    codec, _dt, _shape, off = _parse(buf)
+    if codec != CODECS["shm"]:
+        return None
+    raw = bytes(memoryview(buf)[off:])
+    return raw[:raw.index(b"\0")].decode()
 
 
 def is_bf16(buf) -> bool:

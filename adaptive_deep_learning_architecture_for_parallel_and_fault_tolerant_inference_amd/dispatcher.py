@@ -131,7 +131,7 @@ class DEFER:
                  transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
                  quarantine_s: float = 30.0, hb_timeout: float = 0.06, precision: str = "bf16",
-                 ingest: str = "auto", preprocess: str = "none") -> None:
+                 ingest: str = "auto", preprocess: str = "none", links: str = "auto") -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
         the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
         ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
@@ -144,7 +144,11 @@ class DEFER:
         ingest: "auto" = requests go through same-host shared memory to a local
         stage 0 (transport/shm.py; only a descriptor crosses the socket), "tcp" =
         always inline.  preprocess: Keras preprocess_input mode stage 0 applies on
-        the GPU to uint8 image requests ("none", "caffe", "tf", "torch")."""
+        the GPU to uint8 image requests ("none", "caffe", "tf", "torch").  links:
+        "auto" = a TCP stage -> stage hop between workers that share /dev/shm
+        (equal `shm_domain` in their membership records) carries the frontier
+        in page-locked shared-memory slots, only descriptors on the socket
+        (transport/shm.py LinkPool); "tcp" = always inline."""
         if transport not in ("tcp", "rccl", "gloo"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
@@ -174,6 +178,9 @@ class DEFER:
         self.precision = precision                  # worker compute: "bf16" or "fp32" (reference float32)
         self.prepare_delay = 1.0                    # s after an epoch forms before `prepare` hints go out
         self.preprocess = preprocess
+        if links not in ("auto", "tcp"):
+            raise ValueError(f"unknown links mode {links!r}")
+        self.links = links
         from .transport import shm as _shm
         self._shm = _shm.ShmPool() if ingest == "auto" and _shm.available() else None
         self.quarantine_s = quarantine_s
@@ -520,6 +527,9 @@ class DEFER:
                "next": nxt, "result_addr": [self._result_host(rec), self.result_port], "part_at": list(cuts),
                "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid,
                "precision": self.precision, "preprocess": self.preprocess}
+        if (nxt is not None and self.transport == "tcp" and self.links == "auto" and rec.get("shm_domain")
+                and rec.get("shm_domain") == recs[st + 1].get("shm_domain")):
+            cfg["link"] = "shm"
         if self.transport != "tcp":
             cfg["link_codec"] = self.link_codec
             cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",

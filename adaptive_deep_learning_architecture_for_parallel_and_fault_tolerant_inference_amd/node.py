@@ -37,6 +37,7 @@ import sys
 import threading
 import time
 import traceback
+import uuid
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -64,6 +65,15 @@ def get_local_ip() -> str:
     return ip
 
 
+class _Pending:
+    """A pipelined GPU micro-batch in the send queue: `msg`'s host tensors are
+    ready once `ev` has completed; `links` are its input's link slots."""
+    __slots__ = ("ev", "msg", "links")
+
+    def __init__(self, ev, msg, links):
+        self.ev, self.msg, self.links = ev, msg, links
+
+
 class StageRuntime:
     """One epoch's data plane on this node."""
 
@@ -80,10 +90,22 @@ class StageRuntime:
         if plot_dir:                          # the reference's per-worker plot_model (src/node.py:49)
             from .utils.plot import plot_model, slice_plot_name
             plot_model(g, slice_plot_name(plot_dir, node.node_id, self.epoch))
+        # "shm": the next stage shares this host's /dev/shm, so frontier tensors go
+        # device -> page-locked link slot and only descriptors cross the socket
+        # (transport/shm.py LinkPool); the TCP codec does not apply to such a hop
+        self.link = cfg.get("link", "tcp")
         # GPU stages with a GPU codec compress frontier tensors on a side HIP stream
         # while the next micro-batch computes (two buffer sets ping-pong)
-        self.gpu_codec = self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")
+        self.gpu_codec = (self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")
+                          and self.link != "shm")
         self.compute = node.stage_compute(cfg, g, weights)
+        self._linkpool = None
+        if self.link == "shm":
+            from .transport import shm
+            self._linkpool = shm.LinkPool(prefix=f"adapt-link-{os.getpid()}-e{self.epoch}-s{self.stage}-"
+                                                 f"{uuid.uuid4().hex[:6]}",
+                                          register_device=bool(getattr(self.compute, "gpu", False)))
+        self._attached_links: set = set()     # upstream link segments this epoch mapped
         if self.gpu_codec:
             self._init_gpu_codec()
         self.inq: "queue.Queue" = queue.Queue(maxsize=int(cfg.get("queue", 4)))
@@ -145,6 +167,8 @@ class StageRuntime:
             while not self.stop.is_set():
                 m = recv_message(self.upstream, self.node.state.chunk_size,
                                  keep_encoded=("zvc", "lz4") if self.gpu_codec else ())
+                if m is not None and m.links:
+                    self._attached_links.update(m.links)
                 if m is None:
                     if not self.stop.is_set():
                         # clean EOF inside a live epoch: the upstream process died
@@ -152,6 +176,7 @@ class StageRuntime:
                         raise ConnectionError("upstream closed the link")
                     break
                 if m.epoch != self.epoch:
+                    self._release_links(m.links)
                     continue                     # stale micro-batch from an older epoch
                 while not self.stop.is_set():
                     try:
@@ -161,6 +186,29 @@ class StageRuntime:
                         continue
         except Exception as e:  # noqa: BLE001 - any transport error ends the epoch
             self._fail("recv", e)
+
+    @staticmethod
+    def _release_links(names) -> None:
+        if names:
+            from .transport import shm
+            for n in names:
+                shm.release(n)
+
+    def _link_slot(self, shape, dtype):
+        """`StageCompute.submit` out_slots: a page-locked link slot and its descriptor."""
+        import numpy as np
+        import torch
+        from .transport.shm import ShmRef
+        bf16 = dtype == torch.bfloat16
+        np_dt = np.dtype(np.uint16) if bf16 else np.dtype(str(dtype).replace("torch.", ""))
+        n = 1
+        for v in shape:
+            n *= int(v)
+        slot = self._linkpool.acquire(n * np_dt.itemsize, self.stop)
+        host = torch.from_numpy(slot.view(np_dt, shape))
+        if bf16:
+            host = host.view(torch.bfloat16)
+        return host, ShmRef(slot, np_dt, shape, bf16=bf16)
 
     # ------------------------------------------------ GPU side-stream codec
     def _init_gpu_codec(self) -> None:
@@ -283,15 +331,20 @@ class StageRuntime:
                         break
                     if self.gpu_codec:
                         out = self._compute_gpu(m)
+                        self._release_links(m.links)     # its input copies were synchronous
                     elif self.compute.gpu:
                         # pipelined: H2D, ingest, graph replay and D2H are only enqueued here;
                         # the send thread waits for the event (micro-batch t computes while
-                        # t+1 is received and t-1 is sent)
-                        ev, res = self.compute.submit(m.tensors, m.bf16, m.count)
-                        out = (ev, Message(self.stage + 2, m.req_id, m.epoch, m.count, [r[0] for r in res],
-                                           [r[1] for r in res]))
+                        # t+1 is received and t-1 is sent) and then frees the input link slots
+                        ev, res = self.compute.submit(m.tensors, m.bf16, m.count,
+                                                      out_slots=self._link_slot if self._linkpool else None)
+                        out = _Pending(ev, Message(self.stage + 2, m.req_id, m.epoch, m.count, [r[0] for r in res],
+                                                   [r[1] for r in res]), m.links)
                     else:
                         outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
+                        self._release_links(m.links)
+                        if self._linkpool is not None:
+                            outs = [self._linkpool.put(o, self.stop, bf16=f) for o, f in zip(outs, flags)]
                         out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
                 self.processed += 1
                 while not self.stop.is_set():
@@ -312,12 +365,13 @@ class StageRuntime:
                     m = self.outq.get(timeout=0.1)
                 except queue.Empty:
                     continue
-                if isinstance(m, tuple) and len(m) == 2:   # pipelined GPU micro-batch: outputs on the host at `ev`
-                    ev, m = m
-                    while not ev.query():
+                if isinstance(m, _Pending):                # pipelined GPU micro-batch: outputs on the host at `ev`
+                    while not m.ev.query():
                         if self.stop.is_set():
                             return
                         time.sleep(0.0001)
+                    self._release_links(m.links)           # the input copies out of them are done too
+                    m = m.msg
                 elif isinstance(m, tuple):                 # GPU-encoded frontier (side stream)
                     m = self._finish_gpu_message(m)
                 send_message(self.downstream, m, self.codec, self.node.state.chunk_size)
@@ -340,6 +394,16 @@ class StageRuntime:
         # out of its `with self._busy` block before it calls _fail -> abort
         with self._busy:
             pass
+        if self._linkpool is not None or self._attached_links:
+            # no copy may still be running into or out of a slot that is unmapped below
+            if getattr(self.compute, "gpu", False):
+                import torch
+                torch.cuda.synchronize(self.compute.device)
+            if self._linkpool is not None:
+                self._linkpool.close()
+            from .transport import shm
+            shm.detach(list(self._attached_links))
+            self._attached_links.clear()
 
 
 class Node:
@@ -388,9 +452,10 @@ class Node:
 
     # ---------------------------------------------------------- lifecycle
     def record(self) -> Dict:
+        from .transport import shm
         rec = {"id": self.node_id, "host": self.advertise_host, "data_port": self.data_port,
                "config_port": self.config_port, "device": self.device, "pid": os.getpid(),
-               "state": self.state.state.name, "epoch": self.state.epoch}
+               "state": self.state.state.name, "epoch": self.state.epoch, "shm_domain": shm.domain()}
         try:
             import torch
             if self.device.startswith("cuda"):

@@ -110,6 +110,18 @@ class StageCompute:
                 u8[a.shape[0]:].zero_()
             E.ingest_u8(u8, dst, self.preprocess)
             return
+        want = np.uint16 if dst.dtype == torch.bfloat16 else (np.float32 if dst.dtype == torch.float32 else None)
+        if (want is not None and a.dtype == want and is_bf16 == (dst.dtype == torch.bfloat16)
+                and tuple(a.shape[1:]) == tuple(dst.shape[1:]) and a.shape[0] <= dst.shape[0]):
+            # same layout: one copy straight into the input buffer, async when `a` is
+            # page-locked (a registered shared-memory link slot, released at the event)
+            src = _readonly_tensor(a)
+            if is_bf16:
+                src = src.view(torch.bfloat16)
+            dst[: a.shape[0]].copy_(src, non_blocking=src.is_pinned())
+            if a.shape[0] < dst.shape[0]:
+                dst[a.shape[0]:].zero_()
+            return
         t = to_torch(a, is_bf16, self.device)
         if t.dtype != dst.dtype:
             t = t.to(dst.dtype)
@@ -118,9 +130,11 @@ class StageCompute:
         t = self._pad(t, count)
         dst.copy_(t)
 
-    def submit(self, arrays: Sequence[np.ndarray], bf16_flags: Sequence[bool], count: int):
+    def submit(self, arrays: Sequence[np.ndarray], bf16_flags: Sequence[bool], count: int, out_slots=None):
         """Enqueue one micro-batch (GPU): returns (event, [(array, bf16)]) whose host
-        arrays are valid once the event has completed."""
+        arrays are valid once the event has completed.  `out_slots(shape, dtype)`
+        -> (host tensor, handle): copy the first `count` rows of each output into
+        that tensor (a same-host link slot) and return the handle instead."""
         if len(arrays) != len(self.inputs):
             raise ValueError(f"stage expects {len(self.inputs)} inputs, got {len(arrays)}")
         j = self._tick % self.ex.num_sets
@@ -128,6 +142,16 @@ class StageCompute:
         for name, a, b in zip(self.inputs, arrays, bf16_flags):
             self._feed(name, a, b, count, j)
         outs = self.ex.forward(j)
+        if out_slots is not None:
+            res = []
+            for o in self.outputs:
+                src = outs[o][:count]
+                host, handle = out_slots(tuple(src.shape), src.dtype)
+                host.copy_(src, non_blocking=True)
+                res.append((handle, src.dtype == torch.bfloat16))
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            return ev, res
         if not self._pinned:
             for _ in range(self.host_ring):
                 self._pinned.append({o: torch.empty(tuple(outs[o].shape), dtype=outs[o].dtype, pin_memory=True)

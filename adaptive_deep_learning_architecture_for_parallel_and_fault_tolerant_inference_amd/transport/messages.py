@@ -24,6 +24,7 @@ from typing import List, Optional
 import numpy as np
 
 from .. import codec as C
+from . import shm
 from ..node_state import socket_recv, socket_send, socket_send_parts
 
 MAGIC = b"ADPT"
@@ -38,6 +39,9 @@ class Message:
     count: int
     tensors: List[np.ndarray] = field(default_factory=list)
     bf16: List[bool] = field(default_factory=list)     # tensor carries bfloat16 bits (uint16 view)
+    # same-host link slots (transport/shm.py LinkPool) the tensors are views of: the
+    # receiver clears their hand-off flags once its copy out of them has completed
+    links: List[str] = field(default_factory=list)
 
 
 def send_message(sock: socket.socket, m: Message, codec: str = "lz4", chunk_size: int = 512000,
@@ -71,7 +75,7 @@ def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int 
     magic, part, rid, epoch, count, nt = HDR.unpack(h)
     if magic != MAGIC:
         raise ValueError("bad data-plane message magic")
-    ts, bf = [], []
+    ts, bf, links = [], [], []
     for _ in range(nt):
         buf = socket_recv(sock, chunk_size, timeout_ms)
         if not buf:
@@ -81,7 +85,10 @@ def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int 
             ts.append(buf)
         else:
             ts.append(C.decode(buf, copy=False))      # read-only view of the received frame
-    return Message(part, rid, epoch, count, ts, bf)
+            name = C.shm_name(buf) if C.codec_of(buf) == "shm" else None
+            if name is not None and shm.is_link(name):
+                links.append(name)
+    return Message(part, rid, epoch, count, ts, bf, links)
 
 
 def connect(host: str, port: int, timeout: float = 5.0, hello: Optional[bytes] = None) -> socket.socket:

@@ -16,12 +16,25 @@ Segments are plain files under /dev/shm opened with os.open + mmap (not
 `multiprocessing.shared_memory`, whose resource tracker would unlink a
 segment when an *attaching* worker exits); the dispatcher unlinks its pool on
 shutdown.
+
+Stage -> stage links (`LinkPool`): when two consecutive stages of a pipeline
+share a host (the same `domain()`), the sending stage copies its frontier
+tensors device -> host straight into a page-locked slot and sends only the
+descriptor; the receiving stage copies host -> device from its own mapping of
+the same pages.  The reference ships every activation through a loopback TCP
+socket (`src/node.py:163-179`): the ResNet-50 2-stage frontier is 57 MB per
+bs=32 batch.  A link slot carries a 64-byte header whose first byte is the
+hand-off flag: the sender sets it when it fills the slot, the receiver clears
+it once its copy out of the slot has completed, and the sender only reuses
+slots whose flag is clear (so the receiver's pace is the link's
+back-pressure).
 """
 from __future__ import annotations
 
 import mmap
 import os
 import threading
+import time
 import uuid
 from typing import Dict, List, Optional, Tuple
 
@@ -34,14 +47,33 @@ def available() -> bool:
     return os.path.isdir(SHM_DIR) and os.access(SHM_DIR, os.W_OK)
 
 
-class Slot:
-    __slots__ = ("pool", "name", "nbytes", "mm", "index")
+def domain() -> Optional[str]:
+    """Identity of this process's /dev/shm: two processes can exchange slots
+    iff their domains are equal (same kernel boot and the same tmpfs mount, so
+    containers with private /dev/shm mounts do not match)."""
+    if not available():
+        return None
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = "?"
+    st = os.stat(SHM_DIR)
+    return f"{boot}:{st.st_dev}"
 
-    def __init__(self, pool: "ShmPool", name: str, nbytes: int, mm: mmap.mmap, index: int):
+
+LINK_HDR = 64          # link slots: byte 0 = hand-off flag, data from this offset
+
+
+class Slot:
+    __slots__ = ("pool", "name", "nbytes", "mm", "index", "offset")
+
+    def __init__(self, pool, name: str, nbytes: int, mm: mmap.mmap, index: int, offset: int = 0):
         self.pool, self.name, self.nbytes, self.mm, self.index = pool, name, nbytes, mm, index
+        self.offset = offset
 
     def view(self, dtype, shape) -> np.ndarray:
-        return np.ndarray(shape, dtype=dtype, buffer=self.mm, offset=0)
+        return np.ndarray(shape, dtype=dtype, buffer=self.mm, offset=self.offset)
 
     def release(self) -> None:
         self.pool.release(self)
@@ -99,6 +131,90 @@ class ShmPool:
             self._free.clear()
 
 
+class LinkPool:
+    """Sender side of a same-host stage -> stage link (module docstring)."""
+
+    def __init__(self, prefix: Optional[str] = None, max_slots: int = 6, register_device: bool = False):
+        self.prefix = prefix or f"adapt-link-{os.getpid()}-{uuid.uuid4().hex[:8]}"
+        self.max_slots = max_slots
+        self.register_device = register_device
+        self._lock = threading.Lock()
+        self._by_size: Dict[int, List[Slot]] = {}
+        self._all: List[Slot] = []
+        self._registered: List[int] = []
+
+    def _create(self, nbytes: int) -> Slot:
+        name = f"{self.prefix}-{len(self._all)}"
+        fd = os.open(os.path.join(SHM_DIR, name), os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+        try:
+            os.ftruncate(fd, LINK_HDR + nbytes)
+            mm = mmap.mmap(fd, LINK_HDR + nbytes)
+        finally:
+            os.close(fd)
+        s = Slot(self, name, nbytes, mm, len(self._all), offset=LINK_HDR)
+        self._all.append(s)
+        if self.register_device:          # the device -> host copy is then an async DMA into the slot
+            import torch
+            addr = np.frombuffer(mm, dtype=np.uint8).ctypes.data
+            try:
+                rc = torch.cuda.cudart().cudaHostRegister(int(addr), LINK_HDR + nbytes, 0)
+                if (int(rc[0]) if isinstance(rc, tuple) else int(rc)) == 0:
+                    self._registered.append(int(addr))
+            except Exception:  # noqa: BLE001 - a pageable copy still works, just slower
+                pass
+        return s
+
+    def acquire(self, nbytes: int, stop: Optional[threading.Event] = None) -> Slot:
+        """A slot of `nbytes` whose flag is clear (the receiver is done with it),
+        flagged as in flight; waits while all `max_slots` slots of that size are."""
+        while True:
+            with self._lock:
+                same = self._by_size.setdefault(nbytes, [])
+                for s in same:
+                    if s.mm[0] == 0:
+                        s.mm[0] = 1
+                        return s
+                if len(same) < self.max_slots:
+                    s = self._create(nbytes)
+                    same.append(s)
+                    s.mm[0] = 1
+                    return s
+            if stop is not None and stop.is_set():
+                raise RuntimeError("link stopped while waiting for a free slot")
+            time.sleep(0.0002)
+
+    def put(self, arr: np.ndarray, stop: Optional[threading.Event] = None, bf16: bool = False) -> "ShmRef":
+        arr = np.ascontiguousarray(arr)
+        s = self.acquire(arr.nbytes, stop)
+        np.copyto(s.view(arr.dtype, arr.shape), arr)
+        return ShmRef(s, arr.dtype, arr.shape, bf16=bf16)
+
+    def close(self) -> None:
+        with self._lock:
+            for addr in self._registered:
+                try:
+                    import torch
+                    torch.cuda.cudart().cudaHostUnregister(addr)
+                except Exception:  # noqa: BLE001
+                    pass
+            self._registered.clear()
+            for s in self._all:
+                try:
+                    s.mm.close()
+                except (BufferError, ValueError):
+                    pass
+                try:
+                    os.unlink(os.path.join(SHM_DIR, s.name))
+                except FileNotFoundError:
+                    pass
+            self._all.clear()
+            self._by_size.clear()
+
+
+def is_link(name: str) -> bool:
+    return name.startswith("adapt-link-")
+
+
 class _Attached:
     def __init__(self, name: str):
         path = os.path.join(SHM_DIR, name)
@@ -117,8 +233,9 @@ class ShmRef:
     """A request tensor that lives in a pool slot: on the wire it is the "shm"
     codec container (segment name + offset), not the bytes."""
 
-    def __init__(self, slot: Slot, dtype, shape: Tuple[int, ...]):
+    def __init__(self, slot: Slot, dtype, shape: Tuple[int, ...], bf16: bool = False):
         self.slot, self.dtype, self.shape = slot, np.dtype(dtype), tuple(int(v) for v in shape)
+        self.bf16 = bf16
 
     @property
     def array(self) -> np.ndarray:
@@ -126,7 +243,8 @@ class ShmRef:
 
     def container(self) -> bytes:
         from .. import codec as C
-        return C.wrap(self.slot.name.encode() + b"\0" + (0).to_bytes(8, "little"), "shm", self.dtype, self.shape)
+        return C.wrap(self.slot.name.encode() + b"\0" + int(self.slot.offset).to_bytes(8, "little"), "shm",
+                      self.dtype, self.shape, bf16=self.bf16)
 
 
 # worker processes on a GPU set this: mapped segments are page-locked for DMA
@@ -158,6 +276,31 @@ def view(name: str, offset: int, dtype, shape: Tuple[int, ...], register_device:
     if offset + n > a.size:
         raise ValueError(f"shm {name}: {offset + n} bytes past its {a.size}-byte segment")
     return a.arr[offset:offset + n].view(dtype).reshape(shape)
+
+
+def release(name: str) -> None:
+    """Receiver side of a link: the copy out of slot `name` has completed."""
+    attach(name).arr[0] = 0
+
+
+def detach(names) -> None:
+    """Unmap the given attached segments (a finished epoch's link slots)."""
+    with _att_lock:
+        for n in names:
+            a = _attached.pop(n, None)
+            if a is None:
+                continue
+            if a.registered:
+                try:
+                    import torch
+                    torch.cuda.cudart().cudaHostUnregister(int(a.arr.ctypes.data))
+                except Exception:  # noqa: BLE001
+                    pass
+            a.arr = None
+            try:
+                a.mm.close()
+            except (BufferError, ValueError):
+                pass                       # a view is still alive: the mapping goes with it
 
 
 def detach_all() -> None:

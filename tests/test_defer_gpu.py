@@ -48,7 +48,7 @@ def test_defer_two_gpu_stages_side_stream_codec(codec):
     multi-tensor cut of BASELINE config 2."""
     m = resnet("resnet50", seed=0)
     d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
-              codec=codec, min_workers=2)
+              codec=codec, min_workers=2, links="tcp")
     d.membership_server.start()
     nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"g{i}",
                   heartbeat_ttl=1.0) for i in range(2)]
@@ -123,6 +123,36 @@ def test_defer_two_gpu_stages_other_families(name, cut):
         got = np.concatenate([outq.get(timeout=120) for _ in xs])
         want = m.predict(np.concatenate(xs), device="cpu")
         assert np.abs(got - want).sum(-1).max() < 0.1
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
+
+
+def test_defer_two_gpu_stages_shared_memory_link():
+    """Two GPU stages on one host: the frontier goes device -> page-locked link
+    slot -> device (transport/shm.py LinkPool), only descriptors on the TCP hop;
+    slots are recycled through the hand-off flag."""
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
+              min_workers=2)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"s{i}",
+                  heartbeat_ttl=1.0) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["conv3_block1_1_conv"], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(4)
+        xs = [rng.standard_normal((4, 224, 224, 3)).astype(np.float32) for _ in range(12)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=120) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert np.abs(got - want).sum(-1).max() < 0.1
+        first = next(n for n in nodes if n.node_id == d.pipeline.workers[0])
+        assert first.runtime.link == "shm" and 1 <= len(first.runtime._linkpool._all) <= 2 * 6
     finally:
         d.shutdown(stop_workers=True)
         for n in nodes:

@@ -349,7 +349,7 @@ def test_plot_model_and_per_slice_plots(tmp_path, monkeypatch):
     dot = open(path if path.endswith(".dot") else str(tmp_path / "small.dot")).read()
     assert dot.startswith('digraph "small"') and '"cat" -> "mp"' in dot and dot.count("->") == 19
     monkeypatch.setenv("ADAPT_PLOT_DIR", str(tmp_path / "plots"))
-    d = DEFER(membership_port=0, result_port=0, worker_wait=10, ordered=True, batch=2)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=10, ordered=True, batch=2, min_workers=2)
     d.membership_server.start()
     nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu", node_id=f"p{i}",
                   heartbeat_ttl=0.5) for i in range(2)]

@@ -1,0 +1,118 @@
+"""Same-host stage -> stage links through shared memory (transport/shm.py
+LinkPool): the frontier goes into a slot, only a descriptor crosses the TCP
+hop (the reference sends every activation through the socket,
+`src/node.py:163-179`).  CPU workers in-process; the GPU path (device -> page-
+locked slot -> device) is exercised by tests/test_shm_links_gpu.py.
+"""
+import os
+import queue
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.dispatcher import DEFER
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.model import resnet
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.node import Node
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.transport import shm
+
+pytestmark = pytest.mark.skipif(not shm.available(), reason="no writable /dev/shm")
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    return resnet("resnet_tiny", input_shape=(32, 32, 3), classes=10, seed=5)
+
+
+def _wait(pred, timeout=30.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if pred():
+            return True
+        time.sleep(0.05)
+    return False
+
+
+def _links():
+    """This process's link segments (xdist workers run other pipelines at the same time)."""
+    return sorted(f for f in os.listdir(shm.SHM_DIR) if f.startswith(f"adapt-link-{os.getpid()}-"))
+
+
+def _run(tiny, links, n_nodes=3, kill=False):
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, ordered=True, batch=2, weight_codec="lz4",
+              min_workers=n_nodes, replicas=1, links=links)
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu",
+                  node_id=f"{links}{i}", heartbeat_ttl=2.0) for i in range(n_nodes)]
+    for nd in nodes:
+        nd.run(block=False)
+    before = set(_links())
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        cuts = ["conv3_block1_out", "conv4_block1_out"][: n_nodes - 1]
+        threading.Thread(target=d.run_defer, args=(tiny, cuts, inq, outq), daemon=True).start()
+        assert _wait(lambda: d.pipeline is not None)
+        rng = np.random.default_rng(3)
+        xs = [rng.standard_normal((2, 32, 32, 3)).astype(np.float32) for _ in range(16)]
+        want = tiny.predict(np.concatenate(xs), device="cpu")
+        for x in xs[:8]:
+            inq.put(x)
+        got = [outq.get(timeout=60) for _ in range(8)]
+        stages = [next(nd for nd in nodes if nd.node_id == w) for w in d.pipeline.workers]
+        info = [(nd.runtime.link, None if nd.runtime._linkpool is None else
+                 (len(nd.runtime._linkpool._all), nd.runtime._linkpool.max_slots)) for nd in stages]
+        if kill:
+            e0 = d.pipeline.epoch
+            stages[1].stop()                               # the middle stage: both its links break
+            assert _wait(lambda: d.pipeline is not None and d.pipeline.epoch > e0)
+        for x in xs[8:]:
+            inq.put(x)
+        got += [outq.get(timeout=60) for _ in range(8)]
+        time.sleep(0.2)
+        assert outq.empty()                                # exactly once
+        np.testing.assert_allclose(np.concatenate(got), want, rtol=1e-4, atol=1e-5)
+        return info, before
+    finally:
+        d.shutdown(stop_workers=True)
+        for nd in nodes:
+            nd.stop()
+
+
+def test_same_host_hops_use_shared_memory_slots(tiny):
+    info, before = _run(tiny, "auto")
+    assert [lk for lk, _ in info] == ["shm", "shm", "tcp"]       # the last hop goes to the dispatcher
+    for _, (n_slots, max_slots) in info[:2]:
+        assert 1 <= n_slots <= max_slots                        # slots are recycled, not one per request
+    assert set(_links()) <= before                              # every link segment unlinked at shutdown
+
+
+def test_links_tcp_keeps_frontier_on_the_socket(tiny):
+    info, _ = _run(tiny, "tcp")
+    assert [lk for lk, _ in info] == ["tcp", "tcp", "tcp"] and all(p is None for _, p in info)
+
+
+def test_shm_link_survives_a_stage_kill(tiny):
+    info, before = _run(tiny, "auto", n_nodes=3, kill=True)
+    assert info[0][0] == "shm"
+    assert set(_links()) <= before
+
+
+def test_link_pool_handoff_flag():
+    pool = shm.LinkPool(max_slots=2)
+    try:
+        a = pool.put(np.arange(6, dtype=np.float32))
+        b = pool.put(np.arange(6, dtype=np.float32) + 1)
+        assert a.slot is not b.slot and a.slot.mm[0] == 1 and b.slot.mm[0] == 1
+        stop = threading.Event()
+        stop.set()
+        with pytest.raises(RuntimeError):                     # both in flight: the sender waits
+            pool.acquire(24, stop)
+        name = a.slot.name
+        np.testing.assert_array_equal(shm.view(name, shm.LINK_HDR, np.float32, (6,)), np.arange(6))
+        shm.release(name)                                     # receiver side: copy done
+        c = pool.acquire(24)
+        assert c is a.slot
+        shm.detach([name])
+    finally:
+        pool.close()
