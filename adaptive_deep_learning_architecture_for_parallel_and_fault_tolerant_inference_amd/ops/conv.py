@@ -310,12 +310,12 @@ def stem_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool: bool 
 # The reference's precision (Keras float32, `src/node.py:177`): conv / GEMM on
 # the fp32 matrix cores, csrc/kernels/conv_f32.hip.  Tiles (BM, BN) per cfg id
 # mirror ADAPT_F32_CFGS there; K tiles are 16 floats.
-F32_BK = 16
-F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+F32_BK = 32
+F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (64, 256)}
 
 
 def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, device,
-                  row_align: int = 128) -> PackedConv:
+                  row_align: int = 256) -> PackedConv:
     """[Npad][Kpad] fp32 weights, k = (kh, kw, ci) with ci innermost; no channel padding."""
     kh, kw, cin, cout = kernel_hwio.shape
     K = kh * kw * cin
@@ -341,7 +341,7 @@ def choose_cfg_f32(M: int, N: int, Kpad: int, occupancy: int = 2):
                 continue
             blocks = tiles * ks
             waves = math.ceil(blocks / (NUM_CUS * occupancy))
-            eff = {0: 1.0, 1: 0.93, 2: 0.93, 3: 0.8}[cfg]
+            eff = {0: 1.0, 1: 0.93, 2: 0.93, 3: 0.8, 4: 1.0, 5: 1.0}[cfg]
             t = waves * bm * bn * (Kpad / ks) / eff
             if ks > 1:
                 t += M * N * (ks + 1) * 2.0          # slab write + reduce read (fp32), arbitrary units

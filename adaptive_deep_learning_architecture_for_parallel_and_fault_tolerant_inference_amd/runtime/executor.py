@@ -426,8 +426,65 @@ class SliceExecutor:
                 cfg, ks = conv_ops.choose_cfg(B * OH * OW, pc.cout, pc.Kpad)
             self.cfg[i] = (int(cfg), int(ks))
         self._ensure_ws()
-        if tune and not self.fp32:
-            self.autotune()
+        if tune:
+            self.autotune_f32() if self.fp32 else self.autotune()
+
+    @staticmethod
+    def _time_graph(fn, reps: int) -> float:
+        """ms per call of `fn`, `reps` calls captured in one hipGraph (device time only)."""
+        fn()
+        torch.cuda.synchronize()
+        gg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gg):
+            for _ in range(reps):
+                fn()
+        gg.replay()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(3):
+            gg.replay()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / (3 * reps)
+
+    def autotune_f32(self, reps: int = 10, persist: bool = True) -> Dict[str, List]:
+        """fp32 path: time every (tile cfg, split-K) of conv_f32.hip per conv
+        problem in isolation and keep the fastest ("f32|" keys in the table)."""
+        results: Dict[str, List] = {}
+        done: Dict[str, Tuple[int, int]] = {}
+        for i, st in enumerate(self.steps):
+            if st.kind not in ("conv", "dense") or i in self._dense_part:
+                continue
+            B, H, W, C, OH, OW, pc = self._conv_geom(i)
+            M, N = B * OH * OW, pc.cout
+            key = "f32|" + conv_key(B, H, W, C, pc)
+            if key in done:
+                self.cfg[i] = done[key]
+                continue
+            x = torch.randn(self.bufs(0)[st.ins[0]].shape, device=self.device)
+            out = torch.empty(M * N, dtype=torch.float32, device=self.device)
+            ktiles = pc.Kpad // conv_ops.F32_BK
+            best = None
+            for cfg in conv_ops.F32_TILES:
+                for ks in (1, 2, 4, 8, 16):
+                    if ks > 1 and ktiles // ks < 2:
+                        continue
+                    ws = torch.empty(ks * M * N, dtype=torch.float32, device=self.device) if ks > 1 else None
+                    try:
+                        t = self._time_graph(lambda: conv_ops.conv_forward_f32(x, pc, out, cfg=cfg, ksplit=ks,
+                                                                               workspace=ws), reps)
+                    except (RuntimeError, ValueError):
+                        continue
+                    if best is None or t < best[0]:
+                        best = (t, cfg, ks)
+            if best:
+                results[key] = [best[1], best[2], round(best[0] * 1000, 2)]
+                done[key] = (best[1], best[2])
+                self.cfg[i] = (best[1], best[2])
+        self._ensure_ws()
+        if persist:
+            save_tuning(results)
+        return results
 
     def autotune(self, reps: int = 20, persist: bool = True, refine: int = 3) -> Dict[str, List]:
         """Time every (tile cfg, split-K) candidate per conv problem in isolation,

@@ -8,14 +8,17 @@
 // m = (img, oh, ow) over the NHWC output, n = output channel, k = (kh, kw, ci)
 // with ci innermost; weights packed [Npad][Kpad] fp32 (BN folded on the host).
 //
-// Tiling (BM x BN x 16 per block, 4 waves on a WM x WN grid, wave tile TM x TN):
+// Tiling (BM x BN x 32 per block, 4 waves on a WM x WN grid, wave tile TM x TN):
 // * the K permutation trick: an MFMA 16x16x4 takes k-slot q (q = lane / 16)
-//   from every lane group; over the 4 MFMAs of one 16-wide K tile, lane group q
+//   from every lane group; over the 4 MFMAs of one 16-wide K half, lane group q
 //   supplies k = 4q + s at step s.  A and B use the same permutation, so the
 //   sum is the plain dot product and each lane fetches ONE float4 per fragment
-//   row per K tile (ds_read_b128) instead of four scalar reads;
-// * LDS rows of 16 floats, float4 chunk index XOR-swizzled with (row >> 2) & 3:
-//   the 16 rows a 16-lane group reads land on 16 distinct 4-bank groups;
+//   row per K half (ds_read_b128) instead of four scalar reads;
+// * K tiles of 32 (two halves per barrier: twice the MFMA work between
+//   barriers of the 16-wide v1, which left the loads' latency exposed);
+// * LDS rows of 32 floats (128 B), float4 chunk index XOR-swizzled with
+//   (row >> 1) & 7: the 16 rows a 16-lane group reads land on 16 distinct
+//   16-byte slots of the 256-byte bank row;
 // * register-prefetch double buffer: the next K tile is loaded from global
 //   while the MFMAs of this one run, one barrier per K tile;
 // * epilogue straight from the accumulators: for each of its 4 rows a 16-lane
@@ -42,16 +45,19 @@ struct ConvF32Params {
 
 namespace {
 
-constexpr int FBK = 16;          // fp32 elements per K tile (4 float4 chunks)
+constexpr int FBK = 32;          // fp32 elements per K tile (8 float4 chunks)
+constexpr int FCH = FBK / 4;
 constexpr int FNT = 256;
 
-__device__ __forceinline__ int fswz(int r, int c) { return r * FBK + ((c ^ ((r >> 2) & 3)) << 2); }
+__device__ __forceinline__ int fswz(int r, int c) { return r * FBK + ((c ^ ((r >> 1) & 7)) << 2); }
 
-template <int BM, int BN, int WM, int WN, bool PURE, bool VEC>
+// TAPK: Cin % FBK == 0, so a K tile never straddles a filter tap: the tap and
+// its first channel are computed once per tile (wave-uniform), not per chunk
+template <int BM, int BN, int WM, int WN, bool PURE, bool VEC, bool TAPK>
 __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int ACH = BM * 4 / FNT, BCH = BN * 4 / FNT;      // float4 chunks per thread per K tile
+  constexpr int ACH = BM * FCH / FNT, BCH = BN * FCH / FNT;  // float4 chunks per thread per K tile
   static_assert(WM * WN == 4 && ACH >= 1 && BCH >= 1, "tile");
   __shared__ __attribute__((aligned(16))) float sa[2][BM * FBK];
   __shared__ __attribute__((aligned(16))) float sb[2][BN * FBK];
@@ -70,7 +76,7 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
   const int ohw = p.OH * p.OW;
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
-    const int m = m0 + (tid + i * FNT) / 4;
+    const int m = m0 + (tid + i * FNT) / FCH;
     if (m < p.M) {
       if (PURE) {
         a_base[i] = m * p.Cin;
@@ -91,10 +97,24 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
   auto load = [&](int kt) {
+    int t_ci0 = 0, t_kh = 0, t_kw = 0;
+    if (TAPK) {
+      const int kk0 = kt * FBK;
+      const int tap = kk0 / p.Cin;
+      t_ci0 = kk0 - tap * p.Cin;
+      t_kh = tap / p.KW;
+      t_kw = tap - t_kh * p.KW;
+    }
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int c = (tid + i * FNT) & 3;
+      const int c = (tid + i * FNT) % FCH;
       const int k = kt * FBK + c * 4;
+      if (TAPK) {
+        const int ih = a_ih0[i] + t_kh, iw = a_iw0[i] + t_kw;
+        ra[i] = (a_base[i] >= 0 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+                    ? *(const f32x4*)(p.x + a_base[i] + (ih * p.W + iw) * p.Cin + t_ci0 + c * 4) : z4;
+        continue;
+      }
       if (a_base[i] < 0 || k >= p.K) { ra[i] = z4; continue; }
       if (PURE) {
         ra[i] = *(const f32x4*)(p.x + a_base[i] + k);
@@ -120,7 +140,7 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * FNT, row = c >> 2, ch = c & 3;
+      const int c = tid + i * FNT, row = c / FCH, ch = c % FCH;
       rb[i] = *(const f32x4*)(p.w + (size_t)(n0 + row) * p.Kpad + kt * FBK + ch * 4);
     }
   };
@@ -128,12 +148,12 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * FNT;
-      *(f32x4*)(&sa[buf][fswz(c >> 2, c & 3)]) = ra[i];
+      *(f32x4*)(&sa[buf][fswz(c / FCH, c % FCH)]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * FNT;
-      *(f32x4*)(&sb[buf][fswz(c >> 2, c & 3)]) = rb[i];
+      *(f32x4*)(&sb[buf][fswz(c / FCH, c % FCH)]) = rb[i];
     }
   };
 
@@ -144,6 +164,26 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = z4;
   const int fr = lane & 15, fq = lane >> 4;
 
+  // the residual this lane adds in the epilogue, requested before the K loop so
+  // its latency hides under the MFMAs (read one by one after the loop, each of
+  // the FM*FN*4 loads was a serial round trip: the fp32 "_out" convs spent most
+  // of their time there)
+  const bool pre_res = p.res != nullptr && p.ksplit == 1;
+  f32x4 rres[FM][FN];
+  if (pre_res) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + i * 16 + fq * 4 + r;
+          rres[i][j][r] = (n < p.N && m < p.M) ? p.res[(size_t)m * p.N + n] : 0.f;
+        }
+    }
+  }
+
   if (kt0 < kt1) {
     load(kt0);
     store(0);
@@ -152,18 +192,21 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
       if (more) load(kt + 1);
-      f32x4 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *(const f32x4*)(&sa[buf][fswz(wm * TM + i * 16 + fr, fq)]);
+      for (int h = 0; h < 2; ++h) {
+        f32x4 af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = *(const f32x4*)(&sb[buf][fswz(wn * TN + j * 16 + fr, fq)]);
+        for (int i = 0; i < FM; ++i) af[i] = *(const f32x4*)(&sa[buf][fswz(wm * TM + i * 16 + fr, h * 4 + fq)]);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int j = 0; j < FN; ++j) bfr[j] = *(const f32x4*)(&sb[buf][fswz(wn * TN + j * 16 + fr, h * 4 + fq)]);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      }
       if (more) store(buf ^ 1);
       __syncthreads();
       buf ^= 1;
@@ -190,7 +233,7 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
           continue;
         }
         v += b;
-        if (p.res) v += p.res[o];
+        if (pre_res) v += rres[i][j][r];
         p.out[o] = act_relu(v, p.relu);
       }
   }
@@ -211,9 +254,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_f32(ConvF32Params p) {
 template <int BM, int BN, int WM, int WN>
 hipError_t launch_f32(const ConvF32Params& p, bool pure, bool vec, hipStream_t s) {
   dim3 grid(((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN), p.ksplit), block(FNT);
-  if (pure) hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, true, true>), grid, block, 0, s, p);
-  else if (vec) hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, true>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, false>), grid, block, 0, s, p);
+  if (pure) hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, true, true, false>), grid, block, 0, s, p);
+  else if (vec && p.Cin % FBK == 0)
+    hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, true, true>), grid, block, 0, s, p);
+  else if (vec) hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, true, false>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((conv_f32_kernel<BM, BN, WM, WN, false, false, false>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
@@ -224,7 +269,9 @@ hipError_t launch_f32(const ConvF32Params& p, bool pure, bool vec, hipStream_t s
   X(0, 128, 128, 2, 2)    \
   X(1, 128, 64, 2, 2)     \
   X(2, 64, 128, 2, 2)     \
-  X(3, 64, 64, 2, 2)
+  X(3, 64, 64, 2, 2)      \
+  X(4, 256, 64, 4, 1)     \
+  X(5, 64, 256, 1, 4)
 
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
