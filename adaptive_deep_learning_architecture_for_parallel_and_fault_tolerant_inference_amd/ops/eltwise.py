@@ -313,6 +313,85 @@ def eltwise_f32(a: torch.Tensor, out: torch.Tensor, b: Optional[torch.Tensor] = 
     return out
 
 
+def dwconv_f32(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, stride: int,
+               pads=((0, 0), (0, 0)), act: int = 0, alpha: float = 0.3, stream=None) -> torch.Tensor:
+    """fp32 depthwise conv: x [B,H,W,C], w [KH,KW,C] (BN folded), bias [C], out [B,OH,OW,C]; any ActMode."""
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    _chk(w, torch.float32, "w"); _chk(bias, torch.float32, "bias")
+    B, H, W, C = x.shape
+    KH, KW, Cw = w.shape
+    _, OH, OW, C2 = out.shape
+    (pt, _), (pl, _) = pads
+    if Cw != C or C2 != C or bias.numel() != C:
+        raise ValueError("dwconv_f32: channel counts differ")
+    kernels().dwconv_f32(ptr(x), ptr(w), ptr(bias), ptr(out), B, H, W, C, OH, OW, KH, KW, int(stride), int(pt),
+                         int(pl), int(act), float(alpha), stream_handle(stream))
+    return out
+
+
+def avgpool_f32(x: torch.Tensor, out: torch.Tensor, k, s: int, pads=((0, 0), (0, 0)), stream=None) -> torch.Tensor:
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    kh, kw = (k, k) if isinstance(k, int) else k
+    B, H, W, C = x.shape
+    _, OH, OW, C2 = out.shape
+    (pt, _), (pl, _) = pads
+    if C2 != C:
+        raise ValueError("avgpool_f32: channel counts differ")
+    kernels().avgpool_f32(ptr(x), ptr(out), B, H, W, C, OH, OW, kh, kw, int(s), int(pt), int(pl),
+                          stream_handle(stream))
+    return out
+
+
+def concat_f32(xs, out: torch.Tensor, stream=None) -> torch.Tensor:
+    """Channel concat of fp32 NHWC tensors (true channel counts)."""
+    _chk(out, torch.float32, "out")
+    Cy = out.shape[-1]
+    pixels = out.numel() // Cy
+    if sum(x.shape[-1] for x in xs) != Cy:
+        raise ValueError("concat_f32: channel counts do not add up")
+    off = 0
+    for i, x in enumerate(xs):
+        _chk(x, torch.float32, f"x{i}")
+        if x.numel() // x.shape[-1] != pixels:
+            raise ValueError(f"concat_f32: input {i} shape {tuple(x.shape)} does not match {tuple(out.shape)}")
+        kernels().concat_f32(ptr(x), x.shape[-1], ptr(out), Cy, off, pixels, stream_handle(stream))
+        off += x.shape[-1]
+    return out
+
+
+def binary_f32(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, op: str, act_mode: int = 0,
+               stream=None) -> torch.Tensor:
+    """fp32 out = act(a <op> b); b has a's shape or one channel row per image (squeeze-excite broadcast)."""
+    _chk(a, torch.float32, "a"); _chk(b, torch.float32, "b"); _chk(out, torch.float32, "out")
+    C = a.shape[-1]
+    if out.numel() != a.numel() or b.shape[-1] != C:
+        raise ValueError("binary_f32: bad shapes")
+    bcast = 0
+    if b.numel() != a.numel():
+        B = a.shape[0]
+        if b.numel() != B * C:
+            raise ValueError(f"binary_f32: cannot broadcast {tuple(b.shape)} over {tuple(a.shape)}")
+        bcast = a.numel() // (B * C)
+    kernels().binary_f32(ptr(a), ptr(b), ptr(out), a.numel(), C, bcast, BIN_OPS[op], int(act_mode),
+                         stream_handle(stream))
+    return out
+
+
+def affine_act_f32(x: torch.Tensor, out: torch.Tensor, scale: Optional[torch.Tensor] = None,
+                   shift: Optional[torch.Tensor] = None, act: int = 0, alpha: float = 0.3,
+                   stream=None) -> torch.Tensor:
+    """fp32 out = act(x * scale[c] + shift[c]) (or act(x)), any channel count and ActMode."""
+    _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
+    if out.numel() != x.numel():
+        raise ValueError("affine_act_f32: element counts differ")
+    C = x.shape[-1]
+    if scale is not None and (scale.numel() != C or shift is None or shift.numel() != C):
+        raise ValueError("affine_act_f32: scale/shift need one value per channel")
+    kernels().affine_act_f32(ptr(x), ptr(scale), ptr(shift), ptr(out), x.numel(), C, int(act), float(alpha),
+                             stream_handle(stream))
+    return out
+
+
 def pad_f32(x: torch.Tensor, out: torch.Tensor, pad_t: int, pad_l: int, stream=None) -> torch.Tensor:
     _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
     B, H, W, C = x.shape

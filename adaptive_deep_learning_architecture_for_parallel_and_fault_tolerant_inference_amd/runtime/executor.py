@@ -75,7 +75,8 @@ def _nbytes(shape, dtype) -> int:
 class SliceExecutor:
     """Runs one (sub)graph for a fixed batch on one device with our HIP kernels."""
 
-    FP32_KINDS = ("conv", "dense", "maxpool", "gap", "softmax", "add", "bn", "relu", "pad", "copy")
+    FP32_KINDS = ("conv", "dense", "maxpool", "gap", "softmax", "add", "bn", "relu", "pad", "copy",
+                  "dwconv", "avgpool", "concat", "act", "binary", "affine")
 
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device="cuda",
                  outputs: Optional[Sequence[str]] = None, tune: bool = False, num_sets: int = 1,
@@ -236,6 +237,29 @@ class SliceExecutor:
                 sc = gm / np.sqrt(var + eps)
                 self.packed[i] = (torch.tensor(sc, dtype=torch.float32, device=dev),
                                   torch.tensor(bt - mu * sc, dtype=torch.float32, device=dev))
+            elif st.kind == "dwconv":
+                p = st.p
+                k = weights[f"{p['conv']}/depthwise_kernel"][..., 0]          # (kh, kw, C), multiplier 1
+                bn = None
+                eps = 1e-3
+                if p["bn"]:
+                    bn = bn_params(weights, p["bn"])
+                    eps = self.g.layers[p["bn"]].attrs.get("epsilon", 1e-3)
+                kf, bf = conv_ops.fold_bn(k[:, :, None, :], weights.get(f"{p['conv']}/bias"), bn, eps)
+                self.packed[i] = (torch.tensor(np.ascontiguousarray(kf[:, :, 0, :]), dtype=torch.float32, device=dev),
+                                  torch.tensor(bf, dtype=torch.float32, device=dev))
+            elif st.kind == "affine":            # Keras Rescaling / Normalization: y = x * scale + shift
+                L = self.g.layers[st.p["layer"]]
+                c = L.out_shape[-1]
+                if L.op == "rescale":
+                    sc = np.broadcast_to(np.asarray(L.attrs.get("scale", 1.0), np.float64), (c,))
+                    sh = np.broadcast_to(np.asarray(L.attrs.get("offset", 0.0), np.float64), (c,))
+                else:
+                    mu = weights[f"{L.name}/mean"].astype(np.float64)
+                    sd = np.maximum(np.sqrt(weights[f"{L.name}/variance"].astype(np.float64)), 1e-7)
+                    sc, sh = 1.0 / sd, -mu / sd
+                self.packed[i] = (torch.tensor(np.ascontiguousarray(sc), dtype=torch.float32, device=dev),
+                                  torch.tensor(np.ascontiguousarray(sh), dtype=torch.float32, device=dev))
 
     def _folded(self, weights: Dict[str, np.ndarray], p: Dict):
         """BN-folded (kernel HWIO, bias) of a conv step's parameters."""
@@ -778,6 +802,21 @@ class SliceExecutor:
         elif k == "pad":
             (pt, _), (pl, _) = st.p["pad"]
             E.pad_f32(b[st.ins[0]], b[st.out], pt, pl, stream=stream)
+        elif k == "dwconv":
+            w, bias = self.packed[i]
+            E.dwconv_f32(b[st.ins[0]], w, bias, b[st.out], st.p["stride"], st.p["pads"], act=st.p["relu"],
+                         stream=stream)
+        elif k == "avgpool":
+            E.avgpool_f32(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], st.p["pads"], stream=stream)
+        elif k == "concat":
+            E.concat_f32([b[t] for t in st.ins], b[st.out], stream=stream)
+        elif k == "act":
+            E.affine_act_f32(b[st.ins[0]], b[st.out], act=st.p["mode"], alpha=st.p["alpha"], stream=stream)
+        elif k == "binary":
+            E.binary_f32(b[st.ins[0]], b[st.ins[1]], b[st.out], st.p["fn"], st.p["act"], stream=stream)
+        elif k == "affine":
+            sc, sh = self.packed[i]
+            E.affine_act_f32(b[st.ins[0]], b[st.out], sc, sh, stream=stream)
         elif k == "copy":
             src, dst = b[st.ins[0]], b[st.out]
             if stream is not None:

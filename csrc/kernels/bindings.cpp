@@ -205,6 +205,27 @@ PYBIND11_MODULE(_C, m) {
   m.def("pad_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int pt, int pl, u64 s) {
     check(adapt::pad_f32(P<const float>(x), P<float>(y), B, H, W, C, OH, OW, pt, pl, S(s)), "pad_f32");
   });
+  m.def("dwconv_f32", [](u64 x, u64 w, u64 b, u64 y, int B, int H, int W, int C, int OH, int OW, int KH, int KW,
+                         int Sd, int pt, int pl, int act, float alpha, u64 s) {
+    check(adapt::dwconv_f32(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), B, H, W, C, OH, OW,
+                            KH, KW, Sd, pt, pl, act, alpha, S(s)), "dwconv_f32");
+  });
+  m.def("avgpool_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int Sd, int pt,
+                          int pl, u64 s) {
+    check(adapt::avgpool_f32(P<const float>(x), P<float>(y), B, H, W, C, OH, OW, KH, KW, Sd, pt, pl, S(s)),
+          "avgpool_f32");
+  });
+  m.def("concat_f32", [](u64 x, int Cx, u64 y, int Cy, int off, size_t pixels, u64 s) {
+    check(adapt::concat_f32(P<const float>(x), Cx, P<float>(y), Cy, off, pixels, S(s)), "concat_f32");
+  });
+  m.def("binary_f32", [](u64 a, u64 b, u64 y, size_t n, int C, int bcast_hw, int op, int act, u64 s) {
+    check(adapt::binary_f32(P<const float>(a), P<const float>(b), P<float>(y), n, C, bcast_hw, op, act, S(s)),
+          "binary_f32");
+  });
+  m.def("affine_act_f32", [](u64 x, u64 sc, u64 sh, u64 y, size_t n, int C, int act, float alpha, u64 s) {
+    check(adapt::affine_act_f32(P<const float>(x), P<const float>(sc), P<const float>(sh), P<float>(y), n, C, act,
+                                alpha, S(s)), "affine_act_f32");
+  });
   m.def("zfp_gpu_maxw", &adapt::zfp_gpu_maxw);
   m.def("zfp_gpu_nblocks", [](std::vector<int64_t> shape) {
     return adapt::zfp_gpu_nblocks(shape.data(), (int)shape.size());

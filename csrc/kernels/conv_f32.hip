@@ -370,6 +370,113 @@ __global__ __launch_bounds__(256) void eltwise_f32_kernel(const float* __restric
   }
 }
 
+// ---- the other families' layers (MobileNetV2 / EfficientNet / DenseNet / InceptionV3) in fp32:
+// plain element-per-thread kernels over the true channel count (fp32 activations carry no padding)
+
+// depthwise conv, multiplier 1, BN folded: y[b][oh][ow][c] = act(sum x * w[kh][kw][c] + bias[c])
+__global__ __launch_bounds__(256) void dwconv_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ y,
+                                                         int B, int H, int W, int C, int OH, int OW, int KH, int KW,
+                                                         int S, int pad_t, int pad_l, int act, float alpha) {
+  const size_t total = (size_t)B * OH * OW * C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    size_t r = i / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    float acc = bias ? bias[c] : 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int ih = oh * S - pad_t + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int iw = ow * S - pad_l + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        acc = fmaf(x[(((size_t)b * H + ih) * W + iw) * C + c], w[(kh * KW + kw) * C + c], acc);
+      }
+    }
+    y[i] = act_f(acc, act, alpha);
+  }
+}
+
+// average pool, padding excluded from the count (Keras)
+__global__ __launch_bounds__(256) void avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                          int H, int W, int C, int OH, int OW, int KH, int KW, int S,
+                                                          int pad_t, int pad_l) {
+  const size_t total = (size_t)B * OH * OW * C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    size_t r = i / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    float acc = 0.f;
+    int n = 0;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int ih = oh * S - pad_t + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int iw = ow * S - pad_l + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        acc += x[(((size_t)b * H + ih) * W + iw) * C + c];
+        ++n;
+      }
+    }
+    y[i] = n ? acc / (float)n : 0.f;
+  }
+}
+
+// one input of a channel concat: y[p][off + c] = x[p][c]
+__global__ __launch_bounds__(256) void concat_f32_kernel(const float* __restrict__ x, int Cx, float* __restrict__ y,
+                                                         int Cy, int off, size_t pixels) {
+  const size_t total = pixels * Cx;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = i / Cx;
+    y[p * Cy + off + (i - p * Cx)] = x[i];
+  }
+}
+
+// y = act(a <op> b) (BinOp codes of layers.hip); b is a's shape or one [C] row per image (bcast_hw pixels)
+__global__ __launch_bounds__(256) void binary_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         float* __restrict__ y, size_t n, int C, int bcast_hw, int op,
+                                                         int act) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    size_t bi = i;
+    if (bcast_hw) {
+      const size_t pix = i / C;
+      bi = (pix / bcast_hw) * C + (i % C);
+    }
+    const float p = a[i], q = b[bi];
+    float r;
+    switch (op) {
+      case 1: r = p - q; break;
+      case 2: r = p * q; break;
+      case 3: r = fmaxf(p, q); break;
+      case 4: r = fminf(p, q); break;
+      case 5: r = 0.5f * (p + q); break;
+      default: r = p + q;
+    }
+    y[i] = act_f(r, act);
+  }
+}
+
+// y = act(x * scale[c] + shift[c]) (scale null: y = act(x)); any channel count
+__global__ __launch_bounds__(256) void affine_act_f32_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, float* __restrict__ y,
+                                                             size_t n, int C, int act, float alpha) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float v = x[i];
+    if (scale) {
+      const int c = (int)(i % C);
+      v = v * scale[c] + shift[c];
+    }
+    y[i] = act_f(v, act, alpha);
+  }
+}
+
 __global__ __launch_bounds__(256) void pad_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H,
                                                       int W, int C, int OH, int OW, int pad_t, int pad_l) {
   const size_t total = (size_t)B * OH * OW * C;
@@ -419,6 +526,39 @@ hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH,
                    hipStream_t s) {
   hipLaunchKernelGGL(pad_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C)), dim3(256), 0, s, x, y, B, H, W, C, OH,
                      OW, pad_t, pad_l);
+  return hipGetLastError();
+}
+
+hipError_t dwconv_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int OH,
+                      int OW, int KH, int KW, int S, int pad_t, int pad_l, int act, float alpha, hipStream_t s) {
+  hipLaunchKernelGGL(dwconv_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C)), dim3(256), 0, s, x, w, bias, y, B, H,
+                     W, C, OH, OW, KH, KW, S, pad_t, pad_l, act, alpha);
+  return hipGetLastError();
+}
+
+hipError_t avgpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int S,
+                       int pad_t, int pad_l, hipStream_t s) {
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C)), dim3(256), 0, s, x, y, B, H, W, C,
+                     OH, OW, KH, KW, S, pad_t, pad_l);
+  return hipGetLastError();
+}
+
+hipError_t concat_f32(const float* x, int Cx, float* y, int Cy, int off, size_t pixels, hipStream_t s) {
+  if (off + Cx > Cy) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(concat_f32_kernel, dim3(grid_for(pixels * Cx)), dim3(256), 0, s, x, Cx, y, Cy, off, pixels);
+  return hipGetLastError();
+}
+
+hipError_t binary_f32(const float* a, const float* b, float* y, size_t n, int C, int bcast_hw, int op, int act,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(binary_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, a, b, y, n, C, bcast_hw, op, act);
+  return hipGetLastError();
+}
+
+hipError_t affine_act_f32(const float* x, const float* scale, const float* shift, float* y, size_t n, int C, int act,
+                          float alpha, hipStream_t s) {
+  if ((scale == nullptr) != (shift == nullptr)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(affine_act_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, scale, shift, y, n, C, act, alpha);
   return hipGetLastError();
 }
 

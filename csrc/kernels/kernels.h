@@ -111,6 +111,15 @@ hipError_t eltwise_f32(const float* a, const float* b, const float* scale, const
                        int C, int op, int relu, hipStream_t s);
 hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int pad_t, int pad_l,
                    hipStream_t s);
+hipError_t dwconv_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int OH,
+                      int OW, int KH, int KW, int S, int pad_t, int pad_l, int act, float alpha, hipStream_t s);
+hipError_t avgpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int S,
+                       int pad_t, int pad_l, hipStream_t s);
+hipError_t concat_f32(const float* x, int Cx, float* y, int Cy, int off, size_t pixels, hipStream_t s);
+hipError_t binary_f32(const float* a, const float* b, float* y, size_t n, int C, int bcast_hw, int op, int act,
+                      hipStream_t s);
+hipError_t affine_act_f32(const float* x, const float* scale, const float* shift, float* y, size_t n, int C, int act,
+                          float alpha, hipStream_t s);
 // reversible zfp-style float32 codec on the GPU (zfp_gpu.hip), bit-exact with the host v2 container
 uint32_t zfp_gpu_maxw(int nd);
 uint64_t zfp_gpu_nblocks(const int64_t* shape, int nd);

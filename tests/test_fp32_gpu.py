@@ -147,3 +147,32 @@ def test_resnet50_bf16_logits_and_top1():
     top2 = np.sort(want, -1)[:, -2:]
     clear = (top2[:, 1] - top2[:, 0]) > 2 * rel * scale
     assert (logits.argmax(-1) == want.argmax(-1))[clear].all()
+
+
+@pytest.mark.parametrize("name", ["mobilenet_v2", "densenet121", "efficientnetb0", "inception_v3"])
+def test_other_families_fp32_logits_match_oracle(name):
+    """fp32 execution of the other Keras application families (depthwise conv,
+    average pool, concat, swish / sigmoid, squeeze-excite multiply, rescaling /
+    normalization layers on the fp32 kernels): logits vs the fp32 CPU oracle."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import \
+        init_weights
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.zoo import \
+        build_model
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.reference import \
+        ReferenceExecutor
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import \
+        SliceExecutor
+    g = build_model(name)
+    w = init_weights(g, seed=0)
+    shape = tuple(g.layers[g.input].out_shape)
+    x = np.random.default_rng(5).uniform(0, 255, (2,) + shape).astype(np.float32)
+    ex = SliceExecutor(g, w, batch=2, device="cuda:0", precision="fp32")
+    probs = ex(torch.from_numpy(x).cuda())
+    logits = ex.logits().double().cpu().numpy()
+    feat_name = g.layers[g.output].inputs[0]
+    feat = ReferenceExecutor(g, w, device="cpu").run({g.input: torch.from_numpy(x)}, outputs=[feat_name])[feat_name]
+    want = feat.double().reshape(2, -1).numpy() @ w[f"{g.output}/kernel"].astype(np.float64) + w[f"{g.output}/bias"]
+    rel = np.abs(logits - want).max() / np.abs(want).max()
+    assert rel <= 1e-3, f"{name} fp32 logits rel err {rel}"
+    assert (logits.argmax(-1) == want.argmax(-1)).all()
+    assert torch.isfinite(probs).all()
