@@ -51,6 +51,17 @@ __device__ __forceinline__ float act_f(float v, int mode, float alpha = 0.3f) {
   }
 }
 
+// Activation with the mode range fixed at compile time: GEN = false keeps a
+// kernel's inner loop to the ReLU family's two selects (the full switch of
+// act_f, expanded per element, made the memory-bound bn / add / dwconv
+// kernels instruction-bound: DenseNet121's unfused BN 5x slower);
+// launchers pick GEN = mode > ACT_RELU6.
+template <bool GEN>
+__device__ __forceinline__ float actx(float v, int mode, float alpha = 0.3f) {
+  if constexpr (GEN) return act_f(v, mode, alpha);
+  else return act_relu(v, mode);
+}
+
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): consecutive logical tiles land on the same XCD so neighbouring
 // tiles that share an A panel hit the same L2.

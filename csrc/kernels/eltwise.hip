@@ -39,6 +39,7 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float* __restrict
   }
 }
 
+template <bool GEN>
 __global__ __launch_bounds__(256) void bn_act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                      const float* __restrict__ scale, const float* __restrict__ shift,
                                                      size_t chunks, int C, int relu) {
@@ -50,12 +51,13 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const bf16* __restrict__ x,
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float f = bf2f(v.e[t]) * scale[c0 + t] + shift[c0 + t];
-      o.e[t] = f2bf(act_f(f, relu));
+      o.e[t] = f2bf(actx<GEN>(f, relu));
     }
     ((u32x4*)y)[i] = o.u;
   }
 }
 
+template <bool GEN>
 __global__ __launch_bounds__(256) void add_act_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
                                                       bf16* __restrict__ y, size_t chunks, int relu) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < chunks; i += (size_t)gridDim.x * blockDim.x) {
@@ -65,19 +67,20 @@ __global__ __launch_bounds__(256) void add_act_kernel(const bf16* __restrict__ a
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float f = bf2f(va.e[t]) + bf2f(vb.e[t]);
-      o.e[t] = f2bf(act_f(f, relu));
+      o.e[t] = f2bf(actx<GEN>(f, relu));
     }
     ((u32x4*)y)[i] = o.u;
   }
 }
 
+template <bool GEN>
 __global__ __launch_bounds__(256) void relu_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, size_t chunks,
                                                    int mode) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < chunks; i += (size_t)gridDim.x * blockDim.x) {
     V8 v, o;
     v.u = ((const u32x4*)x)[i];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(bf2f(v.e[t]), mode));
+    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(bf2f(v.e[t]), mode));
     ((u32x4*)y)[i] = o.u;
   }
 }
@@ -186,17 +189,22 @@ hipError_t input_pack(const float* x, bf16* y, size_t pixels, int C, int Cp, hip
 hipError_t bn_act(const bf16* x, bf16* y, const float* scale, const float* shift, size_t elems, int C, int relu,
                   hipStream_t s) {
   size_t chunks = elems / 8;
-  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, scale, shift, chunks, C, relu);
+  if (relu > ACT_RELU6)
+    hipLaunchKernelGGL(bn_act_kernel<true>, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, scale, shift, chunks, C, relu);
+  else
+    hipLaunchKernelGGL(bn_act_kernel<false>, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, scale, shift, chunks, C, relu);
   return hipGetLastError();
 }
 hipError_t add_act(const bf16* a, const bf16* b, bf16* y, size_t elems, int relu, hipStream_t s) {
   size_t chunks = elems / 8;
-  hipLaunchKernelGGL(add_act_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a, b, y, chunks, relu);
+  if (relu > ACT_RELU6) hipLaunchKernelGGL(add_act_kernel<true>, dim3(grid_for(chunks)), dim3(256), 0, s, a, b, y, chunks, relu);
+  else hipLaunchKernelGGL(add_act_kernel<false>, dim3(grid_for(chunks)), dim3(256), 0, s, a, b, y, chunks, relu);
   return hipGetLastError();
 }
 hipError_t relu(const bf16* x, bf16* y, size_t elems, int mode, hipStream_t s) {
   size_t chunks = elems / 8;
-  hipLaunchKernelGGL(relu_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, chunks, mode);
+  if (mode > ACT_RELU6) hipLaunchKernelGGL(relu_kernel<true>, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, chunks, mode);
+  else hipLaunchKernelGGL(relu_kernel<false>, dim3(grid_for(chunks)), dim3(256), 0, s, x, y, chunks, mode);
   return hipGetLastError();
 }
 hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,

@@ -20,6 +20,7 @@ inline unsigned grid_of(size_t n) {
 // Depthwise KHxKW conv (depth multiplier 1): y[b,oh,ow,c] = act(sum_taps x * w[kh][kw][c] + bias[c]),
 // BN folded into w/bias on the host; zero padding is implicit (pad_t / pad_l, Keras 'same' or a folded
 // ZeroPadding2D).  w: fp32 [KH][KW][Cp].
+template <bool GEN>
 __global__ __launch_bounds__(256) void dwconv_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias, bf16* __restrict__ y, int B,
                                                      int H, int W, int Cp, int OH, int OW, int KH, int KW,
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16* __restrict__ x,
     }
     V8 o;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(acc[t], act));
+    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(acc[t], act));
     *(u32x4*)(y + i * 8) = o.u;
   }
 }
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16* __restrict__ x,
 // 3x3 specialisation: a thread owns OWG consecutive output pixels of one row and one 8-channel chunk, so
 // each input column of the (OWG-1)*S+3 it touches is loaded once per filter row (6 loads per row instead of
 // 12 at stride 1, 9 instead of 12 at stride 2) and the row's three weight vectors stay in registers.
-template <int S, int OWG>
+template <int S, int OWG, bool GEN>
 __global__ __launch_bounds__(256) void dwconv3_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ bias, bf16* __restrict__ y, int B,
                                                       int H, int W, int Cp, int OH, int OW, int pad_t, int pad_l,
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const bf16* __restrict__ x
       if (ow0 + j >= OW) break;
       V8 o;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(acc[j][t], act));
+      for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(acc[j][t], act));
       *(u32x4*)(y + (((size_t)b * OH + oh) * OW + ow0 + j) * Cp + c0) = o.u;
     }
   }
@@ -197,13 +198,14 @@ __global__ __launch_bounds__(256) void concat_scalar_kernel(const bf16* __restri
 }
 
 // Standalone activation (any ActMode, LeakyReLU slope alpha) over bf16 chunks.
+template <bool GEN>
 __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, size_t chunks,
                                                   int mode, float alpha) {
   for (size_t i = gtid(); i < chunks; i += gstride()) {
     V8 v, o;
     v.u = ((const u32x4*)x)[i];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(act_f(bf2f(v.e[t]), mode, alpha));
+    for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(bf2f(v.e[t]), mode, alpha));
     ((u32x4*)y)[i] = o.u;
   }
 }
@@ -212,6 +214,7 @@ __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf
 // with b, where b is either the same shape or one [Cp] row per image (bcast_hw = H*W pixels share it: the
 // squeeze-excite Multiply of EfficientNet, x * se[b, 1, 1, c]).
 enum BinOp { BIN_ADD = 0, BIN_SUB, BIN_MUL, BIN_MAX, BIN_MIN, BIN_AVG };
+template <bool GEN>
 __global__ __launch_bounds__(256) void binary_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
                                                      bf16* __restrict__ y, size_t chunks, int cpr, int bcast_hw,
                                                      int op, int act) {
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(256) void binary_kernel(const bf16* __restrict__ a,
         case BIN_AVG: r = 0.5f * (p + q); break;
         default: r = p + q;
       }
-      o.e[t] = f2bf(act_f(r, act));
+      o.e[t] = f2bf(actx<GEN>(r, act));
     }
     ((u32x4*)y)[i] = o.u;
   }
@@ -343,15 +346,20 @@ hipError_t gap_large(const bf16* x, bf16* y, float* y32, float* part, int B, int
 
 hipError_t act(const bf16* x, bf16* y, size_t elems, int mode, float alpha, hipStream_t s) {
   if (elems % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(act_kernel, dim3(grid_of(elems / 8)), dim3(256), 0, s, x, y, elems / 8, mode, alpha);
+  if (mode > ACT_RELU6) hipLaunchKernelGGL(act_kernel<true>, dim3(grid_of(elems / 8)), dim3(256), 0, s, x, y, elems / 8, mode, alpha);
+  else hipLaunchKernelGGL(act_kernel<false>, dim3(grid_of(elems / 8)), dim3(256), 0, s, x, y, elems / 8, mode, alpha);
   return hipGetLastError();
 }
 
 hipError_t binary(const bf16* a, const bf16* b, bf16* y, size_t elems, int Cp, int bcast_hw, int op, int act_mode,
                   hipStream_t s) {
   if (elems % 8 || Cp % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(binary_kernel, dim3(grid_of(elems / 8)), dim3(256), 0, s, a, b, y, elems / 8, Cp / 8, bcast_hw,
-                     op, act_mode);
+  if (act_mode > ACT_RELU6)
+    hipLaunchKernelGGL(binary_kernel<true>, dim3(grid_of(elems / 8)), dim3(256), 0, s, a, b, y, elems / 8, Cp / 8,
+                       bcast_hw, op, act_mode);
+  else
+    hipLaunchKernelGGL(binary_kernel<false>, dim3(grid_of(elems / 8)), dim3(256), 0, s, a, b, y, elems / 8, Cp / 8,
+                       bcast_hw, op, act_mode);
   return hipGetLastError();
 }
 
@@ -370,13 +378,21 @@ hipError_t dwconv(const bf16* x, const float* w, const float* bias, bf16* y, int
   constexpr int OWG = 4;
   const size_t t3 = (size_t)B * OH * ((OW + OWG - 1) / OWG) * (Cp / 8);
   if (KH == 3 && KW == 3 && stride == 1 && t3 >= 512 * 256) {
-    hipLaunchKernelGGL((dwconv3_kernel<1, OWG>), dim3(grid_of(t3)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp, OH,
-                       OW, pad_t, pad_l, act);
+    if (act > ACT_RELU6)
+      hipLaunchKernelGGL((dwconv3_kernel<1, OWG, true>), dim3(grid_of(t3)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp,
+                         OH, OW, pad_t, pad_l, act);
+    else
+      hipLaunchKernelGGL((dwconv3_kernel<1, OWG, false>), dim3(grid_of(t3)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp,
+                         OH, OW, pad_t, pad_l, act);
     return hipGetLastError();
   }
   const size_t total = (size_t)B * OH * OW * (Cp / 8);
-  hipLaunchKernelGGL(dwconv_kernel, dim3(grid_of(total)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp, OH, OW, KH,
-                     KW, stride, pad_t, pad_l, act);
+  if (act > ACT_RELU6)
+    hipLaunchKernelGGL(dwconv_kernel<true>, dim3(grid_of(total)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp, OH, OW,
+                       KH, KW, stride, pad_t, pad_l, act);
+  else
+    hipLaunchKernelGGL(dwconv_kernel<false>, dim3(grid_of(total)), dim3(256), 0, s, x, w, bias, y, B, H, W, Cp, OH, OW,
+                       KH, KW, stride, pad_t, pad_l, act);
   return hipGetLastError();
 }
 
