@@ -281,12 +281,22 @@ def maxpool_f32(x: torch.Tensor, out: torch.Tensor, k: int, s: int, pad_t: int =
     return out
 
 
-def gap_f32(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+def gap_f32(x: torch.Tensor, out: torch.Tensor, stream=None, scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 GAP; maps of >= GAP_LARGE_HW pixels take the sliced two-pass kernel and its fp32 `scratch`
+    (gap_scratch_elems)."""
     _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
     B, H, W, C = x.shape
     if out.numel() != B * C or C % 4:
         raise ValueError("fp32 GAP: out must be [B][C], C a multiple of 4")
-    kernels().gap_f32(ptr(x), ptr(out), B, H * W, C, stream_handle(stream))
+    need = gap_scratch_elems(B, H * W, C)
+    if need:
+        if scratch is None:
+            scratch = torch.empty(need, dtype=torch.float32, device=x.device)
+        if scratch.numel() < need or scratch.dtype != torch.float32:
+            raise ValueError(f"fp32 gap over {H}x{W}: needs an fp32 scratch of {need} elements")
+        kernels().gap_large_f32(ptr(x), ptr(out), ptr(scratch), B, H * W, C, stream_handle(stream))
+    else:
+        kernels().gap_f32(ptr(x), ptr(out), B, H * W, C, stream_handle(stream))
     return out
 
 

@@ -333,7 +333,7 @@ class SliceExecutor:
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
         self._gap_part: Dict[int, torch.Tensor] = {}
         for i, st in enumerate(self.steps):
-            if st.kind == "gap" and self.device.type == "cuda" and not self.fp32:
+            if st.kind == "gap" and self.device.type == "cuda":
                 shp = self.shape_of(st.ins[0])
                 if len(shp) == 4:
                     need = E.gap_scratch_elems(shp[0], shp[1] * shp[2], shp[3])
@@ -789,7 +789,7 @@ class SliceExecutor:
             E.maxpool_f32(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, st.p.get("pad_zero", True),
                           stream=stream)
         elif k == "gap":
-            E.gap_f32(b[st.ins[0]], b[st.out], stream=stream)
+            E.gap_f32(b[st.ins[0]], b[st.out], stream=stream, scratch=self._gap_part.get(i))
         elif k == "softmax":
             E.softmax_rows(b[st.ins[0]], b[st.out], stream=stream)
         elif k == "add":

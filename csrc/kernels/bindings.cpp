@@ -198,6 +198,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_f32", [](u64 x, u64 y, int B, int HW, int C, u64 s) {
     check(adapt::gap_f32(P<const float>(x), P<float>(y), B, HW, C, S(s)), "gap_f32");
   });
+  m.def("gap_large_f32", [](u64 x, u64 y, u64 part, int B, int HW, int C, u64 s) {
+    check(adapt::gap_large_f32(P<const float>(x), P<float>(y), P<float>(part), B, HW, C, S(s)), "gap_large_f32");
+  });
   m.def("eltwise_f32", [](u64 a, u64 b, u64 scale, u64 shift, u64 y, size_t n, int C, int op, int relu, u64 s) {
     check(adapt::eltwise_f32(P<const float>(a), P<const float>(b), P<const float>(scale), P<const float>(shift),
                              P<float>(y), n, C, op, relu, S(s)), "eltwise_f32");

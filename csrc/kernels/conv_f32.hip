@@ -25,6 +25,9 @@
 //   group writes 16 consecutive floats (64 B) of the output row;
 // * split-K: fp32 partial slabs + a reduce launch that applies the epilogue.
 #include "kernels.h"
+#include <algorithm>
+#include <cstdint>
+#include <initializer_list>
 
 namespace adapt {
 
@@ -348,6 +351,49 @@ __global__ __launch_bounds__(256) void gap_f32_kernel(const float* __restrict__ 
   *(f32x4*)(y + (size_t)b * C + c4 * 4) = s * inv;
 }
 
+// GAP over large maps (the squeeze-excite pools of EfficientNet run over up to
+// 112x112 pixels: one thread per channel chunk walking every pixel left most
+// of the chip idle): pass 1, grid (S pixel slices, B); a block sums its slice
+// for up to 256 float4 channel chunks (the other threads stride the pixels)
+// and reduces in LDS; pass 2 adds the S partials and divides by HW.
+__global__ __launch_bounds__(256) void gap_part_f32_kernel(const float* __restrict__ x, float* __restrict__ part,
+                                                           int HW, int C, int S) {
+  __shared__ f32x4 red[256];
+  const int b = blockIdx.y, sl = blockIdx.x;
+  const int C4 = C / 4;
+  const int p0 = (int)((long long)HW * sl / S), p1 = (int)((long long)HW * (sl + 1) / S);
+  for (int cg = 0; cg < C4; cg += 256) {
+    const int nc = min(256, C4 - cg);
+    const int lanes = 256 / nc;
+    const int ch = threadIdx.x % nc, pl = threadIdx.x / nc;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (pl < lanes) {
+      const float* base = x + (size_t)b * HW * C + (size_t)(cg + ch) * 4;
+      for (int q = p0 + pl; q < p1; q += lanes) acc += *(const f32x4*)(base + (size_t)q * C);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < nc) {
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int l = 0; l < lanes; ++l) sum += red[l * nc + threadIdx.x];
+      *(f32x4*)(part + ((size_t)b * S + sl) * C + (size_t)(cg + threadIdx.x) * 4) = sum;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void gap_finish_f32_kernel(const float* __restrict__ part, float* __restrict__ y,
+                                                             int B, int HW, int C, int S) {
+  const size_t total = (size_t)B * C;
+  const float inv = 1.f / (float)HW;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = i / C, c = i % C;
+    float sum = 0.f;
+    for (int sl = 0; sl < S; ++sl) sum += part[(b * S + sl) * C + c];
+    y[i] = sum * inv;
+  }
+}
+
 // elementwise fp32: mode 0 add(+act) a+b, 1 bn affine y = x*scale[c]+shift[c] (+act), 2 act only
 __global__ __launch_bounds__(256) void eltwise_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                           const float* __restrict__ scale,
@@ -374,6 +420,7 @@ __global__ __launch_bounds__(256) void eltwise_f32_kernel(const float* __restric
 // plain element-per-thread kernels over the true channel count (fp32 activations carry no padding)
 
 // depthwise conv, multiplier 1, BN folded: y[b][oh][ow][c] = act(sum x * w[kh][kw][c] + bias[c])
+template <bool GEN>
 __global__ __launch_bounds__(256) void dwconv_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ y,
                                                          int B, int H, int W, int C, int OH, int OW, int KH, int KW,
@@ -396,7 +443,7 @@ __global__ __launch_bounds__(256) void dwconv_f32_kernel(const float* __restrict
         acc = fmaf(x[(((size_t)b * H + ih) * W + iw) * C + c], w[(kh * KW + kw) * C + c], acc);
       }
     }
-    y[i] = act_f(acc, act, alpha);
+    y[i] = actx<GEN>(acc, act, alpha);
   }
 }
 
@@ -439,6 +486,7 @@ __global__ __launch_bounds__(256) void concat_f32_kernel(const float* __restrict
 }
 
 // y = act(a <op> b) (BinOp codes of layers.hip); b is a's shape or one [C] row per image (bcast_hw pixels)
+template <bool GEN>
 __global__ __launch_bounds__(256) void binary_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                          float* __restrict__ y, size_t n, int C, int bcast_hw, int op,
                                                          int act) {
@@ -458,11 +506,12 @@ __global__ __launch_bounds__(256) void binary_f32_kernel(const float* __restrict
       case 5: r = 0.5f * (p + q); break;
       default: r = p + q;
     }
-    y[i] = act_f(r, act);
+    y[i] = actx<GEN>(r, act);
   }
 }
 
 // y = act(x * scale[c] + shift[c]) (scale null: y = act(x)); any channel count
+template <bool GEN>
 __global__ __launch_bounds__(256) void affine_act_f32_kernel(const float* __restrict__ x,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift, float* __restrict__ y,
@@ -473,8 +522,135 @@ __global__ __launch_bounds__(256) void affine_act_f32_kernel(const float* __rest
       const int c = (int)(i % C);
       v = v * scale[c] + shift[c];
     }
-    y[i] = act_f(v, act, alpha);
+    y[i] = actx<GEN>(v, act, alpha);
   }
+}
+
+// ---- the same layers four channels per thread (every family's channel counts are multiples of 4): one
+// 16-byte load / store per tap and 32-bit index math; the launchers take these whenever C % 4 == 0 and the
+// tensor indexes in 32 bits, the scalar kernels above otherwise
+
+template <bool GEN>
+__device__ __forceinline__ f32x4 actx4(f32x4 v, int mode, float alpha = 0.3f) {
+  v[0] = actx<GEN>(v[0], mode, alpha); v[1] = actx<GEN>(v[1], mode, alpha);
+  v[2] = actx<GEN>(v[2], mode, alpha); v[3] = actx<GEN>(v[3], mode, alpha);
+  return v;
+}
+
+template <bool GEN, int K>
+__global__ __launch_bounds__(256) void dwconv_f32v_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, float* __restrict__ y,
+                                                          int B, int H, int W, int C, int OH, int OW, int KH, int KW,
+                                                          int S, int pad_t, int pad_l, int act, float alpha) {
+  if constexpr (K > 0) { KH = K; KW = K; }
+  const int C4 = C >> 2;
+  const unsigned total = (unsigned)B * OH * OW * C4;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    unsigned r = i / C4;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    f32x4 acc = bias ? *(const f32x4*)(bias + c4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* xb = x + (unsigned)b * H * W * C + c4 * 4;
+#pragma unroll
+    for (int kh = 0; kh < (K > 0 ? K : KH); ++kh) {
+      const int ih = oh * S - pad_t + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+      for (int kw = 0; kw < (K > 0 ? K : KW); ++kw) {
+        const int iw = ow * S - pad_l + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const f32x4 xv = *(const f32x4*)(xb + (unsigned)(ih * W + iw) * C);
+        const f32x4 wv = *(const f32x4*)(w + (kh * KW + kw) * C + c4 * 4);
+        acc += xv * wv;
+      }
+    }
+    *(f32x4*)(y + i * 4) = actx4<GEN>(acc, act, alpha);
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool_f32v_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                           int H, int W, int C, int OH, int OW, int KH, int KW, int S,
+                                                           int pad_t, int pad_l) {
+  const int C4 = C >> 2;
+  const unsigned total = (unsigned)B * OH * OW * C4;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    unsigned r = i / C4;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    const int h0 = max(oh * S - pad_t, 0), h1 = min(oh * S - pad_t + KH, H);
+    const int w0 = max(ow * S - pad_l, 0), w1 = min(ow * S - pad_l + KW, W);
+    const float* xb = x + (unsigned)b * H * W * C + c4 * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ih = h0; ih < h1; ++ih)
+      for (int iw = w0; iw < w1; ++iw) acc += *(const f32x4*)(xb + (unsigned)(ih * W + iw) * C);
+    const int n = (h1 - h0) * (w1 - w0);
+    *(f32x4*)(y + i * 4) = n > 0 ? acc * (1.f / (float)n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+__global__ __launch_bounds__(256) void concat_f32v_kernel(const float* __restrict__ x, int Cx, float* __restrict__ y,
+                                                          int Cy, int off, unsigned pixels) {
+  const int C4 = Cx >> 2;
+  const unsigned total = pixels * C4;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned p = i / C4;
+    *(f32x4*)(y + p * Cy + off + (i - p * C4) * 4) = *(const f32x4*)(x + i * 4);
+  }
+}
+
+template <bool GEN>
+__global__ __launch_bounds__(256) void binary_f32v_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                          float* __restrict__ y, unsigned n4, int C, int bcast_hw,
+                                                          int op, int act) {
+  const int C4 = C >> 2;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    unsigned bi = i;
+    if (bcast_hw) {
+      const unsigned pix = i / C4;
+      bi = (pix / bcast_hw) * C4 + (i - pix * C4);
+    }
+    const f32x4 p = *(const f32x4*)(a + i * 4), q = *(const f32x4*)(b + bi * 4);
+    f32x4 r;
+    switch (op) {
+      case 1: r = p - q; break;
+      case 2: r = p * q; break;
+      case 3: for (int j = 0; j < 4; ++j) r[j] = fmaxf(p[j], q[j]); break;
+      case 4: for (int j = 0; j < 4; ++j) r[j] = fminf(p[j], q[j]); break;
+      case 5: r = 0.5f * (p + q); break;
+      default: r = p + q;
+    }
+    *(f32x4*)(y + i * 4) = actx4<GEN>(r, act);
+  }
+}
+
+template <bool GEN>
+__global__ __launch_bounds__(256) void affine_act_f32v_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, float* __restrict__ y,
+                                                              unsigned n4, int C, int act, float alpha) {
+  const int C4 = C >> 2;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    f32x4 v = *(const f32x4*)(x + i * 4);
+    if (scale) {
+      const int c = (int)(i % C4) * 4;
+      v = v * *(const f32x4*)(scale + c) + *(const f32x4*)(shift + c);
+    }
+    *(f32x4*)(y + i * 4) = actx4<GEN>(v, act, alpha);
+  }
+}
+
+// 16-byte paths need 16-byte aligned bases and a 32-bit index space
+bool vec_ok(std::initializer_list<const void*> ps, size_t n) {
+  if (n >= (size_t(1) << 31)) return false;
+  for (const void* p : ps)
+    if (reinterpret_cast<uintptr_t>(p) & 15) return false;
+  return true;
 }
 
 __global__ __launch_bounds__(256) void pad_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H,
@@ -514,6 +690,16 @@ hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s
   return hipGetLastError();
 }
 
+hipError_t gap_large_f32(const float* x, float* y, float* part, int B, int HW, int C, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  const int S = gap_large_slices(B, HW);
+  hipLaunchKernelGGL(gap_part_f32_kernel, dim3(S, B), dim3(256), 0, s, x, part, HW, C, S);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gap_finish_f32_kernel, dim3(grid_for((size_t)B * C)), dim3(256), 0, s, part, y, B, HW, C, S);
+  return hipGetLastError();
+}
+
 hipError_t eltwise_f32(const float* a, const float* b, const float* scale, const float* shift, float* y, size_t n,
                        int C, int op, int relu, hipStream_t s) {
   if (n % 4 || C % 4) return hipErrorInvalidValue;
@@ -531,34 +717,91 @@ hipError_t pad_f32(const float* x, float* y, int B, int H, int W, int C, int OH,
 
 hipError_t dwconv_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int OH,
                       int OW, int KH, int KW, int S, int pad_t, int pad_l, int act, float alpha, hipStream_t s) {
-  hipLaunchKernelGGL(dwconv_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C)), dim3(256), 0, s, x, w, bias, y, B, H,
-                     W, C, OH, OW, KH, KW, S, pad_t, pad_l, act, alpha);
+  const size_t n = (size_t)B * OH * OW * C;
+  if (C % 4 == 0 && vec_ok({x, w, bias, y}, std::max(n, (size_t)B * H * W * C))) {
+    const dim3 gv(grid_for(n / 4));
+#define DWV(G, K)                                                                                                     \
+  hipLaunchKernelGGL((dwconv_f32v_kernel<G, K>), gv, dim3(256), 0, s, x, w, bias, y, B, H, W, C, OH, OW, KH, KW, S, \
+                     pad_t, pad_l, act, alpha)
+    const int k = (KH == KW && (KH == 3 || KH == 5)) ? KH : 0;
+    const bool gen = act > ACT_RELU6;
+    if (k == 3) { if (gen) DWV(true, 3); else DWV(false, 3); }
+    else if (k == 5) { if (gen) DWV(true, 5); else DWV(false, 5); }
+    else { if (gen) DWV(true, 0); else DWV(false, 0); }
+#undef DWV
+    return hipGetLastError();
+  }
+  const dim3 g(grid_for(n));
+  if (act > ACT_RELU6)
+    hipLaunchKernelGGL(dwconv_f32_kernel<true>, g, dim3(256), 0, s, x, w, bias, y, B, H, W, C, OH, OW, KH, KW, S, pad_t,
+                       pad_l, act, alpha);
+  else
+    hipLaunchKernelGGL(dwconv_f32_kernel<false>, g, dim3(256), 0, s, x, w, bias, y, B, H, W, C, OH, OW, KH, KW, S, pad_t,
+                       pad_l, act, alpha);
   return hipGetLastError();
 }
 
 hipError_t avgpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int S,
                        int pad_t, int pad_l, hipStream_t s) {
-  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(grid_for((size_t)B * OH * OW * C)), dim3(256), 0, s, x, y, B, H, W, C,
+  const size_t n = (size_t)B * OH * OW * C;
+  if (C % 4 == 0 && vec_ok({x, y}, std::max(n, (size_t)B * H * W * C))) {
+    hipLaunchKernelGGL(avgpool_f32v_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, x, y, B, H, W, C, OH, OW, KH, KW, S,
+                       pad_t, pad_l);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, B, H, W, C,
                      OH, OW, KH, KW, S, pad_t, pad_l);
   return hipGetLastError();
 }
 
 hipError_t concat_f32(const float* x, int Cx, float* y, int Cy, int off, size_t pixels, hipStream_t s) {
   if (off + Cx > Cy) return hipErrorInvalidValue;
+  if (Cx % 4 == 0 && Cy % 4 == 0 && off % 4 == 0 && vec_ok({x, y}, pixels * Cy)) {
+    hipLaunchKernelGGL(concat_f32v_kernel, dim3(grid_for(pixels * Cx / 4)), dim3(256), 0, s, x, Cx, y, Cy, off,
+                       (unsigned)pixels);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(concat_f32_kernel, dim3(grid_for(pixels * Cx)), dim3(256), 0, s, x, Cx, y, Cy, off, pixels);
   return hipGetLastError();
 }
 
 hipError_t binary_f32(const float* a, const float* b, float* y, size_t n, int C, int bcast_hw, int op, int act,
                       hipStream_t s) {
-  hipLaunchKernelGGL(binary_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, a, b, y, n, C, bcast_hw, op, act);
+  if (C % 4 == 0 && n % 4 == 0 && vec_ok({a, b, y}, n)) {
+    const dim3 gv(grid_for(n / 4));
+    if (act > ACT_RELU6)
+      hipLaunchKernelGGL(binary_f32v_kernel<true>, gv, dim3(256), 0, s, a, b, y, (unsigned)(n / 4), C, bcast_hw, op, act);
+    else
+      hipLaunchKernelGGL(binary_f32v_kernel<false>, gv, dim3(256), 0, s, a, b, y, (unsigned)(n / 4), C, bcast_hw, op,
+                         act);
+    return hipGetLastError();
+  }
+  if (act > ACT_RELU6)
+    hipLaunchKernelGGL(binary_f32_kernel<true>, dim3(grid_for(n)), dim3(256), 0, s, a, b, y, n, C, bcast_hw, op, act);
+  else
+    hipLaunchKernelGGL(binary_f32_kernel<false>, dim3(grid_for(n)), dim3(256), 0, s, a, b, y, n, C, bcast_hw, op, act);
   return hipGetLastError();
 }
 
 hipError_t affine_act_f32(const float* x, const float* scale, const float* shift, float* y, size_t n, int C, int act,
                           float alpha, hipStream_t s) {
   if ((scale == nullptr) != (shift == nullptr)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(affine_act_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, scale, shift, y, n, C, act, alpha);
+  if (C % 4 == 0 && n % 4 == 0 && vec_ok({x, scale, shift, y}, n)) {
+    const dim3 gv(grid_for(n / 4));
+    if (act > ACT_RELU6)
+      hipLaunchKernelGGL(affine_act_f32v_kernel<true>, gv, dim3(256), 0, s, x, scale, shift, y, (unsigned)(n / 4), C, act,
+                         alpha);
+    else
+      hipLaunchKernelGGL(affine_act_f32v_kernel<false>, gv, dim3(256), 0, s, x, scale, shift, y, (unsigned)(n / 4), C,
+                         act, alpha);
+    return hipGetLastError();
+  }
+  if (act > ACT_RELU6)
+    hipLaunchKernelGGL(affine_act_f32_kernel<true>, dim3(grid_for(n)), dim3(256), 0, s, x, scale, shift, y, n, C, act,
+                       alpha);
+  else
+    hipLaunchKernelGGL(affine_act_f32_kernel<false>, dim3(grid_for(n)), dim3(256), 0, s, x, scale, shift, y, n, C, act,
+                       alpha);
   return hipGetLastError();
 }
 

@@ -100,6 +100,53 @@ def test_f32_layers():
     assert torch.equal(p.cpu(), F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1)).permute(0, 2, 3, 1))
 
 
+@pytest.mark.parametrize("shape", [(2, 56, 56, 96), (3, 33, 40, 1160), (1, 112, 112, 32)])
+def test_gap_f32_large_map_sliced(shape):
+    """Maps of >= GAP_LARGE_HW pixels take the two-pass sliced kernel (C/4 > 256 exercises the channel groups)."""
+    x = torch.from_numpy(np.random.default_rng(4).standard_normal(shape).astype(np.float32))
+    B, H, W, Cc = shape
+    assert H * W >= E.GAP_LARGE_HW
+    g = torch.empty((B, Cc), device="cuda")
+    E.gap_f32(x.cuda(), g)
+    torch.cuda.synchronize()
+    want = x.double().mean(dim=(1, 2))
+    assert torch.allclose(g.cpu().double(), want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("C", [8, 6])             # 4-channel vector kernels / scalar fallback
+@pytest.mark.parametrize("k,stride", [(3, 1), (5, 2), (2, 1)])
+def test_f32_dwconv_avgpool_vector_and_scalar(C, k, stride):
+    rng = np.random.default_rng(7)
+    x = torch.from_numpy(rng.standard_normal((2, 13, 11, C)).astype(np.float32))
+    w = torch.from_numpy(rng.standard_normal((k, k, C)).astype(np.float32))
+    bias = torch.from_numpy(rng.standard_normal(C).astype(np.float32))
+    p = k // 2
+    OH, OW = (13 + 2 * p - k) // stride + 1, (11 + 2 * p - k) // stride + 1
+    xt = F.pad(x.permute(0, 3, 1, 2).double(), (p, p, p, p))
+    for act, fn in ((1, lambda t: t.clamp_min(0)), (3, lambda t: t * torch.sigmoid(t))):
+        y = torch.empty((2, OH, OW, C), device="cuda")
+        E.dwconv_f32(x.cuda(), w.cuda(), bias.cuda(), y, stride, ((p, p), (p, p)), act=act)
+        want = F.conv2d(xt, w.double().permute(2, 0, 1).unsqueeze(1), bias.double(), stride=stride, groups=C)
+        assert torch.allclose(y.cpu().double(), fn(want).permute(0, 2, 3, 1), rtol=1e-5, atol=1e-5)
+    y = torch.empty((2, OH, OW, C), device="cuda")
+    E.avgpool_f32(x.cuda(), y, k, stride, ((p, p), (p, p)))
+    want = F.avg_pool2d(xt, k, stride, count_include_pad=False) if p == 0 else \
+        F.avg_pool2d(x.permute(0, 3, 1, 2).double(), k, stride, padding=p, count_include_pad=False)
+    assert torch.allclose(y.cpu().double(), want.permute(0, 2, 3, 1), rtol=1e-5, atol=1e-6)
+    a = x.cuda()
+    se = torch.from_numpy(rng.standard_normal((2, C)).astype(np.float32)).cuda()
+    o = torch.empty_like(a)
+    E.binary_f32(a, se, o, "mul")
+    assert torch.allclose(o, a * se[:, None, None, :], rtol=1e-6, atol=1e-6)
+    sc, sh = torch.rand(C, device="cuda"), torch.rand(C, device="cuda")
+    E.affine_act_f32(a, o, sc, sh, act=3)
+    t = a * sc + sh
+    assert torch.allclose(o, t * torch.sigmoid(t), rtol=1e-5, atol=1e-5)
+    cat = torch.empty((2, 13, 11, 2 * C), device="cuda")
+    E.concat_f32([a, o], cat)
+    assert torch.equal(cat, torch.cat([a, o], dim=-1))
+
+
 def _oracle_logits(g, w, x):
     from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops.reference import \
         ReferenceExecutor
