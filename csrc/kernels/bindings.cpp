@@ -198,7 +198,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_f32", [](u64 x, u64 y, int B, int HW, int C, u64 s) {
     check(adapt::gap_f32(P<const float>(x), P<float>(y), B, HW, C, S(s)), "gap_f32");
   });
-  m.def("set_store_policy", [](int v) { check(adapt::set_store_policy(v), "set_store_policy"); });
   m.def("gap_large_f32", [](u64 x, u64 y, u64 part, int B, int HW, int C, u64 s) {
     check(adapt::gap_large_f32(P<const float>(x), P<float>(y), P<float>(part), B, HW, C, S(s)), "gap_large_f32");
   });

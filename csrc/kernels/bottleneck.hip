@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256, 2) void bottleneck_kernel(BottleneckParams p) 
       const int gy = ty * BT + (px >> 3), gx = tx * BT + (px & 7);
       const u32x4 v = *(const u32x4*)(os + sw<32>(px, c));
       if constexpr (ABL & 8) asm volatile("" ::"v"(v));
-      else store_out16(p.out + (((size_t)img * p.H + gy) * p.W + gx) * CO + c * 8, v, ST_BOTTLENECK);
+      else *(u32x4*)(p.out + (((size_t)img * p.H + gy) * p.W + gx) * CO + c * 8) = v;
     }
   }
 }
@@ -357,7 +357,5 @@ hipError_t bottleneck_forward(const BottleneckParams& p, int cin, bool proj, hip
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
-
-ADAPT_STORE_POLICY_SETTER(bottleneck)
 
 }  // namespace adapt

@@ -56,39 +56,6 @@ __device__ __forceinline__ float act_f(float v, int mode, float alpha = 0.3f) {
 // act_f, expanded per element, made the memory-bound bn / add / dwconv
 // kernels instruction-bound: DenseNet121's unfused BN 5x slower);
 // launchers pick GEN = mode > ACT_RELU6.
-// 16-byte output store, plain or write-through (sc1).  A write-through line
-// leaves the XCD's L2 at once instead of staying dirty until the end-of-kernel
-// L2 write-back that every dependent launch waits for; a plain line stays in
-// this XCD's L2 for a same-XCD reader.  Which pays depends on the producer, so
-// the choice is a per-site bit of g_store_policy (one copy per translation
-// unit, all set together by set_store_policy(); measured by
-// tools/store_policy_ab.py).  The trailing s_nop keeps hipcc's next
-// instruction from overwriting the data registers before the store reads them.
-enum StoreSite {
-  ST_CONV = 1,          // implicit-GEMM conv epilogues (bf16 tiles)
-  ST_SPLITK = 2,        // split-K fp32 partial slabs
-  ST_BOTTLENECK = 4,    // fused bottleneck block output
-  ST_STEM = 8,          // fused stem output
-  ST_ELTWISE = 16,      // BN / add / relu / pad element-wise kernels
-  ST_LAYERS = 32,       // depthwise / pool / concat / activation / binary kernels
-  ST_HEAD = 64,         // GAP feature rows of the classifier head
-};
-#ifndef ADAPT_STORE_POLICY_DEFAULT
-#define ADAPT_STORE_POLICY_DEFAULT (ST_CONV | ST_BOTTLENECK)
-#endif
-static __device__ int g_store_policy = ADAPT_STORE_POLICY_DEFAULT;
-#define ADAPT_STORE_POLICY_SETTER(tag)                                                  \
-  hipError_t set_store_policy_##tag(int v) {                                           \
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_store_policy), &v, sizeof(v));               \
-  }
-
-__device__ __forceinline__ void store_out16(void* p, u32x4 v, int site) {
-  if (g_store_policy & site)
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-  else
-    *(u32x4*)p = v;
-}
-
 template <bool GEN>
 __device__ __forceinline__ float actx(float v, int mode, float alpha = 0.3f) {
   if constexpr (GEN) return act_f(v, mode, alpha);

@@ -406,7 +406,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
       V8 o;
 #pragma unroll
       for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-      store_out16((bf16*)d.base + (size_t)m * d.ld + d.col, o.u, ST_CONV);
+      *(u32x4*)((bf16*)d.base + (size_t)m * d.ld + d.col) = o.u;
     }
   }
 }
@@ -559,7 +559,5 @@ hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pu
   }
   return hipErrorInvalidValue;
 }
-
-ADAPT_STORE_POLICY_SETTER(conv_glds)
 
 }  // namespace adapt

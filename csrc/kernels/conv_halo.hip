@@ -288,6 +288,4 @@ hipError_t conv_halo_launch(const ConvParams& p, int cfg, hipStream_t s, bool ou
   return hipErrorInvalidValue;
 }
 
-ADAPT_STORE_POLICY_SETTER(conv_halo)
-
 }  // namespace adapt

@@ -195,8 +195,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvParams p) {
       if (m >= p.M || n >= p.N) continue;
       const float* e = epi + row * EPI_LD + cc * 8;
       f32x4 v0 = *(const f32x4*)e, v1 = *(const f32x4*)(e + 4);
-      store_out16(slab + (size_t)m * p.N + n, __builtin_bit_cast(u32x4, (v0)), ST_SPLITK);
-      store_out16(slab + (size_t)m * p.N + n + 4, __builtin_bit_cast(u32x4, (v1)), ST_SPLITK);
+      *(f32x4*)(slab + (size_t)m * p.N + n) = v0;
+      *(f32x4*)(slab + (size_t)m * p.N + n + 4) = v1;
     }
     return;
   }
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvParams p) {
       V8 o;
 #pragma unroll
       for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-      store_out16((bf16*)d.base + (size_t)m * d.ld + d.col, o.u, ST_CONV);
+      *(u32x4*)((bf16*)d.base + (size_t)m * d.ld + d.col) = o.u;
     }
   }
 }
@@ -305,7 +305,5 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
   else hipLaunchKernelGGL((conv_splitk_reduce<false>), dim3(blocks), dim3(256), 0, s, p);
   return hipGetLastError();
 }
-
-ADAPT_STORE_POLICY_SETTER(conv_igemm)
 
 }  // namespace adapt

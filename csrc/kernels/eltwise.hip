@@ -30,11 +30,11 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float* __restrict
     for (int t = 0; t < 8; ++t) o.e[t] = f2bf(0.f);
     const float* src = x + p * C;
     for (int c = 0; c < C && c < 8; ++c) o.e[c] = f2bf(src[c]);
-    store_out16(y + p * Cp, o.u, ST_ELTWISE);
+    *(u32x4*)(y + p * Cp) = o.u;
     for (int c = 8; c < Cp; c += 8) {
       V8 z;
       for (int t = 0; t < 8; ++t) z.e[t] = f2bf((c + t) < C ? src[c + t] : 0.f);
-      store_out16(y + p * Cp + c, z.u, ST_ELTWISE);
+      *(u32x4*)(y + p * Cp + c) = z.u;
     }
   }
 }
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const bf16* __restrict__ x,
       float f = bf2f(v.e[t]) * scale[c0 + t] + shift[c0 + t];
       o.e[t] = f2bf(actx<GEN>(f, relu));
     }
-    store_out16((u32x4*)y + i, o.u, ST_ELTWISE);
+    ((u32x4*)y)[i] = o.u;
   }
 }
 
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void add_act_kernel(const bf16* __restrict__ a
       float f = bf2f(va.e[t]) + bf2f(vb.e[t]);
       o.e[t] = f2bf(actx<GEN>(f, relu));
     }
-    store_out16((u32x4*)y + i, o.u, ST_ELTWISE);
+    ((u32x4*)y)[i] = o.u;
   }
 }
 
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void relu_kernel(const bf16* __restrict__ x, b
     v.u = ((const u32x4*)x)[i];
 #pragma unroll
     for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(bf2f(v.e[t]), mode));
-    store_out16((u32x4*)y + i, o.u, ST_ELTWISE);
+    ((u32x4*)y)[i] = o.u;
   }
 }
 
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const bf16* __restrict__ x
     V8 o;
 #pragma unroll
     for (int t = 0; t < 8; ++t) o.e[t] = f2bf((any_pad && pad_zero) ? fmaxf(m[t], 0.f) : m[t]);
-    store_out16(y + i * 8, o.u, ST_ELTWISE);
+    *(u32x4*)(y + i * 8) = o.u;
   }
 }
 
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void pad_kernel(const bf16* __restrict__ x, bf
     u32x4 v = {0u, 0u, 0u, 0u};
     if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
       v = *(const u32x4*)(x + (((size_t)b * H + ih) * W + iw) * C + cc * 8);
-    store_out16(y + i * 8, v, ST_ELTWISE);
+    *(u32x4*)(y + i * 8) = v;
   }
 }
 
@@ -232,22 +232,6 @@ hipError_t pad(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int O
   size_t total = (size_t)B * OH * OW * (C / 8);
   hipLaunchKernelGGL(pad_kernel, dim3(grid_for(total)), dim3(256), 0, s, x, y, B, H, W, C, OH, OW, pad_t, pad_l);
   return hipGetLastError();
-}
-
-ADAPT_STORE_POLICY_SETTER(eltwise)
-
-hipError_t set_store_policy_conv_glds(int v);
-hipError_t set_store_policy_conv_igemm(int v);
-hipError_t set_store_policy_conv_halo(int v);
-hipError_t set_store_policy_bottleneck(int v);
-hipError_t set_store_policy_stem(int v);
-hipError_t set_store_policy_layers(int v);
-hipError_t set_store_policy_head(int v);
-
-hipError_t set_store_policy(int v) {
-  hipError_t e = set_store_policy_eltwise(v);
-  if (e == hipSuccess) e = set_store_policy_conv_glds(v); if (e == hipSuccess) e = set_store_policy_conv_igemm(v); if (e == hipSuccess) e = set_store_policy_conv_halo(v); if (e == hipSuccess) e = set_store_policy_bottleneck(v); if (e == hipSuccess) e = set_store_policy_stem(v); if (e == hipSuccess) e = set_store_policy_layers(v); if (e == hipSuccess) e = set_store_policy_head(v);
-  return e;
 }
 
 }  // namespace adapt

@@ -94,7 +94,7 @@ __device__ __forceinline__ void fused_epilogue(const ConvParams& p, const float*
         V8 o;
 #pragma unroll
         for (int t = 0; t < 8; ++t) o.e[t] = f2bf(v[t]);
-        store_out16((bf16*)d.base + (size_t)m * d.ld + d.col, o.u, ST_CONV);
+        *(u32x4*)((bf16*)d.base + (size_t)m * d.ld + d.col) = o.u;
       }
     }
   }

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void gap2_kernel(const bf16* __restrict__ x, b
     r[t] = a * inv;
     o.e[t] = f2bf(r[t]);
   }
-  if (y) store_out16(y + (size_t)b * C + cc * 8, o.u, ST_HEAD);
+  if (y) *(u32x4*)(y + (size_t)b * C + cc * 8) = o.u;
   if (y32) {
     float* d = y32 + (size_t)b * C + cc * 8;
 #pragma unroll
@@ -233,7 +233,5 @@ hipError_t dense_small(const bf16* x, const bf16* w, const float* bias, float* p
                        probs, M, N, ks);
   return hipGetLastError();
 }
-
-ADAPT_STORE_POLICY_SETTER(head)
 
 }  // namespace adapt

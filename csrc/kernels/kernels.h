@@ -106,8 +106,6 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
 hipError_t maxpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
                        int pad_l, int pad_zero, hipStream_t s);
 hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
-// per-site write-through store mask of every kernel (StoreSite bits, common.h)
-hipError_t set_store_policy(int v);
 // fp32 GAP over large maps: part = [B][gap_large_slices][C] fp32 scratch
 hipError_t gap_large_f32(const float* x, float* y, float* part, int B, int HW, int C, hipStream_t s);
 // op 0: y = act(a + b); op 1: y = act(a * scale[c] + shift[c]); op 2: y = act(a)

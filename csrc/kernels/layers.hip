@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const bf16* __restrict__ x,
     V8 o;
 #pragma unroll
     for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(acc[t], act));
-    store_out16(y + i * 8, o.u, ST_LAYERS);
+    *(u32x4*)(y + i * 8) = o.u;
   }
 }
 
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void dwconv3_kernel(const bf16* __restrict__ x
       V8 o;
 #pragma unroll
       for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(acc[j][t], act));
-      store_out16(y + (((size_t)b * OH + oh) * OW + ow0 + j) * Cp + c0, o.u, ST_LAYERS);
+      *(u32x4*)(y + (((size_t)b * OH + oh) * OW + ow0 + j) * Cp + c0) = o.u;
     }
   }
 }
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const bf16* __restrict__ x
     V8 o;
 #pragma unroll
     for (int t = 0; t < 8; ++t) o.e[t] = f2bf(acc[t] * inv);
-    store_out16(y + i * 8, o.u, ST_LAYERS);
+    *(u32x4*)(y + i * 8) = o.u;
   }
 }
 
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void act_kernel(const bf16* __restrict__ x, bf
     v.u = ((const u32x4*)x)[i];
 #pragma unroll
     for (int t = 0; t < 8; ++t) o.e[t] = f2bf(actx<GEN>(bf2f(v.e[t]), mode, alpha));
-    store_out16((u32x4*)y + i, o.u, ST_LAYERS);
+    ((u32x4*)y)[i] = o.u;
   }
 }
 
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void binary_kernel(const bf16* __restrict__ a,
       }
       o.e[t] = f2bf(actx<GEN>(r, act));
     }
-    store_out16((u32x4*)y + i, o.u, ST_LAYERS);
+    ((u32x4*)y)[i] = o.u;
   }
 }
 
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void gmp_kernel(const bf16* __restrict__ x, bf
 #pragma unroll
   for (int t = 0; t < 8; ++t)
     o.e[t] = f2bf(fmaxf(fmaxf(part[0][ch][t], part[1][ch][t]), fmaxf(part[2][ch][t], part[3][ch][t])));
-  store_out16(y + (size_t)b * Cp + cc * 8, o.u, ST_LAYERS);
+  *(u32x4*)(y + (size_t)b * Cp + cc * 8) = o.u;
 }
 
 // Global average pool over LARGE maps (EfficientNet's squeeze-excite at 112x112 .. 28x28), where head.hip's
@@ -419,7 +419,5 @@ hipError_t concat_into(const bf16* x, int Cx, int Cpx, bf16* y, int Cpy, int off
   }
   return hipGetLastError();
 }
-
-ADAPT_STORE_POLICY_SETTER(layers)
 
 }  // namespace adapt

@@ -146,7 +146,8 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
       const int rr = pix / OW, ow = pix - rr * OW;
       const int oh = r0 + rr;
       if (oh >= OH) continue;
-      store_out16(out + (((size_t)img * OH + oh) * OW + ow) * 64 + ch8 * 8, *(const u32x4*)(stage + stage_off(rr, ow, ch8)), ST_STEM);
+      *(u32x4*)(out + (((size_t)img * OH + oh) * OW + ow) * 64 + ch8 * 8) =
+          *(const u32x4*)(stage + stage_off(rr, ow, ch8));
     }
     return;
   }
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
     V8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o.e[e] = f2bf(m[e]);
-    store_out16(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8, o.u, ST_STEM);
+    *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = o.u;
   }
 }
 
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
           for (int e = 0; e < 4; ++e) m.h[e] = __builtin_elementwise_max(m.h[e], v.h[e]);
         }
       }
-      store_out16(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8, m.u, ST_STEM);
+      *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = m.u;
     }
     __syncthreads();                                       // ring slots of rows 2t-pp, 2t-pp+1 are free
   }
@@ -373,7 +374,5 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
   }
   return hipGetLastError();
 }
-
-ADAPT_STORE_POLICY_SETTER(stem)
 
 }  // namespace adapt
