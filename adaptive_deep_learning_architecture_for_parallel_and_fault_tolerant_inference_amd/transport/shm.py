@@ -260,13 +260,15 @@ def attach(name: str, register_device: bool = False) -> _Attached:
         a = _attached.get(name)
         if a is None:
             a = _attached[name] = _Attached(name)
-    if register_device and not a.registered:
-        import torch
-        try:
-            rc = torch.cuda.cudart().cudaHostRegister(int(a.arr.ctypes.data), a.size, 0)
-            a.registered = int(rc) == 0 if not isinstance(rc, tuple) else int(rc[0]) == 0
-        except Exception:  # noqa: BLE001 - a pageable copy still works, just slower
-            a.registered = False
+        if register_device and not a.registered:
+            # under the lock: a second concurrent register of the same pages would
+            # fail and leave the first registration untracked (never unregistered)
+            import torch
+            try:
+                rc = torch.cuda.cudart().cudaHostRegister(int(a.arr.ctypes.data), a.size, 0)
+                a.registered = int(rc) == 0 if not isinstance(rc, tuple) else int(rc[0]) == 0
+            except Exception:  # noqa: BLE001 - a pageable copy still works, just slower
+                a.registered = False
     return a
 
 
@@ -279,8 +281,14 @@ def view(name: str, offset: int, dtype, shape: Tuple[int, ...], register_device:
 
 
 def release(name: str) -> None:
-    """Receiver side of a link: the copy out of slot `name` has completed."""
-    attach(name).arr[0] = 0
+    """Receiver side of a link: the copy out of slot `name` has completed.  A
+    segment this process no longer maps (its epoch was torn down and detached)
+    is left alone: re-mapping it would leak the mapping, and the sender's pool
+    may already have unlinked the file."""
+    with _att_lock:
+        a = _attached.get(name)
+        if a is not None and a.arr is not None:
+            a.arr[0] = 0
 
 
 def detach(names) -> None:

@@ -116,3 +116,17 @@ def test_link_pool_handoff_flag():
         shm.detach([name])
     finally:
         pool.close()
+
+
+def test_release_after_detach_is_a_no_op():
+    pool = shm.LinkPool(max_slots=1)
+    try:
+        a = pool.put(np.arange(4, dtype=np.float32))
+        name = a.slot.name
+        np.testing.assert_array_equal(shm.view(name, shm.LINK_HDR, np.float32, (4,)), np.arange(4))
+        shm.detach([name])
+        shm.release(name)                                     # late release of a torn-down epoch's slot
+        assert name not in shm._attached                      # not mapped again
+        assert a.slot.mm[0] == 1                              # and the sender's flag is untouched
+    finally:
+        pool.close()
