@@ -41,14 +41,18 @@ __global__ __launch_bounds__(NW * 64, 1) void glds_feed(const char* __restrict__
   if (threadIdx.x == 0) sink[blockIdx.x] = *(unsigned*)(smem + lane * 4);
 }
 
-template <int NW, int PIECES>
+// register staging: every loaded dword is folded into an XOR that is stored at
+// the end, so no load can be dropped (the first version kept only one LDS word
+// live and hipcc removed the loads: its rows were invalid).  DSW = also write the
+// batch to LDS (ds_write_b128) as a conv kernel's register-staged A/B would.
+template <int NW, int PIECES, bool DSW>
 __global__ __launch_bounds__(NW * 64, 1) void reg_feed(const char* __restrict__ src, size_t region, int iters,
                                                        unsigned* sink) {
   __shared__ __attribute__((aligned(16))) char smem[2 * NW * PIECES * 1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   size_t off = ((size_t)blockIdx.x * 65536 + wave * PIECES * 1024) & (region - 1);
   u32x4 r[PIECES];
-  unsigned acc = 0;
+  u32x4 acc = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int p = 0; p < PIECES; ++p) r[p] = *(const u32x4*)(src + ((off + p * 1024 + lane * 16) & (region - 1)));
   for (int it = 0; it < iters; ++it) {
@@ -56,15 +60,21 @@ __global__ __launch_bounds__(NW * 64, 1) void reg_feed(const char* __restrict__ 
     u32x4 n[PIECES];
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) n[p] = *(const u32x4*)(src + ((off + p * 1024 + lane * 16) & (region - 1)));
-    char* dst = smem + (it & 1) * NW * PIECES * 1024 + wave * PIECES * 1024;
+    if (DSW) {
+      char* dst = smem + (it & 1) * NW * PIECES * 1024 + wave * PIECES * 1024;
 #pragma unroll
-    for (int p = 0; p < PIECES; ++p) *(u32x4*)(dst + p * 1024 + lane * 16) = r[p];
-    __syncthreads();
-    acc ^= *(const unsigned*)(smem + ((it & 1) * NW * PIECES * 1024 + ((lane * 52) & 1023)));   // keeps the stores live
+      for (int p = 0; p < PIECES; ++p) *(u32x4*)(dst + p * 1024 + lane * 16) = r[p];
+    }
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) acc ^= r[p];
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) r[p] = n[p];
   }
-  if (threadIdx.x == 0) sink[blockIdx.x] = acc;
+  if (DSW) {
+    __syncthreads();
+    acc.x ^= *(const unsigned*)(smem + threadIdx.x * 4);
+  }
+  sink[blockIdx.x * NW * 64 + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
 template <typename F>
@@ -89,7 +99,7 @@ int main() {
   unsigned* sink;
   CHECK(hipMalloc(&src, big));
   CHECK(hipMemset(src, 1, big));
-  CHECK(hipMalloc(&sink, 4096 * 4));
+  CHECK(hipMalloc(&sink, 256 * 1024 * 4));
   const int blocks = 256, iters = 400;
   printf("%-34s %8s %10s %12s\n", "variant", "region", "us", "B/clk/CU@2.1");
   for (size_t region : {(size_t)1 << 20, (size_t)16 << 20, big}) {
@@ -107,10 +117,13 @@ int main() {
     RUN("glds nw8 p4 depth4", (glds_feed<8, 4, 4>), 8, 4);
     RUN("glds nw16 p2 depth3", (glds_feed<16, 2, 3>), 16, 2);
     RUN("glds nw16 p2 depth4", (glds_feed<16, 2, 4>), 16, 2);
-    RUN("reg nw4 p4", (reg_feed<4, 4>), 4, 4);
-    RUN("reg nw8 p2", (reg_feed<8, 2>), 8, 2);
-    RUN("reg nw8 p4", (reg_feed<8, 4>), 8, 4);
-    RUN("reg nw16 p2", (reg_feed<16, 2>), 16, 2);
+    RUN("reg nw4 p4", (reg_feed<4, 4, false>), 4, 4);
+    RUN("reg nw8 p2", (reg_feed<8, 2, false>), 8, 2);
+    RUN("reg nw8 p4", (reg_feed<8, 4, false>), 8, 4);
+    RUN("reg nw16 p2", (reg_feed<16, 2, false>), 16, 2);
+    RUN("reg nw16 p4", (reg_feed<16, 4, false>), 16, 4);
+    RUN("reg+ds_write nw8 p4", (reg_feed<8, 4, true>), 8, 4);
+    RUN("reg+ds_write nw16 p2", (reg_feed<16, 2, true>), 16, 2);
   }
   return 0;
 }
