@@ -753,8 +753,11 @@ class Node:
                 rt = self.runtime
                 st = {"epoch": self.state.epoch, "state": self.state.state.name,
                       "processed": rt.processed if rt else 0, "error": rt.error if rt else None}
-                conn.sendall(ACK)
-                socket_send(json.dumps(st).encode(), conn, CTRL_CHUNK)
+                try:
+                    conn.sendall(ACK)
+                    socket_send(json.dumps(st).encode(), conn, CTRL_CHUNK)
+                except (OSError, RuntimeError):
+                    return                  # the prober gave up (bounded liveness probe, shutdown): nothing to report
             elif op == "shutdown":
                 conn.sendall(ACK)
                 threading.Thread(target=self.stop, daemon=True).start()

@@ -36,6 +36,22 @@ def kernels():
     return _C
 
 
+def private_stream(device) -> "torch.cuda.ExternalStream":
+    """A non-blocking HIP stream of the caller's own.  torch.cuda.Stream() hands
+    out streams of a shared round-robin pool, so two threads can get the same
+    one: a hipGraph captured on a pool stream (a worker preparing its next slice
+    in the background) could then take in, or be invalidated by, another
+    thread's work.  Every capture runs on one of these.  Like pool streams they
+    live as long as the process (one per executor; destroying them under
+    PyTorch's current-stream bookkeeping is not worth the risk)."""
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    with torch.cuda.device(dev):
+        h = kernels().stream_create()
+    return torch.cuda.ExternalStream(h, device=dev)
+
+
 def stream_handle(stream=None) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)

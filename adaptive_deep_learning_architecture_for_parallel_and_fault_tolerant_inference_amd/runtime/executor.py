@@ -32,6 +32,7 @@ import torch
 from ..graph.ir import Graph, bn_params
 from ..ops import conv as conv_ops
 from ..ops import eltwise as E
+from ..ops._lib import private_stream
 from .plan import Step, compile_plan
 
 TUNING_FILE = Path(__file__).resolve().parent.parent / "tuning" / "gfx950_conv.json"
@@ -551,7 +552,7 @@ class SliceExecutor:
                         torch.cuda.synchronize(self.device)
                         # time device work only: `reps` launches captured in one hipGraph
                         gg = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(gg):
+                        with torch.cuda.graph(gg, stream=self._capture_stream()):
                             for _ in range(reps):
                                 conv_ops.conv_forward(x, pc, out, cfg=cfg, ksplit=ks, workspace=ws, counters=ctr,
                                                       **extra)
@@ -583,13 +584,13 @@ class SliceExecutor:
     def _graph_time(self, rounds: int = 5, reps: int = 10) -> float:
         """Median ms per replay of the whole slice, freshly captured."""
         g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(device=self.device)
+        s = self._capture_stream()
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             self._launch(0)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=s):
             self._launch(0)
         g.replay()
         times = []
@@ -656,7 +657,7 @@ class SliceExecutor:
         for a, j in side.items():
             joins.setdefault(j, []).append(a)
         if side and self._side_stream is None:
-            self._side_stream = torch.cuda.Stream(device=self.device)
+            self._side_stream = private_stream(self.device)
         done: Dict[int, torch.cuda.Event] = {}
         main_stream = stream
         for i, st in enumerate(self.steps):
@@ -839,7 +840,7 @@ class SliceExecutor:
         mode="thread_local" lets other threads keep launching and synchronising
         while this one captures (a worker preparing its next slice in the
         background of a serving epoch)."""
-        s = torch.cuda.Stream(device=self.device)
+        s = self._capture_stream()
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for j in range(self.num_sets):
@@ -848,10 +849,16 @@ class SliceExecutor:
         torch.cuda.synchronize(self.device)
         for j in range(self.num_sets):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=mode):
+            # a private capture stream: with a pool stream, another thread's work could land in this capture
+            with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
                 self._launch(j)
             self._graphs[j] = g
         torch.cuda.synchronize(self.device)
+
+    def _capture_stream(self):
+        if getattr(self, "_cap_stream", None) is None:
+            self._cap_stream = private_stream(self.device)
+        return self._cap_stream
 
     @property
     def captured(self) -> bool:

@@ -13,7 +13,10 @@ use `device_inputs()` / `device_outputs()` directly and never touch the host.
 the same host), the ingest kernel (uint8 images -> preprocessed fp32), the
 graph replay and the D2H of the outputs are all enqueued on the stream and
 only an event comes back, so the host receives t+1 and sends t-1 while t
-computes (two buffer sets alternate).  `run_host()` is its synchronous form.
+computes (two buffer sets alternate).  Uploads from page-locked memory run on
+a copy stream of their own, so the H2D of t+1 overlaps the replay of t: set
+j's upload waits for the event that retired set j's previous replay, and the
+replay waits for the upload's event.  `run_host()` is the synchronous form.
 """
 from __future__ import annotations
 
@@ -78,6 +81,9 @@ class StageCompute:
         self.host_ring = max(2, int(host_ring))
         self._pinned: List[Dict[str, torch.Tensor]] = []
         self._pin_next = 0
+        self._h2d = None                      # copy stream for page-locked uploads (created on first use)
+        self._set_free: List[Optional[torch.cuda.Event]] = []   # set j's last replay has retired
+        self._uploads: List[torch.cuda.Event] = []              # this micro-batch's side-stream uploads
         if self.gpu:
             from .executor import SliceExecutor
             self.ex = SliceExecutor(g, weights, batch, device=self.device, outputs=self.outputs, num_sets=num_sets,
@@ -94,8 +100,30 @@ class StageCompute:
         pad = torch.zeros((self.batch - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return torch.cat([t, pad])
 
+    def _upload(self, dst: torch.Tensor, src: torch.Tensor, rows: int, j: int) -> None:
+        """dst[:rows] <- src (page-locked host memory), zero-fill dst[rows:]: on the copy
+        stream, after set j's previous replay; the replay of this set waits for it."""
+        cur = torch.cuda.current_stream(self.device)
+        if self._h2d is None:
+            from ..ops._lib import private_stream
+            self._h2d = private_stream(self.device)
+        if len(self._set_free) <= j:
+            self._set_free.extend([None] * (j + 1 - len(self._set_free)))
+        with torch.cuda.stream(self._h2d):
+            if self._set_free[j] is not None:
+                self._h2d.wait_event(self._set_free[j])
+            else:
+                self._h2d.wait_stream(cur)          # first use: after whatever set the buffer up
+            dst[:rows].copy_(src, non_blocking=True)
+            if rows < dst.shape[0]:
+                dst[rows:].zero_()
+            ev = torch.cuda.Event()
+            ev.record(self._h2d)
+        self._uploads.append(ev)
+
     def _feed(self, name: str, a: np.ndarray, is_bf16: bool, count: int, j: int) -> None:
-        """Host array -> input buffer `name` of set j, on the current stream."""
+        """Host array -> input buffer `name` of set j (page-locked sources through the
+        copy stream, `_upload`; the rest on the current stream)."""
         from ..ops import eltwise as E
         dst = self.ex.input_buf(name, j)
         if a.dtype == np.uint8 and dst.dtype == torch.float32 and tuple(a.shape[1:]) == tuple(dst.shape[1:]):
@@ -104,10 +132,13 @@ class StageCompute:
             if u8 is None:
                 u8 = self._u8[key] = torch.zeros(tuple(dst.shape), dtype=torch.uint8, device=self.device)
             src = _readonly_tensor(a)
-            # async when `a` is page-locked (a registered shm slot); the slot outlives the request
-            u8[: a.shape[0]].copy_(src, non_blocking=src.is_pinned())
-            if a.shape[0] < dst.shape[0]:
-                u8[a.shape[0]:].zero_()
+            if src.is_pinned():             # a registered shm slot; it outlives the request
+                self._upload(u8, src, a.shape[0], j)
+                self._wait_uploads()
+            else:
+                u8[: a.shape[0]].copy_(src)
+                if a.shape[0] < dst.shape[0]:
+                    u8[a.shape[0]:].zero_()
             E.ingest_u8(u8, dst, self.preprocess)
             return
         want = np.uint16 if dst.dtype == torch.bfloat16 else (np.float32 if dst.dtype == torch.float32 else None)
@@ -118,7 +149,10 @@ class StageCompute:
             src = _readonly_tensor(a)
             if is_bf16:
                 src = src.view(torch.bfloat16)
-            dst[: a.shape[0]].copy_(src, non_blocking=src.is_pinned())
+            if src.is_pinned():             # a registered shared-memory link slot, released at the event
+                self._upload(dst, src, a.shape[0], j)
+                return
+            dst[: a.shape[0]].copy_(src)
             if a.shape[0] < dst.shape[0]:
                 dst[a.shape[0]:].zero_()
             return
@@ -141,7 +175,15 @@ class StageCompute:
         self._tick += 1
         for name, a, b in zip(self.inputs, arrays, bf16_flags):
             self._feed(name, a, b, count, j)
+        self._wait_uploads()
         outs = self.ex.forward(j)
+        if self._h2d is not None:
+            # set j's buffers may be overwritten once this replay has retired
+            free = torch.cuda.Event()
+            free.record(torch.cuda.current_stream(self.device))
+            if len(self._set_free) <= j:
+                self._set_free.extend([None] * (j + 1 - len(self._set_free)))
+            self._set_free[j] = free
         if out_slots is not None:
             res = []
             for o in self.outputs:
@@ -170,6 +212,12 @@ class StageCompute:
             else:
                 res.append((h.numpy(), False))
         return ev, res
+
+    def _wait_uploads(self) -> None:
+        cur = torch.cuda.current_stream(self.device)
+        for ev in self._uploads:
+            cur.wait_event(ev)
+        self._uploads.clear()
 
     def run_host(self, arrays: Sequence[np.ndarray], bf16_flags: Sequence[bool], count: int
                  ) -> Tuple[List[np.ndarray], List[bool]]:

@@ -198,6 +198,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_f32", [](u64 x, u64 y, int B, int HW, int C, u64 s) {
     check(adapt::gap_f32(P<const float>(x), P<float>(y), B, HW, C, S(s)), "gap_f32");
   });
+  // a HIP stream of the caller's own: PyTorch's torch.cuda.Stream() hands out pool streams round-robin, so a
+  // serving thread's copy stream could be the very stream another thread is capturing a graph on
+  m.def("stream_create", []() {
+    hipStream_t st = nullptr;
+    check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream_create");
+    return (u64)(uintptr_t)st;
+  });
+  m.def("stream_destroy", [](u64 st) { check(hipStreamDestroy((hipStream_t)(uintptr_t)st), "stream_destroy"); });
   m.def("gap_large_f32", [](u64 x, u64 y, u64 part, int B, int HW, int C, u64 s) {
     check(adapt::gap_large_f32(P<const float>(x), P<float>(y), P<float>(part), B, HW, C, S(s)), "gap_large_f32");
   });
