@@ -89,9 +89,10 @@ def cmd_serve(argv):
     ap.add_argument("--replicas", default=None, help="pipeline replicas: auto (live // stages) or N")
     ap.add_argument("--ingest", default="auto", choices=["auto", "tcp"],
                     help="auto: same-host shared-memory request slots; tcp: inline on the socket")
-    ap.add_argument("--links", default="auto", choices=["auto", "tcp"],
-                    help="auto: stage->stage hops between workers sharing /dev/shm carry shared-memory slots; "
-                         "tcp: inline on the socket")
+    ap.add_argument("--links", default="auto", choices=["auto", "dev", "shm", "tcp"],
+                    help="stage->stage hops between workers on one host: auto = device-to-device IPC slots when "
+                         "both are GPU workers, else page-locked shared-memory slots; shm = always host slots; "
+                         "tcp = inline on the socket")
     ap.add_argument("--uint8", action="store_true", help="send uint8 images (4x fewer bytes), preprocessed on the GPU")
     ap.add_argument("--preprocess", default="none", choices=["none", "caffe", "tf", "torch"],
                     help="Keras preprocess_input mode applied by stage 0 to uint8 requests")

@@ -27,8 +27,10 @@ import numpy as np
 from ..native import runtime
 
 # "shm": the payload is a reference (segment name + offset) to a same-host
-# shared-memory slot holding the raw array (transport/shm.py)
-CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3, "zvc": 4, "shm": 5}
+# shared-memory slot holding the raw array (transport/shm.py); "dev": the same
+# for a device link slot (device memory exported by IPC handle), decoded to a
+# `shm.DevArray` that only a GPU stage consumes
+CODECS = {"none": 0, "lz4": 1, "zfp+lz4": 2, "zfp": 3, "zvc": 4, "shm": 5, "dev": 6}
 _CODEC_NAMES = {v: k for k, v in CODECS.items()}
 # dtype codes (bf16 travels as raw 16-bit words)
 DTYPES = {0: np.float32, 1: np.float64, 2: np.float16, 3: np.uint16, 4: np.int32, 5: np.int64, 6: np.uint8,
@@ -133,13 +135,18 @@ def decode(buf, threads: int = 4, copy: bool = True) -> np.ndarray:
         off = int.from_bytes(raw[cut + 1:cut + 9], "little")
         a = shm.view(raw[:cut].decode(), off, np_dt, shape, register_device=shm.REGISTER_DEVICE)
         return a.copy() if copy else a
+    if codec == 6:
+        from ..transport import shm
+        raw = bytes(body)
+        cut = raw.index(b"\0")
+        return shm.DevArray(raw[:cut].decode(), int.from_bytes(raw[cut + 1:cut + 9], "little"), np_dt, shape)
     raise ValueError(f"unknown codec id {codec}")
 
 
 def shm_name(buf) -> Optional[str]:
-    """Segment name of a "shm" container (None for every other codec)."""
+    """Segment name of a "shm" or "dev" container (None for every other codec)."""
     codec, _dt, _shape, off = _parse(buf)
-    if codec != CODECS["shm"]:
+    if codec not in (CODECS["shm"], CODECS["dev"]):
         return None
     raw = bytes(memoryview(buf)[off:])
     return raw[:raw.index(b"\0")].decode()

@@ -147,8 +147,13 @@ class DEFER:
         the GPU to uint8 image requests ("none", "caffe", "tf", "torch").  links:
         "auto" = a TCP stage -> stage hop between workers that share /dev/shm
         (equal `shm_domain` in their membership records) carries the frontier
-        in page-locked shared-memory slots, only descriptors on the socket
-        (transport/shm.py LinkPool); "tcp" = always inline."""
+        in slots, only descriptors on the socket: device memory exported by IPC
+        handle when both workers are GPU workers (a device-to-device copy,
+        transport/shm.py DeviceLinkPool), page-locked host slots otherwise
+        (LinkPool); "dev" = the same; "shm" = host slots even between GPU workers;
+        "tcp" = always inline."""
+        if links not in ("auto", "dev", "shm", "tcp"):
+            raise ValueError(f"unknown links mode {links!r}")
         if transport not in ("tcp", "rccl", "gloo"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
@@ -178,8 +183,6 @@ class DEFER:
         self.precision = precision                  # worker compute: "bf16" or "fp32" (reference float32)
         self.prepare_delay = 1.0                    # s after an epoch forms before `prepare` hints go out
         self.preprocess = preprocess
-        if links not in ("auto", "tcp"):
-            raise ValueError(f"unknown links mode {links!r}")
         self.links = links
         from .transport import shm as _shm
         self._shm = _shm.ShmPool() if ingest == "auto" and _shm.available() else None
@@ -527,9 +530,11 @@ class DEFER:
                "next": nxt, "result_addr": [self._result_host(rec), self.result_port], "part_at": list(cuts),
                "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid,
                "precision": self.precision, "preprocess": self.preprocess}
-        if (nxt is not None and self.transport == "tcp" and self.links == "auto" and rec.get("shm_domain")
-                and rec.get("shm_domain") == recs[st + 1].get("shm_domain")):
-            cfg["link"] = "shm"
+        if (nxt is not None and self.transport == "tcp" and self.links in ("auto", "dev", "shm")
+                and rec.get("shm_domain") and rec.get("shm_domain") == recs[st + 1].get("shm_domain")):
+            # same host: device link when both stages are GPU workers (IPC, device to device), else host slots
+            both_gpu = all(str(r.get("device", "")).startswith("cuda") for r in (rec, recs[st + 1]))
+            cfg["link"] = "dev" if both_gpu and self.links in ("auto", "dev") else "shm"
         if self.transport != "tcp":
             cfg["link_codec"] = self.link_codec
             cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
@@ -550,10 +555,13 @@ class DEFER:
             recs = [dict(self.workers[w]) for w in members]
         errs: List[BaseException] = []
         ok = [False] * k
+        hops = ["tcp"] * max(k - 1, 0)          # stage -> stage link kinds, for the epoch record
 
         def one(st):
             try:
                 cfg = self._stage_cfg(epoch, st, k, cuts, recs, rid)
+                if st < k - 1:
+                    hops[st] = cfg.get("link", self.transport)
                 ok[st] = self._acquire_and_configure_worker(st + 1, members[st], cfg) is not None
             except BaseException as e:  # noqa: BLE001 - reported below
                 errs.append(e)
@@ -574,7 +582,7 @@ class DEFER:
             self._ensure_session(w)
         p = Pipeline(epoch, list(cuts), list(members), recs, s0, replica=rid)
         self._log(f"epoch {epoch}: replica {rid}, {k} stages on {members} cuts={cuts} "
-                  f"({(time.time() - t0) * 1e3:.0f} ms)")
+                  f"({(time.time() - t0) * 1e3:.0f} ms)" + (f" links={','.join(hops)}" if hops else ""))
         return p
 
     def _install(self, p: Pipeline) -> None:

@@ -92,15 +92,23 @@ class StageRuntime:
             plot_model(g, slice_plot_name(plot_dir, node.node_id, self.epoch))
         # "shm": the next stage shares this host's /dev/shm, so frontier tensors go
         # device -> page-locked link slot and only descriptors cross the socket
-        # (transport/shm.py LinkPool); the TCP codec does not apply to such a hop
+        # (transport/shm.py LinkPool); "dev": both stages are GPU workers on the host,
+        # so the slots are device memory exported by IPC handle (DeviceLinkPool) and
+        # the hop is a device-to-device copy; the TCP codec applies to neither
         self.link = cfg.get("link", "tcp")
+        if self.link == "dev" and not str(node.device).startswith("cuda"):
+            self.link = "shm"
         # GPU stages with a GPU codec compress frontier tensors on a side HIP stream
         # while the next micro-batch computes (two buffer sets ping-pong)
         self.gpu_codec = (self.codec in ("zvc", "lz4") and str(node.device).startswith("cuda")
-                          and self.link != "shm")
+                          and self.link == "tcp")
         self.compute = node.stage_compute(cfg, g, weights)
         self._linkpool = None
-        if self.link == "shm":
+        if self.link == "dev":
+            from .transport import shm
+            self._linkpool = shm.DeviceLinkPool(node.device, prefix=f"adapt-link-{os.getpid()}-e{self.epoch}-"
+                                                                    f"s{self.stage}-{uuid.uuid4().hex[:6]}")
+        elif self.link == "shm":
             from .transport import shm
             self._linkpool = shm.LinkPool(prefix=f"adapt-link-{os.getpid()}-e{self.epoch}-s{self.stage}-"
                                                  f"{uuid.uuid4().hex[:6]}",
@@ -204,6 +212,10 @@ class StageRuntime:
         n = 1
         for v in shape:
             n *= int(v)
+        if self.link == "dev":
+            from .transport.shm import DevRef
+            ds = self._linkpool.acquire_dev(n * np_dt.itemsize, self.stop)
+            return ds, DevRef(ds, np_dt, shape, bf16=bf16)
         slot = self._linkpool.acquire(n * np_dt.itemsize, self.stop)
         host = torch.from_numpy(slot.view(np_dt, shape))
         if bf16:
@@ -343,7 +355,7 @@ class StageRuntime:
                     else:
                         outs, flags = self.compute.run_host(m.tensors, m.bf16, m.count)
                         self._release_links(m.links)
-                        if self._linkpool is not None:
+                        if self._linkpool is not None and self.link == "shm":
                             outs = [self._linkpool.put(o, self.stop, bf16=f) for o, f in zip(outs, flags)]
                         out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
                 self.processed += 1

@@ -100,8 +100,8 @@ class StageCompute:
         pad = torch.zeros((self.batch - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return torch.cat([t, pad])
 
-    def _upload(self, dst: torch.Tensor, src: torch.Tensor, rows: int, j: int) -> None:
-        """dst[:rows] <- src (page-locked host memory), zero-fill dst[rows:]: on the copy
+    def _upload(self, dst: torch.Tensor, src, rows: int, j: int) -> None:
+        """dst[:rows] <- src (page-locked host memory, or a device link slot), zero-fill dst[rows:]: on the copy
         stream, after set j's previous replay; the replay of this set waits for it."""
         cur = torch.cuda.current_stream(self.device)
         if self._h2d is None:
@@ -114,7 +114,11 @@ class StageCompute:
                 self._h2d.wait_event(self._set_free[j])
             else:
                 self._h2d.wait_stream(cur)          # first use: after whatever set the buffer up
-            dst[:rows].copy_(src, non_blocking=True)
+            if isinstance(src, torch.Tensor):
+                dst[:rows].copy_(src, non_blocking=True)
+            else:                                   # a device link slot (DevArray): device to device
+                from ..ops._lib import kernels, stream_handle
+                kernels().memcpy_async(int(dst.data_ptr()), src.ptr, src.nbytes, stream_handle(self._h2d))
             if rows < dst.shape[0]:
                 dst[rows:].zero_()
             ev = torch.cuda.Event()
@@ -125,7 +129,16 @@ class StageCompute:
         """Host array -> input buffer `name` of set j (page-locked sources through the
         copy stream, `_upload`; the rest on the current stream)."""
         from ..ops import eltwise as E
+        from ..transport.shm import DevArray
         dst = self.ex.input_buf(name, j)
+        if isinstance(a, DevArray):
+            want = np.dtype(np.uint16) if dst.dtype == torch.bfloat16 else np.dtype(np.float32)
+            if (a.dtype != want or is_bf16 != (dst.dtype == torch.bfloat16)
+                    or tuple(a.shape[1:]) != tuple(dst.shape[1:]) or a.shape[0] > dst.shape[0]):
+                raise ValueError(f"device link tensor {a.shape} {a.dtype} does not match input {name} "
+                                 f"{tuple(dst.shape)} {dst.dtype}")
+            self._upload(dst, a, a.shape[0], j)
+            return
         if a.dtype == np.uint8 and dst.dtype == torch.float32 and tuple(a.shape[1:]) == tuple(dst.shape[1:]):
             key = (name, j)
             u8 = self._u8.get(key)

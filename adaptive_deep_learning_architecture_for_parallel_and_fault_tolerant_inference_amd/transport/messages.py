@@ -85,7 +85,7 @@ def recv_message(sock: socket.socket, chunk_size: int = 512000, timeout_ms: int 
             ts.append(buf)
         else:
             ts.append(C.decode(buf, copy=False))      # read-only view of the received frame
-            name = C.shm_name(buf) if C.codec_of(buf) == "shm" else None
+            name = C.shm_name(buf) if C.codec_of(buf) in ("shm", "dev") else None
             if name is not None and shm.is_link(name):
                 links.append(name)
     return Message(part, rid, epoch, count, ts, bf, links)

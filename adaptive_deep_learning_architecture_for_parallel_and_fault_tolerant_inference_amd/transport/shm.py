@@ -28,6 +28,16 @@ hand-off flag: the sender sets it when it fills the slot, the receiver clears
 it once its copy out of the slot has completed, and the sender only reuses
 slots whose flag is clear (so the receiver's pace is the link's
 back-pressure).
+
+Device links (`DeviceLinkPool`): when both stages are GPU workers on the host,
+the slot's payload lives in device memory instead.  Each slot is a hipMalloc
+allocation exported by IPC handle; its shared-memory segment keeps the same
+64-byte hand-off header, and the handle is stored after that header.  The
+sender copies device -> slot (device to device), and the receiver opens the
+handle once per slot and copies slot -> its input buffer.  On one GPU that is
+an HBM-to-HBM copy, and across GPUs a peer copy over xGMI.  There is no bounce
+through host memory: the host-slot link moves the 2-stage ResNet-50 frontier
+(57 MB) over PCIe twice per batch.
 """
 from __future__ import annotations
 
@@ -211,6 +221,124 @@ class LinkPool:
             self._by_size.clear()
 
 
+IPC_HANDLE = 64        # sizeof(hipIpcMemHandle_t)
+# device link segment: hand-off header, then pid (u64) | device pointer (u64) | IPC handle
+DEV_HDR = LINK_HDR + 16 + IPC_HANDLE
+
+
+class _DevSlot:
+    """Sender side of one device link slot: `copy_` is the device -> slot copy."""
+    __slots__ = ("slot", "ptr", "nbytes")
+
+    def __init__(self, slot: Slot, ptr: int, nbytes: int):
+        self.slot, self.ptr, self.nbytes = slot, ptr, nbytes
+
+    def copy_(self, src, non_blocking: bool = True) -> None:
+        import torch
+        from ..ops._lib import kernels, stream_handle
+        if not src.is_contiguous() or src.numel() * src.element_size() > self.nbytes:
+            raise ValueError("device link slot: source must be contiguous and fit the slot")
+        kernels().memcpy_async(self.ptr, int(src.data_ptr()), src.numel() * src.element_size(),
+                               stream_handle(torch.cuda.current_stream(src.device)))
+
+
+class DeviceLinkPool(LinkPool):
+    """LinkPool whose slots are device allocations (module docstring)."""
+
+    def __init__(self, device, prefix: Optional[str] = None, max_slots: int = 6):
+        super().__init__(prefix=prefix, max_slots=max_slots)
+        import torch
+        self.device = torch.device(device)
+        self._dev: Dict[str, int] = {}
+
+    def _create(self, nbytes: int) -> Slot:
+        import torch
+        from ..ops._lib import kernels
+        K = kernels()
+        name = f"{self.prefix}-{len(self._all)}"
+        with torch.cuda.device(self.device):
+            ptr = K.dev_alloc(max(nbytes, 1))
+            handle = K.ipc_handle(ptr)
+        fd = os.open(os.path.join(SHM_DIR, name), os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+        try:
+            os.ftruncate(fd, DEV_HDR)
+            mm = mmap.mmap(fd, DEV_HDR)
+        finally:
+            os.close(fd)
+        mm[LINK_HDR:LINK_HDR + 16] = os.getpid().to_bytes(8, "little") + int(ptr).to_bytes(8, "little")
+        if len(handle) != IPC_HANDLE:
+            raise RuntimeError(f"device link: IPC handle of {len(handle)} bytes, expected {IPC_HANDLE}")
+        mm[LINK_HDR + 16:DEV_HDR] = handle
+        s = Slot(self, name, nbytes, mm, len(self._all), offset=0)
+        self._all.append(s)
+        self._dev[name] = ptr
+        return s
+
+    def acquire_dev(self, nbytes: int, stop: Optional[threading.Event] = None) -> _DevSlot:
+        s = self.acquire(nbytes, stop)
+        return _DevSlot(s, self._dev[s.name], s.nbytes)
+
+    def close(self) -> None:
+        """Callers synchronise the device first (no copy may still target a slot)."""
+        import torch
+        from ..ops._lib import kernels
+        with self._lock:
+            for ptr in self._dev.values():
+                try:
+                    with torch.cuda.device(self.device):
+                        kernels().dev_free(ptr)
+                except Exception:  # noqa: BLE001 - teardown: the process may be exiting
+                    pass
+            self._dev.clear()
+        super().close()
+
+
+class DevArray:
+    """Receiver side of a device link tensor: `ptr` is the slot's device address in
+    this process (the IPC mapping is opened once per slot and cached)."""
+    __slots__ = ("name", "offset", "dtype", "shape")
+
+    def __init__(self, name: str, offset: int, dtype, shape: Tuple[int, ...]):
+        self.name, self.offset, self.dtype, self.shape = name, int(offset), np.dtype(dtype), tuple(shape)
+
+    @property
+    def nbytes(self) -> int:
+        return int(np.prod(self.shape)) * self.dtype.itemsize
+
+    @property
+    def ptr(self) -> int:
+        return dev_ptr(self.name) + self.offset
+
+
+class DevRef:
+    """Sender side: a tensor in a device link slot; on the wire the "dev" descriptor."""
+
+    def __init__(self, slot: _DevSlot, dtype, shape: Tuple[int, ...], bf16: bool = False):
+        self.slot, self.dtype, self.shape = slot, np.dtype(dtype), tuple(int(v) for v in shape)
+        self.bf16 = bf16
+
+    def container(self) -> bytes:
+        from .. import codec as C
+        return C.wrap(self.slot.slot.name.encode() + b"\0" + (0).to_bytes(8, "little"), "dev",
+                      self.dtype, self.shape, bf16=self.bf16)
+
+
+def dev_ptr(name: str) -> int:
+    """Device address of device link slot `name` in this process: the sender's own
+    pointer when the sender is this process, else its IPC mapping (opened once)."""
+    a = attach(name)
+    with _att_lock:
+        if a.dptr is None:
+            pid = int.from_bytes(bytes(a.mm[LINK_HDR:LINK_HDR + 8]), "little")
+            if pid == os.getpid():
+                a.dptr = int.from_bytes(bytes(a.mm[LINK_HDR + 8:LINK_HDR + 16]), "little")
+            else:
+                from ..ops._lib import kernels
+                a.dptr = kernels().ipc_open(bytes(a.mm[LINK_HDR + 16:DEV_HDR]))
+                a.ipc = True
+        return a.dptr
+
+
 def is_link(name: str) -> bool:
     return name.startswith("adapt-link-")
 
@@ -227,6 +355,8 @@ class _Attached:
         self.size = size
         self.arr = np.frombuffer(self.mm, dtype=np.uint8)
         self.registered = False
+        self.dptr: Optional[int] = None      # device link slot: its device address in this process
+        self.ipc = False                     # ... opened from an IPC handle (closed at detach)
 
 
 class ShmRef:
@@ -298,6 +428,13 @@ def detach(names) -> None:
             a = _attached.pop(n, None)
             if a is None:
                 continue
+            if a.ipc and a.dptr is not None:
+                try:
+                    from ..ops._lib import kernels
+                    kernels().ipc_close(a.dptr)
+                except Exception:  # noqa: BLE001
+                    pass
+                a.dptr = None
             if a.registered:
                 try:
                     import torch

@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -206,6 +207,32 @@ PYBIND11_MODULE(_C, m) {
     return (u64)(uintptr_t)st;
   });
   m.def("stream_destroy", [](u64 st) { check(hipStreamDestroy((hipStream_t)(uintptr_t)st), "stream_destroy"); });
+  // device link slots (transport/shm.py DeviceLinkPool): one allocation per slot, exported by IPC handle
+  m.def("dev_alloc", [](size_t n) {
+    void* p = nullptr;
+    check(hipMalloc(&p, n), "dev_alloc");
+    return (u64)(uintptr_t)p;
+  });
+  m.def("dev_free", [](u64 p) { check(hipFree((void*)(uintptr_t)p), "dev_free"); });
+  m.def("ipc_handle", [](u64 p) {
+    hipIpcMemHandle_t h;
+    check(hipIpcGetMemHandle(&h, (void*)(uintptr_t)p), "ipc_handle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  });
+  m.def("ipc_open", [](py::bytes hb) {
+    std::string b = hb;
+    if (b.size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("ipc_open: bad handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, b.data(), sizeof(h));
+    void* p = nullptr;
+    check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "ipc_open");
+    return (u64)(uintptr_t)p;
+  });
+  m.def("ipc_close", [](u64 p) { check(hipIpcCloseMemHandle((void*)(uintptr_t)p), "ipc_close"); });
+  m.def("memcpy_async", [](u64 dst, u64 src, size_t n, u64 st) {
+    check(hipMemcpyAsync((void*)(uintptr_t)dst, (const void*)(uintptr_t)src, n, hipMemcpyDefault, S(st)),
+          "memcpy_async");
+  });
   m.def("gap_large_f32", [](u64 x, u64 y, u64 part, int B, int HW, int C, u64 s) {
     check(adapt::gap_large_f32(P<const float>(x), P<float>(y), P<float>(part), B, HW, C, S(s)), "gap_large_f32");
   });

@@ -129,13 +129,15 @@ def test_defer_two_gpu_stages_other_families(name, cut):
             n.stop()
 
 
-def test_defer_two_gpu_stages_shared_memory_link():
-    """Two GPU stages on one host: the frontier goes device -> page-locked link
-    slot -> device (transport/shm.py LinkPool), only descriptors on the TCP hop;
-    slots are recycled through the hand-off flag."""
+@pytest.mark.parametrize("links", ["dev", "shm"])
+def test_defer_two_gpu_stages_shared_memory_link(links):
+    """Two GPU stages on one host: the frontier goes device -> link slot -> device,
+    only descriptors on the TCP hop; slots are recycled through the hand-off flag.
+    "dev": the slots are device memory (DeviceLinkPool; in one process the
+    receiver uses the sender's pointer), "shm": page-locked host slots."""
     m = resnet("resnet50", seed=0)
     d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
-              min_workers=2)
+              min_workers=2, links=links)
     d.membership_server.start()
     nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"s{i}",
                   heartbeat_ttl=1.0) for i in range(2)]
@@ -152,8 +154,49 @@ def test_defer_two_gpu_stages_shared_memory_link():
         want = m.predict(np.concatenate(xs), device="cpu")
         assert np.abs(got - want).sum(-1).max() < 0.1
         first = next(n for n in nodes if n.node_id == d.pipeline.workers[0])
-        assert first.runtime.link == "shm" and 1 <= len(first.runtime._linkpool._all) <= 2 * 6
+        assert first.runtime.link == links and 1 <= len(first.runtime._linkpool._all) <= 2 * 6
     finally:
         d.shutdown(stop_workers=True)
         for n in nodes:
             n.stop()
+
+
+def test_defer_device_link_across_processes():
+    """Two GPU worker PROCESSES (as `serve --spawn 2` starts them): the stage ->
+    stage hop is a device link, and the receiver opens the sender's slots by IPC
+    handle (hipIpcOpenMemHandle) and copies device to device."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=120, batch=4, ordered=True, weight_codec="lz4",
+              min_workers=2, links="auto")
+    d.membership_server.start()
+    pkg = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
+    procs = [subprocess.Popen([sys.executable, "-m", f"{pkg}.node", "--membership-port", str(d.membership_port),
+                               "--data-port", "0", "--config-port", "0", "--device", "cuda:0", "--id", f"p{i}",
+                               "--ttl", "2.0"], start_new_session=True) for i in range(2)]
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["conv3_block1_1_conv"], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(6)
+        xs = [rng.standard_normal((4, 224, 224, 3)).astype(np.float32) for _ in range(10)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=180) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert np.abs(got - want).sum(-1).max() < 0.1
+        assert any("links=dev" in ev for _, ev in d.events), d.events
+    finally:
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)

@@ -130,3 +130,17 @@ def test_release_after_detach_is_a_no_op():
         assert a.slot.mm[0] == 1                              # and the sender's flag is untouched
     finally:
         pool.close()
+
+
+def test_device_link_descriptor_roundtrip():
+    """The "dev" container carries a device link slot's name and offset; the receiver
+    decodes it to a DevArray (its device address is resolved lazily on the GPU)."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd import codec as C
+    buf = C.wrap(b"adapt-link-1-e2-s0-abc-3\0" + (256).to_bytes(8, "little"), "dev", np.uint16, (4, 28, 28, 128),
+                 bf16=True)
+    a = C.decode(buf, copy=False)
+    assert isinstance(a, shm.DevArray)
+    assert (a.name, a.offset, a.dtype, a.shape) == ("adapt-link-1-e2-s0-abc-3", 256, np.dtype(np.uint16),
+                                                    (4, 28, 28, 128))
+    assert a.nbytes == 4 * 28 * 28 * 128 * 2
+    assert C.codec_of(buf) == "dev" and C.is_bf16(buf) and C.shm_name(buf) == a.name and shm.is_link(a.name)

@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--kill-at", type=float, default=5.0)
     ap.add_argument("--ttl", type=float, default=0.5)
     ap.add_argument("--inflight", type=int, default=8)
+    ap.add_argument("--links", default="auto", choices=["auto", "dev", "shm", "tcp"],
+                    help="same-host stage->stage hops (DEFER links)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
 
@@ -54,7 +56,7 @@ def main():
     cuts, _ = plan_cuts(m.graph, a.workers, batch=a.batch)
     d = DEFER(membership_port=0, result_port=0, worker_wait=120, batch=a.batch, codec=a.codec, weight_codec="lz4",
               max_inflight=a.inflight, task_timeout=30, min_workers=a.workers, transport=a.transport,
-              replicas=a.replicas)
+              replicas=a.replicas, links=a.links)
     d.membership_server.start()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     procs = {}
