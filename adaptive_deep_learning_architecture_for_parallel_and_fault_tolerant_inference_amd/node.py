@@ -378,10 +378,11 @@ class StageRuntime:
                 except queue.Empty:
                     continue
                 if isinstance(m, _Pending):                # pipelined GPU micro-batch: outputs on the host at `ev`
-                    while not m.ev.query():
-                        if self.stop.is_set():
-                            return
-                        time.sleep(0.0001)
+                    # a blocking wait with the GIL released: a 10 kHz query/sleep loop here took
+                    # GIL time from the compute and receive threads of this stage
+                    m.ev.synchronize()
+                    if self.stop.is_set():
+                        return
                     self._release_links(m.links)           # the input copies out of them are done too
                     m = m.msg
                 elif isinstance(m, tuple):                 # GPU-encoded frontier (side stream)
