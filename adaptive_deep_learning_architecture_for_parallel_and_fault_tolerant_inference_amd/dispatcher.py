@@ -535,6 +535,14 @@ class DEFER:
             # same host: device link when both stages are GPU workers (IPC, device to device), else host slots
             both_gpu = all(str(r.get("device", "")).startswith("cuda") for r in (rec, recs[st + 1]))
             cfg["link"] = "dev" if both_gpu and self.links in ("auto", "dev") else "shm"
+        if str(rec.get("device", "")).startswith("cuda"):
+            # a GPU stage replays its two micro-batch sets on two streams, unless other live
+            # workers share its GPU (same host, same device): they already keep it busy, and
+            # measured on one MI355X two processes x two streams lost 18 % to one stream each
+            with self.worker_lock:
+                peers = [r for r in self.workers.values()
+                         if r.get("shm_domain") == rec.get("shm_domain") and r.get("device") == rec.get("device")]
+            cfg["stage_streams"] = 1 if len(peers) > 1 else 2
         if self.transport != "tcp":
             cfg["link_codec"] = self.link_codec
             cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",

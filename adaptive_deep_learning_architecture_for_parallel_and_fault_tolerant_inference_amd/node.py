@@ -561,15 +561,19 @@ class Node:
 
     # -------------------------------------------------- stage computes
     @staticmethod
-    def compute_shape(cfg: Dict, device: str) -> Tuple[int, int, bool]:
-        """(num_sets, host_ring, graph) the epoch runtime for `cfg` builds its
-        StageCompute with: one definition for configure and prepare."""
+    def compute_shape(cfg: Dict, device: str) -> Tuple[int, int, bool, int]:
+        """(num_sets, host_ring, graph, streams) the epoch runtime for `cfg` builds
+        its StageCompute with: one definition for configure and prepare."""
         graph = bool(cfg.get("graph", True))
         if cfg.get("transport", "tcp") == "tcp":
             # GPU stages double-buffer (pipelined submit / GPU codec); the host ring of
-            # output buffers outlives the bounded queues between the stage's threads
-            return (2 if str(device).startswith("cuda") else 1), int(cfg.get("queue", 4)) + 4, graph
-        return int(cfg.get("nsets", 2)), 8, graph
+            # output buffers outlives the bounded queues between the stage's threads.
+            # streams: the two sets replay on two streams unless the dispatcher saw
+            # other workers on this GPU (they already keep it busy)
+            gpu = str(device).startswith("cuda")
+            return ((2 if gpu else 1), int(cfg.get("queue", 4)) + 4, graph,
+                    (int(cfg.get("stage_streams", 2)) if gpu else 1))
+        return int(cfg.get("nsets", 2)), 8, graph, 1
 
     def _compute_key(self, cfg: Dict) -> Optional[tuple]:
         key = cfg.get("cache_key")
@@ -583,7 +587,7 @@ class Node:
         epoch or by `prepare`), else built now and cached."""
         from .runtime.stage import StageCompute
         key = self._compute_key(cfg)
-        num_sets, host_ring, graph = self.compute_shape(cfg, self.device)
+        num_sets, host_ring, graph, streams = self.compute_shape(cfg, self.device)
         while key is not None:
             with self._computes_lock:
                 c = self._computes.get(key)
@@ -596,7 +600,7 @@ class Node:
             ev.wait(60)                             # a prepare is building this one right now
         try:
             c = StageCompute(g, weights, int(cfg["batch"]), self.device, graph_capture=graph, num_sets=num_sets,
-                             host_ring=host_ring, capture_mode=capture_mode,
+                             host_ring=host_ring, capture_mode=capture_mode, streams=streams,
                              precision=cfg.get("precision", "bf16"), preprocess=cfg.get("preprocess", "none"))
         finally:
             if key is not None:

@@ -81,10 +81,15 @@ class SliceExecutor:
 
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device="cuda",
                  outputs: Optional[Sequence[str]] = None, tune: bool = False, num_sets: int = 1,
-                 precision: str = "bf16"):
+                 precision: str = "bf16", private_sets: bool = False):
         """precision: "bf16" (bf16 activations / weights, fp32 accumulation: the
         fast path) or "fp32" (fp32 activations and weights on the fp32 matrix
-        cores: the reference's Keras float32 numerics, csrc/kernels/conv_f32.hip)."""
+        cores: the reference's Keras float32 numerics, csrc/kernels/conv_f32.hip).
+        private_sets: every buffer set also gets its own internal activation arena
+        and scratch (split-K workspace, stream-K counters, head / GAP partials), so
+        the sets' graphs may replay concurrently on different streams (a serving
+        stage keeps two micro-batches in flight); by default the sets share them
+        and replay one after the other."""
         if precision not in ("bf16", "fp32"):
             raise ValueError(f"precision must be bf16 or fp32, got {precision!r}")
         self.g = g
@@ -92,6 +97,7 @@ class SliceExecutor:
         self.device = torch.device(device)
         self.outputs = list(outputs or g.output_names)
         self.num_sets = num_sets
+        self.private_sets = bool(private_sets) and num_sets > 1
         self.precision = precision
         self.fp32 = precision == "fp32"
         self.steps: List[Step] = compile_plan(g, self.outputs, fp32=self.fp32)
@@ -277,7 +283,6 @@ class SliceExecutor:
         """Per-set frontier buffers + liveness-reused internal activation buffers."""
         dev = self.device
         in_names = list(self.g.input_names)
-        keep = set(self.outputs)
         # relay outputs (slice inputs forwarded unchanged) get their own output buffers
         self.relay = [o for o in self.outputs if o in in_names]
         self.sets: List[Dict[str, torch.Tensor]] = []
@@ -289,6 +294,37 @@ class SliceExecutor:
                 key = o + "#out" if o in in_names else o
                 s[key] = torch.empty(self.shape_of(o), dtype=self.dtype_of(o), device=dev)
             self.sets.append(s)
+        self._alloc_private()
+        self._priv: List[Dict[str, object]] = []
+        self._bound = 0
+        if self.private_sets:
+            self._priv.append(self._private_state())
+            for _ in range(1, self.num_sets):
+                self._alloc_private()
+                self._priv.append(self._private_state())
+            self._bound = self.num_sets - 1        # the live attributes are the last set's
+            self._bind(0)
+
+    _PRIVATE = ("internal", "_arena", "_logits", "_dense_part", "_gap_part", "_ws", "_ctr", "_ws_side", "_ctr_side")
+
+    def _private_state(self) -> Dict[str, object]:
+        return {k: getattr(self, k) for k in self._PRIVATE}
+
+    def _bind(self, set_idx: int) -> None:
+        """private_sets: make set `set_idx`'s arena and scratch the current ones (the
+        bound set's workspace, possibly grown meanwhile by _ensure_ws, is saved first)."""
+        if not self.private_sets:
+            return
+        self._priv[self._bound].update(self._private_state())
+        for k, v in self._priv[set_idx].items():
+            setattr(self, k, v)
+        self._bound = set_idx
+
+    def _alloc_private(self) -> None:
+        """The internal activation arena and the per-launch scratch of one set (or
+        of all sets together, without private_sets)."""
+        dev = self.device
+        keep = set(self.outputs)
         last_use: Dict[str, int] = {}
         for i, st in enumerate(self.steps):
             for t in st.ins:
@@ -344,7 +380,8 @@ class SliceExecutor:
         self._ctr: Optional[torch.Tensor] = None
         self._ws_side: Optional[torch.Tensor] = None
         self._ctr_side: Optional[torch.Tensor] = None
-        self._side_stream: Optional[torch.cuda.Stream] = None
+        if not hasattr(self, "_side_stream"):
+            self._side_stream: Optional[torch.cuda.Stream] = None
 
     def _side_schedule(self) -> Dict[int, int]:
         """{step i: join step j} for convs that form an independent branch: the
@@ -374,7 +411,8 @@ class SliceExecutor:
         return side
 
     def bufs(self, set_idx: int = 0):
-        return ChainMap(self.sets[set_idx], self.internal)
+        internal = self._priv[set_idx]["internal"] if self.private_sets and set_idx != self._bound else self.internal
+        return ChainMap(self.sets[set_idx], internal)
 
     @property
     def inputs(self) -> Dict[str, torch.Tensor]:
@@ -388,7 +426,8 @@ class SliceExecutor:
         return s[name + "#out"] if name in self.relay else s[name]
 
     def workspace_bytes(self) -> int:
-        n = sum(b.numel() for b in self._arena)
+        arenas = [p["_arena"] for p in self._priv] if self.private_sets else [self._arena]
+        n = sum(b.numel() for a in arenas for b in a)
         n += sum(t.numel() * t.element_size() for s in self.sets for t in s.values())
         return n
 
@@ -646,6 +685,9 @@ class SliceExecutor:
 
     # -------------------------------------------------------------- run
     def _launch(self, set_idx: int = 0, stream=None) -> None:
+        if self.private_sets:
+            self._bind(set_idx)
+            self._ensure_ws()              # this set's workspace, sized for the configs in force
         b = self.bufs(set_idx)
         # ADAPT_DEBUG_SYNC=1: synchronize after every step so a faulting or
         # failing kernel is reported with its step (the AMD_SERIALIZE_KERNEL

@@ -16,7 +16,12 @@ only an event comes back, so the host receives t+1 and sends t-1 while t
 computes (two buffer sets alternate).  Uploads from page-locked memory run on
 a copy stream of their own, so the H2D of t+1 overlaps the replay of t: set
 j's upload waits for the event that retired set j's previous replay, and the
-replay waits for the upload's event.  `run_host()` is the synchronous form.
+replay waits for the upload's event.  Each buffer set also has a compute
+stream of its own (ingest, replay and output copies of set j run on stream j),
+so micro-batches t and t+1 overlap on the GPU the way `bench.py --streams 2`
+does (ADAPT_STAGE_STREAMS=1 keeps one stream).  Results still leave in order:
+the send thread waits for the events in FIFO order.  `run_host()` is the
+synchronous form.
 """
 from __future__ import annotations
 
@@ -68,7 +73,7 @@ class StageCompute:
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device: str = "cpu",
                  outputs: Optional[Sequence[str]] = None, graph_capture: bool = True, num_sets: int = 1,
                  host_ring: int = 8, capture_mode: str = "global", precision: str = "bf16",
-                 preprocess: str = "none"):
+                 preprocess: str = "none", streams: int = 2):
         self.g = g
         self.preprocess = preprocess          # uint8 image inputs: Keras preprocess_input mode (ops/eltwise.py)
         self._u8: Dict[Tuple[str, int], torch.Tensor] = {}
@@ -84,10 +89,17 @@ class StageCompute:
         self._h2d = None                      # copy stream for page-locked uploads (created on first use)
         self._set_free: List[Optional[torch.cuda.Event]] = []   # set j's last replay has retired
         self._uploads: List[torch.cuda.Event] = []              # this micro-batch's side-stream uploads
+        self._cstreams: List = []                                # per-set compute streams (created on first use)
+        self.multi_stream = False
         if self.gpu:
+            import os
             from .executor import SliceExecutor
+            # concurrent sets: set j replays on its own stream (submit), so the sets must not
+            # share the executor's internal arena and scratch
+            self.multi_stream = (num_sets > 1 and int(streams) > 1
+                                 and os.environ.get("ADAPT_STAGE_STREAMS", "") != "1")
             self.ex = SliceExecutor(g, weights, batch, device=self.device, outputs=self.outputs, num_sets=num_sets,
-                                    precision=precision)
+                                    precision=precision, private_sets=self.multi_stream)
             if graph_capture:
                 self.ex.capture(mode=capture_mode)
         else:
@@ -186,6 +198,18 @@ class StageCompute:
             raise ValueError(f"stage expects {len(self.inputs)} inputs, got {len(arrays)}")
         j = self._tick % self.ex.num_sets
         self._tick += 1
+        if self.multi_stream:
+            if not self._cstreams:
+                from ..ops._lib import private_stream
+                cur = torch.cuda.current_stream(self.device)
+                self._cstreams = [private_stream(self.device) for _ in range(self.ex.num_sets)]
+                for cs in self._cstreams:
+                    cs.wait_stream(cur)             # after whatever set the buffers up
+            with torch.cuda.stream(self._cstreams[j]):
+                return self._submit(j, arrays, bf16_flags, count, out_slots)
+        return self._submit(j, arrays, bf16_flags, count, out_slots)
+
+    def _submit(self, j: int, arrays, bf16_flags, count: int, out_slots):
         for name, a, b in zip(self.inputs, arrays, bf16_flags):
             self._feed(name, a, b, count, j)
         self._wait_uploads()
