@@ -42,6 +42,20 @@ static std::pair<const uint8_t*, size_t> view(const py::buffer& b, py::buffer_in
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "ADAPT host runtime: framing transport, LZ4 frame codec, reversible zfp-style codec";
 
+  // ---------------------------------------------------------- bulk copy
+  // dst[:n] = src[:n] on `threads` threads, GIL released: the dispatcher copies every
+  // request into a shared-memory ingest slot (19 MB per bs=32 fp32 batch), which one
+  // thread's memcpy makes the serving bottleneck
+  m.def("copy_into", [](py::buffer dst, py::buffer src, int threads) {
+    py::buffer_info di = dst.request(true), si = src.request();
+    const size_t n = (size_t)(si.size * si.itemsize);
+    if ((size_t)(di.size * di.itemsize) < n) throw std::runtime_error("copy_into: destination too small");
+    uint8_t* d = static_cast<uint8_t*>(di.ptr);
+    const uint8_t* sp = static_cast<const uint8_t*>(si.ptr);
+    NoGil ng;
+    parallel_copy(d, sp, n, threads);
+  });
+
   // ---------------------------------------------------------- heartbeats
   m.def("hb_sender_start", [](const std::string& host, int port, const std::string& id, int period_us) {
     return reinterpret_cast<uintptr_t>(hb_sender_start(host, port, id, period_us));

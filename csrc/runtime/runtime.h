@@ -68,4 +68,7 @@ std::vector<std::pair<std::string, double>> hb_monitor_ages(void* h);   // id ->
 void hb_monitor_forget(void* h, const std::string& id);
 void hb_monitor_stop(void* h);
 
+// ---- bulk host copy split over threads (framing.cpp)
+void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n, int threads);
+
 }  // namespace adapt_rt

@@ -175,3 +175,16 @@ def test_zfp_wire_codec_cpu_round_trip():
     out = torch.empty_like(t)
     dec.decode(n, out)
     assert torch.equal(out, t)
+
+
+def test_parallel_copy_into_matches_numpy():
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.native import runtime
+    rng = np.random.default_rng(9)
+    for n in (7, 1 << 20, (3 << 20) + 13):
+        src = rng.integers(0, 256, n, dtype=np.uint8)
+        for th in (1, 3, 4, 16):
+            dst = np.zeros(n + 5, np.uint8)
+            runtime().copy_into(dst, src, th)
+            assert np.array_equal(dst[:n], src) and not dst[n:].any()
+    with pytest.raises(RuntimeError):
+        runtime().copy_into(np.zeros(3, np.uint8), np.zeros(4, np.uint8), 2)
