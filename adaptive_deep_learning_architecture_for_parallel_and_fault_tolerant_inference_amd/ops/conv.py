@@ -57,7 +57,10 @@ _CFG_EFF = {0: 1.0, 4: 0.97, 1: 0.86, 2: 0.86, 3: 0.66, 5: 0.42}
 
 def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
     """v2 configs walk K tap-major in 64-channel slices: they need Cin % 64 == 0;
-    v3 (halo) configs take 3x3/s1/p1 convs only (the row count is checked at launch)."""
+    v3 (halo) configs take 3x3/s1/p1 convs only (the row count is checked at launch);
+    pointwise configs (PW_CFGS) take 1x1 stride-1 convs of the shapes pw_wide.hip has."""
+    if cfg in PW_CFGS:
+        return pure and pw_supported(pc)
     if cfg in V1_CFGS:
         return True
     if cfg in HALO_PATCH:
@@ -213,6 +216,11 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         raise ValueError("residual must be bf16 with the output's shape")
     if cfg is None:
         cfg, ksplit = choose_cfg(M, N, pc.Kpad)
+    if cfg in PW_CFGS:                     # persistent pointwise kernel (pw_wide.hip)
+        if ksplit != 1 or ns or out_f32 or OH != H or OW != W:
+            raise ValueError(f"pointwise config {cfg}: single bf16 output, no split-K")
+        return pw_forward(x.reshape(M, C), pc, out.view(M, N), None if residual is None else residual.view(M, N),
+                          relu=int(relu), cfg=cfg, blocks=NUM_CUS, stream=stream)
     bm, bn = CFG_TILES[cfg]
     if pc.w.shape[0] < math.ceil(N / bn) * bn:
         raise ValueError("packed weights not padded to the tile's N")
@@ -396,6 +404,43 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
     kernels().conv_f32_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C, OH, OW,
                                N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.K, pc.Kpad, int(relu),
                                max(1, int(ksplit)), int(cfg), stream_handle(stream))
+    return out
+
+
+# ------------------------------------------------- persistent pointwise conv
+# csrc/kernels/pw_wide.hip: 1x1 / stride 1, K <= 128, N = 4 x 64 x waves, weights held in
+# registers by each wave for the whole launch (ResNet stage 3's 128 -> 512 "_out" convs)
+PW_CFGS = {60: 16, 61: 32}                   # config id -> pixels per tile
+
+
+def pw_supported(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 1, 0, 0, 0, 0)
+            and pc.cin == pc.Kpad and pc.cout == pc.w.shape[0] and not pc.n_split
+            and bool(kernels().pw_res_supported(int(pc.cin), int(pc.cout))))
+
+
+def pw_fragments(pc: "PackedConv") -> torch.Tensor:
+    """pc.w ([N][K] bf16) in MFMA fragment order (pack_fragments), cached on pc."""
+    wf = getattr(pc, "_pw_frag", None)
+    if wf is None:
+        N, K = pc.w.shape
+        wf = pc.w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(-1)
+        pc._pw_frag = wf
+    return wf
+
+
+def pw_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, residual: Optional[torch.Tensor] = None,
+               relu: int = 0, cfg: int = 61, blocks: int = 256, stream=None) -> torch.Tensor:
+    if not pw_supported(pc):
+        raise ValueError("pw conv: needs a 1x1 stride-1 conv with (K, N) in (128, 512) / (64, 256)")
+    M = x.numel() // pc.cin
+    for t, n in ((x, "x"), (out, "out"), (residual, "residual")):
+        if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous()):
+            raise ValueError(f"pw conv: {n} must be contiguous bf16")
+    if x.shape[-1] != pc.cin or out.numel() != M * pc.cout or (residual is not None and residual.numel() != M * pc.cout):
+        raise ValueError(f"pw conv: x {tuple(x.shape)} / out {tuple(out.shape)} do not match {pc.cin} -> {pc.cout}")
+    kernels().pw_res_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(residual), ptr(out), M, pc.cin,
+                             pc.cout, int(relu), PW_CFGS[cfg], int(blocks), stream_handle(stream))
     return out
 
 

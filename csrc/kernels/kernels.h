@@ -142,6 +142,19 @@ struct BottleneckParams {
   int B, H, W;
 };
 hipError_t bottleneck_forward(const BottleneckParams& p, int cin, bool proj, hipStream_t s);
+// persistent pointwise conv, weights register-resident per wave (pw_wide.hip):
+// out[m][n] = act(x[m] . W[n] + bias[n] (+ res[m][n])), x [M][K], W in MFMA fragment order
+struct PwParams {
+  const bf16* x;
+  const bf16* w;
+  const float* bias;
+  const bf16* res;
+  bf16* out;
+  int M;
+  int relu;
+};
+int pw_res_supported(int K, int N);
+hipError_t pw_res_forward(const PwParams& p, int K, int N, int pt, int blocks, hipStream_t s);
 // serving ingest (ingest.hip): uint8 NHWC -> fp32, y = x[rev(c)] * scale[c] + shift[c] (host scale/shift, C <= 4)
 hipError_t ingest_u8(const uint8_t* x, float* y, size_t n, int C, int reverse, const float* scale,
                      const float* shift, hipStream_t s);
