@@ -36,7 +36,10 @@ CFG_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64
              46: (224, 64), 47: (112, 128), 48: (224, 64), 49: (64, 128), 50: (224, 64), 51: (224, 64),
              52: (112, 64),
              # v2, 16 waves per block (conv_glds.hip ids 53-58)
-             53: (128, 128), 54: (128, 128), 55: (256, 128), 56: (128, 256), 57: (256, 128), 58: (128, 128)}
+             53: (128, 128), 54: (128, 128), 55: (256, 128), 56: (128, 256), 57: (256, 128), 58: (128, 128),
+             # v2, two K-groups of waves per block (conv_glds.hip ADAPT_GLDS_KG_CFGS)
+             62: (64, 128), 63: (128, 128), 64: (64, 256), 65: (128, 128), 66: (64, 128), 67: (128, 64),
+             68: (64, 64), 69: (128, 256), 70: (256, 128)}
 V1_CFGS = (0, 1, 2, 3, 4, 5)
 # halo configs: patch capacity in pixels (must match ADAPT_HALO_CFGS)
 HALO_PATCH = {40: 352, 41: 192, 42: 288, 43: 96, 44: 144, 45: 384, 46: 352, 47: 192, 48: 384, 49: 96, 50: 320,

@@ -83,20 +83,31 @@ struct GldsShape {
 // base ~= DMA-only + compute-only.  Loader waves only issue pieces and wait for
 // them (counted vmcnt, then the shared barrier); compute waves only ds_read and
 // MFMA, so the two overlap.
-template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32, int ABL = 0, int NL = 0>
+//
+// KG = 2: two K-groups of WM x WN compute waves per block.  Each 64-wide K tile
+// is two 32-wide MFMA K steps; group g runs step g only, so a wave covers a
+// (BM/WM) x (BN/WN) sub-tile twice as large as the KG = 1 block of the same
+// wave count and reads a quarter to a third fewer LDS fragment bytes per MFMA
+// (the ablation's no-DMA/skeleton rows: the fragment ds_reads are ~6 us of a
+// stage-4 3x3).  The two partial accumulators meet in the fp32 epilogue tile.
+template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32, int ABL = 0, int NL = 0,
+          int KG = 1>
 __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __restrict__ zero, char* smem,
                                           int tile, int kt0, int kt1, int split_idx, const SkSeg& sk) {
   using S = GldsShape<BM, BN, WM, WN, STAGES>;
-  constexpr int NW = S::NW;                  // compute waves
-  constexpr int NT = (NW + NL) * 64;         // all threads of the block
-  constexpr int NWI = NL > 0 ? NL : NW;      // waves that issue the LDS-DMA pieces
+  constexpr int NW = S::NW;                  // compute waves per K-group
+  constexpr int NWC = NW * KG;               // compute waves
+  constexpr int NT = (NWC + NL) * 64;        // all threads of the block
+  constexpr int NWI = NL > 0 ? NL : NWC;     // waves that issue the LDS-DMA pieces
+  constexpr int NKS = 2 / KG;                // 32-wide MFMA K steps per wave per K tile
+  static_assert(KG == 1 || (KG == 2 && NL == 0), "K-groups");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_INS = BM / (8 * NWI), B_INS = BN / (8 * NWI);   // glds instructions per issuing wave per tile
   constexpr int LPW = A_INS + B_INS;
   constexpr int TILE_A = BM * 128, STAGE_BYTES = S::STAGE_BYTES;
   constexpr int EPI_LD = BN + 4;
-  static_assert((NW == 4 || NW == 8 || NW == 16) && A_INS * 8 * NWI == BM && B_INS * 8 * NWI == BN,
+  static_assert((NWC == 4 || NWC == 8 || NWC == 16) && A_INS * 8 * NWI == BM && B_INS * 8 * NWI == BN,
                 "waves / tile split");
   static_assert(STAGES >= 2 && S::LDS_BYTES + 16 <= 160 * 1024, "stages");
   static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
@@ -105,7 +116,9 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool loader = NL > 0 && wave >= NW;  // wave-uniform
   const int iwave = NL > 0 ? (loader ? wave - NW : 0) : wave;   // index among the issuing waves
-  const int wm = (loader ? 0 : wave) / WN, wn = (loader ? 0 : wave) % WN;
+  const int kg = KG > 1 ? wave / NW : 0;     // K-group: first 32-wide MFMA K step it runs
+  const int wsub = (loader ? 0 : wave) % NW;
+  const int wm = wsub / WN, wn = wsub % WN;
 
   const int tilesN = (p.N + BN - 1) / BN;
   const int tm = tile / tilesN, tn = tile % tilesN;
@@ -227,7 +240,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     for (int s = 0; s < STAGES - 1; ++s) issue(s);
   }
 
-  constexpr int MT = 2 * FM * FN;          // MFMAs per wave per K tile
+  constexpr int MT = NKS * FM * FN;        // MFMAs per wave per K tile
   for (int t = 0; t < nk; ++t) {
     // tile t must have landed (the issuing waves' counted wait + the barrier
     // orders it for every reader); the STAGES-2 tiles issued after it stay in flight
@@ -246,9 +259,10 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
     }
     const char* sa = smem + (t % STAGES) * STAGE_BYTES;
     const char* sb = sa + TILE_A;
-    bf16x8 af[2][FM], bfr[2][FN];
+    bf16x8 af[NKS][FM], bfr[NKS][FN];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int kq = (ks + kg) * 4 + fq;     // 16-byte chunk of this lane's K slice
       if constexpr (ABL & 8) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) af[ks][i] = (bf16x8){};
@@ -256,14 +270,14 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
         for (int j = 0; j < FN; ++j) bfr[ks][j] = (bf16x8){};
       } else {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) af[ks][i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, ks * 4 + fq));
+        for (int i = 0; i < FM; ++i) af[ks][i] = *(const bf16x8*)(sa + swz2(wm * TM + i * 16 + fr, kq));
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[ks][j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, ks * 4 + fq));
+        for (int j = 0; j < FN; ++j) bfr[ks][j] = *(const bf16x8*)(sb + swz2(wn * TN + j * 16 + fr, kq));
       }
     }
     if constexpr (ABL & 1) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < NKS; ++ks) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[ks][i]));
 #pragma unroll
@@ -271,7 +285,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
       }
     } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -284,7 +298,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
       // serialise in front of the MFMA block)
       issue(nslot);
       constexpr int MPP = MT / LPW > 0 ? MT / LPW : 1;
-      __builtin_amdgcn_sched_group_barrier(0x100, 4 * (FM + FN), 0);   // ds_read
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * NKS * (FM + FN), 0);   // ds_read
 #pragma unroll
       for (int q = 0; q < LPW; ++q) {
         __builtin_amdgcn_sched_group_barrier(0x008, MPP, 0);          // MFMA
@@ -300,7 +314,7 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
 
   // ---- epilogue (as conv_igemm.hip)
   float* epi = (float*)smem;
-  if (!loader) {
+  if (!loader && kg == 0) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -311,6 +325,20 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
       }
   }
   __syncthreads();
+  if constexpr (KG > 1) {
+    // K-group 1 adds its partial sums onto group 0's (same fragment layout)
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = wn * TN + j * 16 + fr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) epi[(wm * TM + i * 16 + fq * 4 + r) * EPI_LD + col] += acc[i][j][r];
+        }
+    }
+    __syncthreads();
+  }
   constexpr int CPR = BN / 8;
   constexpr int NCH = BM * CPR;
   if (p.ksplit > 1) {
@@ -415,8 +443,9 @@ __device__ __forceinline__ void glds_tile(const ConvParams& p, const bf16* __res
 // (b) stream-K (p.ksplit < 0): the tiles x K-tiles iteration space is cut into
 // equal contiguous ranges of p.sk_iters, one per block, so ~200-tile problems
 // keep every CU busy instead of leaving a quarter of the chip idle.
-template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32, int ABL = 0, int NL = 0>
-__global__ __launch_bounds__((WM * WN + NL) * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
+template <int BM, int BN, int WM, int WN, int STAGES, bool ILV, bool PURE, bool OUT_F32, int ABL = 0, int NL = 0,
+          int KG = 1>
+__global__ __launch_bounds__((WM * WN * KG + NL) * 64, 1) void conv_glds_kernel(ConvParams p, const bf16* __restrict__ zero) {
   using S = GldsShape<BM, BN, WM, WN, STAGES>;
   __shared__ __attribute__((aligned(16))) char smem[S::LDS_BYTES + 16];
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -426,7 +455,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64, 1) void conv_glds_kernel(ConvP
     const int kt_per = (kt + p.ksplit - 1) / p.ksplit;
     const int kt0 = blockIdx.y * kt_per;
     const int kt1 = min(kt, kt0 + kt_per);
-    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32, ABL, NL>(p, zero, smem, tile, kt0, kt1, blockIdx.y,
+    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32, ABL, NL, KG>(p, zero, smem, tile, kt0, kt1, blockIdx.y,
                                                                    SkSeg{-1, 1, 0, 0});
     return;
   }
@@ -443,7 +472,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64, 1) void conv_glds_kernel(ConvP
       const int g_first = (tile * kt) / iters, g_last = ((tile + 1) * kt - 1) / iters;
       sk = SkSeg{sk_slot(g, tile, kt, iters), g_last - g_first + 1, g - g_first, g_first};
     }
-    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32, ABL, NL>(p, zero, smem, tile, kbeg, kend, 0, sk);
+    glds_tile<BM, BN, WM, WN, STAGES, ILV, PURE, OUT_F32, ABL, NL, KG>(p, zero, smem, tile, kbeg, kend, 0, sk);
     it += kend - kbeg;
     __syncthreads();   // the next segment's DMA reuses the epilogue's LDS
   }
@@ -496,6 +525,19 @@ __device__ __attribute__((aligned(64))) bf16 g_zero_page[64];
   X(57, 256, 128, 4, 4, 3, true)   \
   X(58, 128, 128, 4, 4, 2, true)
 
+// 62-70: two K-groups (KG = 2) of WM x WN waves, 8 waves per block; per-wave
+// sub-tiles of 32x64 .. 64x128 (see glds_tile)
+#define ADAPT_GLDS_KG_CFGS(X)       \
+  X(62, 64, 128, 2, 2, 4, true)     \
+  X(63, 128, 128, 2, 2, 3, true)    \
+  X(64, 64, 256, 1, 4, 3, true)     \
+  X(65, 128, 128, 2, 2, 4, true)    \
+  X(66, 64, 128, 2, 2, 3, true)     \
+  X(67, 128, 64, 2, 2, 4, true)     \
+  X(68, 64, 64, 2, 2, 4, true)      \
+  X(69, 128, 256, 2, 2, 3, true)    \
+  X(70, 256, 128, 2, 2, 3, true)
+
 // 53-58: 16 waves (4 per SIMD) per block: twice the LDS-DMA pieces in flight per
 // CU at the same tile size.  Measured (profiles/conv_bench_v7_16w.txt): within
 // 1-2 % of the 8-wave tiles on every ResNet-50 shape (ahead only on the stage-3
@@ -521,12 +563,13 @@ bool conv_glds_cfg_tile(int cfg, int* bm, int* bn) {
   switch (cfg) {
 #define X(id, BM_, BN_, WM_, WN_, S_, I_) case id: *bm = BM_; *bn = BN_; return true;
     ADAPT_GLDS_CFGS(X)
+    ADAPT_GLDS_KG_CFGS(X)
 #undef X
   }
   return false;
 }
 
-template <int BM, int BN, int WM, int WN, int S, bool ILV>
+template <int BM, int BN, int WM, int WN, int S, bool ILV, int KG = 1>
 static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, bool out_f32) {
   static bf16* zero = nullptr;
   if (!zero) {
@@ -534,7 +577,7 @@ static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, boo
     if (e != hipSuccess) return e;
   }
   const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
-  dim3 grid(tilesM * tilesN, p.ksplit), block(WM * WN * 64);
+  dim3 grid(tilesM * tilesN, p.ksplit), block(WM * WN * KG * 64);
   if (p.ksplit < 0) {
     int g, iters;
     conv_sk_plan(tilesM * tilesN, p.Kpad / BK2, -p.ksplit, &g, &iters);
@@ -542,11 +585,11 @@ static hipError_t launch_glds(const ConvParams& p, hipStream_t s, bool pure, boo
     grid = dim3(g, 1);
   }
   if (pure) {
-    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, true>), grid, block, 0, s, p, zero);
-    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, false>), grid, block, 0, s, p, zero);
+    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, true, 0, 0, KG>), grid, block, 0, s, p, zero);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, true, false, 0, 0, KG>), grid, block, 0, s, p, zero);
   } else {
-    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, false, true>), grid, block, 0, s, p, zero);
-    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, false, false>), grid, block, 0, s, p, zero);
+    if (out_f32) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, false, true, 0, 0, KG>), grid, block, 0, s, p, zero);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, S, ILV, false, false, 0, 0, KG>), grid, block, 0, s, p, zero);
   }
   return hipGetLastError();
 }
@@ -555,6 +598,9 @@ hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pu
   switch (cfg) {
 #define X(id, BM_, BN_, WM_, WN_, S_, I_) case id: return launch_glds<BM_, BN_, WM_, WN_, S_, I_>(p, s, pure, out_f32);
     ADAPT_GLDS_CFGS(X)
+#undef X
+#define X(id, BM_, BN_, WM_, WN_, S_, I_) case id: return launch_glds<BM_, BN_, WM_, WN_, S_, I_, 2>(p, s, pure, out_f32);
+    ADAPT_GLDS_KG_CFGS(X)
 #undef X
   }
   return hipErrorInvalidValue;

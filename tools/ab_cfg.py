@@ -24,8 +24,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--key", required=True)
-    ap.add_argument("--cfg", type=int, required=True)
+    ap.add_argument("--key", default="")
+    ap.add_argument("--cfg", type=int, default=-1)
+    ap.add_argument("--set", action="append", default=[],
+                    help="KEYPARTS@CFG@KSPLIT, repeatable: switch several conv groups in the B variant")
+    ap.add_argument("--ksplit", type=int, default=1, help="split-K (> 1) or stream-K (< 0) of the switched convs")
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--json", default="")
     a = ap.parse_args()
@@ -33,16 +36,23 @@ def main():
     w = init_weights(g, 0)
     x = torch.randn((a.batch,) + tuple(g.layers[g.input].out_shape), device="cuda")
     exs = {}
-    for variant in ("tuned", f"cfg {a.cfg}"):
+    sets = [(k, int(c), int(ks)) for k, c, ks in (x.split("@") for x in a.set)]
+    if a.key:
+        sets.append((a.key, a.cfg, a.ksplit))
+    if not sets:
+        ap.error("--key/--cfg or --set required")
+    bname = f"cfg {a.cfg}" if len(sets) == 1 and a.key else "switched"
+    for variant in ("tuned", bname):
         ex = SliceExecutor(g, w, a.batch)
         if variant != "tuned":
             hit = []
             for i in list(ex.cfg):
                 B, H, W, C, OH, OW, pc = ex._conv_geom(i)
                 ck = conv_key(B, H, W, C, pc)
-                if all(part in ck for part in a.key.split(",")):
-                    ex.cfg[i] = (a.cfg, 1)
-                    hit.append(ex.steps[i].out)
+                for key, cfg, ks in sets:
+                    if all(part in ck for part in key.split(",")):
+                        ex.cfg[i] = (cfg, ks)
+                        hit.append(f"{ex.steps[i].out}->{cfg}/{ks}")
             print(f"{variant}: switched {hit}")
             ex._ensure_ws()
         ex.input_buf(g.input).copy_(x.to(ex.input_buf(g.input).dtype)[..., :ex.input_buf(g.input).shape[-1]]
@@ -56,7 +66,7 @@ def main():
         ex.forward(0)
         torch.cuda.synchronize()
         outs[v] = ex.output_buf(ex.outputs[0]).float().clone()
-    diff = (outs["tuned"] - outs[f"cfg {a.cfg}"]).abs().max().item()
+    diff = (outs["tuned"] - outs[bname]).abs().max().item()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {v: [] for v in exs}
     for r in range(a.rounds):
@@ -69,7 +79,7 @@ def main():
             e1.record()
             e1.synchronize()
             res[v].append(e0.elapsed_time(e1) / 50)
-    rec = {"model": a.model, "batch": a.batch, "key": a.key, "cfg": a.cfg, "max_abs_diff": diff,
+    rec = {"model": a.model, "batch": a.batch, "sets": sets, "max_abs_diff": diff,
            "ms_median": {v: statistics.median(t) for v, t in res.items()}}
     for v, t in res.items():
         m = statistics.median(t)

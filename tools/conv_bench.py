@@ -78,7 +78,7 @@ def bench(shape, only=None, reps=20, ks_list=(1, 2, 3, 4, 6, 8, -1, -2)):
     rows.sort()
     print(f"\n== B{B} {H}x{W}x{Cin} -> {Cout} k{k} s{s}  M={M} N={N} K={pc.K}  "
           f"{flop / 1e9:.2f} GFLOP {byts / 1e6:.1f} MB")
-    for t, cfg, ks, blocks in rows[:8]:
+    for t, cfg, ks, blocks in rows[:30]:
         print(f"  cfg {cfg:2d} {str(C.CFG_TILES[cfg]):10s} ks {ks}  blocks {blocks:5d}  {t:7.2f} us  "
               f"{flop / t / 1e6:7.1f} TF/s  {byts / t / 1e3:6.2f} TB/s")
     return rows
