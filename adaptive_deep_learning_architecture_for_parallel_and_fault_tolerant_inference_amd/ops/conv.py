@@ -11,6 +11,7 @@ launch inside its buffers (done before every launch).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -505,3 +506,69 @@ def bottleneck_forward(x: torch.Tensor, pb: PackedBottleneck, out: torch.Tensor,
     kernels().bottleneck_forward(ptr(x), ptr(pb.w1), ptr(pb.w2), ptr(pb.w3), ptr(pb.b1), ptr(pb.b2), ptr(pb.b3),
                                  ptr(out), B, H, W, pb.cin, bool(pb.proj), stream_handle(stream))
     return out
+
+
+# ------------------------------------------------------- fused 1x1 pair
+# `_out` of block k (1x1 CIN -> CO + BN + residual + ReLU) and `_1` of block k+1
+# (1x1 CO -> CM + BN + ReLU) in one launch (csrc/kernels/pw_pair.hip): y stays
+# in LDS for the second GEMM and is written once, as the next residual.
+PAIR_BM = {128: 112}                  # pixels per workgroup by CIN (ResNet stage 3: 224 tiles, one round)
+# (CIN, CO, CM, BM) instances (must match ADAPT_PAIR_CFGS in pw_pair.hip)
+PAIR_CFGS = {(128, 512, 128, 112), (128, 512, 128, 64)}
+
+
+@dataclass
+class PackedPair:
+    w3: torch.Tensor
+    b3: torch.Tensor
+    w1: torch.Tensor
+    b1: torch.Tensor
+    cin: int
+    co: int
+    cm: int
+    bm: int = 0               # pixels per workgroup, fixed when packed (ADAPT_PAIR_BM overrides the table)
+
+
+def pair_bm(cin: int) -> int:
+    """Pixels per workgroup for a pair with CIN input channels; ADAPT_PAIR_BM="128:32,256:16"
+    overrides the table per CIN (0 disables the fusion for that CIN)."""
+    table = dict(PAIR_BM)
+    for kv in os.environ.get("ADAPT_PAIR_BM", "").split(","):
+        if ":" in kv:
+            c, b = kv.split(":")
+            table[int(c)] = int(b)
+    return table.get(cin, 0)
+
+
+def pair_supported(cin: int, co: int, cm: int, bm: Optional[int] = None) -> bool:
+    bm = pair_bm(cin) if bm is None else bm
+    return (cin, co, cm, bm) in PAIR_CFGS
+
+
+def pack_pair(k3, b3, k1, b1, device="cuda") -> PackedPair:
+    """HWIO kernels (BN folded) of the two 1x1 convs."""
+    if k3.shape[:2] != (1, 1) or k1.shape[:2] != (1, 1) or k1.shape[2] != k3.shape[3]:
+        raise ValueError(f"fused 1x1 pair: shapes {k3.shape} -> {k1.shape}")
+
+    def dev(a, dt=torch.bfloat16):
+        return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device=device, dtype=dt).contiguous()
+    return PackedPair(w3=dev(pack_fragments(k3[0, 0].T)), b3=dev(b3, torch.float32),
+                      w1=dev(pack_fragments(k1[0, 0].T)), b1=dev(b1, torch.float32),
+                      cin=k3.shape[2], co=k3.shape[3], cm=k1.shape[3], bm=pair_bm(k3.shape[2]))
+
+
+def pair_forward(x: torch.Tensor, res: torch.Tensor, pp: PackedPair, y: torch.Tensor, z: torch.Tensor,
+                 bm: Optional[int] = None, stream=None):
+    bm = (pp.bm or pair_bm(pp.cin)) if bm is None else bm
+    for t in (x, res, y, z):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.device != x.device:
+            raise ValueError("fused 1x1 pair: contiguous bf16 tensors on one device")
+    M = x.numel() // pp.cin
+    if x.shape[-1] != pp.cin or res.numel() != M * pp.co or y.numel() != M * pp.co or z.numel() != M * pp.cm:
+        raise ValueError(f"fused 1x1 pair: x {tuple(x.shape)} res {tuple(res.shape)} y {tuple(y.shape)} "
+                         f"z {tuple(z.shape)} for {pp.cin}->{pp.co}->{pp.cm}")
+    if not pair_supported(pp.cin, pp.co, pp.cm, bm):
+        raise ValueError(f"fused 1x1 pair: no kernel for {pp.cin}->{pp.co}->{pp.cm} at {bm} pixels per block")
+    kernels().pw_pair_forward(ptr(x), ptr(pp.w3), ptr(pp.b3), ptr(res), ptr(pp.w1), ptr(pp.b1), ptr(y), ptr(z),
+                              M, pp.cin, pp.co, pp.cm, bm, stream_handle(stream))
+    return y, z

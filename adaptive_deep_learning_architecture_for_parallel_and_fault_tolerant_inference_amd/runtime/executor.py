@@ -167,6 +167,11 @@ class SliceExecutor:
                 if p["proj"] is not None:
                     kp, bp = self._folded(weights, p["proj"])
                 self.packed[i] = conv_ops.pack_bottleneck(k1, b1, k2, b2, k3, b3, kp, bp, device=dev)
+            elif st.kind == "pair":
+                p = st.p
+                k3, b3 = self._folded(weights, p["c3"])
+                k1, b1 = self._folded(weights, p["c1"])
+                self.packed[i] = conv_ops.pack_pair(k3, b3, k1, b1, device=dev)
             elif st.kind == "stem":
                 p = st.p
                 k = weights[f"{p['conv']}/kernel"]
@@ -491,7 +496,7 @@ class SliceExecutor:
             self.cfg[i] = (int(cfg), int(ks))
         self._ensure_ws()
         if tune:
-            self.autotune_f32() if self.fp32 else self.autotune()
+            self.autotune_f32() if self.fp32 else self.autotune(verbose=os.environ.get("ADAPT_TUNE_VERBOSE", "0") == "1")
 
     @staticmethod
     def _time_graph(fn, reps: int) -> float:
@@ -550,7 +555,7 @@ class SliceExecutor:
             save_tuning(results)
         return results
 
-    def autotune(self, reps: int = 20, persist: bool = True, refine: int = 3) -> Dict[str, List]:
+    def autotune(self, reps: int = 20, persist: bool = True, refine: int = 3, verbose: bool = False) -> Dict[str, List]:
         """Time every (tile cfg, split-K) candidate per conv problem in isolation,
         then (refine > 1) re-decide each problem among its `refine` best
         candidates by replaying the WHOLE captured slice: isolated timings miss
@@ -615,9 +620,14 @@ class SliceExecutor:
                 results[key] = [best[1], best[2], round(best[0] * 1000, 2)]
                 done[key] = (best[1], best[2])
                 self.cfg[i] = (best[1], best[2])
+                if verbose:
+                    print(f"autotune {key}: cfg {best[1]} ksplit {best[2]} {best[0] * 1000:.2f} us", flush=True)
         self._ensure_ws()
+        # ADAPT_TUNE_REFINE: how many of each problem's best isolated candidates
+        # are re-timed inside the whole captured slice
+        refine = int(os.environ.get("ADAPT_TUNE_REFINE", refine))
         if refine > 1 and ranked:
-            self._refine_in_graph(ranked, results, refine, prev)
+            self._refine_in_graph(ranked, results, refine, prev, verbose)
         if persist:
             save_tuning(results)
         return results
@@ -646,7 +656,8 @@ class SliceExecutor:
         del g
         return sorted(times)[len(times) // 2]
 
-    def _refine_in_graph(self, ranked, results, top: int, prev: Optional[Dict[str, List]] = None) -> None:
+    def _refine_in_graph(self, ranked, results, top: int, prev: Optional[Dict[str, List]] = None,
+                         verbose: bool = False) -> None:
         steps_of: Dict[str, List[int]] = {}
         for i, st in enumerate(self.steps):
             if st.kind in ("conv", "dense") and i not in self._dense_part:
@@ -677,6 +688,8 @@ class SliceExecutor:
                 self._ensure_ws()
                 tt = self._graph_time()
                 if tt < base * 0.997:
+                    if verbose:
+                        print(f"refine {key}: cfg {cfg} ksplit {ks}: slice {base:.4f} -> {tt:.4f} ms", flush=True)
                     base, cur = tt, (cfg, ks)
                     results[key] = [cfg, ks, round(t * 1000, 2)]
                 else:
@@ -722,6 +735,9 @@ class SliceExecutor:
                 E.input_pack(b[st.ins[0]], b[st.out], stream=stream)
             elif k == "bottleneck":
                 conv_ops.bottleneck_forward(b[st.ins[0]], self.packed[i], b[st.out], stream=stream)
+            elif k == "pair":
+                conv_ops.pair_forward(b[st.ins[0]], b[st.ins[1]], self.packed[i], b[st.out], b[st.p["out2"]],
+                                      stream=stream)
             elif k == "stem":
                 conv_ops.stem_forward(b[st.ins[0]], self.packed[i], b[st.out], pool=st.p["pool"],
                                       pool_pad=st.p["pool_pad"], stream=stream)

@@ -319,6 +319,9 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
         return steps
     if os.environ.get("ADAPT_FUSED_BOTTLENECK", "1") == "1":
         steps = fuse_bottlenecks(g, steps, outset)
+    # off by default: measured slower in the whole-model A/B (profiles/r2/experiments/pair/)
+    if os.environ.get("ADAPT_FUSED_PAIR", "0") == "1":
+        steps = fuse_pairs(g, steps, outset)
     if os.environ.get("ADAPT_NO_STEM", "0") != "1":
         steps = _fuse_stem(g, steps, outset)
     if os.environ.get("ADAPT_NO_SIBLINGS", "0") != "1":
@@ -381,6 +384,45 @@ def fuse_bottlenecks(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step
              "proj": steps[proj].p if proj is not None else None, "cin": xl.out_shape[2]}
         repl[j3] = Step("bottleneck", s3.out, [x], covers, p)
         drop.update(jj for jj in group if jj != j3)
+    return [repl.get(j, st) for j, st in enumerate(steps) if j not in drop]
+
+
+def fuse_pairs(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
+    """1x1 (CIN -> CO) + BN + residual + ReLU (block k's ``_out``) followed by the
+    1x1 (CO -> CM) + BN + ReLU that is the next block's ``_1`` ==> one ``pair``
+    step with two outputs (csrc/kernels/pw_pair.hip): y is still written (it is
+    the next residual) but the second GEMM reads it from LDS, and the pair is
+    one launch.  Only the stride-1 pairs inside a ResNet stage qualify.  Both
+    outputs land in their own named buffers, so either may be a slice frontier."""
+    from ..ops.conv import pair_supported   # static shape table, no device needed
+
+    def conv1x1(st: Step, relu: int, res: bool) -> bool:
+        p = st.p
+        return (st.kind == "conv" and p.get("kernel") == (1, 1) and p.get("stride") == 1
+                and p.get("pads") == ((0, 0), (0, 0)) and p.get("relu") == relu and bool(p.get("residual")) == res
+                and not p.get("packed_input") and not p.get("sibling"))
+
+    drop: Set[int] = set()
+    repl: Dict[int, Step] = {}
+    for ja, a in enumerate(steps):
+        if ja in drop or ja in repl or not conv1x1(a, 1, True):
+            continue
+        users = [j for j, st in enumerate(steps) if a.out in st.ins]
+        firsts = [j for j in users if steps[j].ins[0] == a.out and conv1x1(steps[j], 1, False)
+                  and len(steps[j].ins) == 1]
+        if len(firsts) != 1 or firsts[0] <= ja or firsts[0] in repl:
+            continue
+        jb = firsts[0]
+        b = steps[jb]
+        xl = g.layers[a.ins[0].split("#")[0]]
+        if len(xl.out_shape) != 3:
+            continue
+        cin, co, cm = xl.out_shape[2], a.p["filters"], b.p["filters"]
+        if not pair_supported(cin, co, cm):
+            continue
+        p = {"c3": a.p, "c1": b.p, "out2": b.out, "cin": cin, "co": co, "cm": cm}
+        repl[ja] = Step("pair", a.out, list(a.ins), a.covers + b.covers, p)
+        drop.add(jb)
     return [repl.get(j, st) for j, st in enumerate(steps) if j not in drop]
 
 

@@ -292,6 +292,13 @@ PYBIND11_MODULE(_C, m) {
                               P<const float>(b1), P<const float>(b2), P<const float>(b3), P<bf16>(out), B, H, W};
     check(adapt::bottleneck_forward(p, cin, proj, S(s)), "bottleneck_forward");
   });
+  m.def("pw_pair_forward", [](u64 x, u64 w3, u64 b3, u64 res, u64 w1, u64 b1, u64 y, u64 z, int M, int cin, int co,
+                              int cm, int bm, u64 s) {
+    adapt::PwPairParams p{P<const bf16>(x), P<const bf16>(w3), P<const float>(b3), P<const bf16>(res),
+                          P<const bf16>(w1), P<const float>(b1), P<bf16>(y), P<bf16>(z), M};
+    check(adapt::pw_pair_forward(p, cin, co, cm, bm, S(s)), "pw_pair_forward");
+  });
+  m.def("pw_pair_supported", [](int cin, int co, int cm, int bm) { return adapt::pw_pair_supported(cin, co, cm, bm); });
   m.def("ingest_u8", [](u64 x, u64 y, size_t n, int C, int reverse, std::vector<float> scale,
                         std::vector<float> shift, u64 s) {
     if ((int)scale.size() < C || (int)shift.size() < C) throw std::runtime_error("ingest_u8: scale/shift per channel");

@@ -142,6 +142,21 @@ struct BottleneckParams {
   int B, H, W;
 };
 hipError_t bottleneck_forward(const BottleneckParams& p, int cin, bool proj, hipStream_t s);
+// fused 1x1 pair across a ResNet block boundary (pw_pair.hip):
+// y = relu(x . W3^T + b3 + res) [M][CO], z = relu(y . W1^T + b1) [M][CM]; W3 / W1 in MFMA fragment order
+struct PwPairParams {
+  const bf16* x;
+  const bf16* w3;
+  const float* b3;
+  const bf16* res;
+  const bf16* w1;
+  const float* b1;
+  bf16* y;
+  bf16* z;
+  int M;
+};
+bool pw_pair_supported(int cin, int co, int cm, int bm);
+hipError_t pw_pair_forward(const PwPairParams& p, int cin, int co, int cm, int bm, hipStream_t s);
 // persistent pointwise conv, weights register-resident per wave (pw_wide.hip):
 // out[m][n] = act(x[m] . W[n] + bias[n] (+ res[m][n])), x [M][K], W in MFMA fragment order
 struct PwParams {

@@ -152,6 +152,27 @@ def test_plan_fused_bottlenecks(r50):
     assert k0.count("bottleneck") == 1 and k0.count("conv") == 2
 
 
+def test_plan_fused_pairs(r50, monkeypatch):
+    """ADAPT_FUSED_PAIR=1: each stride-1 `_out` -> next `_1` pair of stage 3 becomes
+    one two-output `pair` step (3 in ResNet-50); stages 4 and 5 have no kernel
+    instance and stay unfused; a slice cut at the second conv's output still
+    produces it (as the pair's second output)."""
+    monkeypatch.setenv("ADAPT_FUSED_PAIR", "1")
+    steps = compile_plan(r50)
+    pairs = [s for s in steps if s.kind == "pair"]
+    assert [s.out for s in pairs] == [f"conv3_block{i}_out" for i in (1, 2, 3)]
+    assert [s.p["out2"] for s in pairs[:2]] == ["conv3_block2_1_relu", "conv3_block3_1_relu"]
+    assert pairs[0].ins == ["conv3_block1_2_relu", "conv3_block1_0_bn"]
+    assert (pairs[0].p["cin"], pairs[0].p["co"], pairs[0].p["cm"]) == (128, 512, 128)
+    outs = {s.out for s in steps} | {s.p.get("out2") for s in steps}
+    assert "conv3_block2_1_relu" in outs and "conv4_block2_1_relu" in outs
+    s = partition(r50, ["conv3_block2_1_relu"])
+    k0 = compile_plan(subgraph(r50, s[0]))
+    assert k0[-1].kind == "pair" and k0[-1].p["out2"] == "conv3_block2_1_relu"
+    monkeypatch.setenv("ADAPT_FUSED_PAIR", "0")
+    assert not any(x.kind == "pair" for x in compile_plan(r50))
+
+
 def test_plan_unfused_at_cut(r50):
     s = partition(r50, ["conv3_block1_1_conv"])
     st2 = compile_plan(subgraph(r50, s[1]))

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--set", action="append", default=[],
                     help="KEYPARTS@CFG@KSPLIT, repeatable: switch several conv groups in the B variant")
     ap.add_argument("--ksplit", type=int, default=1, help="split-K (> 1) or stream-K (< 0) of the switched convs")
+    ap.add_argument("--env-a", default="", help="K=V;... set while building the A (tuned) executor")
+    ap.add_argument("--env-b", default="", help="K=V;... set while building the B executor (plan switches)")
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--json", default="")
     a = ap.parse_args()
@@ -39,11 +41,21 @@ def main():
     sets = [(k, int(c), int(ks)) for k, c, ks in (x.split("@") for x in a.set)]
     if a.key:
         sets.append((a.key, a.cfg, a.ksplit))
-    if not sets:
-        ap.error("--key/--cfg or --set required")
+    if not sets and not a.env_b:
+        ap.error("--key/--cfg, --set or --env-b required")
     bname = f"cfg {a.cfg}" if len(sets) == 1 and a.key else "switched"
     for variant in ("tuned", bname):
+        env = dict(kv.split("=", 1) for kv in (a.env_a if variant == "tuned" else a.env_b).split(";") if kv)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         ex = SliceExecutor(g, w, a.batch)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        if env:
+            print(f"{variant}: built with {env}, {len(ex.steps)} steps")
         if variant != "tuned":
             hit = []
             for i in list(ex.cfg):
