@@ -512,9 +512,9 @@ def bottleneck_forward(x: torch.Tensor, pb: PackedBottleneck, out: torch.Tensor,
 # `_out` of block k (1x1 CIN -> CO + BN + residual + ReLU) and `_1` of block k+1
 # (1x1 CO -> CM + BN + ReLU) in one launch (csrc/kernels/pw_pair.hip): y stays
 # in LDS for the second GEMM and is written once, as the next residual.
-PAIR_BM = {128: 112}                  # pixels per workgroup by CIN (ResNet stage 3: 224 tiles, one round)
+PAIR_BM = {128: 16}                   # pixels per tile of the persistent kernel, by CIN (ResNet stage 3)
 # (CIN, CO, CM, BM) instances (must match ADAPT_PAIR_CFGS in pw_pair.hip)
-PAIR_CFGS = {(128, 512, 128, 112), (128, 512, 128, 64)}
+PAIR_CFGS = {(128, 512, 128, 16)}
 
 
 @dataclass

@@ -37,7 +37,11 @@ def parse(argv=None):
     ap.add_argument("--part-at", default="")
     ap.add_argument("--codec", default="none", choices=["none", "lz4", "zvc"])
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--atol", type=float, default=5e-3)
+    # Softmax probabilities of a random-init bf16 ResNet move by a few 1e-3 under any change of
+    # summation order: the cut itself (conv -> bf16 -> standalone BN instead of the fused epilogue)
+    # gave 2.6e-3 / 7.3e-3 without / with the fused 1x1 pairs, and the same unsliced model with and
+    # without the pairs differs by 3.3e-3 at batch 4 (split-K vs whole-K sums; profiles/r2/experiments/pair/)
+    ap.add_argument("--atol", type=float, default=1e-2)
     ap.add_argument("--p2p-bw", action="store_true")
     ap.add_argument("--out", default="")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],

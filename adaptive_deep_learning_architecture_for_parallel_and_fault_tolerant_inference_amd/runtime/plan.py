@@ -319,8 +319,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
         return steps
     if os.environ.get("ADAPT_FUSED_BOTTLENECK", "1") == "1":
         steps = fuse_bottlenecks(g, steps, outset)
-    # off by default: measured slower in the whole-model A/B (profiles/r2/experiments/pair/)
-    if os.environ.get("ADAPT_FUSED_PAIR", "0") == "1":
+    # ADAPT_FUSED_PAIR=0 keeps the two launches (A/B: profiles/r2/experiments/pair/)
+    if os.environ.get("ADAPT_FUSED_PAIR", "1") == "1":
         steps = fuse_pairs(g, steps, outset)
     if os.environ.get("ADAPT_NO_STEM", "0") != "1":
         steps = _fuse_stem(g, steps, outset)

@@ -60,8 +60,9 @@ def test_pair_rejects_bad_shapes():
 
 
 def test_resnet50_with_pairs_matches_unfused(monkeypatch):
-    """Whole ResNet-50 with the opt-in pair fusion (ADAPT_FUSED_PAIR=1) against the
-    default plan on the same weights and input: same logits up to bf16 rounding."""
+    """Whole ResNet-50 with the pair fusion (default) against the plan without it
+    (ADAPT_FUSED_PAIR=0) on the same weights and input: same logits up to bf16
+    rounding (bit-identical at bs=32, where the unfused convs do not split K)."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     resnet = importlib.import_module(f"{PKG}.models.resnet")

@@ -33,7 +33,7 @@ def gtime(fn, reps=20):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--bm", default="112,64")
+    ap.add_argument("--bm", default="16")
     ap.add_argument("--only-pair", action="store_true")
     a = ap.parse_args()
     M, cin, co, cm = 32 * 28 * 28, 128, 512, 128
