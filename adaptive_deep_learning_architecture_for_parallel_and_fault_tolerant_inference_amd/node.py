@@ -541,6 +541,17 @@ class Node:
         for t in list(self.threads):
             if t.name == "node-prepare" and t is not threading.current_thread():
                 t.join(timeout=60)
+        # ... and any StageCompute a config handler or stage runtime is building
+        # (capturing a hipGraph) right now: no capture may outlive the node, since
+        # while one runs PyTorch marks the default CUDA generator as capturing and
+        # a CUDA RNG call on any other thread of the process fails
+        deadline = time.monotonic() + 60
+        while time.monotonic() < deadline:
+            with self._computes_lock:
+                pending = list(self._building.values())
+            if not pending:
+                break
+            pending[0].wait(max(0.0, deadline - time.monotonic()))
 
     def _publish(self, **kw) -> None:
         if self.registration is not None:
@@ -685,7 +696,7 @@ class Node:
                 conn, _ = self.config_sock.accept()
             except OSError:
                 break
-            threading.Thread(target=self._handle_config, args=(conn,), daemon=True).start()
+            threading.Thread(target=self._handle_config, args=(conn,), daemon=True, name="node-config").start()
 
     def _handle_config(self, conn: socket.socket) -> None:
         try:
