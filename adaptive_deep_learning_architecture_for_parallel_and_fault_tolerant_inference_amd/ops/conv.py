@@ -65,6 +65,8 @@ def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
     pointwise configs (PW_CFGS) take 1x1 stride-1 convs of the shapes pw_wide.hip has."""
     if cfg in PW_CFGS:
         return pure and pw_supported(pc)
+    if cfg in RR3_CFGS:
+        return rr3_supported(pc)
     if cfg in V1_CFGS:
         return True
     if cfg in HALO_PATCH:
@@ -220,6 +222,10 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         raise ValueError("residual must be bf16 with the output's shape")
     if cfg is None:
         cfg, ksplit = choose_cfg(M, N, pc.Kpad)
+    if cfg in RR3_CFGS:                    # register-resident-filter 3x3 (conv3x3_rr.hip)
+        if ksplit != 1 or ns or out_f32 or residual is not None or (H, W) != (28, 28) or OH != H or OW != W:
+            raise ValueError(f"3x3 config {cfg}: 28x28 stride-1 bf16 output, no residual / split-K")
+        return rr3_forward(x, pc, out, relu=int(relu), stream=stream)
     if cfg in PW_CFGS:                     # persistent pointwise kernel (pw_wide.hip)
         if ksplit != 1 or ns or out_f32 or OH != H or OW != W:
             raise ValueError(f"pointwise config {cfg}: single bf16 output, no split-K")
@@ -445,6 +451,27 @@ def pw_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, residual: O
         raise ValueError(f"pw conv: x {tuple(x.shape)} / out {tuple(out.shape)} do not match {pc.cin} -> {pc.cout}")
     kernels().pw_res_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(residual), ptr(out), M, pc.cin,
                              pc.cout, int(relu), PW_CFGS[cfg], int(blocks), stream_handle(stream))
+    return out
+
+
+RR3_CFGS = {71}                               # 3x3 with the filter resident in VGPRs (conv3x3_rr.hip)
+
+
+def rr3_supported(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (3, 3, 1, 1, 1, 1, 1)
+            and pc.cin == 128 and pc.cout == 128 and pc.Kpad == 9 * 128 and not pc.n_split)
+
+
+def rr3_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, relu: int = 1, stream=None) -> torch.Tensor:
+    if not rr3_supported(pc):
+        raise ValueError("rr3 conv: needs a 3x3 / s1 / p1 conv 128 -> 128")
+    if x.dim() != 4 or tuple(x.shape[1:]) != (28, 28, 128) or tuple(out.shape) != tuple(x.shape):
+        raise ValueError(f"rr3 conv: x {tuple(x.shape)} out {tuple(out.shape)} (needs B x 28 x 28 x 128)")
+    for t in (x, out):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise ValueError("rr3 conv: contiguous bf16 NHWC tensors")
+    kernels().conv3x3_rr_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(out), int(x.shape[0]), 28, 28,
+                                 128, int(relu), stream_handle(stream))
     return out
 
 

@@ -156,6 +156,17 @@ struct PwPairParams {
   int M;
 };
 bool pw_pair_supported(int cin, int co, int cm, int bm);
+// 3x3 / s1 / p1 conv with the filter resident in VGPRs (conv3x3_rr.hip): out = act(conv(x) + bias)
+struct Conv3x3RRParams {
+  const bf16* x;
+  const bf16* wfrag;   // [Npad][9*C] packed in MFMA fragment order
+  const float* bias;
+  bf16* out;
+  int B;
+  int relu;
+};
+bool conv3x3_rr_supported(int C, int H, int W);
+hipError_t conv3x3_rr_forward(const Conv3x3RRParams& p, int C, int H, int W, hipStream_t s);
 hipError_t pw_pair_forward(const PwPairParams& p, int cin, int co, int cm, int bm, hipStream_t s);
 // persistent pointwise conv, weights register-resident per wave (pw_wide.hip):
 // out[m][n] = act(x[m] . W[n] + bias[n] (+ res[m][n])), x [M][K], W in MFMA fragment order
