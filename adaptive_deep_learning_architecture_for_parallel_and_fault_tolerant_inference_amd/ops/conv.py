@@ -225,7 +225,8 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
     if cfg in RR3_CFGS:                    # register-resident-filter 3x3 (conv3x3_rr.hip)
         if ksplit != 1 or ns or out_f32 or residual is not None or (H, W) != (28, 28) or OH != H or OW != W:
             raise ValueError(f"3x3 config {cfg}: 28x28 stride-1 bf16 output, no residual / split-K")
-        return rr3_forward(x, pc, out, relu=int(relu), stream=stream)
+        rr3_forward(x, pc, out.view(x.shape[0], OH, OW, N), relu=int(relu), stream=stream)
+        return out
     if cfg in PW_CFGS:                     # persistent pointwise kernel (pw_wide.hip)
         if ksplit != 1 or ns or out_f32 or OH != H or OW != W:
             raise ValueError(f"pointwise config {cfg}: single bf16 output, no split-K")

@@ -72,14 +72,15 @@ def bench(shape, only=None, reps=20, ks_list=(1, 2, 3, 4, 6, 8, -1, -2)):
             except (RuntimeError, ValueError) as e:
                 print("skip", cfg, ks, e)
                 continue
-            bm, bn = C.CFG_TILES[cfg]
-            blocks = C.sk_plan(M, N, pc.Kpad, cfg, -ks)[1] if ks < 0 else math.ceil(M / bm) * math.ceil(N / bn) * ks
+            bm, bn = C.CFG_TILES.get(cfg, (0, 0))
+            blocks = (C.sk_plan(M, N, pc.Kpad, cfg, -ks)[1] if ks < 0 else
+                      math.ceil(M / bm) * math.ceil(N / bn) * ks if bm else 0)
             rows.append((t, cfg, ks, blocks))
     rows.sort()
     print(f"\n== B{B} {H}x{W}x{Cin} -> {Cout} k{k} s{s}  M={M} N={N} K={pc.K}  "
           f"{flop / 1e9:.2f} GFLOP {byts / 1e6:.1f} MB")
     for t, cfg, ks, blocks in rows[:30]:
-        print(f"  cfg {cfg:2d} {str(C.CFG_TILES[cfg]):10s} ks {ks}  blocks {blocks:5d}  {t:7.2f} us  "
+        print(f"  cfg {cfg:2d} {str(C.CFG_TILES.get(cfg, '-')):10s} ks {ks}  blocks {blocks:5d}  {t:7.2f} us  "
               f"{flop / t / 1e6:7.1f} TF/s  {byts / t / 1e3:6.2f} TB/s")
     return rows
 
