@@ -26,8 +26,14 @@ namespace {
 
 typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int rswz(int r, int c) {   // 16-byte chunk c of a 256-byte pixel row r
-  return r * 256 + ((c ^ (r & 15)) << 4);
+// 16-byte chunk c of a 256-byte pixel row r.  The 16 pixels of a B fragment are
+// consecutive output pixels, which wrap from one 28-wide output row to the next
+// inside the 30-wide halo, and the taps shift them by 0..2 columns: a plain
+// c ^ (r & 15) leaves 624 extra LDS cycles per tile in the ds_read_b128 lane
+// groups; the rotation (c + 10 r) mod 16 was the best of an exhaustive search
+// over affine swizzles (432).
+__device__ __forceinline__ int rswz(int r, int c) {
+  return r * 256 + (((c + 10 * r) & 15) << 4);
 }
 
 }  // namespace
