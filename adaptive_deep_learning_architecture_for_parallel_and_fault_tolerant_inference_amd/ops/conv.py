@@ -225,7 +225,7 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
     if cfg in RR3_CFGS:                    # register-resident-filter 3x3 (conv3x3_rr.hip)
         if ksplit != 1 or ns or out_f32 or residual is not None or (H, W) != (28, 28) or OH != H or OW != W:
             raise ValueError(f"3x3 config {cfg}: 28x28 stride-1 bf16 output, no residual / split-K")
-        rr3_forward(x, pc, out.view(x.shape[0], OH, OW, N), relu=int(relu), stream=stream)
+        rr3_forward(x, pc, out.view(x.shape[0], OH, OW, N), relu=int(relu), kg=RR3_CFGS[cfg], stream=stream)
         return out
     if cfg in PW_CFGS:                     # persistent pointwise kernel (pw_wide.hip)
         if ksplit != 1 or ns or out_f32 or OH != H or OW != W:
@@ -455,7 +455,7 @@ def pw_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, residual: O
     return out
 
 
-RR3_CFGS = {71}                               # 3x3 with the filter resident in VGPRs (conv3x3_rr.hip)
+RR3_CFGS = {71: 1, 72: 2}                     # 3x3 with the filter resident in VGPRs (conv3x3_rr.hip) -> K groups
 
 
 def rr3_supported(pc: "PackedConv") -> bool:
@@ -463,7 +463,8 @@ def rr3_supported(pc: "PackedConv") -> bool:
             and pc.cin == 128 and pc.cout == 128 and pc.Kpad == 9 * 128 and not pc.n_split)
 
 
-def rr3_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, relu: int = 1, stream=None) -> torch.Tensor:
+def rr3_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, relu: int = 1, kg: int = 1,
+                stream=None) -> torch.Tensor:
     if not rr3_supported(pc):
         raise ValueError("rr3 conv: needs a 3x3 / s1 / p1 conv 128 -> 128")
     if x.dim() != 4 or tuple(x.shape[1:]) != (28, 28, 128) or tuple(out.shape) != tuple(x.shape):
@@ -472,7 +473,7 @@ def rr3_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, relu: int 
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise ValueError("rr3 conv: contiguous bf16 NHWC tensors")
     kernels().conv3x3_rr_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(out), int(x.shape[0]), 28, 28,
-                                 128, int(relu), stream_handle(stream))
+                                 128, int(relu), int(kg), stream_handle(stream))
     return out
 
 

@@ -298,9 +298,10 @@ PYBIND11_MODULE(_C, m) {
                           P<const bf16>(w1), P<const float>(b1), P<bf16>(y), P<bf16>(z), M};
     check(adapt::pw_pair_forward(p, cin, co, cm, bm, S(s)), "pw_pair_forward");
   });
-  m.def("conv3x3_rr_forward", [](u64 x, u64 wfrag, u64 bias, u64 out, int B, int H, int W, int C, int relu, u64 s) {
+  m.def("conv3x3_rr_forward", [](u64 x, u64 wfrag, u64 bias, u64 out, int B, int H, int W, int C, int relu, int kg,
+                                 u64 s) {
     adapt::Conv3x3RRParams p{P<const bf16>(x), P<const bf16>(wfrag), P<const float>(bias), P<bf16>(out), B, relu};
-    check(adapt::conv3x3_rr_forward(p, C, H, W, S(s)), "conv3x3_rr_forward");
+    check(adapt::conv3x3_rr_forward(p, C, H, W, kg, S(s)), "conv3x3_rr_forward");
   });
   m.def("pw_pair_supported", [](int cin, int co, int cm, int bm) { return adapt::pw_pair_supported(cin, co, cm, bm); });
   m.def("ingest_u8", [](u64 x, u64 y, size_t n, int C, int reverse, std::vector<float> scale,

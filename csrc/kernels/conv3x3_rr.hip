@@ -38,10 +38,15 @@ __device__ __forceinline__ int rswz(int r, int c) {
 
 }  // namespace
 
-template <int C, int H, int W, int TR>
-__global__ __launch_bounds__(C / 16 * 64, 1) void conv3x3_rr_kernel(Conv3x3RRParams p) {
-  constexpr int NWV = C / 16, NT = NWV * 64;
-  constexpr int KS = 9 * C / 32;                 // k-steps (36 for C = 128)
+// KG > 1: KG groups of C/16 waves split the k-steps (fewer resident fragments per
+// wave, KG times the waves per CU for latency hiding); the groups' partial sums
+// meet in an fp32 LDS buffer before the epilogue.
+template <int C, int H, int W, int TR, int KG = 1>
+__global__ __launch_bounds__(C / 16 * KG * 64, 1) void conv3x3_rr_kernel(Conv3x3RRParams p) {
+  constexpr int NCF = C / 16, NWV = NCF * KG, NT = NWV * 64;
+  constexpr int KSA = 9 * C / 32;                // k-steps of the filter (36 for C = 128)
+  constexpr int KS = KSA / KG;                   // k-steps per wave
+  static_assert(KSA % KG == 0, "K groups");
   constexpr int CCH = C / 8;                     // 16-byte chunks per pixel
   constexpr int HW2 = W + 2, HP = (TR + 2) * HW2;
   constexpr int PX = TR * W, PF = (PX + 15) / 16;
@@ -49,11 +54,14 @@ __global__ __launch_bounds__(C / 16 * 64, 1) void conv3x3_rr_kernel(Conv3x3RRPar
   constexpr int OIT = (PX * CCH + NT - 1) / NT;
   static_assert(C == 128 && CCH == 16, "rswz assumes 256-byte pixel rows");
   static_assert(H % TR == 0 && HP * C * 2 <= 160 * 1024 && PF * 16 * C * 2 <= HP * C * 2, "tile");
-  __shared__ __attribute__((aligned(16))) char halo[HP * C * 2];
+  constexpr int RED = KG > 1 ? PX * C * 4 : 0;   // fp32 partial sums of the other K groups
+  __shared__ __attribute__((aligned(16))) char halo[HP * C * 2 + RED];
+  static_assert(HP * C * 2 + RED <= 160 * 1024, "LDS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
+  const int cf = wave % NCF, kg = wave / NCF;    // channel fragment, K group
   const int tiles = p.B * (H / TR);
   const int t = xcd_remap(blockIdx.x, tiles);
   const int img = t / (H / TR), oh0 = (t % (H / TR)) * TR;
@@ -72,8 +80,8 @@ __global__ __launch_bounds__(C / 16 * 64, 1) void conv3x3_rr_kernel(Conv3x3RRPar
   const bf16x8* wf = (const bf16x8*)p.wfrag;
   bf16x8 wr[KS];
 #pragma unroll
-  for (int k = 0; k < KS; ++k) wr[k] = wf[(wave * KS + k) * 64 + lane];
-  const f32x4 bias = *(const f32x4*)(p.bias + wave * 16 + fq * 4);
+  for (int k = 0; k < KS; ++k) wr[k] = wf[(cf * KSA + kg * KS + k) * 64 + lane];
+  const f32x4 bias = *(const f32x4*)(p.bias + cf * 16 + fq * 4);
 #pragma unroll
   for (int it = 0; it < HIT; ++it) {
     const int i = tid + it * NT;
@@ -91,24 +99,60 @@ __global__ __launch_bounds__(C / 16 * 64, 1) void conv3x3_rr_kernel(Conv3x3RRPar
   f32x4 acc[PF];
 #pragma unroll
   for (int f = 0; f < PF; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if constexpr (KG == 1) {
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const int toff = (tap / 3) * HW2 + tap % 3;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = (tap / 3) * HW2 + tap % 3;
 #pragma unroll
-    for (int cc = 0; cc < C / 32; ++cc) {
+      for (int cc = 0; cc < C / 32; ++cc) {
+#pragma unroll
+        for (int f = 0; f < PF; ++f) {
+          const bf16x8 a = *(const bf16x8*)(halo + rswz(hb[f] + toff, cc * 4 + fq));
+          acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[tap * (C / 32) + cc], a, acc[f], 0, 0, 0);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int ks = kg * KS + k, tap = ks / (C / 32), cc = ks % (C / 32);   // wave-uniform
+      const int toff = (tap / 3) * HW2 + tap % 3;
 #pragma unroll
       for (int f = 0; f < PF; ++f) {
         const bf16x8 a = *(const bf16x8*)(halo + rswz(hb[f] + toff, cc * 4 + fq));
-        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[tap * (C / 32) + cc], a, acc[f], 0, 0, 0);
+        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[k], a, acc[f], 0, 0, 0);
+      }
+    }
+    // K groups 1.. park their partial sums (fp32, [pixel][channel]) past the halo
+    float* red = (float*)(halo + HP * C * 2);
+    const int chr = cf * 16 + fq * 4;
+    for (int g = 1; g < KG; ++g) {
+      if (kg == g) {
+#pragma unroll
+        for (int f = 0; f < PF; ++f) {
+          const int px = f * 16 + fr;
+          if (px < PX) {
+            f32x4* q = (f32x4*)(red + px * C + chr);
+            *q = g == 1 ? acc[f] : *q + acc[f];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int f = 0; f < PF; ++f) {
+        const int px = f * 16 + fr;
+        if (px < PX) acc[f] += *(const f32x4*)(red + px * C + chr);
       }
     }
   }
   __syncthreads();                               // every halo read done: stage the output tile over it
-  const int ch = wave * 16 + fq * 4;
+  const int ch = cf * 16 + fq * 4;
 #pragma unroll
   for (int f = 0; f < PF; ++f) {
     const int px = f * 16 + fr;
-    if (px < PX) {
+    if (kg == 0 && px < PX) {
       bf16x4v o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = f2bf(p.relu ? fmaxf(acc[f][e] + bias[e], 0.f) : acc[f][e] + bias[e]);
@@ -126,10 +170,12 @@ __global__ __launch_bounds__(C / 16 * 64, 1) void conv3x3_rr_kernel(Conv3x3RRPar
 
 bool conv3x3_rr_supported(int C, int H, int W) { return C == 128 && H == 28 && W == 28; }
 
-hipError_t conv3x3_rr_forward(const Conv3x3RRParams& p, int C, int H, int W, hipStream_t s) {
+hipError_t conv3x3_rr_forward(const Conv3x3RRParams& p, int C, int H, int W, int kg, hipStream_t s) {
   if (!conv3x3_rr_supported(C, H, W) || p.B < 1) return hipErrorInvalidValue;
   constexpr int TR = 4;
-  hipLaunchKernelGGL((conv3x3_rr_kernel<128, 28, 28, TR>), dim3(p.B * (28 / TR)), dim3(512), 0, s, p);
+  if (kg == 2) hipLaunchKernelGGL((conv3x3_rr_kernel<128, 28, 28, TR, 2>), dim3(p.B * (28 / TR)), dim3(1024), 0, s, p);
+  else if (kg == 1) hipLaunchKernelGGL((conv3x3_rr_kernel<128, 28, 28, TR, 1>), dim3(p.B * (28 / TR)), dim3(512), 0, s, p);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

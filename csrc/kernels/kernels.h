@@ -166,7 +166,7 @@ struct Conv3x3RRParams {
   int relu;
 };
 bool conv3x3_rr_supported(int C, int H, int W);
-hipError_t conv3x3_rr_forward(const Conv3x3RRParams& p, int C, int H, int W, hipStream_t s);
+hipError_t conv3x3_rr_forward(const Conv3x3RRParams& p, int C, int H, int W, int kg, hipStream_t s);
 hipError_t pw_pair_forward(const PwPairParams& p, int cin, int co, int cm, int bm, hipStream_t s);
 // persistent pointwise conv, weights register-resident per wave (pw_wide.hip):
 // out[m][n] = act(x[m] . W[n] + bias[n] (+ res[m][n])), x [M][K], W in MFMA fragment order

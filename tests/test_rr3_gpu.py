@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("B", [1, 3, 32])
 @pytest.mark.parametrize("relu", [True, False])
-def test_rr3_matches_torch(B, relu):
+@pytest.mark.parametrize("cfg", sorted(C.RR3_CFGS))
+def test_rr3_matches_torch(B, relu, cfg):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     g = torch.Generator().manual_seed(B)
@@ -22,9 +23,9 @@ def test_rr3_matches_torch(B, relu):
     kern = (torch.randn(3, 3, 128, 128, generator=g) / math.sqrt(9 * 128)).numpy()
     bias = (torch.randn(128, generator=g) * 0.1).numpy()
     pc = C.pack_conv(kern, bias, 1, ((1, 1), (1, 1)), "cuda")
-    assert C.cfg_supported(71, pc, False)
+    assert C.cfg_supported(cfg, pc, False)
     out = torch.empty(B, 28, 28, 128, device="cuda", dtype=torch.bfloat16)
-    C.conv_forward(x, pc, out, relu=relu, cfg=71)
+    C.conv_forward(x, pc, out, relu=relu, cfg=cfg)
     torch.cuda.synchronize()
     w = torch.from_numpy(kern).cuda().to(torch.bfloat16).float().permute(3, 2, 0, 1)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w, torch.from_numpy(bias).cuda(), padding=1).permute(0, 2, 3, 1)
