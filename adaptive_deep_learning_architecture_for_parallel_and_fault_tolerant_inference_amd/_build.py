@@ -115,8 +115,32 @@ def build_runtime(verbose: bool = False, jobs: int = 8) -> Path:
     return lib
 
 
+def comm_lib_path() -> Path:
+    return PKG_DIR / f"_comm{EXT}"
+
+
+def build_comm(verbose: bool = False) -> Path:
+    """``_comm``: native RCCL p2p layer (csrc/comm).  Host code only; the RCCL
+    entry points are resolved at run time from the librccl PyTorch mapped, so
+    nothing links against a second copy."""
+    src_dir = CSRC / "comm"
+    srcs = sorted(src_dir.glob("*.cpp"))
+    out_dir = BUILD / "comm"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    lib = comm_lib_path()
+    if not _newer(lib, srcs + list(src_dir.glob("*.h"))):
+        return lib
+    cmd = [HIPCC, "-O2", "-fPIC", "-std=c++17", "-shared", "-Wall", "-pthread", f"-I{ROCM}/include",
+           f"-I{src_dir}"] + _py_includes() + [str(s) for s in srcs] + ["-ldl", "-o", str(lib)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    return lib
+
+
 def build_all(verbose: bool = False) -> None:
     build_runtime(verbose)
+    build_comm(verbose)
     build_kernels(verbose)
 
 

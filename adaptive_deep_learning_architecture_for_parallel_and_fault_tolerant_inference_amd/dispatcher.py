@@ -28,7 +28,14 @@ references five undefined methods and five undefined attributes (SURVEY
   de-duplicates results by request id, emits them in completion order (or
   request order with ``ordered=True``) and releases credits;
 * `_task_watchdog` — a request older than `task_timeout` means its pipeline
-  is stuck: re-form that replica and replay;
+  is stuck: re-form that replica and replay (the last resort);
+* hang watch (`_hang_check`) — every heartbeat carries the worker's
+  completed-micro-batch counter; a replica that holds work while one of its
+  stages' counters has not advanced for max(`hang_factor` x the replica's
+  measured micro-batch period, `hang_min_s`) has a *wedged but alive* stage
+  (the reference keeps a per-hop `start_time` for this,
+  `src/dispatcher.py:186-194`): the earliest-stalled stage is quarantined
+  and the replica re-formed and replayed as for a kill;
 * failure detection, fastest first: the per-worker *session* connection
   (EOF the moment a worker process dies), a stage's LINK_ERROR report (broken
   hop), the result link's EOF, the membership lease (host death), the task
@@ -130,8 +137,9 @@ class DEFER:
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
                  transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
-                 quarantine_s: float = 30.0, hb_timeout: float = 0.06, precision: str = "bf16",
-                 ingest: str = "auto", preprocess: str = "none", links: str = "auto") -> None:
+                 quarantine_s: float = 30.0, hb_timeout: float = 0.25, precision: str = "bf16",
+                 ingest: str = "auto", preprocess: str = "none", links: str = "auto",
+                 hang_factor: float = 20.0, hang_min_s: float = 0.2) -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
         the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
         ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
@@ -151,7 +159,12 @@ class DEFER:
         handle when both workers are GPU workers (a device-to-device copy,
         transport/shm.py DeviceLinkPool), page-locked host slots otherwise
         (LinkPool); "dev" = the same; "shm" = host slots even between GPU workers;
-        "tcp" = always inline."""
+        "tcp" = always inline.  hb_timeout: heartbeat silence that counts as a
+        dead worker (0.06 s is the fault benchmarks' setting; the 0.25 s default
+        tolerates a heartbeat thread delayed on a loaded host).  hang_factor /
+        hang_min_s: a stage whose progress counter stands still for
+        max(hang_factor x micro-batch period, hang_min_s) while its replica
+        holds work is hung."""
         if links not in ("auto", "dev", "shm", "tcp"):
             raise ValueError(f"unknown links mode {links!r}")
         if transport not in ("tcp", "rccl", "gloo"):
@@ -232,6 +245,14 @@ class DEFER:
         self._hb = None
         self._hb_port = 0
         self._hb_suspects: set = set()
+        self.hang_factor = hang_factor
+        self.hang_min_s = hang_min_s
+        self._rep_period: Dict[int, Tuple[int, float]] = {}   # replica -> (epoch, EWMA busy completion interval)
+        self._rep_last_done: Dict[int, Tuple[int, float]] = {}
+        self.hangs: List[dict] = []
+        self._epoch_results: Dict[int, int] = {}    # epoch -> results received from its last stage
+        self._epoch_t0: Dict[int, float] = {}       # epoch -> when it was installed
+        self._hung_epochs: set = set()
         try:
             from .native import runtime
             self._hb = runtime().hb_monitor_start(0)
@@ -440,13 +461,92 @@ class DEFER:
         if p is not None:
             self._mark_dirty(p.replica, f"worker {wid} {why}", wid=wid)
 
+    def _note_done(self, replica: Optional[int], epoch: Optional[int], busy: bool) -> None:
+        """Per-replica micro-batch period: EWMA of completion intervals measured
+        while the replica still held other work (its bottleneck stage time)."""
+        if replica is None:
+            return
+        now = time.time()
+        last = self._rep_last_done.get(replica)
+        self._rep_last_done[replica] = (epoch, now)
+        if last is None or last[0] != epoch or not busy:
+            return
+        dt = now - last[1]
+        ep, old = self._rep_period.get(replica, (epoch, None))
+        self._rep_period[replica] = (epoch, dt if old is None or ep != epoch else 0.8 * old + 0.2 * dt)
+
+    def hang_threshold(self, replica: int, epoch: int, stage_s: float = 0.0) -> Optional[float]:
+        """Seconds without progress that make a stage of `replica` hung:
+        max(hang_factor x the stage's own reported time per micro-batch (else
+        the replica's measured period), hang_min_s).  None until the epoch has
+        completed work (its first micro-batches may be captures and warm-ups)."""
+        ent = self._rep_period.get(replica)
+        if ent is None or ent[0] != epoch:
+            return None
+        t = stage_s if stage_s > 0 else ent[1]
+        return max(self.hang_factor * t, self.hang_min_s)
+
+    def _hang_check(self, prog: Dict[str, Tuple[int, float, float, int]]) -> None:
+        """Find the stage the oldest request of a replica is stuck in and call it
+        hung once it has made no progress for its threshold.
+
+        Micro-batches pass the stages of a pipeline in order, so after C results
+        of epoch e came back, every stage that completed more than C micro-batches
+        of e has passed the oldest unfinished one; the first stage that completed
+        at most C holds it (or it is in transfer to it).  Starved stages further
+        down and back-pressured ones further up are never blamed."""
+        now = time.time()
+        with self._rep_lock:
+            reps = list(self.replicas.values())
+        for p in reps:
+            if p.replica in self._dirty or p.epoch in self._hung_epochs or \
+                    self.hang_threshold(p.replica, p.epoch) is None:
+                continue
+            with self.inflight_lock:
+                oldest_task = max((now - t["start_time"] for t in self.inflight_tasks.values()
+                                   if t["replica"] == p.replica and t["epoch"] == p.epoch), default=0.0)
+            if oldest_task <= self.hang_min_s:
+                continue
+            done = self._epoch_results.get(p.epoch, 0)
+            t0 = self._epoch_t0.get(p.epoch, now)
+            for idx, wid in enumerate(p.workers):
+                ent = prog.get(wid)
+                if ent is None:
+                    break                                # no heartbeat session: nothing to judge
+                n, age, stage_s, ep = ent
+                if ep != p.epoch:
+                    n, age = 0, now - t0                 # nothing completed in this epoch yet
+                age = min(age, now - t0)
+                if n > done:
+                    continue                             # passed the oldest request
+                thr = self.hang_threshold(p.replica, p.epoch, stage_s)
+                if age > thr and oldest_task > thr:
+                    self.hangs.append({"t": now, "worker": wid, "stage": idx, "replica": p.replica,
+                                       "epoch": p.epoch, "stalled_ms": round(age * 1e3, 1),
+                                       "threshold_ms": round(thr * 1e3, 1), "completed": n, "results": done})
+                    METRICS.inc("stages_hung")
+                    self._hung_epochs.add(p.epoch)
+                    self._quarantine[wid] = now + self.quarantine_s
+                    self._mark_dirty(p.replica, f"worker {wid} (stage {idx}) hung: no progress for "
+                                                f"{age * 1e3:.0f} ms (threshold {thr * 1e3:.0f} ms) holding "
+                                                f"request #{done + 1} of epoch {p.epoch}", epoch=p.epoch)
+                break
+
     def _hb_watch(self) -> None:
         """Poll the native heartbeat monitor: a member silent for `hb_timeout`
         is dead for placement purposes.  A suspect that beats again (a stall,
-        not a death) is released and offered like a joining worker."""
+        not a death) is released and offered like a joining worker.  A member
+        that beats but makes no progress while its replica holds work is hung
+        (`_hang_check`)."""
         from .native import runtime
         rt = runtime()
         while not self._shutdown_event.wait(0.005):
+            try:
+                prog = {w: (c, a, st, ep) for w, c, a, st, ep in rt.hb_monitor_progress(self._hb)}
+                if prog:
+                    self._hang_check(prog)
+            except Exception as e:  # noqa: BLE001 - the hang watch must never stop the heartbeat watch
+                self._log(f"hang check failed: {type(e).__name__}: {e}")
             ages = dict(rt.hb_monitor_ages(self._hb))
             members = self._assigned()
             for wid, age in ages.items():
@@ -463,6 +563,20 @@ class DEFER:
                     self._log(f"worker {wid} beats again: offered as a spare")
                     self._join_pending = True
                     self._reconf_needed.set()
+
+    def inject_fault(self, wid: str, fault: str = "hang") -> None:
+        """Fault injection over the control channel (tests, tools/fault_bench.py):
+        ``"hang"`` wedges worker `wid`'s compute loops (its process, sessions and
+        heartbeats keep running), ``"clear"`` releases them."""
+        with self.worker_lock:
+            rec = dict(self.workers[wid])
+        s = socket.create_connection((rec["host"], int(rec["config_port"])), timeout=5)
+        try:
+            socket_send(json.dumps({"cmd": "inject", "fault": fault}).encode(), s, CTRL_CHUNK)
+            if s.recv(1) != ACK:
+                raise RuntimeError(f"worker {wid} refused fault {fault!r}")
+        finally:
+            s.close()
 
     # ---------------------------------------------------------- configure
     def _send_full_configuration(self, rec: dict, manifest: Optional[SliceManifest], arrays: Optional[list],
@@ -594,6 +708,7 @@ class DEFER:
         return p
 
     def _install(self, p: Pipeline) -> None:
+        self._epoch_t0[p.epoch] = time.time()
         with self._rep_lock:
             old = self.replicas.get(p.replica)
             self.replicas[p.replica] = p
@@ -1002,12 +1117,16 @@ class DEFER:
         self.concurrency_sem.release()
 
     def _complete(self, m: Message, output_stream: "queue.Queue") -> None:
+        self._epoch_results[m.epoch] = self._epoch_results.get(m.epoch, 0) + 1
         with self.inflight_lock:
             task = self.inflight_tasks.pop(m.req_id, None)
         if task is None:
             METRICS.inc("results_duplicate_dropped")
             return                                   # duplicate from a replay: drop
         self._release_input(task)
+        with self.inflight_lock:
+            busy = any(t["replica"] == task.get("replica") for t in self.inflight_tasks.values())
+        self._note_done(task.get("replica"), task.get("epoch"), busy)
         METRICS.observe("request_latency_ms", (time.time() - task["start_time"]) * 1e3)
         METRICS.inc("results")
         TRACER.event("complete", req=m.req_id, epoch=m.epoch, count=m.count)

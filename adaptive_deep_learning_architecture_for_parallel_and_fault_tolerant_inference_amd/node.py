@@ -68,10 +68,11 @@ def get_local_ip() -> str:
 class _Pending:
     """A pipelined GPU micro-batch in the send queue: `msg`'s host tensors are
     ready once `ev` has completed; `links` are its input's link slots."""
-    __slots__ = ("ev", "msg", "links")
+    __slots__ = ("ev", "msg", "links", "t_submit")
 
     def __init__(self, ev, msg, links):
         self.ev, self.msg, self.links = ev, msg, links
+        self.t_submit = time.perf_counter()
 
 
 class StageRuntime:
@@ -122,6 +123,8 @@ class StageRuntime:
         self.upstream: Optional[socket.socket] = None
         self.downstream: Optional[socket.socket] = None
         self.processed = 0
+        self._busy_s = 0.0                       # host compute time of the last synchronous micro-batch
+        self._last_done = 0.0
         self.threads = []
         self.error: Optional[str] = None
         # held while a micro-batch runs on `compute`: abort() waits on it, so a
@@ -338,6 +341,8 @@ class StageRuntime:
                 except queue.Empty:
                     continue
                 self.node.state.state = StateEnum.BUSY
+                self.node.fault_point(self.stop)
+                t_c = time.perf_counter()
                 with self._busy:
                     if self.stop.is_set():
                         break
@@ -358,6 +363,7 @@ class StageRuntime:
                         if self._linkpool is not None and self.link == "shm":
                             outs = [self._linkpool.put(o, self.stop, bf16=f) for o, f in zip(outs, flags)]
                         out = Message(self.stage + 2, m.req_id, m.epoch, m.count, outs, flags)
+                        self._busy_s = time.perf_counter() - t_c
                 self.processed += 1
                 while not self.stop.is_set():
                     try:
@@ -377,10 +383,16 @@ class StageRuntime:
                     m = self.outq.get(timeout=0.1)
                 except queue.Empty:
                     continue
+                busy = None
                 if isinstance(m, _Pending):                # pipelined GPU micro-batch: outputs on the host at `ev`
                     # a blocking wait with the GIL released: a 10 kHz query/sleep loop here took
                     # GIL time from the compute and receive threads of this stage
                     m.ev.synchronize()
+                    t_done = time.perf_counter()
+                    # device busy time of this micro-batch: from its submission (or the previous
+                    # completion, if it queued behind that one) to its completion
+                    busy = t_done - max(m.t_submit, self._last_done)
+                    self._last_done = t_done
                     if self.stop.is_set():
                         return
                     self._release_links(m.links)           # the input copies out of them are done too
@@ -388,6 +400,7 @@ class StageRuntime:
                 elif isinstance(m, tuple):                 # GPU-encoded frontier (side stream)
                     m = self._finish_gpu_message(m)
                 send_message(self.downstream, m, self.codec, self.node.state.chunk_size)
+                self.node.note_progress(self.epoch, busy_s=busy if busy is not None else self._busy_s)
         except Exception as e:  # noqa: BLE001
             self._fail("send", e)
 
@@ -462,6 +475,14 @@ class Node:
         self._sessions = 0
         self._stop = threading.Event()
         self.threads = []
+        # completed micro-batches (all epochs), carried by every heartbeat so the
+        # dispatcher can tell a wedged-but-alive stage from a slow one
+        self._progress = 0                               # micro-batches completed in `_prog_epoch`
+        self._prog_epoch = 0
+        self._stage_s = 0.0                              # EWMA of this worker's busy time per micro-batch
+        self._hb_handles: set = set()
+        self._hb_lock = threading.Lock()
+        self._hang = threading.Event()                   # fault injection: "hang"
 
     # ---------------------------------------------------------- lifecycle
     def record(self) -> Dict:
@@ -523,6 +544,42 @@ class Node:
             except Exception:  # noqa: BLE001
                 pass
             self._publish(**rec)
+
+    # ------------------------------------------------- progress / faults
+    def note_progress(self, epoch: int, n: int = 1, busy_s: Optional[float] = None) -> None:
+        """A micro-batch of `epoch` finished (`busy_s`: the time this stage spent
+        on it): publish the epoch's counter and the per-micro-batch time on the
+        heartbeats.  The dispatcher compares the counters of a replica's stages
+        with the results it received to find the stage a request is stuck in."""
+        with self._hb_lock:
+            if epoch != self._prog_epoch:
+                if epoch < self._prog_epoch:
+                    return                                # a straggler of a retired epoch
+                self._prog_epoch, self._progress = epoch, 0
+            self._progress += n
+            if busy_s is not None and busy_s > 0:
+                self._stage_s = busy_s if self._stage_s == 0 else 0.8 * self._stage_s + 0.2 * busy_s
+            if self._hb_handles:
+                from .native import runtime
+                rt = runtime()
+                for h in self._hb_handles:
+                    rt.hb_sender_progress(h, self._progress, int(self._stage_s * 1e9), self._prog_epoch)
+
+    def inject_fault(self, kind: str) -> None:
+        """Fault injection (tests, tools/fault_bench.py): ``"hang"`` wedges this
+        worker's compute loops at their next micro-batch while every other
+        thread (heartbeat, sessions, config server) keeps running - the
+        failure a heartbeat alone cannot see; ``"clear"`` releases them."""
+        if kind == "hang":
+            self._hang.set()
+        elif kind == "clear":
+            self._hang.clear()
+        else:
+            raise ValueError(f"unknown fault {kind!r}")
+
+    def fault_point(self, stop: threading.Event) -> None:
+        while self._hang.is_set() and not stop.is_set() and not self._stop.is_set():
+            time.sleep(0.005)
 
     def stop(self) -> None:
         self._stop.set()
@@ -723,6 +780,13 @@ class Node:
                                      name="node-prepare")
                 t.start()
                 self.threads.append(t)
+            elif op == "inject":
+                try:
+                    self.inject_fault(str(cmd.get("fault")))
+                    conn.sendall(ACK)
+                except ValueError as e:
+                    conn.sendall(NAK)
+                    socket_send(str(e).encode(), conn, CTRL_CHUNK)
             elif op == "session":
                 # liveness channel: the dispatcher holds this connection open and
                 # sees EOF the moment this process dies (no lease TTL to wait for)
@@ -736,6 +800,10 @@ class Node:
                     try:
                         hb = runtime().hb_sender_start(conn.getpeername()[0], int(cmd["hb_port"]), self.node_id,
                                                        int(cmd.get("hb_period_us", 5000)))
+                        with self._hb_lock:
+                            runtime().hb_sender_progress(hb, self._progress, int(self._stage_s * 1e9),
+                                                         self._prog_epoch)
+                            self._hb_handles.add(hb)
                     except RuntimeError:
                         hb = None
                 conn.settimeout(0.5)
@@ -751,6 +819,8 @@ class Node:
                 finally:
                     if hb is not None:
                         from .native import runtime
+                        with self._hb_lock:
+                            self._hb_handles.discard(hb)
                         runtime().hb_sender_stop(hb)
             elif op == "configure":
                 if cmd.get("cached"):

@@ -9,17 +9,20 @@ its resident weights, HIP context and captured graphs:
 
 * the dispatcher hosts the rendezvous `TCPStore`; the prefix
   ``adapt/epoch{e}/`` isolates epochs,
-* ``nccl`` (= RCCL over xGMI) for GPU stages, ``gloo`` for CPU stages / tests,
-* every wait is *abortable*: NCCL work is waited on with stream
-  dependencies plus host polling of CUDA events, gloo work with
-  `is_completed()` polling, both checking an abort flag;
-* a *stall watch* stands in for ``ncclCommGetAsyncError``: a send the peer
-  has not taken within ``stall_s`` (receivers post their receives a buffer set
-  ahead, so a healthy send completes within a few stage times) raises
-  `LinkStalled` from the next wait, which fails the epoch -> LINK_ERROR ->
-  re-plan.  The backend's own op timeout is set far out (``op_timeout_s``): an
-  idle pipeline legitimately keeps receives posted for as long as no request
-  comes, and the NCCL watchdog must not tear the worker down for that.
+* ``nccl`` (= RCCL over xGMI) for GPU stages goes through the *native* comm
+  layer (`parallel/rccl.py` over `csrc/comm/rccl_p2p.cpp`): one non-blocking
+  2-rank communicator per adjacent stage pair, each on its own HIP stream, an
+  ``ncclCommGetAsyncError`` watch thread per communicator, and
+  ``ncclCommAbort`` on abort.  ``gloo`` serves CPU stages and the host-staged
+  rehearsal of GPU stages;
+* every wait is *abortable*: RCCL work is waited on with stream dependencies
+  plus host polling of HIP events (which also checks the async-error state),
+  gloo work with `is_completed()` polling, both checking an abort flag;
+* a wedged but *alive* peer is found by the dispatcher's progress watch (each
+  worker's heartbeat carries its completed-micro-batch counter), not here; the
+  send-age *stall watch* below is only a last-resort bound (``stall_s``).  The
+  backend op timeout is set far out (``op_timeout_s``): an idle pipeline
+  legitimately keeps receives posted for as long as no request comes.
 """
 from __future__ import annotations
 
@@ -37,7 +40,8 @@ class Aborted(RuntimeError):
 
 
 class LinkStalled(RuntimeError):
-    """A send was not taken by its peer within the stall bound."""
+    """A send was not taken by its peer within the stall bound, or the link's
+    communicator reported an asynchronous error."""
 
 
 def make_store_server(host: str = "0.0.0.0", port: int = 0) -> dist.TCPStore:
@@ -54,15 +58,17 @@ class EpochGroup:
         self.abort_flag = threading.Event()
         self.stall_s = stall_s
         self._sends: list = []                   # (work, posted_at) not yet seen complete
+        self.links = None
+        self.pg = None
         store = dist.TCPStore(store_host, store_port, None, False, timeout=datetime.timedelta(seconds=timeout_s))
         self.store = dist.PrefixStore(f"adapt/epoch{epoch}/", store)
         to = datetime.timedelta(seconds=op_timeout_s)
         if backend == "nccl":
+            from .rccl import PairLinks
             if device is not None:
                 torch.cuda.set_device(device)
-            opts = dist.ProcessGroupNCCL.Options()
-            opts._timeout = to
-            self.pg = dist.ProcessGroupNCCL(self.store, rank, world, opts)
+            self.links = PairLinks(self.store, "rccl", rank, rank - 1 if rank > 0 else None,
+                                   rank + 1 if rank < world - 1 else None, device, timeout_s=timeout_s)
         elif backend == "gloo":
             self.pg = dist.ProcessGroupGloo(self.store, rank, world, to)
         else:
@@ -74,14 +80,44 @@ class EpochGroup:
             self.ctl = dist.ProcessGroupGloo(dist.PrefixStore("ctl/", self.store), rank, world, to)
 
     # ------------------------------------------------------------- p2p
+    def _after(self):
+        """Event on the caller's stream: the link stream starts behind it (the
+        compute that filled a send buffer / last read a receive buffer)."""
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
     def isend(self, t: torch.Tensor, dst: int, tag: int = 0):
-        w = self.pg.send([t], dst, tag)
-        if self.backend == "nccl":               # gloo send work only completes inside wait()
+        return self.isend_many([t], dst, tag)[0]
+
+    def isend_many(self, ts, dst: int, tag: int = 0) -> list:
+        """Send several tensors to `dst`.  RCCL: one grouped enqueue (order-matched
+        with the peer's `irecv_many`; tags are not used).  gloo: one send each."""
+        if self.links is not None:
+            if dst != self.links.next:
+                raise ValueError(f"rank {self.rank} has no link to {dst}")
+            w = self.links.isend(list(ts), after=self._after())
             self._sends.append((w, time.monotonic()))
-        return w
+            return [w]
+        return [self.pg.send([t], dst, tag + k) for k, t in enumerate(ts)]
+
+    def irecv(self, t: torch.Tensor, src: int, tag: int = 0):
+        return self.irecv_many([t], src, tag)[0]
+
+    def irecv_many(self, ts, src: int, tag: int = 0) -> list:
+        if self.links is not None:
+            if src != self.links.prev:
+                raise ValueError(f"rank {self.rank} has no link from {src}")
+            return [self.links.irecv(list(ts), after=self._after())]
+        return [self.pg.recv([t], src, tag + k) for k, t in enumerate(ts)]
 
     def check_stall(self) -> None:
-        """Raise `LinkStalled` if a posted send has waited longer than `stall_s`."""
+        """Raise `LinkStalled` if a link's communicator reported an async error,
+        or a posted send has waited longer than `stall_s`."""
+        if self.links is not None:
+            bad = self.links.failed()
+            if bad and not self.abort_flag.is_set():
+                raise LinkStalled(f"epoch {self.epoch}: {bad}")
         if not self._sends:
             return
         now = time.monotonic()
@@ -98,9 +134,6 @@ class EpochGroup:
             keep.append((w, t0))
         self._sends = keep
 
-    def irecv(self, t: torch.Tensor, src: int, tag: int = 0):
-        return self.pg.recv([t], src, tag)
-
     def wait(self, work, poll_s: float = 0.0002) -> None:
         """Abortable wait.  NCCL: make the current stream depend on the work
         (host returns immediately; host-side progress is bounded elsewhere by
@@ -112,10 +145,22 @@ class EpochGroup:
             return
         self.wait_host(work, poll_s)
 
+    def wait_all(self, works) -> None:
+        for w in works or []:
+            self.wait(w)
+
     def wait_host(self, work, poll_s: float = 0.0002) -> None:
         """Abortable wait on a host (gloo) work item: gloo p2p work only progresses
         inside wait(), so it runs on a helper thread that an abort can abandon."""
         if work is None:
+            return
+        if self.links is not None and hasattr(work, "wait_host"):
+            try:
+                work.wait_host(self.abort_flag)
+            except Exception as e:  # noqa: BLE001
+                if self.abort_flag.is_set():
+                    raise Aborted(f"epoch {self.epoch} aborted") from e
+                raise LinkStalled(f"epoch {self.epoch}: {e}") from e
             return
         done = threading.Event()
         err: list = []
@@ -145,6 +190,8 @@ class EpochGroup:
             if self.abort_flag.is_set():
                 raise Aborted(f"epoch {self.epoch} aborted")
             n += 1
+            if self.links is not None and n % 20 == 0:     # native async-error state: two atomic loads
+                self.check_stall()
             if n % 1000 == 0:                    # ~0.1 s
                 self.check_stall()
                 if timeout_s is not None and time.monotonic() - t0 > timeout_s:
@@ -159,6 +206,11 @@ class EpochGroup:
 
     def abort(self) -> None:
         self.abort_flag.set()
+        if self.links is not None:
+            try:
+                self.links.abort()
+            except Exception:  # noqa: BLE001
+                pass
         for pg in (self.pg, self.ctl):
             if pg is None:
                 continue

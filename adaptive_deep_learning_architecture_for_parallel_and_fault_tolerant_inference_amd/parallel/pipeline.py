@@ -14,10 +14,12 @@ One process per MI355X holds one slice.  Per micro-batch tick a stage:
 4. posts `isend` of its outputs to the next stage and `irecv` of the
    micro-batch after next into this set's input buffers.
 
-With the ``nccl`` backend (= RCCL on ROCm) device tensors go straight onto
-the wire: each stage pair gets its own communicator and HIP stream, and
-torch orders the RCCL stream after the compute stream, so send(t-1),
-recv(t+1) and compute(t) overlap on different hardware queues.
+With RCCL (``links``: a `parallel.rccl.PairLinks` over the native comm layer)
+device tensors go straight onto the wire: each stage pair gets its own
+non-blocking communicator and HIP stream, every grouped send/recv starts
+behind an event of the compute stream, and the compute stream waits on the
+transfer's event, so send(t-1), recv(t+1) and compute(t) overlap on different
+hardware queues without the host ever blocking.
 
 ``host_staged=True`` stages device tensors through host memory and uses a
 CPU backend (gloo).  It exists for CPU-only tests and for rehearsing the
@@ -57,8 +59,9 @@ class StageLink:
 
     def __init__(self, compute: Callable[[int], None], in_bufs: List[List[torch.Tensor]],
                  out_bufs: List[List[torch.Tensor]], prev_rank: Optional[int], next_rank: Optional[int],
-                 group=None, host_staged: bool = False):
+                 group=None, host_staged: bool = False, links=None):
         self.compute = compute
+        self.links = links
         self.in_bufs = in_bufs
         self.out_bufs = out_bufs
         self.prev = prev_rank
@@ -75,13 +78,23 @@ class StageLink:
             self.in_host = [[mirror(t) for t in s] for s in in_bufs]
             self.out_host = [[mirror(t) for t in s] for s in out_bufs]
 
+    @staticmethod
+    def _now():
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
     def _irecv(self, j: int):
+        if self.links is not None:       # one grouped receive of the whole frontier
+            return [self.links.irecv(self.in_bufs[j], after=self._now())]
         if not self.host_staged:
             return [dist.irecv(t, src=self.prev, group=self.group) for t in self.in_bufs[j]]
         return [_HostRecv(dist.irecv(h, src=self.prev, group=self.group), h, d)
                 for h, d in zip(self.in_host[j], self.in_bufs[j])]
 
     def _isend(self, j: int):
+        if self.links is not None:
+            return [self.links.isend(self.out_bufs[j], after=self._now())]
         if not self.host_staged:
             return [dist.isend(t, dst=self.next, group=self.group) for t in self.out_bufs[j]]
         works = []
@@ -160,8 +173,9 @@ class CompressedStageLink(StageLink):
 
     def __init__(self, compute: Callable[[int], None], in_bufs: List[List[torch.Tensor]],
                  out_bufs: List[List[torch.Tensor]], prev_rank: Optional[int], next_rank: Optional[int],
-                 codec: str = "lz4", group=None, ctl_group=None, host_staged: bool = False):
-        StageLink.__init__(self, compute, in_bufs, out_bufs, prev_rank, next_rank, group=group, host_staged=False)
+                 codec: str = "lz4", group=None, ctl_group=None, host_staged: bool = False, links=None):
+        StageLink.__init__(self, compute, in_bufs, out_bufs, prev_rank, next_rank, group=group, host_staged=False,
+                           links=links)
         from ..codec.wire import WireCodec
         self.host_staged = host_staged
         self.ctl = ctl_group
@@ -207,7 +221,9 @@ class CompressedStageLink(StageLink):
         self.size_recv[j] = None
         sizes = [int(v) for v in self.size_in[j].tolist()]
         works = []
-        for k, (d, nb) in enumerate(zip(self.dec[j], sizes)):
+        if self.links is not None:
+            works.append(self.links.irecv([d.wire[:nb] for d, nb in zip(self.dec[j], sizes)], after=self._now()))
+        for k, (d, nb) in enumerate(zip(self.dec[j], sizes) if self.links is None else []):
             if self.staged:
                 h = self.host_in[j][k]
                 dist.recv(h[:nb], src=self.prev, group=self.group)
@@ -229,7 +245,14 @@ class CompressedStageLink(StageLink):
         self.size_out[j].copy_(torch.tensor(sizes, dtype=torch.int64))
         self.size_send[j] = dist.isend(self.size_out[j], dst=self.next, group=self.ctl, tag=self.SIZE_TAG)
         works = []
-        for k, (e, nb) in enumerate(zip(self.enc[j], sizes)):
+        if self.links is not None:
+            for e, nb in zip(self.enc[j], sizes):
+                self.raw_bytes += e.n
+                self.wire_bytes += nb
+            ev = torch.cuda.Event()
+            ev.record(self.side)                            # behind set j's encode
+            works.append(self.links.isend([e.wire[:nb] for e, nb in zip(self.enc[j], sizes)], after=ev))
+        for k, (e, nb) in enumerate(zip(self.enc[j], sizes) if self.links is None else []):
             self.raw_bytes += e.n
             self.wire_bytes += nb
             if self.staged:

@@ -76,6 +76,9 @@ class DPJob:
         return {o: self.ex.output_buf(o) for o in self.ex.outputs}
 
 
+_JOB_SEQ = [0]      # every rank builds its jobs in the same order: a fresh store prefix per job
+
+
 class PipelineJob:
     """One stage of a (replicated) pipeline; step() = `stages` micro-batch ticks."""
 
@@ -103,18 +106,27 @@ class PipelineJob:
             self.ex.capture()
         rk = stage_ranks(self.stage, stages, self.replica)
         self.prev, self.next = rk["prev"], rk["next"]
+        self.links = None
+        if not host_staged and torch.device(device).type == "cuda":
+            # RCCL over xGMI through the native comm layer: one non-blocking 2-rank
+            # communicator per adjacent stage pair (unique ids over the job's store)
+            from .rccl import PairLinks
+            from torch.distributed import distributed_c10d as c10d
+            _JOB_SEQ[0] += 1
+            self.links = PairLinks(c10d._get_default_store(), f"pp{stages}/job{_JOB_SEQ[0]}", rank, self.prev,
+                                   self.next, device)
         in_bufs = [[self.ex.input_buf(n, j) for n in sl.inputs] for j in range(nsets)]
         out_bufs = [[self.ex.output_buf(n, j) for n in sl.outputs] for j in range(nsets)]
         self.codec = codec
         if codec == "none":
             self.link = StageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next,
-                                  host_staged=host_staged)
+                                  host_staged=host_staged, links=self.links)
         else:
             # byte counts ride a host (gloo) control group; with host staging the
             # default group already is gloo
             ctl = None if host_staged else dist.new_group(backend="gloo")
             self.link = CompressedStageLink(lambda j: self.ex.forward(j), in_bufs, out_bufs, self.prev, self.next,
-                                            codec=codec, ctl_group=ctl, host_staged=host_staged)
+                                            codec=codec, ctl_group=ctl, host_staged=host_staged, links=self.links)
         self.images_per_step = batch * world          # stages ticks x replicas x batch / stages-per-image
         self.global_batch = batch * world
         self.parallelism = f"pp{stages}" if self.replicas == 1 else f"pp{stages}xdp{self.replicas}"
@@ -141,6 +153,13 @@ class PipelineJob:
 
     def finish(self) -> None:
         self.link.drain()
+
+    def close(self) -> None:
+        """Orderly teardown of the RCCL links (every rank of the pipeline calls it)."""
+        if self.links is not None:
+            torch.cuda.synchronize(self.ex.device)
+            self.links.destroy()
+            self.links = None
 
 
 def build_job(g, weights, mode: str, world: int, rank: int, device, batch: int = 32, stages: int = 0,

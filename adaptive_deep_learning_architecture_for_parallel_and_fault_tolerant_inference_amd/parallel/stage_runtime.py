@@ -286,8 +286,10 @@ class CollectiveStageRuntime:
             h_out = [[pinned(t) for t in [self.meta_out[j]] + self.out_bufs[j]] for j in range(self.nsets)]
 
         def post_recv(j):
+            # one grouped RCCL receive (meta + frontier) per tick; gloo: one recv per tensor,
+            # tags 16*j + k (a set's tags never collide with the next set's)
             dst = h_in[j] if staged else [self.meta_in[j]] + self.in_bufs[j]
-            return [G.irecv(t, self.prev, 2 * j + (1 if k else 0)) for k, t in enumerate(dst)]
+            return G.irecv_many(dst, self.prev, 16 * j)
 
         def land(j):
             if staged:                                   # pinned -> device (the next irecv reuses the mirror)
@@ -301,9 +303,10 @@ class CollectiveStageRuntime:
                 for h, d in zip(h_out[j], src):
                     h.copy_(d)
                 src = h_out[j]
-            return [G.isend(t, self.next, 2 * j + (1 if k else 0)) for k, t in enumerate(src)]
+            return G.isend_many(src, self.next, 16 * j)
 
         tick = 0
+        t_tick = time.perf_counter()
         try:
             if self.prev is not None:
                 for j in range(self.nsets):
@@ -322,6 +325,8 @@ class CollectiveStageRuntime:
                 for w in send_w[j] or []:
                     G.wait(w)
                 send_w[j] = None
+                self.node.fault_point(self.stop)
+                t_c = time.perf_counter()
                 self._compute(j)
                 if self.gpu:
                     ev = torch.cuda.Event()
@@ -336,6 +341,10 @@ class CollectiveStageRuntime:
                 if self.prev is not None:
                     recv_w[j] = post_recv(j)
                 self.processed += 1
+                # CPU: the compute itself; GPU: one loop period (host run-ahead is bounded by the events)
+                now = time.perf_counter()
+                self.node.note_progress(self.epoch, busy_s=(now - t_c) if not self.gpu else now - t_tick)
+                t_tick = now
                 tick += 1
         except Exception as e:  # noqa: BLE001
             if not isinstance(e, Aborted):
@@ -434,6 +443,8 @@ class CollectiveStageRuntime:
                     raise Aborted("stopped")
             if self.gpu and self.enc is not None and self.enc[j]:
                 torch.cuda.current_stream(self.dev).wait_event(self.enc[j][-1].done)
+            self.node.fault_point(self.stop)
+            t_c = time.perf_counter()
             self._compute(j)
             if self.gpu:
                 ev = torch.cuda.Event()
@@ -450,4 +461,5 @@ class CollectiveStageRuntime:
                     G.wait_event(self.events[j])
                 self._emit_result(j)
             self.processed += 1
+            self.node.note_progress(self.epoch, busy_s=time.perf_counter() - t_c if not self.gpu else None)
             tick += 1

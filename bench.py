@@ -9,7 +9,12 @@ N GPUs:        python bench.py --gpus N           (starts N rank processes itsel
                python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
                    --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
-Parallelism (``--mode``):
+Precision: the reference computes in Keras float32 (`src/node.py:177`,
+`test/local_infer.py:22`), so the primary ``value`` is fp32 end to end
+(fp32 activations and weights on the fp32 matrix cores).  The same run also
+times the bf16 build (fp32 accumulation) and reports it as ``value_bf16``.
+
+Parallelism (``--mode``) of the headline:
   dp    every GPU runs the whole model on its own bs=32 batch (replicas)
   pp    the model is cut into N stages (balanced planner or --part-at), one per
         GPU; bs=32 micro-batches stream through RCCL send/recv over xGMI
@@ -17,6 +22,12 @@ Parallelism (``--mode``):
 A step = one bs=32 batch per pipeline replica slot: dp processes 32*N images
 per step, pp keeps N micro-batches in flight and completes N per step, so
 per-GPU work is fixed as N grows (weak scaling) in every mode.
+
+With N > 1 the same invocation then times the reference's own topology, an
+N-stage pipeline over the native RCCL p2p layer (`parallel/rccl.py`), checks
+the last stage's logits against an unsliced forward of the same input, and
+measures the stage-0 -> stage-1 p2p rate; that lands in the ``pp`` sub-object
+(and the rate in `tuning/gfx950_links.json` for the planner).
 """
 from __future__ import annotations
 
@@ -33,7 +44,7 @@ import torch.distributed as dist
 PKG = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
                     help="ranks (one per GPU); without torchrun the script launches them itself")
@@ -51,22 +62,181 @@ def parse():
                     help="independent bs=--batch micro-batches in flight per GPU (dp mode)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = host-staged rehearsal (several ranks per GPU)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                    help="compute precision: bf16 (fp32 accumulation) or fp32 end to end (the reference's "
-                         "Keras float32, on the fp32 matrix cores)")
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="headline precision: fp32 end to end (the reference's Keras float32, default) or bf16 "
+                         "(fp32 accumulation)")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 companion timing (value_bf16)")
+    ap.add_argument("--no-pp", action="store_true", help="N > 1: skip the pipeline sub-benchmark")
+    ap.add_argument("--pp-dtype", default="", choices=["", "bf16", "fp32"],
+                    help="precision of the pipeline sub-benchmark (default: --dtype)")
     ap.add_argument("--codec", default="none", choices=["none", "lz4", "zvc"],
                     help="pp/ppdp: compress stage-boundary activations on a side stream (BASELINE config 3)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 BASELINE_IMG_S = None   # the reference publishes no absolute number
 MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152", "vgg16": "VGG16",
                "vgg19": "VGG19", "mobilenet_v2": "MobileNetV2", "densenet121": "DenseNet121",
                "efficientnetb0": "EfficientNetB0", "inception_v3": "InceptionV3"}
+# logits tolerance of a pipelined forward against the unsliced one: a cut changes
+# where bf16 rounding happens (a fused epilogue becomes a stored bf16 frontier)
+PP_LOGIT_RTOL = {"bf16": 5e-2, "fp32": 1e-3}
 
 
-def main():
-    args = parse()
+def make_record(args, world: int, n_gpus: int, backend: str, value: float, elapsed: float, image, job,
+                bf16: dict = None, pp: dict = None) -> dict:
+    """The one JSON line rank 0 prints (the driver's contract)."""
+    rec = {
+        "metric": f"images/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} bs={args.batch}",
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / BASELINE_IMG_S, 4) if BASELINE_IMG_S else None),
+        "dtype": args.dtype,
+        "data": f"synthetic {'x'.join(map(str, image))} NHWC fp32 input, random-init weights (seeded)",
+        "config": {"model": args.model, "global_batch": job["global_batch"], "seq_len": None,
+                   "image": list(image), "parallelism": job["parallelism"], "part_at": job["part_at"],
+                   "micro_batch": args.batch, "hipgraph": not args.no_graph,
+                   "ranks": world, "backend": backend if world > 1 else None},
+    }
+    if job.get("codec"):
+        rec["config"]["codec"] = job["codec"]
+        rec["config"]["wire_ratio"] = job.get("wire_ratio")
+    if bf16:
+        rec["value_bf16"] = round(bf16["value"], 2)
+        rec["ms_per_step_bf16"] = round(bf16["elapsed"] / args.steps * 1e3, 4)
+    if pp is not None:
+        rec["pp"] = pp
+    return rec
+
+
+def make_pp_record(value: float, elapsed: float, steps: int, stages: int, part_at, dtype: str, ok: bool,
+                   max_logit_rel: float, top1_agree: float, p2p_gbps, rccl_ranks: int, backend: str) -> dict:
+    return {"value": round(value, 2), "unit": "images/s", "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "stages": stages, "part_at": list(part_at), "dtype": dtype, "ok": bool(ok),
+            "max_logit_rel": (round(max_logit_rel, 6) if max_logit_rel is not None else None),
+            "top1_agree": top1_agree,
+            "p2p_GBps": (round(p2p_gbps, 2) if p2p_gbps else None), "rccl_ranks": rccl_ranks,
+            "backend": backend}
+
+
+def _max_over_ranks(x: float, world: int, dev, backend: str) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    t = t.to(dev) if backend == "nccl" else t
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def timed(job, steps: int, warmup: int, dev, world: int, backend: str) -> float:
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize;
+    returns the slowest rank's seconds."""
+    if hasattr(job, "set_total_steps"):
+        job.set_total_steps(warmup + steps)
+    for _ in range(warmup):
+        job.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        job.step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if hasattr(job, "finish"):
+        job.finish()
+    return _max_over_ranks(elapsed, world, dev, backend)
+
+
+def _p2p_rate(job, dev, world: int, backend: str, mib: int = 64, reps: int = 10):
+    """Stage 0 -> stage 1 rate on the pipeline's own link (bytes/s), or None."""
+    n = mib << 20
+    buf = torch.empty(n, dtype=torch.uint8, device=dev)
+    links = getattr(job, "links", None)
+    role = job.stage if job.replica == 0 and job.stage < 2 else None
+    for it in range(2):                                 # warm-up round, then the timed round
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        if role is not None:
+            for _ in range(reps):
+                if links is not None:
+                    w = links.isend([buf]) if role == 0 else links.irecv([buf])
+                elif role == 0:
+                    dist.send(buf.cpu() if backend != "nccl" else buf, job.next)
+                else:
+                    tmp = buf.cpu() if backend != "nccl" else buf
+                    dist.recv(tmp, job.prev)
+                    if tmp is not buf:
+                        buf.copy_(tmp)
+            if links is not None:
+                w.wait_host(timeout_s=60)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0 if role is not None else 0.0
+    dt = _max_over_ranks(dt, world, dev, backend)
+    return n * reps / dt if dt > 0 else None
+
+
+def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, resnet, runner, executor):
+    """The reference's layer-partitioned chain over RCCL, verified against an unsliced forward."""
+    dtype = args.pp_dtype or args.dtype
+    part_at = [s for s in args.part_at.split(",") if s] if args.mode == "pp" else []
+    job = runner.build_job(g, weights, mode="pp", world=world, rank=rank, device=dev, batch=args.batch,
+                           part_at=part_at, graph=not args.no_graph, host_staged=(backend != "nccl"),
+                           codec=args.codec, precision=dtype)
+    image = tuple(g.layers[g.input].out_shape)
+    x = torch.randn((args.batch,) + image, generator=torch.Generator().manual_seed(4321)).to(dev)
+    job.set_synthetic_input(x)
+    elapsed = timed(job, args.steps, args.warmup, dev, world, backend)
+    value = job.images_per_step * args.steps / elapsed
+    rate = _p2p_rate(job, dev, world, backend)
+    ok, rel, top1 = 1, None, None
+    if job.next is None:                       # last stage: logits vs the unsliced model on its own GPU
+        full = executor.SliceExecutor(g, weights, args.batch, device=dev, precision=dtype)
+        full(x)
+        want = full.logits().double()
+        got = job.ex.logits().double()
+        rel = ((got - want).abs().max() / want.abs().max()).item()
+        top1 = (got.argmax(-1) == want.argmax(-1)).float().mean().item()
+        ok = int(rel <= PP_LOGIT_RTOL[dtype] and top1 == 1.0)
+        del full
+    flag = torch.tensor([ok, rel if rel is not None else 0.0, top1 if top1 is not None else 1.0],
+                        dtype=torch.float64)
+    flag = flag.to(dev) if backend == "nccl" else flag
+    # MIN over ok/top1 and MAX over rel: gather everything
+    flags = [torch.zeros_like(flag) for _ in range(world)]
+    dist.all_gather(flags, flag)
+    oks = [int(f[0].item()) for f in flags]
+    last = flags[world - 1] if job.replicas == 1 else max(flags, key=lambda f: f[1].item())
+    native = getattr(job, "links", None) is not None
+    if native and rank == 0 and rate:
+        from importlib import import_module
+        planner = import_module(f"{PKG}.graph.planner")
+        try:
+            planner.LINK_FILE.write_text(json.dumps({"link_bw": rate, "source": "bench.py pp stage0->1 RCCL p2p",
+                                                     "mib": 64}))
+        except OSError:
+            pass
+    rec = make_pp_record(value, elapsed, args.steps, job.stages, job.part_at, dtype, min(oks) == 1,
+                         last[1].item(), last[2].item(), rate / 1e9 if rate else None,
+                         world if native else 0, "rccl-native" if native else backend)
+    if hasattr(job, "close"):
+        job.close()
+    return rec
+
+
+def main(argv=None):
+    args = parse(argv)
     from importlib import import_module
     launch = import_module(f"{PKG}.parallel.launch")
     if args.gpus > 1 and not launch.launched_by_torchrun():
@@ -97,44 +267,43 @@ def main():
     resnet = import_module(f"{PKG}.models.resnet")
     zoo = import_module(f"{PKG}.models.zoo")
     runner = import_module(f"{PKG}.parallel.runner")
+    executor = import_module(f"{PKG}.runtime.executor")
 
     g = zoo.build_model(args.model)
     weights = resnet.init_weights(g, seed=args.seed)
     part_at = [s for s in args.part_at.split(",") if s]
-    job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
-                           stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune,
-                           host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec,
-                           precision=args.dtype)
-    # synthetic input, resident on device (data="synthetic")
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     image = tuple(g.layers[g.input].out_shape)          # 224x224x3 (ResNet-50); the model's own size otherwise
-    job.set_synthetic_input(torch.randn((args.batch,) + image, generator=gen, device=dev))
 
-    if hasattr(job, "set_total_steps"):
-        job.set_total_steps(args.warmup + args.steps)
-    for _ in range(args.warmup):
-        job.step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        job.step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if hasattr(job, "finish"):
-        job.finish()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        t = t.to(dev) if backend == "nccl" else t
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    images = job.images_per_step * args.steps
-    value = images / elapsed
+    def headline(precision: str):
+        job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
+                               stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune,
+                               host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec,
+                               precision=precision)
+        # synthetic input, resident on device (data="synthetic")
+        gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+        job.set_synthetic_input(torch.randn((args.batch,) + image, generator=gen, device=dev))
+        elapsed = timed(job, args.steps, args.warmup, dev, world, backend)
+        info = {"global_batch": job.global_batch, "parallelism": job.parallelism, "part_at": job.part_at}
+        link = getattr(job, "link", None)
+        if args.codec != "none" and link is not None:
+            info["codec"] = args.codec
+            info["wire_ratio"] = round(link.ratio, 4) if link.ratio else None
+        value = job.images_per_step * args.steps / elapsed
+        if hasattr(job, "close"):
+            job.close()
+        del job
+        torch.cuda.empty_cache()
+        return value, elapsed, info
+
+    value, elapsed, info = headline(args.dtype)
+    bf16 = None
+    if args.dtype == "fp32" and not args.no_bf16:
+        v16, e16, _ = headline("bf16")
+        bf16 = {"value": v16, "elapsed": e16}
+    pp = None
+    if world > 1 and not args.no_pp and args.mode == "dp":
+        pp = run_pp(args, g, weights, world, rank, dev, backend, resnet, runner, executor)
+
     n_gpus = 1
     if world > 1:
         # distinct physical devices: ranks rehearsing on one GPU count once
@@ -142,29 +311,8 @@ def main():
         dist.all_gather_object(devs, (socket.gethostname(), dev_idx))
         n_gpus = launch.distinct_devices(devs)
     if rank == 0:
-        rec = {
-            "metric": (f"images/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} bs={args.batch}"),
-            "value": round(value, 2),
-            "unit": "images/s",
-            "n_gpus": n_gpus,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": (round(value / BASELINE_IMG_S, 4) if BASELINE_IMG_S else None),
-            "dtype": args.dtype,
-            "data": f"synthetic {'x'.join(map(str, image))} NHWC fp32 input, random-init weights (seeded)",
-            "config": {"model": args.model, "global_batch": job.global_batch, "seq_len": None,
-                       "image": list(image), "parallelism": job.parallelism, "part_at": job.part_at,
-                       "micro_batch": args.batch, "hipgraph": not args.no_graph,
-                       "ranks": world, "backend": backend if world > 1 else None},
-        }
-        link = getattr(job, "link", None)
-        if args.codec != "none" and link is not None:
-            rec["config"]["codec"] = args.codec
-            rec["config"]["wire_ratio"] = round(link.ratio, 4) if link.ratio else None
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(make_record(args, world, n_gpus, backend, value, elapsed, image, info, bf16, pp)),
+              flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

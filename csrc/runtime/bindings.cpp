@@ -64,6 +64,10 @@ PYBIND11_MODULE(_runtime, m) {
     NoGil nogil;
     hb_sender_stop(reinterpret_cast<void*>(h));
   });
+  m.def("hb_sender_progress", [](uintptr_t h, uint64_t v, uint64_t stage_ns, uint64_t epoch) {
+    hb_sender_progress(reinterpret_cast<void*>(h), v, stage_ns, epoch);
+  }, py::arg("h"), py::arg("value"), py::arg("stage_ns") = 0, py::arg("epoch") = 0);
+  m.def("hb_monitor_progress", [](uintptr_t h) { return hb_monitor_progress(reinterpret_cast<void*>(h)); });
   m.def("hb_monitor_start", [](int port) { return reinterpret_cast<uintptr_t>(hb_monitor_start(port)); });
   m.def("hb_monitor_port", [](uintptr_t h) { return hb_monitor_port(reinterpret_cast<void*>(h)); });
   m.def("hb_monitor_ages", [](uintptr_t h) { return hb_monitor_ages(reinterpret_cast<void*>(h)); });

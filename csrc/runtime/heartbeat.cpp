@@ -8,6 +8,13 @@
 // the ages: a worker silent for a few periods has stopped executing.  Both
 // threads are plain C++ threads, so a worker busy in Python (GIL held by the
 // compute loop) keeps beating.
+//
+// Every datagram also carries the worker's completed-micro-batch counter
+// (`hb_sender_progress`).  A worker whose heartbeat thread runs but whose
+// counter stands still while its pipeline holds work is *hung* (a wedged GPU
+// queue, a deadlocked compute loop): the monitor timestamps each counter change
+// so the dispatcher can tell a stalled stage from a dead one (the reference's
+// per-hop `start_time` registry serves that purpose, `src/dispatcher.py:186-194`).
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -23,6 +30,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -36,6 +44,9 @@ using Clock = std::chrono::steady_clock;
 struct Sender {
   int fd = -1;
   std::atomic<bool> stop{false};
+  std::atomic<uint64_t> progress{0};
+  std::atomic<uint64_t> stage_ns{0};                    // the worker's measured time per micro-batch
+  std::atomic<uint64_t> epoch{0};                       // epoch the counter belongs to
   std::thread th;
 };
 
@@ -47,6 +58,10 @@ struct Monitor {
   std::mutex mu;
   std::map<std::string, Clock::time_point> last;
   std::map<std::string, uint64_t> count;
+  std::map<std::string, uint64_t> prog;                 // last reported progress counter
+  std::map<std::string, Clock::time_point> prog_t;      // when it last changed
+  std::map<std::string, uint64_t> stage_ns;             // reported time per micro-batch (0 = unknown)
+  std::map<std::string, uint64_t> epoch;                // epoch of the reported counter
 };
 }  // namespace
 
@@ -73,12 +88,26 @@ void* hb_sender_start(const std::string& host, int port, const std::string& id, 
       msg = id;
       msg.push_back('\0');
       msg.append(reinterpret_cast<const char*>(&seq), sizeof(seq));
+      const uint64_t prog = s->progress.load(std::memory_order_relaxed);
+      msg.append(reinterpret_cast<const char*>(&prog), sizeof(prog));
+      const uint64_t sns = s->stage_ns.load(std::memory_order_relaxed);
+      msg.append(reinterpret_cast<const char*>(&sns), sizeof(sns));
+      const uint64_t ep = s->epoch.load(std::memory_order_relaxed);
+      msg.append(reinterpret_cast<const char*>(&ep), sizeof(ep));
       ++seq;
       (void)send(s->fd, msg.data(), msg.size(), MSG_DONTWAIT);   // a lost datagram is just a missed beat
       std::this_thread::sleep_for(std::chrono::microseconds(period));
     }
   });
   return s;
+}
+
+void hb_sender_progress(void* h, uint64_t value, uint64_t stage_ns, uint64_t epoch) {
+  auto* s = static_cast<Sender*>(h);
+  if (s == nullptr) return;
+  s->epoch.store(epoch, std::memory_order_relaxed);
+  s->progress.store(value, std::memory_order_relaxed);
+  if (stage_ns) s->stage_ns.store(stage_ns, std::memory_order_relaxed);
 }
 
 void hb_sender_stop(void* h) {
@@ -114,10 +143,29 @@ void* hb_monitor_start(int port) {
       ssize_t n = recv(m->fd, buf, sizeof(buf) - 1, MSG_DONTWAIT);
       if (n <= 0) continue;
       buf[n] = 0;
-      std::string id(buf, strnlen(buf, static_cast<size_t>(n)));
+      const size_t idlen = strnlen(buf, static_cast<size_t>(n));
+      std::string id(buf, idlen);
+      const auto now = Clock::now();
       std::lock_guard<std::mutex> g(m->mu);
-      m->last[id] = Clock::now();
+      m->last[id] = now;
       m->count[id] += 1;
+      if (static_cast<size_t>(n) >= idlen + 1 + 2 * sizeof(uint64_t)) {
+        uint64_t prog = 0, ep = 0;
+        std::memcpy(&prog, buf + idlen + 1 + sizeof(uint64_t), sizeof(prog));
+        if (static_cast<size_t>(n) >= idlen + 1 + 4 * sizeof(uint64_t))
+          std::memcpy(&ep, buf + idlen + 1 + 3 * sizeof(uint64_t), sizeof(ep));
+        auto it = m->prog.find(id);
+        if (it == m->prog.end() || it->second != prog || m->epoch[id] != ep) {
+          m->prog[id] = prog;
+          m->prog_t[id] = now;
+          m->epoch[id] = ep;
+        }
+        if (static_cast<size_t>(n) >= idlen + 1 + 3 * sizeof(uint64_t)) {
+          uint64_t sns = 0;
+          std::memcpy(&sns, buf + idlen + 1 + 2 * sizeof(uint64_t), sizeof(sns));
+          m->stage_ns[id] = sns;
+        }
+      }
     }
   });
   return m;
@@ -135,11 +183,26 @@ std::vector<std::pair<std::string, double>> hb_monitor_ages(void* h) {
   return out;
 }
 
+std::vector<std::tuple<std::string, uint64_t, double, double, uint64_t>> hb_monitor_progress(void* h) {
+  auto* m = static_cast<Monitor*>(h);
+  std::vector<std::tuple<std::string, uint64_t, double, double, uint64_t>> out;
+  const auto now = Clock::now();
+  std::lock_guard<std::mutex> g(m->mu);
+  for (const auto& kv : m->prog)
+    out.emplace_back(kv.first, kv.second, std::chrono::duration<double>(now - m->prog_t[kv.first]).count(),
+                     static_cast<double>(m->stage_ns[kv.first]) * 1e-9, m->epoch[kv.first]);
+  return out;
+}
+
 void hb_monitor_forget(void* h, const std::string& id) {
   auto* m = static_cast<Monitor*>(h);
   std::lock_guard<std::mutex> g(m->mu);
   m->last.erase(id);
   m->count.erase(id);
+  m->prog.erase(id);
+  m->prog_t.erase(id);
+  m->stage_ns.erase(id);
+  m->epoch.erase(id);
 }
 
 void hb_monitor_stop(void* h) {

@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <string>
 #include <utility>
+#include <tuple>
 #include <vector>
 
 namespace adapt_rt {
@@ -62,6 +63,11 @@ bool recv_frame(int fd, std::vector<uint8_t>& out, size_t chunk, int timeout_ms,
 // ---- liveness heartbeats over UDP (heartbeat.cpp): GIL-free sender / monitor threads
 void* hb_sender_start(const std::string& host, int port, const std::string& id, int period_us);
 void hb_sender_stop(void* h);
+// completed-micro-batch counter of `epoch` and measured seconds-per-micro-batch (ns, 0 = keep), carried by
+// every beat
+void hb_sender_progress(void* h, uint64_t value, uint64_t stage_ns, uint64_t epoch);
+// id -> (progress counter, seconds since it last changed, reported seconds per micro-batch, epoch)
+std::vector<std::tuple<std::string, uint64_t, double, double, uint64_t>> hb_monitor_progress(void* h);
 void* hb_monitor_start(int port);
 int hb_monitor_port(void* h);
 std::vector<std::pair<std::string, double>> hb_monitor_ages(void* h);   // id -> seconds since its last beat

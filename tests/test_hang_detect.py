@@ -1,0 +1,131 @@
+"""Hang (no-progress) detection on CPU: a stage whose compute loop wedges while
+its process, sessions and heartbeat thread stay alive.
+
+The reference tracks every hop's `start_time` for a watchdog
+(`src/dispatcher.py:186-194,302-304`) but never defines the watchdog.  Here
+each worker's native heartbeat carries its completed-micro-batch counter; the
+dispatcher declares a stage hung when its replica holds work and the counter
+has not advanced for max(hang_factor x measured period, hang_min_s), then
+re-forms and replays as for a kill.
+"""
+import os
+import queue
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.dispatcher import DEFER
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.model import resnet
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.native import runtime
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
+
+
+def _spawn_worker(port, wid):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    return subprocess.Popen([sys.executable, "-m", f"{PKG}.node", "--membership-port", str(port), "--data-port", "0",
+                             "--config-port", "0", "--device", "cpu", "--id", wid, "--ttl", "1.0"],
+                            env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    return resnet("resnet_tiny", input_shape=(32, 32, 3), classes=10, seed=5)
+
+
+def test_heartbeat_carries_progress_counter():
+    rt = runtime()
+    mon = rt.hb_monitor_start(0)
+    snd = rt.hb_sender_start("127.0.0.1", rt.hb_monitor_port(mon), "w0", 1000)
+    try:
+        time.sleep(0.05)
+        rt.hb_sender_progress(snd, 7)
+        time.sleep(0.02)
+        prog = {w: (c, a, st, ep) for w, c, a, st, ep in rt.hb_monitor_progress(mon)}
+        assert prog["w0"][0] == 7 and prog["w0"][1] < 0.1 and prog["w0"][2] == 0.0
+        rt.hb_sender_progress(snd, 8, 3_000_000, 2)
+        time.sleep(0.12)
+        prog = {w: (c, a, st, ep) for w, c, a, st, ep in rt.hb_monitor_progress(mon)}
+        assert prog["w0"][0] == 8 and prog["w0"][1] >= 0.1          # beats continue, counter stands still
+        assert abs(prog["w0"][2] - 3e-3) < 1e-9 and prog["w0"][3] == 2
+        ages = dict(rt.hb_monitor_ages(mon))
+        assert ages["w0"] < 0.05
+    finally:
+        rt.hb_sender_stop(snd)
+        rt.hb_monitor_stop(mon)
+
+
+@pytest.mark.parametrize("transport", ["tcp", "gloo"])
+def test_hung_stage_detected_and_replayed_exactly_once(tiny, transport):
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=1, max_inflight=4, weight_codec="lz4",
+              min_workers=3, replicas=1, task_timeout=30, transport=transport, hang_min_s=0.2, hang_factor=20)
+    d.membership_server.start()
+    procs = [_spawn_worker(d.membership_port, f"h{i}") for i in range(3)]
+    stop = threading.Event()
+    try:
+        inq, outq = queue.Queue(8), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, ["conv3_block1_out", "conv4_block1_out"], inq, outq),
+                         daemon=True).start()
+        x = np.random.default_rng(3).standard_normal((1, 32, 32, 3)).astype(np.float32)
+        want = tiny.predict(x, device="cpu")
+        sent = [0]
+
+        def feeder():
+            while not stop.is_set():
+                try:
+                    inq.put(x, timeout=0.05)
+                    sent[0] += 1
+                except queue.Full:
+                    continue
+
+        threading.Thread(target=feeder, daemon=True).start()
+        res = [outq.get(timeout=120) for _ in range(40)]
+        assert len(d.pipeline.workers) == 3
+        victim = d.pipeline.workers[1]
+        assert d.hang_threshold(d.pipeline.replica, d.pipeline.epoch) is not None
+        t_hang = time.time()
+        d.inject_fault(victim, "hang")              # over the worker's control channel
+        t_end = time.time() + 60
+        while not d.recoveries and time.time() < t_end:
+            try:
+                res.append(outq.get(timeout=0.05))
+            except queue.Empty:
+                pass
+        assert d.hangs, d.events[-5:]
+        h = d.hangs[0]
+        detect_ms = (h["t"] - t_hang) * 1e3
+        print(f"{transport}: hung stage {h['stage']} ({h['worker']}) detected {detect_ms:.0f} ms after the hang, "
+              f"threshold {h['threshold_ms']} ms")
+        assert h["worker"] == victim and h["stage"] == 1
+        assert detect_ms < 300.0
+        for _ in range(20):
+            res.append(outq.get(timeout=120))
+        stop.set()
+        d.inject_fault(victim, "clear")      # the wedged stage wakes up: its stale outputs must not leak out
+        time.sleep(0.5)
+        total = sent[0] - inq.qsize()
+        while len(res) < total:
+            res.append(outq.get(timeout=120))
+        time.sleep(0.5)
+        assert outq.empty()                                  # exactly once
+        assert len(res) == total
+        for y in res:
+            np.testing.assert_allclose(y, want, rtol=1e-4, atol=1e-5)
+        assert victim not in d.pipeline.workers and len(d.pipeline.workers) == 2
+        assert d.duplicates_dropped >= 0
+        print(f"{transport}: {total} requests answered exactly once, duplicates dropped {d.duplicates_dropped}")
+    finally:
+        stop.set()
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait(timeout=10)

@@ -63,8 +63,8 @@ def test_rccl_two_stage_multi_tensor_cut_matches_unsliced():
 
 @needs(2)
 def test_rccl_p2p_bandwidth():
-    out = os.path.join(ROOT, "gpurun_out", "p2p_bw.json")
-    os.makedirs(os.path.dirname(out), exist_ok=True)
+    import tempfile
+    out = os.path.join(tempfile.mkdtemp(), "p2p_bw.json")
     r, recs = _check("--gpus", "2", "--p2p-bw", "--out", out)
     assert r.returncode == 0, r.stderr[-3000:]
     assert recs and recs[0]["link_bw"] > 1e9

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Fault-injection benchmark (BASELINE.json config 4: "8-stage with one worker
 killed mid-run"): start a dispatcher and N worker processes, stream requests,
-SIGKILL the worker holding the middle stage at --kill-at seconds, and report
+SIGKILL (``--fault kill``) or wedge (``--fault hang``: its compute loop stops,
+its process and heartbeats keep running) the worker holding the middle stage
+at --kill-at seconds, and report
 
 * detection latency (kill -> lease expiry seen by the dispatcher),
 * reconfiguration time (new epoch formed on the survivors),
@@ -49,6 +51,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=8)
     ap.add_argument("--links", default="auto", choices=["auto", "dev", "shm", "tcp"],
                     help="same-host stage->stage hops (DEFER links)")
+    ap.add_argument("--fault", default="kill", choices=["kill", "hang"])
+    ap.add_argument("--hb-timeout", type=float, default=0.06,
+                    help="heartbeat silence that counts as death (DEFER default 0.25)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
 
@@ -56,7 +61,7 @@ def main():
     cuts, _ = plan_cuts(m.graph, a.workers, batch=a.batch)
     d = DEFER(membership_port=0, result_port=0, worker_wait=120, batch=a.batch, codec=a.codec, weight_codec="lz4",
               max_inflight=a.inflight, task_timeout=30, min_workers=a.workers, transport=a.transport,
-              replicas=a.replicas, links=a.links)
+              replicas=a.replicas, links=a.links, hb_timeout=a.hb_timeout)
     d.membership_server.start()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     procs = {}
@@ -97,7 +102,10 @@ def main():
         while time.time() - t0 < a.duration:
             if t_kill is None and time.time() - t0 >= a.kill_at:
                 victim = d.pipeline.workers[len(d.pipeline.workers) // 2]
-                os.killpg(procs[victim].pid, signal.SIGKILL)
+                if a.fault == "kill":
+                    os.killpg(procs[victim].pid, signal.SIGKILL)
+                else:
+                    d.inject_fault(victim, "hang")
                 t_kill = time.time()
             try:
                 outq.get(timeout=0.1)
@@ -129,7 +137,8 @@ def main():
     post = ts[ts > (rec["t_ready"] + 1.0)] if rec else np.array([])
     rate_post = (len(post) - 1) / (post[-1] - post[0]) * a.batch if len(post) > 2 else None
     out = {
-        "metric": "recovery-to-steady ms after a worker kill",
+        "metric": f"recovery-to-steady ms after a worker {'kill' if a.fault == 'kill' else 'hang'}",
+        "fault": a.fault, "hangs": d.hangs,
         "value": round(rts[0], 1) if rts else None,
         "unit": "ms",
         "workers": a.workers, "device": a.device, "transport": a.transport, "model": a.model, "batch": a.batch,

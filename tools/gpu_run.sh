@@ -1,0 +1,39 @@
+#!/bin/bash
+# One parameterised GPU pass for gpurun (replaces the per-pass lease scripts).
+#   usage: tools/gpu_run.sh <outdir> <preset>[,<preset>...]
+#   e.g.   gpurun --timeout 1100 -- bash tools/gpu_run.sh r3a suite,smoke,bench,prof
+# Presets (each step has its own time limit; a fault stops the pass, see gpu_steps.sh):
+#   suite     the GPU test suite
+#   rccl      the native RCCL layer tests only + RCCL self-p2p under rocprofv3
+#   smoke     __graft_entry__.smoke()
+#   bench     default bench.py (fp32 headline + bf16 companion), then a longer run
+#   bench152  ResNet-152 (bf16 and fp32)
+#   rehearse  bench.py --gpus 2 --backend gloo (the multi-GPU record, ranks sharing one GPU)
+#   prof      rocprofv3 kernel trace + stats of the fp32 and bf16 benches
+#   fault     4-stage SIGKILL recovery bench (device links)
+# Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+out="$1"; presets="$2"
+[ -n "$out" ] && [ -n "$presets" ] || { echo "usage: $0 <outdir> <preset>[,...]"; exit 2; }
+mkdir -p "gpurun_out/$out"
+steps=()
+IFS=',' read -ra P <<< "$presets"
+for p in "${P[@]}"; do
+  case "$p" in
+    suite)    steps+=("600|$out/pytest_gpu|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread") ;;
+    rccl)     steps+=("180|$out/pytest_rccl|python -u -m pytest tests/test_rccl_native_gpu.py -m gpu -v --timeout 60 --timeout-method thread")
+              steps+=("120|$out/rccl_prof|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/rccl_prof -o run -- python3 tools/rccl_selftest.py") ;;
+    smoke)    steps+=("180|$out/smoke|python -u -c 'import __graft_entry__ as g; g.smoke()'") ;;
+    bench)    steps+=("240|$out/bench_default|python -u bench.py")
+              steps+=("240|$out/bench_long|python -u bench.py --steps 200 --warmup 20") ;;
+    bench152) steps+=("240|$out/bench_r152|python -u bench.py --model resnet152 --steps 50 --warmup 10") ;;
+    rehearse) steps+=("300|$out/bench_gloo2|python -u bench.py --gpus 2 --backend gloo --steps 10 --warmup 3") ;;
+    prof)     steps+=("240|$out/prof_fp32|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_fp32 -o run -- python3 bench.py --no-bf16 --steps 30 --warmup 5")
+              steps+=("240|$out/prof_bf16|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_bf16 -o run -- python3 bench.py --dtype bf16 --steps 50 --warmup 10") ;;
+    fault)    steps+=("300|$out/fault4_dev|python -u tools/fault_bench.py --workers 4 --device cuda:0 --model resnet50 --image 224 --batch 32 --duration 25 --kill-at 10 --links dev --inflight 8 --json gpurun_out/$out/fault_r50_4w_dev.json") ;;
+    *) echo "unknown preset $p"; exit 2 ;;
+  esac
+done
+[ -n "$GPU_EXTRA" ] && steps+=("$GPU_EXTRA")
+exec bash tools/gpu_steps.sh "${steps[@]}"
