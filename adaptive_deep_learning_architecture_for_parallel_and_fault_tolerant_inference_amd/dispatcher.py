@@ -199,6 +199,7 @@ class DEFER:
         self.links = links
         from .transport import shm as _shm
         self._shm = _shm.ShmPool() if ingest == "auto" and _shm.available() else None
+        self._shm_domain: Optional[str] = None
         self.quarantine_s = quarantine_s
         # a worker whose config port does not answer within this many seconds is left
         # out of the next epoch even while its membership lease is still alive
@@ -937,6 +938,15 @@ class DEFER:
     def _local(self, rec: dict) -> bool:
         return rec.get("host") in ("127.0.0.1", "localhost", self.dispatchIP)
 
+    def _shares_shm(self, rec: dict) -> bool:
+        """Worker `rec` can open this process's /dev/shm segments: same host AND the
+        same shm domain (a container with host networking but its own /dev/shm is
+        local by address and still cannot see our slots)."""
+        if self._shm_domain is None:
+            from .transport import shm
+            self._shm_domain = shm.domain()
+        return self._local(rec) and bool(rec.get("shm_domain")) and rec.get("shm_domain") == self._shm_domain
+
     def _send_to_stage0(self, rid: int, x) -> bool:
         """Send request `rid` to the next serving replica (round-robin).  `x` is an
         array or a shared-memory slot reference (sent as its descriptor to a
@@ -949,7 +959,7 @@ class DEFER:
             p = reps[(self._rr + i) % len(reps)]
             if p.stage0 is None or p.replica in self._dirty:
                 continue
-            t = x if not hasattr(x, "container") or self._local(p.records[0]) else x.array
+            t = x if not hasattr(x, "container") or self._shares_shm(p.records[0]) else x.array
             m = Message(1, rid, p.epoch, int(x.shape[0]), [t], [False])
             with self.inflight_lock:
                 if rid in self.inflight_tasks:
@@ -1000,9 +1010,15 @@ class DEFER:
         rid = self._next_req
         self._next_req += 1
         if self._shm is not None:
-            from .transport.shm import ShmRef
+            from .transport.shm import ShmFull, ShmRef
             # the slot is the retained input: a replay re-sends its descriptor
-            data = ShmRef(self._shm.put(data), data.dtype, data.shape)
+            try:
+                data = ShmRef(self._shm.put(data), data.dtype, data.shape)
+            except ShmFull as e:                     # /dev/shm is full: this request travels inline
+                METRICS.inc("ingest_shm_full")
+                if not getattr(self, "_shm_full_logged", False):
+                    self._shm_full_logged = True
+                    self._log(f"shared-memory ingest fell back to inline TCP: {e}")
         with self.inflight_lock:
             self.inflight_tasks[rid] = {"partition": partition_index, "data": data, "start_time": time.time(),
                                         "epoch": None, "replica": None, "replays": 0}

@@ -215,11 +215,19 @@ class StageRuntime:
         n = 1
         for v in shape:
             n *= int(v)
-        if self.link == "dev":
-            from .transport.shm import DevRef
-            ds = self._linkpool.acquire_dev(n * np_dt.itemsize, self.stop)
-            return ds, DevRef(ds, np_dt, shape, bf16=bf16)
-        slot = self._linkpool.acquire(n * np_dt.itemsize, self.stop)
+        from .transport.shm import ShmFull
+        try:
+            if self.link == "dev":
+                from .transport.shm import DevRef
+                ds = self._linkpool.acquire_dev(n * np_dt.itemsize, self.stop)
+                return ds, DevRef(ds, np_dt, shape, bf16=bf16)
+            slot = self._linkpool.acquire(n * np_dt.itemsize, self.stop)
+        except ShmFull:
+            # /dev/shm is full: this tensor travels inline on the TCP hop (page-locked
+            # staging buffer, kept alive by the numpy view until the send)
+            host = torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
+            arr = host.view(torch.int16).numpy().view(np.uint16) if bf16 else host.numpy()
+            return host, arr
         host = torch.from_numpy(slot.view(np_dt, shape))
         if bf16:
             host = host.view(torch.bfloat16)
@@ -288,8 +296,24 @@ class StageRuntime:
             if self.stop.is_set():
                 raise RuntimeError("stage stopped")
         self._set_free[j].clear()
+        from .transport.shm import DevArray
         for name, a, b in zip(self.compute.inputs, m.tensors, m.bf16):
             dst = ex.input_buf(name, j)
+            if isinstance(a, DevArray):
+                # the upstream hop was a device link (its slot holds the raw frontier, only
+                # zvc/lz4 frames stay encoded): device-to-device into the input buffer.  The
+                # caller releases the slot as soon as this returns, so the copy is waited for
+                from .ops._lib import kernels, stream_handle
+                want = np.dtype(np.uint16) if dst.dtype == torch.bfloat16 else np.dtype(np.float32)
+                if (a.dtype != want or tuple(a.shape[1:]) != tuple(dst.shape[1:]) or a.shape[0] > dst.shape[0]):
+                    raise ValueError(f"device link tensor {a.shape} {a.dtype} does not match input {name} "
+                                     f"{tuple(dst.shape)} {dst.dtype}")
+                cur = torch.cuda.current_stream(dst.device)
+                kernels().memcpy_async(int(dst.data_ptr()), a.ptr, a.nbytes, stream_handle(cur))
+                if a.shape[0] < dst.shape[0]:
+                    dst[a.shape[0]:].zero_()
+                cur.synchronize()
+                continue
             if isinstance(a, (bytes, bytearray, memoryview)):
                 if self._gpu_decode(name, a, dst):
                     continue
@@ -426,7 +450,14 @@ class StageRuntime:
                 import torch
                 torch.cuda.synchronize(self.compute.device)
             if self._linkpool is not None:
-                self._linkpool.close()
+                from .transport import shm
+                if isinstance(self._linkpool, shm.DeviceLinkPool):
+                    # IPC-exported device slots: the next stage may still hold them
+                    # open (it tears its epoch down on its own schedule); freed one
+                    # epoch later
+                    self.node.retire_link_pool(self._linkpool)
+                else:
+                    self._linkpool.close()
             from .transport import shm
             shm.detach(list(self._attached_links))
             self._attached_links.clear()
@@ -483,6 +514,7 @@ class Node:
         self._hb_handles: set = set()
         self._hb_lock = threading.Lock()
         self._hang = threading.Event()                   # fault injection: "hang"
+        self._retired_pools: list = []                   # device link pools of the last torn-down epoch
 
     # ---------------------------------------------------------- lifecycle
     def record(self) -> Dict:
@@ -581,6 +613,15 @@ class Node:
         while self._hang.is_set() and not stop.is_set() and not self._stop.is_set():
             time.sleep(0.005)
 
+    def retire_link_pool(self, pool) -> None:
+        """Keep a torn-down epoch's device link pool alive until the next one is
+        retired (or the node stops): importers of its IPC handles finish long
+        before that, so freeing it is never a use-after-free on their side."""
+        with self._hb_lock:
+            old, self._retired_pools = self._retired_pools, [pool]
+        for p in old:
+            p.close(handoff_timeout_s=0.0)
+
     def stop(self) -> None:
         self._stop.set()
         if self.registration is not None:
@@ -588,6 +629,10 @@ class Node:
         with self._rt_lock:
             if self.runtime is not None:
                 self.runtime.abort()
+        with self._hb_lock:
+            old, self._retired_pools = self._retired_pools, []
+        for p in old:
+            p.close(handoff_timeout_s=0.5)
         for s in (self.data_sock, self.config_sock):
             try:
                 s.close()

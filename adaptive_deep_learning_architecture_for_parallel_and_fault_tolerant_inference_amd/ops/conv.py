@@ -325,12 +325,58 @@ def stem_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool: bool 
     return out
 
 
+STEM_F32_K = 176      # 7 filter rows x (8 kw x 3 channels) = 168, padded to 11 halves of 16 (stem_f32.hip SF_K)
+
+
+def pack_stem_f32(kernel_hwio: np.ndarray, bias: np.ndarray, pads, device) -> PackedStem:
+    """conv1 (7x7/s2, 3 -> 64, BN folded) for the fp32 stem: [64][s*24 + kw*3 + c] fp32."""
+    kh, kw, cin, cout = kernel_hwio.shape
+    if (kh, kw, cin, cout) != (7, 7, 3, 64):
+        raise ValueError(f"fp32 stem kernel must be 7x7x3x64, got {kernel_hwio.shape}")
+    wt = np.zeros((64, STEM_F32_K), np.float32)
+    wt[:, :168] = np.pad(np.asarray(kernel_hwio, np.float32).transpose(3, 0, 1, 2),
+                         ((0, 0), (0, 0), (0, 1), (0, 0))).reshape(64, 7 * 8 * 3)
+    (pt, pb), (pl, pr) = pads
+    return PackedStem(w=torch.from_numpy(wt).to(device=device).contiguous(),
+                      bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),
+                      cin=3, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
+
+
+def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pad: int = 1,
+                     stream=None) -> torch.Tensor:
+    """x: [B,H,W,3] fp32 NHWC -> maxpool3x3/s2(relu(conv7x7/s2(x))), fp32 NHWC 64 ch (csrc/kernels/stem_f32.hip)."""
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 4 or x.shape[-1] != 3:
+        raise ValueError("fp32 stem input must be contiguous fp32 NHWC with 3 channels")
+    if ps.w.dtype != torch.float32 or ps.w.shape != (64, STEM_F32_K):
+        raise ValueError("fp32 stem needs weights packed by pack_stem_f32")
+    B, H, W, _ = x.shape
+    OH, OW = ps.out_hw(H, W)
+    PH, PW = (OH + 2 * pool_pad - 3) // 2 + 1, (OW + 2 * pool_pad - 3) // 2 + 1
+    need = B * PH * PW * 64
+    if out.numel() != need or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"fp32 stem output buffer must be contiguous fp32 with {need} elements")
+    kernels().stem_f32_forward(ptr(x), ptr(ps.w), ptr(ps.bias), ptr(out), B, H, W, 3, OH, OW, ps.pad_t, ps.pad_l,
+                               PH, PW, pool_pad, stream_handle(stream))
+    return out
+
+
 # ------------------------------------------------------------------ fp32 path
 # The reference's precision (Keras float32, `src/node.py:177`): conv / GEMM on
-# the fp32 matrix cores, csrc/kernels/conv_f32.hip.  Tiles (BM, BN) per cfg id
-# mirror ADAPT_F32_CFGS there; K tiles are 16 floats.
+# the fp32 matrix cores.  Tiles (BM, BN) per cfg id: 0-5 mirror ADAPT_F32_CFGS
+# (csrc/kernels/conv_f32.hip, register-staged, any Cin), 10-21 ADAPT_F32G_CFGS
+# (csrc/kernels/conv_f32g.hip, LDS-DMA ring, Cin % 32 == 0); K tiles are 32 floats.
 F32_BK = 32
-F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (64, 256)}
+F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (64, 256),
+             10: (128, 128), 11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (256, 128),
+             16: (128, 256), 17: (128, 128), 18: (64, 64), 19: (128, 64), 20: (64, 128), 21: (256, 64)}
+F32G_CFGS = frozenset(range(10, 22))
+
+
+def f32_cfg_supported(cfg: int, cin: int, cout: int) -> bool:
+    """Whether fp32 tile config `cfg` runs a conv with `cin` input / `cout` output channels."""
+    if cfg in F32G_CFGS:
+        return cin % F32_BK == 0 and cout % 4 == 0
+    return cfg in F32_TILES
 
 
 def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, device,
@@ -354,6 +400,8 @@ def choose_cfg_f32(M: int, N: int, Kpad: int, occupancy: int = 2):
     best = None
     ktiles = Kpad // F32_BK
     for cfg, (bm, bn) in F32_TILES.items():
+        if cfg in F32G_CFGS:
+            continue                                 # v2 tiles are chosen by the autotuner (tuning table)
         tiles = math.ceil(M / bm) * math.ceil(N / bn)
         for ks in (1, 2, 4, 8, 16):
             if ks > 1 and ktiles // ks < 8:

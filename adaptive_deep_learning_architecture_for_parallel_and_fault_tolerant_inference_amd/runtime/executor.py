@@ -20,6 +20,7 @@ allocator and the stream / graph API only.
 from __future__ import annotations
 
 import json
+import math
 import os
 import threading
 from collections import ChainMap
@@ -77,7 +78,7 @@ class SliceExecutor:
     """Runs one (sub)graph for a fixed batch on one device with our HIP kernels."""
 
     FP32_KINDS = ("conv", "dense", "maxpool", "gap", "softmax", "add", "bn", "relu", "pad", "copy",
-                  "dwconv", "avgpool", "concat", "act", "binary", "affine")
+                  "dwconv", "avgpool", "concat", "act", "binary", "affine", "stem_f32")
 
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device="cuda",
                  outputs: Optional[Sequence[str]] = None, tune: bool = False, num_sets: int = 1,
@@ -235,6 +236,9 @@ class SliceExecutor:
             if st.kind == "conv":
                 kf, bf = self._folded(weights, st.p)
                 self.packed[i] = conv_ops.pack_conv_f32(kf, bf, st.p["stride"], st.p["pads"], dev)
+            elif st.kind == "stem_f32":
+                kf, bf = self._folded(weights, st.p)
+                self.packed[i] = conv_ops.pack_stem_f32(kf, bf, st.p["pads"], dev)
             elif st.kind == "dense":
                 name = st.p.get("layer", st.out)
                 k = weights[f"{name}/kernel"]
@@ -535,8 +539,13 @@ class SliceExecutor:
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
             for cfg in conv_ops.F32_TILES:
+                if not conv_ops.f32_cfg_supported(cfg, C, pc.cout):
+                    continue
+                bm, bn = conv_ops.F32_TILES[cfg]
+                tiles = math.ceil(M / bm) * math.ceil(N / bn)
                 for ks in (1, 2, 4, 8, 16):
-                    if ks > 1 and ktiles // ks < 2:
+                    # split-K only where the tiles alone leave CUs idle
+                    if ks > 1 and (ktiles // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue
                     ws = torch.empty(ks * M * N, dtype=torch.float32, device=self.device) if ks > 1 else None
                     try:
@@ -845,6 +854,9 @@ class SliceExecutor:
                                       workspace=ws, stream=stream)
             if st.p["softmax"]:
                 E.softmax_rows(dst, b[st.out], stream=stream)
+        elif k == "stem_f32":
+            conv_ops.stem_f32_forward(b[st.ins[0]], self.packed[i], b[st.out], pool_pad=st.p["pool_pad"],
+                                      stream=stream)
         elif k == "maxpool":
             (pt, _), (pl, _) = st.p["pads"]
             E.maxpool_f32(b[st.ins[0]], b[st.out], st.p["pool"], st.p["stride"], pt, pl, st.p.get("pad_zero", True),

@@ -316,6 +316,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
     if missing:
         raise RuntimeError(f"plan does not produce outputs {missing}")
     if fp32:
+        if os.environ.get("ADAPT_NO_STEM", "0") != "1":
+            steps = _fuse_stem_f32(g, steps, outset)
         return steps
     if os.environ.get("ADAPT_FUSED_BOTTLENECK", "1") == "1":
         steps = fuse_bottlenecks(g, steps, outset)
@@ -460,6 +462,36 @@ def merge_siblings(steps: List[Step]) -> List[Step]:
 
 
 STEM_MAX_OW = 112     # csrc/kernels/stem.hip ST_OWMAX
+
+
+def _fuse_stem_f32(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
+    """fp32 path: conv(image, 7x7/s2, 3 -> 64, BN+ReLU) -> maxpool 3x3/s2 pad 1  ==>  one
+    ``stem_f32`` step (csrc/kernels/stem_f32.hip).  The image is the conv's
+    input as it is (the fp32 plan has no pack step)."""
+    def users(t: str) -> List[int]:
+        return [j for j, s in enumerate(steps) if t in s.ins]
+
+    for i, cv in enumerate(steps):
+        if cv.kind != "conv" or len(cv.ins) != 1 or g.layers[cv.ins[0]].op != "input":
+            continue
+        p = cv.p
+        h, w, c = g.layers[cv.ins[0]].out_shape
+        oh, ow = g.layers[p["conv"]].out_shape[:2]
+        (pt, _), (pl, _) = p["pads"]
+        if (p["kernel"] != (7, 7) or p["stride"] != 2 or p["filters"] != 64 or p["relu"] != 1 or p["residual"]
+                or c != 3 or w % 4 or ow > STEM_MAX_OW or pl != 3 or cv.out in outset):
+            continue
+        mu = users(cv.out)
+        if len(mu) != 1 or steps[mu[0]].kind != "maxpool":
+            continue
+        mp = steps[mu[0]]
+        if not (mp.p["pool"] in (3, (3, 3)) and mp.p["stride"] in (2, (2, 2)) and mp.p["pads"] == ((1, 1), (1, 1))):
+            continue
+        stem = Step("stem_f32", mp.out, [cv.ins[0]], list(cv.covers) + list(mp.covers),
+                    {"conv": p["conv"], "bn": p["bn"], "pads": p["pads"], "pool": True, "pool_pad": 1,
+                     "filters": 64})
+        return [stem if j == i else s for j, s in enumerate(steps) if j != mu[0]]
+    return steps
 
 
 def _fuse_stem(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:

@@ -75,6 +75,32 @@ def domain() -> Optional[str]:
 LINK_HDR = 64          # link slots: byte 0 = hand-off flag, data from this offset
 
 
+class ShmFull(OSError):
+    """/dev/shm could not back a new segment (tmpfs size limit): callers fall back
+    to an inline (TCP) or pageable path instead of taking a SIGBUS later."""
+
+
+def _open_reserved(path: str, nbytes: int) -> mmap.mmap:
+    """Create segment `path` of `nbytes` with its pages reserved up front.
+    ftruncate alone succeeds past a tmpfs mount's size limit and the first
+    write into the missing pages raises SIGBUS; posix_fallocate fails with
+    ENOSPC instead, so a full /dev/shm is an exception here."""
+    fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+    try:
+        os.ftruncate(fd, nbytes)
+        try:
+            os.posix_fallocate(fd, 0, nbytes)
+        except OSError as e:
+            try:
+                os.unlink(path)
+            except FileNotFoundError:
+                pass
+            raise ShmFull(e.errno, f"/dev/shm cannot hold {nbytes} more bytes: {e.strerror}") from e
+        return mmap.mmap(fd, nbytes)
+    finally:
+        os.close(fd)
+
+
 class Slot:
     __slots__ = ("pool", "name", "nbytes", "mm", "index", "offset")
 
@@ -119,13 +145,7 @@ class ShmPool:
             if free:
                 return free.pop()
             name = f"{self.prefix}-{len(self._all)}"
-            path = os.path.join(SHM_DIR, name)
-            fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-            try:
-                os.ftruncate(fd, nbytes)
-                mm = mmap.mmap(fd, nbytes)
-            finally:
-                os.close(fd)
+            mm = _open_reserved(os.path.join(SHM_DIR, name), nbytes)
             s = Slot(self, name, nbytes, mm, len(self._all))
             self._all.append(s)
             return s
@@ -170,12 +190,7 @@ class LinkPool:
 
     def _create(self, nbytes: int) -> Slot:
         name = f"{self.prefix}-{len(self._all)}"
-        fd = os.open(os.path.join(SHM_DIR, name), os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-        try:
-            os.ftruncate(fd, LINK_HDR + nbytes)
-            mm = mmap.mmap(fd, LINK_HDR + nbytes)
-        finally:
-            os.close(fd)
+        mm = _open_reserved(os.path.join(SHM_DIR, name), LINK_HDR + nbytes)
         s = Slot(self, name, nbytes, mm, len(self._all), offset=LINK_HDR)
         self._all.append(s)
         if self.register_device:          # the device -> host copy is then an async DMA into the slot
@@ -200,10 +215,16 @@ class LinkPool:
                         s.mm[0] = 1
                         return s
                 if len(same) < self.max_slots:
-                    s = self._create(nbytes)
-                    same.append(s)
-                    s.mm[0] = 1
-                    return s
+                    try:
+                        s = self._create(nbytes)
+                    except ShmFull:
+                        if not same:
+                            raise                 # no slot of this size at all: the caller goes inline
+                        s = None                  # wait for one of the existing slots instead
+                    if s is not None:
+                        same.append(s)
+                        s.mm[0] = 1
+                        return s
             if stop is not None and stop.is_set():
                 raise RuntimeError("link stopped while waiting for a free slot")
             time.sleep(0.0002)
@@ -274,12 +295,12 @@ class DeviceLinkPool(LinkPool):
         with torch.cuda.device(self.device):
             ptr = K.dev_alloc(max(nbytes, 1))
             handle = K.ipc_handle(ptr)
-        fd = os.open(os.path.join(SHM_DIR, name), os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
         try:
-            os.ftruncate(fd, DEV_HDR)
-            mm = mmap.mmap(fd, DEV_HDR)
-        finally:
-            os.close(fd)
+            mm = _open_reserved(os.path.join(SHM_DIR, name), DEV_HDR)
+        except ShmFull:
+            with torch.cuda.device(self.device):
+                K.dev_free(ptr)
+            raise
         mm[LINK_HDR:LINK_HDR + 16] = os.getpid().to_bytes(8, "little") + int(ptr).to_bytes(8, "little")
         if len(handle) != IPC_HANDLE:
             raise RuntimeError(f"device link: IPC handle of {len(handle)} bytes, expected {IPC_HANDLE}")
@@ -293,10 +314,29 @@ class DeviceLinkPool(LinkPool):
         s = self.acquire(nbytes, stop)
         return _DevSlot(s, self._dev[s.name], s.nbytes)
 
-    def close(self) -> None:
-        """Callers synchronise the device first (no copy may still target a slot)."""
+    def close(self, handoff_timeout_s: float = 0.0) -> None:
+        """Callers synchronise the device first (no copy may still target a slot).
+
+        Freeing an IPC-exported allocation while an importer may still copy out
+        of it is undefined (the CUDA IPC contract, which HIP follows).  A torn
+        down epoch's pool is therefore not closed at once: the worker retires it
+        (`Node.retire_link_pool`) and closes it one epoch later, when every
+        importer has long finished or died.  `handoff_timeout_s` additionally
+        waits (bounded) for flagged slots: the receiver of a slot clears the
+        flag once its copy has retired."""
         import torch
         from ..ops._lib import kernels
+        deadline = time.time() + handoff_timeout_s
+        with self._lock:
+            slots = list(self._all)
+        for sl in slots:
+            while time.time() < deadline:
+                try:
+                    if sl.mm[0] == 0:
+                        break
+                except ValueError:                  # already unmapped
+                    break
+                time.sleep(0.001)
         with self._lock:
             for ptr in self._dev.values():
                 try:
@@ -464,12 +504,7 @@ def detach(names) -> None:
 
 
 def detach_all() -> None:
+    """Unmap every attached segment, closing IPC mappings of device slots too."""
     with _att_lock:
-        for a in _attached.values():
-            if a.registered:
-                try:
-                    import torch
-                    torch.cuda.cudart().cudaHostUnregister(int(a.arr.ctypes.data))
-                except Exception:  # noqa: BLE001
-                    pass
-        _attached.clear()
+        names = list(_attached)
+    detach(names)

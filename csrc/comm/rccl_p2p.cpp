@@ -41,9 +41,12 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// Releases the GIL if this thread holds it.  The watch thread is a plain C++
+// thread without a Python thread state: it may call abort(), and releasing a
+// GIL it does not hold is undefined (a fatal error / crash in CPython).
 struct NoGil {
   PyThreadState* st;
-  NoGil() : st(PyEval_SaveThread()) {}
+  NoGil() : st(PyGILState_Check() ? PyEval_SaveThread() : nullptr) {}
   NoGil(const NoGil&) = delete;
   NoGil& operator=(const NoGil&) = delete;
   ~NoGil() noexcept(false) {
@@ -182,9 +185,19 @@ class Comm {
     ncclResult_t st = ncclSuccess;
     ncclResult_t r = api().getAsyncError(comm_, &st);
     if (r != ncclSuccess) st = r;
+    const int forced = forced_err_.load();
+    if (forced != ncclSuccess && st == ncclSuccess) st = (ncclResult_t)forced;
     note(st);
     return (int)st;
   }
+
+  // Fault injection for the failure-path tests: from now on the async-error
+  // poll reports `code` as if RCCL had (a peer died mid-transfer, a remote
+  // error): the watch thread sees it, records it and aborts the communicator.
+  // On one GPU RCCL has no asynchronous error to provoke (the one local
+  // misuse, a self-receive without its send, fails synchronously in
+  // ncclGroupEnd).
+  void inject_async_error(int code) { forced_err_.store(code); }
 
   // Block (GIL released) until every enqueued NCCL call is accepted; raise on
   // error, abort or timeout.  Covers init completion and ncclGroupEnd.
@@ -387,6 +400,7 @@ class Comm {
       ncclResult_t st = ncclSuccess;
       ncclResult_t r = a.getAsyncError(comm_, &st);
       if (r != ncclSuccess) st = r;
+      if (st == ncclSuccess && forced_err_.load() != ncclSuccess) st = (ncclResult_t)forced_err_.load();
       if (st == ncclSuccess) break;
       if (st != ncclInProgress) {
         note(st);
@@ -407,6 +421,7 @@ class Comm {
   std::atomic<bool> aborted_{false};
   std::atomic<int> users_{0};
   std::atomic<int> err_{ncclSuccess};
+  std::atomic<int> forced_err_{ncclSuccess};
   std::mutex msg_mu_;
   std::string err_msg_;
   std::thread watch_;
@@ -482,6 +497,7 @@ PYBIND11_MODULE(_comm, m) {
       .def("abort", &Comm::abort)
       .def("destroy", &Comm::destroy, py::arg("timeout_s") = 10.0)
       .def("start_watch", &Comm::start_watch, py::arg("period_us") = 1000, py::arg("abort_on_error") = true)
+      .def("inject_async_error", &Comm::inject_async_error, py::arg("code") = (int)ncclRemoteError)
       .def("stop_watch", &Comm::stop_watch)
       .def_property_readonly("failed", &Comm::failed)
       .def_property_readonly("aborted", &Comm::aborted)

@@ -31,21 +31,6 @@
 
 namespace adapt {
 
-struct ConvF32Params {
-  const float* x;
-  const float* w;
-  const float* bias;
-  const float* res;
-  float* out;
-  float* ws;
-  int B, H, W, Cin;
-  int OH, OW, N;
-  int KH, KW, stride, pad_t, pad_l;
-  int M, K, Kpad;
-  int relu;
-  int ksplit;
-};
-
 namespace {
 
 constexpr int FBK = 32;          // fp32 elements per K tile (8 float4 chunks)
@@ -291,7 +276,10 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
 #define X(id, BM_, BN_, WM_, WN_) case id: e = launch_f32<BM_, BN_, WM_, WN_>(p, pure, vec, s); break;
     ADAPT_F32_CFGS(X)
 #undef X
-    default: return hipErrorInvalidValue;
+    default:
+      // v2: LDS-DMA ring (conv_f32g.hip); tap-major walk needs Cin % 32 == 0
+      if (!conv_f32g_ok(cfg, Cin, N)) return hipErrorInvalidValue;
+      e = conv_f32g_launch(p, cfg, pure, s);
   }
   if (e != hipSuccess || p.ksplit <= 1) return e;
   size_t total = (size_t)p.M * p.N;

@@ -99,6 +99,26 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
                         int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
                         hipStream_t s);
 // fp32 path (conv_f32.hip): MFMA f32 implicit-GEMM conv / GEMM and fp32 layers
+struct ConvF32Params {
+  const float* x;
+  const float* w;
+  const float* bias;
+  const float* res;
+  float* out;
+  float* ws;
+  int B, H, W, Cin;
+  int OH, OW, N;
+  int KH, KW, stride, pad_t, pad_l;
+  int M, K, Kpad;
+  int relu;
+  int ksplit;
+};
+// fp32 stem (stem_f32.hip): 7x7/s2 conv (+BN, ReLU) + 3x3/s2 max-pool, weights [64][176] fp32
+hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
+                            int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s);
+// v2 fp32 kernel family (conv_f32g.hip, cfg ids >= 10): LDS-DMA ring
+bool conv_f32g_ok(int cfg, int Cin, int N);
+hipError_t conv_f32g_launch(const ConvF32Params& p, int cfg, bool pure, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,

@@ -1,0 +1,200 @@
+// fp32 ResNet stem in one launch: fp32 image -> 7x7/s2 conv (+folded BN, ReLU)
+// -> 3x3/s2 max-pool, on the fp32 matrix cores (v_mfma_f32_16x16x4_f32).  The
+// reference runs these as six Keras float32 layers inside `model.predict`
+// (src/node.py:177; SURVEY §2.4 rows conv1_pad .. pool1_pool).
+//
+// The generic fp32 conv gathers the 3-channel image element by element and
+// writes the 103 MB conv1 output for a separate max-pool: 169 + 29 us at bs=32
+// (profiles/r2/fp32/r50_fp32_bs32_steps_r2r.json).  Here (the bf16 stem v2
+// design, stem.hip, carried to fp32):
+//
+// * one block per (image, group of SF_SP pool rows); each step computes the two
+//   new conv rows a pool row needs (three on the first step) into a 3-row LDS
+//   ring and emits the pool row from it, so the conv output never leaves LDS;
+// * input rows live in a 16-row LDS ring with the 3 channels packed
+//   ([col][c]): the 21 (kw, c) taps of one filter row are 21 consecutive floats,
+//   so K = 7 rows x 24 (kw = 7 carries zero weights) = 168, padded to 176:
+//   84 % of the MFMA work is real (a 4-channel layout would be 66 %);
+// * a step's 2 x 7 pixel tiles x 4 channel tiles are 56 (16 px x 16 ch) units,
+//   7 per wave on 8 waves; a wave always works on the same 16 channels, so its
+//   A operand (the weights: 11 float4 per lane) stays in VGPRs for the launch;
+// * the next step's 4 input rows are loaded into registers before this step's
+//   MFMAs and land in LDS after them;
+// * each unit keeps two accumulators (even / odd K halves): two independent
+//   MFMA chains instead of one 44-long dependent chain.
+#include "kernels.h"
+
+namespace adapt {
+namespace {
+
+constexpr int SF_SP = 7;                     // pool rows per block
+constexpr int SF_WAVES = 8;
+constexpr int SF_NT = SF_WAVES * 64;
+constexpr int SF_OWMAX = 112;
+constexpr int SF_COLS = 2 * SF_OWMAX + 8;    // patch columns (input col + pad_l)
+constexpr int SF_OFF = 4;                    // row origin: even, so 6*ow + j + OFF stays 8-byte aligned
+constexpr int SF_ROWLEN = 704;               // >= SF_OFF + SF_COLS * 3, 16-byte multiple
+constexpr int SF_RING = 16;                  // input-row ring
+constexpr int SF_K = 176;                    // 7 x 24 taps, padded to 11 halves of 16
+constexpr int SF_KH = SF_K / 16;
+static_assert(SF_OFF + SF_COLS * 3 <= SF_ROWLEN, "row length");
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// conv ring [3][112 px][16 chunks of 4 ch], chunk XOR-swizzled by the pixel so
+// the 16 pixels of a C^T fragment store spread over the banks
+__device__ __forceinline__ int cring_off(int slot, int px, int chunk) {
+  return ((slot * SF_OWMAX + px) * 16 + (chunk ^ (px & 15))) * 4;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ out, int H, int W, int OH,
+                                                                 int OW, int pad_t, int pad_l, int PH, int PW,
+                                                                 int pool_pad, int groups) {
+  __shared__ __attribute__((aligned(16))) float patch[SF_RING * SF_ROWLEN];     // 44 KiB
+  __shared__ __attribute__((aligned(16))) float cring[3 * SF_OWMAX * 64];       // 84 KiB
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = logical / groups;
+  const int t0 = (logical - img * groups) * SF_SP;
+  const int t1 = min(PH, t0 + SF_SP);
+  const int tpr = (OW + 15) >> 4;
+  const float* xi = x + (size_t)img * H * W * 3;
+  const int c4row = W * 3 / 4;               // float4 chunks of one image row (W % 4 == 0)
+
+  // zero the whole patch once: pad columns are never written again, rows outside
+  // the image are written as zeros by the staging below
+  for (int i = tid; i < SF_RING * SF_ROWLEN / 4; i += SF_NT) *(f32x4*)(patch + i * 4) = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // input rows [ih_lo, ih_lo + n): loads to registers / stores to their ring slots
+  constexpr int MAXC = (11 * (SF_OWMAX * 2 * 3 / 4) + SF_NT - 1) / SF_NT;   // chunks per thread, 11 rows
+  auto get_rows = [&](f32x4 (&v)[MAXC], int ih_lo, int n) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int idx = tid + k * SF_NT;
+      const int r = idx / c4row, c = idx - r * c4row;
+      const int ih = ih_lo + r;
+      v[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (r < n && (unsigned)ih < (unsigned)H) v[k] = *(const f32x4*)(xi + (size_t)ih * W * 3 + c * 4);
+    }
+  };
+  auto put_rows = [&](const f32x4 (&v)[MAXC], int ih_lo, int n) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int idx = tid + k * SF_NT;
+      const int r = idx / c4row, c = idx - r * c4row;
+      if (r >= n) continue;
+      float* row = patch + ((ih_lo + r + 4 * SF_RING) % SF_RING) * SF_ROWLEN + SF_OFF + pad_l * 3 + c * 4;
+      row[0] = v[k][0]; row[1] = v[k][1]; row[2] = v[k][2]; row[3] = v[k][3];
+    }
+  };
+
+  const int r_first = 2 * t0 - pool_pad;     // first conv row (may be -1)
+  // first step: conv rows r_first .. r_first+2 need input rows 2*r_first-pad_t .. +10
+  __syncthreads();
+  {
+    f32x4 v0[MAXC];
+    get_rows(v0, 2 * r_first - pad_t, 11);
+    put_rows(v0, 2 * r_first - pad_t, 11);
+  }
+  // weights of this wave's 16 channels: A operand, lane = (channel fr, k group fq)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ct = wave & 3;
+  f32x4 wa[SF_KH];
+#pragma unroll
+  for (int h = 0; h < SF_KH; ++h) wa[h] = *(const f32x4*)(w + (size_t)(ct * 16 + fr) * SF_K + h * 16 + fq * 4);
+  const f32x4 b4 = *(const f32x4*)(bias + ct * 16 + fq * 4);
+  // per-lane k layout: half h covers kk = 16h + 4fq .. +3 -> filter row kk / 24, tap j = kk % 24
+  int koff[SF_KH];
+#pragma unroll
+  for (int h = 0; h < SF_KH; ++h) {
+    const int kk = 16 * h + 4 * fq;
+    koff[h] = (kk / 24) * 0x10000 + (kk % 24);                  // (filter row, tap) packed
+  }
+  __syncthreads();
+
+  for (int t = t0; t < t1; ++t) {
+    const bool first = t == t0;
+    const int ra = first ? r_first : 2 * t - pool_pad + 1;     // first conv row this step computes
+    const int nr = first ? 3 : 2;
+    // the next step's 4 input rows, in flight during this step's MFMAs
+    const bool more = t + 1 < t1;
+    const int nxt_lo = 2 * (2 * (t + 1) - pool_pad + 1) - pad_t + 3;   // rows 4(t+1)-... not yet staged
+    f32x4 pv[MAXC];
+    if (more) get_rows(pv, nxt_lo, 4);
+    const int units = nr * tpr;                                 // pixel tiles this step (x 4 channel tiles)
+    for (int u = wave >> 2; u < units; u += SF_WAVES / 4) {
+      const int q = u / tpr;
+      const int r = ra + q;
+      if (r < 0 || r >= OH) continue;                           // wave-uniform
+      const int c0 = (u - q * tpr) * 16;
+      const int ow = min(c0 + fr, OW - 1);                      // ragged last tile: clamp the read, skip the store
+      const int ihb = 2 * r - pad_t;                            // input row of filter row 0
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < SF_KH; ++h) {
+        const int s = koff[h] >> 16, j = koff[h] & 0xffff;
+        const float* src = patch + ((ihb + s + 4 * SF_RING) % SF_RING) * SF_ROWLEN + SF_OFF + 6 * ow + j;
+        const f32x2 lo = *(const f32x2*)src, hi = *(const f32x2*)(src + 2);
+        const f32x4 pb = {lo[0], lo[1], hi[0], hi[1]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (h & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb[e], acc1, 0, 0, 0);
+          else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb[e], acc0, 0, 0, 0);
+        }
+      }
+      // C^T fragment: channel = 16ct + 4fq + e, pixel = c0 + fr
+      if (c0 + fr < OW) {
+        f32x4 y = acc0 + acc1 + b4;
+        y[0] = fmaxf(y[0], 0.f); y[1] = fmaxf(y[1], 0.f); y[2] = fmaxf(y[2], 0.f); y[3] = fmaxf(y[3], 0.f);
+        *(f32x4*)(cring + cring_off((r + 3) % 3, c0 + fr, ct * 4 + fq)) = y;
+      }
+    }
+    if (more) put_rows(pv, nxt_lo, 4);
+    __syncthreads();
+    // pool row t from conv rows 2t-pp .. 2t-pp+2; post-ReLU values are >= 0, so the
+    // zero padding is the 0 the max starts from
+    for (int idx = tid; idx < PW * 16; idx += SF_NT) {
+      const int ch = idx & 15, pw = idx >> 4;
+      f32x4 m = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const int oh = 2 * t - pool_pad + dr;
+        if ((unsigned)oh >= (unsigned)OH) continue;
+#pragma unroll
+        for (int dc = 0; dc < 3; ++dc) {
+          const int oc = 2 * pw - pool_pad + dc;
+          if ((unsigned)oc >= (unsigned)OW) continue;
+          const f32x4 v = *(const f32x4*)(cring + cring_off((oh + 3) % 3, oc, ch));
+          m[0] = fmaxf(m[0], v[0]); m[1] = fmaxf(m[1], v[1]); m[2] = fmaxf(m[2], v[2]); m[3] = fmaxf(m[3], v[3]);
+        }
+      }
+      *(f32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch * 4) = m;
+    }
+    __syncthreads();                                            // ring slots of rows 2t-pp, 2t-pp+1 are free
+  }
+}
+
+// weights [64][176] fp32: k = s * 24 + kw * 3 + c (kw = 7 and k >= 168 zero); image NHWC, C = 3
+bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
+  return C == 3 && W % 4 == 0 && OW >= 1 && OW <= SF_OWMAX && 2 * OW + 8 <= SF_COLS && pool_pad == 1;
+}
+
+hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
+                            int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s) {
+  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || B < 1 || PH < 1 || PW < 1 ||
+      PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
+    return hipErrorInvalidValue;
+  const int groups = (PH + SF_SP - 1) / SF_SP;
+  hipLaunchKernelGGL(stem_pool_f32_kernel, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW, pad_t,
+                     pad_l, PH, PW, pool_pad, groups);
+  return hipGetLastError();
+}
+
+}  // namespace adapt

@@ -200,3 +200,36 @@ def test_defer_device_link_across_processes():
                 p.wait(timeout=30)
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
+
+
+@pytest.mark.parametrize("codec", ["zvc", "lz4"])
+def test_defer_gpu_codec_with_device_link_upstream(codec):
+    """A GPU codec on the TCP edges plus same-host device links (links=auto): the
+    last stage compresses its result on the GPU while its *input* arrives through
+    a device link slot (a DevArray, not an encoded frame)."""
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=4, ordered=True, weight_codec="lz4",
+              codec=codec, min_workers=2, links="auto")
+    d.membership_server.start()
+    nodes = [Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cuda:0", node_id=f"c{i}",
+                  heartbeat_ttl=1.0) for i in range(2)]
+    for n in nodes:
+        n.run(block=False)
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["conv3_block1_1_conv"], inq, outq), daemon=True).start()
+        rng = np.random.default_rng(8)
+        xs = [rng.standard_normal((4, 224, 224, 3)).astype(np.float32) for _ in range(6)]
+        for x in xs:
+            inq.put(x)
+        got = np.concatenate([outq.get(timeout=120) for _ in xs])
+        want = m.predict(np.concatenate(xs), device="cpu")
+        assert np.abs(got - want).sum(-1).max() < 0.1
+        last = next(n for n in nodes if n.node_id == d.pipeline.workers[-1])
+        first = next(n for n in nodes if n.node_id == d.pipeline.workers[0])
+        assert first.runtime.link == "dev" and last.runtime.gpu_codec
+        assert not d.recoveries, d.events
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()

@@ -59,6 +59,9 @@ def test_conv_f32_matches_fp64(shape, ksplit):
     pc = C.pack_conv_f32(kern, bias, s, pads, "cuda")
     out = torch.empty((B, OH, OW, Cout), dtype=torch.float32, device="cuda")
     for cfg in C.F32_TILES:
+        if not C.f32_cfg_supported(cfg, Cin, Cout):
+            continue
+        out.fill_(float("nan"))
         C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out, None if res is None else torch.from_numpy(res).cuda(),
                            relu=relu, cfg=cfg, ksplit=ksplit)
         got = out.cpu().numpy()
@@ -223,3 +226,35 @@ def test_other_families_fp32_logits_match_oracle(name):
     assert rel <= 1e-3, f"{name} fp32 logits rel err {rel}"
     assert (logits.argmax(-1) == want.argmax(-1)).all()
     assert torch.isfinite(probs).all()
+
+
+@pytest.mark.parametrize("B,H", [(2, 224), (1, 64), (3, 112)])
+def test_stem_f32_fused_matches_fp64(B, H):
+    """csrc/kernels/stem_f32.hip: 7x7/s2 conv (+bias, ReLU) + 3x3/s2 max-pool in one launch vs a float64 oracle."""
+    rng = np.random.default_rng(H + B)
+    x = rng.standard_normal((B, H, H, 3)).astype(np.float32)
+    kern = (rng.standard_normal((7, 7, 3, 64)) / np.sqrt(147)).astype(np.float32)
+    bias = (0.1 * rng.standard_normal(64)).astype(np.float32)
+    pads = ((3, 3), (3, 3))
+    conv = _ref_conv(x, kern, bias, 2, pads, None, 1)                    # B, OH, OW, 64
+    t = torch.from_numpy(conv).permute(0, 3, 1, 2)
+    want = F.max_pool2d(F.pad(t, (1, 1, 1, 1)), 3, 2).permute(0, 2, 3, 1).numpy()
+    ps = C.pack_stem_f32(kern, bias, pads, "cuda")
+    out = torch.full(want.shape, float("nan"), dtype=torch.float32, device="cuda")
+    C.stem_f32_forward(torch.from_numpy(x).cuda(), ps, out)
+    got = out.cpu().numpy()
+    err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
+    assert np.isfinite(got).all() and err < 2e-5, f"rel err {err}"
+
+
+def test_resnet50_fp32_plan_uses_fused_stem_and_v2_convs():
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import (
+        build_resnet, init_weights)
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import (
+        SliceExecutor)
+    g = build_resnet("resnet50")
+    ex = SliceExecutor(g, init_weights(g, 0), 32, device="cuda", precision="fp32")
+    kinds = [st.kind for st in ex.steps]
+    assert kinds[0] == "stem_f32" and "maxpool" not in kinds
+    v2 = [c for i, (c, _) in ex.cfg.items() if c in C.F32G_CFGS]
+    print(f"fp32 plan: {len(ex.steps)} steps, {len(v2)} of {len(ex.cfg)} GEMMs on the v2 LDS-DMA kernel")

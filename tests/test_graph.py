@@ -187,3 +187,14 @@ def test_plan_unfused_at_cut(r50):
     assert len(bn) == 1 and bn[0].p["relu"] and bn[0].out == "conv3_block1_1_relu"   # BN + ReLU standalone
     st1 = compile_plan(subgraph(r50, s[0]))
     assert st1[-1].kind == "conv" and st1[-1].out == "conv3_block1_1_conv" and not st1[-1].p["bn"]
+
+
+def test_fp32_plan_fuses_stem_and_pool():
+    """fp32 path (the reference's precision): conv1 7x7/s2 + BN + ReLU + pool1 become one stem_f32 step."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.plan import compile_plan
+    g = build_resnet("resnet50")
+    steps = compile_plan(g, fp32=True)
+    assert steps[0].kind == "stem_f32" and steps[0].out == "pool1_pool"
+    assert "conv1_conv" in steps[0].covers and "pool1_pool" in steps[0].covers
+    assert not any(s.kind == "maxpool" for s in steps)

@@ -108,29 +108,52 @@ def test_nonblocking_init_missing_peer_aborted_from_thread():
     c2.destroy()
 
 
+def test_async_error_aborts_and_unblocks_waiters_then_rebuild():
+    """The failure path of a live link: the communicator's async-error state
+    turns bad (injected: on one GPU RCCL has no asynchronous error to provoke),
+    the watch thread sees it within its poll period and aborts the
+    communicator, a host waiter on the link raises LinkError instead of
+    hanging, and a fresh communicator on the same device works."""
+    r = _rccl()
+    store = dist.HashStore()
+    c = _comm(store, "t/faulty", watch_us=200)
+    x = torch.arange(1 << 16, device="cuda", dtype=torch.int32)
+    y = torch.zeros_like(x)
+    c.p2p(sends=[(x, 0)], recvs=[(y, 0)]).wait_host(timeout_s=30)          # healthy first
+    assert torch.equal(x, y) and not c.failed
+    t0 = time.perf_counter()
+    c._c.inject_async_error()
+    while not c.aborted and time.perf_counter() - t0 < 2.0:
+        time.sleep(0.0005)
+    dt = (time.perf_counter() - t0) * 1e3
+    assert c.failed and c.aborted, "watch thread did not abort the failed communicator"
+    print(f"async error -> communicator aborted by the watch thread in {dt:.2f} ms: {c.error_text}")
+    assert dt < 100.0
+    with pytest.raises(r.LinkError):
+        c.p2p(sends=[(x, 0)], recvs=[(y, 0)])
+    c2 = _comm(store, "t/rebuilt")
+    z = torch.zeros_like(x)
+    c2.p2p(sends=[(x, 0)], recvs=[(z, 0)]).wait_host(timeout_s=30)
+    assert torch.equal(x, z)
+    c2.destroy()
+
+
 def test_recv_without_matching_send_fails_loudly_then_rebuild():
-    """A receive with no matching send must surface as an error (synchronously
-    from the enqueue or through the async-error watch), never as a silent
-    hang; the failed communicator is aborted and a fresh one works."""
+    """A receive with no matching send (world=1: a self-receive without its send)
+    surfaces as a LinkError from the grouped enqueue instead of a hang, and a
+    fresh communicator on the same device then works."""
     r = _rccl()
     store = dist.HashStore()
     c = _comm(store, "t/unmatched", watch_us=200)
     y = torch.zeros(1 << 16, device="cuda", dtype=torch.int32)
-    raised = None
     t0 = time.perf_counter()
-    try:
-        w = c.p2p(recvs=[(y, 0)])
-        w.wait_host(timeout_s=2.0)
-    except Exception as e:  # noqa: BLE001
-        raised = e
+    with pytest.raises(r.LinkError) as ei:
+        c.p2p(recvs=[(y, 0)]).wait_host(timeout_s=5.0)
     dt = (time.perf_counter() - t0) * 1e3
-    if raised is None:
-        c.abort()
-    assert raised is not None, "unmatched self-receive neither failed nor hung"
-    assert isinstance(raised, r.LinkError)
-    print(f"unmatched receive reported in {dt:.1f} ms: {raised}")
+    print(f"unmatched receive reported in {dt:.2f} ms: {ei.value}")
+    assert dt < 100.0
     c.abort()
-    c2 = _comm(store, "t/rebuilt")
+    c2 = _comm(store, "t/unmatched-rebuilt")
     x = torch.full((4096,), 7, device="cuda", dtype=torch.int32)
     z = torch.zeros_like(x)
     c2.p2p(sends=[(x, 0)], recvs=[(z, 0)]).wait_host(timeout_s=30)

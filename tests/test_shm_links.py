@@ -144,3 +144,54 @@ def test_device_link_descriptor_roundtrip():
                                                     (4, 28, 28, 128))
     assert a.nbytes == 4 * 28 * 28 * 128 * 2
     assert C.codec_of(buf) == "dev" and C.is_bf16(buf) and C.shm_name(buf) == a.name and shm.is_link(a.name)
+
+
+def test_full_dev_shm_raises_instead_of_sigbus(monkeypatch):
+    """tmpfs accepts an ftruncate past its size limit and SIGBUSes on the first
+    write; segments are reserved with posix_fallocate, so a full /dev/shm is a
+    ShmFull exception (the dispatcher then sends the request inline)."""
+    import errno
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.transport import shm
+
+    def enospc(fd, off, n):
+        raise OSError(errno.ENOSPC, "No space left on device")
+
+    monkeypatch.setattr(shm.os, "posix_fallocate", enospc)
+    pool = shm.ShmPool()
+    with pytest.raises(shm.ShmFull):
+        pool.put(np.zeros((4, 1024), np.float32))
+    assert not [f for f in os.listdir(shm.SHM_DIR) if f.startswith(pool.prefix)]      # nothing left behind
+    lp = shm.LinkPool()
+    with pytest.raises(shm.ShmFull):
+        lp.acquire(4096)
+    monkeypatch.undo()
+    s = lp.acquire(4096)                        # space again: the link works
+    assert s.nbytes == 4096
+    lp.close()
+    pool.close()
+
+
+def test_dispatcher_ingest_falls_back_inline_when_shm_full(tiny, monkeypatch):
+    import errno
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.transport import shm
+
+    def enospc(fd, off, n):
+        raise OSError(errno.ENOSPC, "No space left on device")
+
+    d = DEFER(membership_port=0, result_port=0, worker_wait=10, batch=2, weight_codec="lz4")
+    d.membership_server.start()
+    node = Node(membership_port=d.membership_port, data_port=0, config_port=0, device="cpu", node_id="f0",
+                heartbeat_ttl=1.0)
+    node.run(block=False)
+    try:
+        monkeypatch.setattr(shm.os, "posix_fallocate", enospc)
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, [], inq, outq), daemon=True).start()
+        x = np.random.default_rng(0).standard_normal((2, 32, 32, 3)).astype(np.float32)
+        inq.put(x)
+        y = outq.get(timeout=60)
+        np.testing.assert_allclose(y, tiny.predict(x, device="cpu"), rtol=1e-4, atol=1e-5)
+        assert any("fell back to inline" in e for _, e in d.events)
+    finally:
+        d.shutdown(stop_workers=True)
+        node.stop()

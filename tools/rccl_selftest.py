@@ -41,5 +41,36 @@ def main(reps: int = 20) -> None:
         sys.exit(1)
 
 
+def unmatched(timeout_s: float = 5.0) -> None:
+    """A world=1 receive with no matching send: RCCL must report it (synchronously
+    or through the async-error watch, which then aborts the communicator), and a
+    fresh communicator must work afterwards."""
+    store = dist.HashStore()
+    c = rccl.RcclComm(store, "unmatched", 1, 0, "cuda:0", watch_us=200)
+    y = torch.zeros(1 << 16, device="cuda", dtype=torch.int32)
+    t0 = time.perf_counter()
+    err = None
+    try:
+        c.p2p(recvs=[(y, 0)]).wait_host(timeout_s=timeout_s)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
+    dt = (time.perf_counter() - t0) * 1e3
+    if not c.aborted:
+        c.abort()
+    c2 = rccl.RcclComm(store, "unmatched-rebuilt", 1, 0, "cuda:0")
+    x = torch.full((4096,), 7, device="cuda", dtype=torch.int32)
+    z = torch.zeros_like(x)
+    c2.p2p(sends=[(x, 0)], recvs=[(z, 0)]).wait_host(timeout_s=30)
+    ok = torch.equal(x, z)
+    c2.destroy()
+    print(json.dumps({"test": "unmatched self-receive", "reported": err, "ms": round(dt, 2),
+                      "rebuilt_ok": bool(ok)}), flush=True)
+    if err is None or not ok:
+        sys.exit(1)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "unmatched":
+        unmatched()
+    else:
+        main()
