@@ -372,6 +372,23 @@ F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64
 F32G_CFGS = frozenset(range(10, 22))
 
 
+def f32_sk_plan(M: int, N: int, Kpad: int, cfg: int, mult: int = 1):
+    """fp32 v2 stream-K launch shape: (tiles, grid, iters per block, fp32 workspace elements)."""
+    bm, bn = F32_TILES[cfg]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    g, it = kernels().conv_f32g_sk_plan(tiles, Kpad // F32_BK, mult)
+    return tiles, g, it, g * 2 * bm * bn
+
+
+def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int:
+    """fp32 workspace a launch needs: split-K slabs or stream-K partial slots."""
+    if ksplit > 1:
+        return ksplit * M * N
+    if ksplit < 0:
+        return f32_sk_plan(M, N, Kpad, cfg, -ksplit)[3]
+    return 0
+
+
 def f32_cfg_supported(cfg: int, cin: int, cout: int) -> bool:
     """Whether fp32 tile config `cfg` runs a conv with `cin` input / `cout` output channels."""
     if cfg in F32G_CFGS:
@@ -422,9 +439,12 @@ def choose_cfg_f32(M: int, N: int, Kpad: int, occupancy: int = 2):
 
 def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: Optional[torch.Tensor] = None,
                      relu: int = 0, cfg: Optional[int] = None, ksplit: int = 1,
-                     workspace: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+                     workspace: Optional[torch.Tensor] = None, stream=None,
+                     counters: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp32 conv / GEMM: x [B,H,W,Cin] (or [M,K]) fp32 -> out [B,OH,OW,Cout] fp32, with
-    act(conv + bias (+ residual)) fused.  ksplit > 1 needs `workspace` (ksplit*M*N fp32)."""
+    act(conv + bias (+ residual)) fused.  ksplit > 1: split-K, needs `workspace`
+    (ksplit*M*N fp32); ksplit < 0 (v2 configs): stream-K over -ksplit x 256 blocks,
+    needs `workspace` (workspace_elems_f32) and `counters` (int32 zeros, one per tile)."""
     if x.dim() == 2:
         B, H, W, C = x.shape[0], 1, 1, x.shape[1]
     else:
@@ -452,9 +472,17 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
     bm, bn = F32_TILES[cfg]
     if pc.w.shape[0] < math.ceil(N / bn) * bn or pc.Kpad % F32_BK:
         raise ValueError("packed fp32 weights not padded to the tile")
-    ws_ptr = 0
-    if ksplit > 1:
-        need = ksplit * M * N
+    ws_ptr = ctr_ptr = 0
+    ksplit = int(ksplit) or 1
+    if ksplit < 0:
+        if cfg not in F32G_CFGS:
+            raise ValueError("fp32 stream-K runs on the v2 configs only")
+        tiles = f32_sk_plan(M, N, pc.Kpad, cfg, -ksplit)[0]
+        if counters is None or counters.numel() < tiles or counters.dtype != torch.int32:
+            raise ValueError(f"fp32 stream-K needs {tiles} int32 tile counters")
+        ctr_ptr = ptr(counters)
+    if ksplit != 1:
+        need = workspace_elems_f32(M, N, pc.Kpad, cfg, ksplit)
         if workspace is None:
             workspace = torch.empty(need, dtype=torch.float32, device=x.device)
         if workspace.numel() < need or workspace.dtype != torch.float32:
@@ -462,7 +490,7 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         ws_ptr = ptr(workspace)
     kernels().conv_f32_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C, OH, OW,
                                N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.K, pc.Kpad, int(relu),
-                               max(1, int(ksplit)), int(cfg), stream_handle(stream))
+                               ksplit, int(cfg), stream_handle(stream), ctr_ptr)
     return out
 
 

@@ -198,7 +198,12 @@ class RcclComm:
         return self._c.abort()
 
     def destroy(self) -> None:
-        self._c.destroy(10.0)
+        """Tear down after the link stream has drained.  ncclCommAbort rather than
+        ncclCommFinalize + ncclCommDestroy: the caller synchronised, so nothing is
+        left to flush, and abort never waits on the peer (a finalize on RCCL 2.26
+        was seen to block for good after an earlier failed group in the process)."""
+        self.stream.synchronize()
+        self._c.abort()
 
 
 def _check_dev(t: torch.Tensor, dev: torch.device) -> None:

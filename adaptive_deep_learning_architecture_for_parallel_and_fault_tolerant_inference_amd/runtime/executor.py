@@ -458,9 +458,11 @@ class SliceExecutor:
         need = ctr = 0
         for i, (cfg, ks) in self.cfg.items():
             if self.fp32:
-                if ks > 1:
+                if ks != 1:
                     B, H, W, C, OH, OW, pc = self._conv_geom(i)
-                    need = max(need, ks * B * OH * OW * pc.cout)
+                    need = max(need, conv_ops.workspace_elems_f32(B * OH * OW, pc.cout, pc.Kpad, cfg, ks))
+                    if ks < 0:
+                        ctr = max(ctr, conv_ops.f32_sk_plan(B * OH * OW, pc.cout, pc.Kpad, cfg, -ks)[0])
                 continue
             if ks != 1:
                 B, H, W, C, OH, OW, pc = self._conv_geom(i)
@@ -543,14 +545,20 @@ class SliceExecutor:
                     continue
                 bm, bn = conv_ops.F32_TILES[cfg]
                 tiles = math.ceil(M / bm) * math.ceil(N / bn)
-                for ks in (1, 2, 4, 8, 16):
-                    # split-K only where the tiles alone leave CUs idle
+                sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
+                for ks in (1, 2, 4, 8, 16) + sks:
+                    # split-K / stream-K only where the tiles alone leave CUs idle
                     if ks > 1 and (ktiles // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue
-                    ws = torch.empty(ks * M * N, dtype=torch.float32, device=self.device) if ks > 1 else None
+                    if ks < 0 and tiles >= 4 * conv_ops.NUM_CUS:
+                        continue
+                    nws = conv_ops.workspace_elems_f32(M, N, pc.Kpad, cfg, ks)
+                    ws = torch.empty(nws, dtype=torch.float32, device=self.device) if nws else None
+                    ctr = (torch.zeros(conv_ops.f32_sk_plan(M, N, pc.Kpad, cfg, -ks)[0], dtype=torch.int32,
+                                       device=self.device) if ks < 0 else None)
                     try:
                         t = self._time_graph(lambda: conv_ops.conv_forward_f32(x, pc, out, cfg=cfg, ksplit=ks,
-                                                                               workspace=ws), reps)
+                                                                               workspace=ws, counters=ctr), reps)
                     except (RuntimeError, ValueError):
                         continue
                     if best is None or t < best[0]:
@@ -841,17 +849,18 @@ class SliceExecutor:
     def _launch_f32(self, i: int, st: Step, b, stream, ws) -> None:
         """One step of the fp32 path (csrc/kernels/conv_f32.hip)."""
         k = st.kind
+        ctr = self._ctr_side if stream is not None and stream is self._side_stream else self._ctr
         if k == "conv":
             cfg, ks = self.cfg[i]
             res = b[st.ins[1]] if len(st.ins) > 1 else None
             conv_ops.conv_forward_f32(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
-                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream)
+                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr)
         elif k == "dense":
             cfg, ks = self.cfg[i]
             x = b[st.ins[0]].reshape(self.batch, -1)
             dst = self._logits[i] if st.p["softmax"] else b[st.out]
             conv_ops.conv_forward_f32(x, self.packed[i], dst, relu=st.p.get("relu", 0), cfg=cfg, ksplit=ks,
-                                      workspace=ws, stream=stream)
+                                      workspace=ws, stream=stream, counters=ctr)
             if st.p["softmax"]:
                 E.softmax_rows(dst, b[st.out], stream=stream)
         elif k == "stem_f32":

@@ -302,6 +302,9 @@ class DeviceLinkPool(LinkPool):
                 K.dev_free(ptr)
             raise
         mm[LINK_HDR:LINK_HDR + 16] = os.getpid().to_bytes(8, "little") + int(ptr).to_bytes(8, "little")
+        # exporter's device ordinal + 1 in the hand-off header (bytes 8..15; byte 0 is the flag):
+        # a receiver on another GPU enables peer access to it before opening the handle
+        mm[8:16] = (int(self.device.index or 0) + 1).to_bytes(8, "little")
         if len(handle) != IPC_HANDLE:
             raise RuntimeError(f"device link: IPC handle of {len(handle)} bytes, expected {IPC_HANDLE}")
         mm[LINK_HDR + 16:DEV_HDR] = handle
@@ -389,7 +392,8 @@ def dev_ptr(name: str) -> int:
                 a.dptr = int.from_bytes(bytes(a.mm[LINK_HDR + 8:LINK_HDR + 16]), "little")
             else:
                 from ..ops._lib import kernels
-                a.dptr = kernels().ipc_open(bytes(a.mm[LINK_HDR + 16:DEV_HDR]))
+                peer = int.from_bytes(bytes(a.mm[8:16]), "little") - 1
+                a.dptr = kernels().ipc_open(bytes(a.mm[LINK_HDR + 16:DEV_HDR]), peer)
                 a.ipc = True
         return a.dptr
 

@@ -184,12 +184,20 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_f32_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, int B, int H, int W, int Cin,
                                int OH, int OW, int N, int KH, int KW, int stride, int pad_t, int pad_l, int K,
-                               int Kpad, int relu, int ksplit, int cfg, u64 s) {
+                               int Kpad, int relu, int ksplit, int cfg, u64 s, u64 counters) {
     py::gil_scoped_release nogil;
     check(adapt::conv_f32_forward(P<const float>(x), P<const float>(w), P<const float>(bias), P<const float>(res),
                                   P<float>(out), P<float>(ws), B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
-                                  K, Kpad, relu, ksplit, cfg, S(s)),
+                                  K, Kpad, relu, ksplit, cfg, S(s), P<int>(counters)),
           "conv_f32_forward");
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("out"), py::arg("ws"), py::arg("B"),
+     py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("N"), py::arg("KH"),
+     py::arg("KW"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("K"), py::arg("Kpad"),
+     py::arg("relu"), py::arg("ksplit"), py::arg("cfg"), py::arg("s"), py::arg("counters") = 0);
+  m.def("conv_f32g_sk_plan", [](int tiles, int kt, int mult) {
+    int g = 0, it = 0;
+    adapt::conv_f32g_sk_plan(tiles, kt, mult, &g, &it);
+    return std::make_pair(g, it);
   });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,
                                int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s) {
@@ -226,14 +234,34 @@ PYBIND11_MODULE(_C, m) {
     check(hipIpcGetMemHandle(&h, (void*)(uintptr_t)p), "ipc_handle");
     return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
   });
-  m.def("ipc_open", [](py::bytes hb) {
+  // open a device link slot exported by another process; `peer` = the exporter's
+  // device ordinal (-1 unknown): when it differs from this thread's device, peer
+  // access to it is enabled explicitly first, so the copy out of the slot is a
+  // direct xGMI peer read rather than whatever the lazy mapping falls back to
+  m.def("ipc_open", [](py::bytes hb, int peer) {
     std::string b = hb;
     if (b.size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("ipc_open: bad handle size");
     hipIpcMemHandle_t h;
     std::memcpy(&h, b.data(), sizeof(h));
+    int cur = 0;
+    check(hipGetDevice(&cur), "ipc_open: hipGetDevice");
+    if (peer >= 0 && peer != cur) {
+      int can = 0;
+      check(hipDeviceCanAccessPeer(&can, cur, peer), "ipc_open: hipDeviceCanAccessPeer");
+      if (!can) throw std::runtime_error("ipc_open: device " + std::to_string(cur) + " cannot access peer " +
+                                         std::to_string(peer));
+      hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) check(e, "ipc_open: hipDeviceEnablePeerAccess");
+      (void)hipGetLastError();               // clear a sticky "already enabled"
+    }
     void* p = nullptr;
     check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "ipc_open");
     return (u64)(uintptr_t)p;
+  }, py::arg("handle"), py::arg("peer") = -1);
+  m.def("device_of", [](u64 p) {
+    hipPointerAttribute_t a;
+    check(hipPointerGetAttributes(&a, (const void*)(uintptr_t)p), "device_of");
+    return a.device;
   });
   m.def("ipc_close", [](u64 p) { check(hipIpcCloseMemHandle((void*)(uintptr_t)p), "ipc_close"); });
   m.def("memcpy_async", [](u64 dst, u64 src, size_t n, u64 st) {

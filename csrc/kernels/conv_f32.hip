@@ -264,14 +264,22 @@ hipError_t launch_f32(const ConvF32Params& p, bool pure, bool vec, hipStream_t s
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,
-                            hipStream_t s) {
+                            hipStream_t s, int* counters) {
   ConvF32Params p{x, w, bias, res, out, ws, B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
-                  B * OH * OW, K, Kpad, relu, ksplit < 1 ? 1 : ksplit};
+                  B * OH * OW, K, Kpad, relu, ksplit == 0 ? 1 : ksplit, counters, 0};
   if (Kpad % FBK || (p.ksplit > 1 && ws == nullptr)) return hipErrorInvalidValue;
+  if (p.ksplit < 0) {
+    // stream-K: v2 configs only
+    int bm, bn, g;
+    if (!conv_f32g_ok(cfg, Cin, N) || !conv_f32g_cfg_tile(cfg, &bm, &bn) || !ws || !counters)
+      return hipErrorInvalidValue;
+    conv_f32g_sk_plan(((p.M + bm - 1) / bm) * ((N + bn - 1) / bn), Kpad / FBK, -p.ksplit, &g, &p.sk_iters);
+  }
   const bool pure = KH == 1 && KW == 1 && stride == 1 && pad_t == 0 && pad_l == 0 && H == OH && W == OW &&
                     Cin % 4 == 0;
   const bool vec = Cin % 4 == 0;
   hipError_t e = hipErrorInvalidValue;
+  if (p.ksplit < 1 && cfg < 10) return hipErrorInvalidValue;
   switch (cfg) {
 #define X(id, BM_, BN_, WM_, WN_) case id: e = launch_f32<BM_, BN_, WM_, WN_>(p, pure, vec, s); break;
     ADAPT_F32_CFGS(X)

@@ -33,6 +33,7 @@
 namespace adapt {
 
 typedef __attribute__((address_space(3))) void lds_void_f32;
+void conv_f32g_sk_plan(int tiles, int kt, int mult, int* grid, int* iters);
 
 namespace {
 constexpr int GBK = 32;          // floats per K tile (one 128-byte LDS row)
@@ -51,9 +52,28 @@ struct F32gShape {
   static constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
 };
 
+// stream-K bookkeeping of one (tile, K-range) segment; slot < 0: whole K range
+struct F32Seg {
+  int slot;      // this segment's fp32 partial slot in p.ws
+  int nseg;      // segments covering the tile
+  int seg;       // this segment's index among them (summation order)
+  int g_first;   // first block covering the tile
+};
+
+__device__ __forceinline__ int f32_sk_slot(int g, int tile, int kt, int iters) {
+  // a block's first segment uses slot 2g, its last (when it started in an earlier tile) 2g+1
+  return 2 * g + ((long long)g * iters >= (long long)tile * kt ? 0 : 1);
+}
+
+constexpr int F32_CPOL_SC1 = 16;   // gfx950 cache policy: sc1 (write-through L2, bypass L1)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, int KG>
-__global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32Params p,
-                                                                         const float* __restrict__ zero) {
+__device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* __restrict__ zero, char* smem,
+                                          int tile, int kt0, int kt1, int split_idx, const F32Seg& sk) {
   using S = F32gShape<BM, BN, STAGES>;
   constexpr int NW = WM * WN;                 // compute waves per K-group
   constexpr int NWA = NW * KG;                // all waves (every wave issues pieces)
@@ -67,7 +87,6 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
   static_assert(A_INS * 8 * NWA == BM && B_INS * 8 * NWA == BN, "waves / tile split");
   static_assert(STAGES >= 2 && S::LDS_BYTES <= 160 * 1024, "stages");
   static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[S::LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -75,12 +94,8 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
   const int wsub = wave % NW;
   const int wm = wsub / WN, wn = wsub % WN;
 
-  const int tilesN = (p.N + BN - 1) / BN, tilesM = (p.M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tilesN = (p.N + BN - 1) / BN;
   const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
-  const int ktiles = p.Kpad / GBK;
-  const int kper = (ktiles + p.ksplit - 1) / p.ksplit;
-  const int kt0 = blockIdx.y * kper, kt1 = min(ktiles, kt0 + kper);
   const int nk = kt1 > kt0 ? kt1 - kt0 : 0;
 
   // ---- per-lane source bookkeeping (rows fixed over the K loop)
@@ -180,7 +195,7 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
   constexpr bool PRE = IT <= 8;
   const int ecc = tid % CPR, erow0 = tid / CPR;
   const int en = n0 + ecc * 4;
-  const bool use_pre = PRE && p.res != nullptr && p.ksplit == 1;
+  const bool use_pre = PRE && p.res != nullptr && p.ksplit == 1 && sk.slot < 0;
   f32x4 rpre[PRE ? IT : 1];
   if (use_pre) {
 #pragma unroll
@@ -263,9 +278,52 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
     }
     __syncthreads();
   }
+  if (sk.slot >= 0) {
+    // stream-K partial tile: publish it with 16-B sc1 stores, one lane counts the
+    // arrival; the tile's last segment adds every partial in segment order
+    // (deterministic) and runs the epilogue.  Nobody waits on anybody, so the
+    // grid never needs to be co-resident (MI355X_MICROARCH.md inter-workgroup
+    // visibility: sc1 stores drained, barrier, counter; sc1 loads on the reader).
+    const __amdgpu_buffer_rsrc_t wsr = f32_ws_rsrc(p.ws);
+    const int base = sk.slot * BM * BN;
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int row = erow0 + u * RPI;
+      if (row >= BM) continue;
+      const u32x4 v = __builtin_bit_cast(u32x4, *(const f32x4*)(epi + row * EPI_LD + ecc * 4));
+      __builtin_amdgcn_raw_buffer_store_b128(v, wsr, (base + row * BN + ecc * 4) * 4, 0, F32_CPOL_SC1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)(smem + S::LDS_BYTES);       // the 16 bytes past the ring / epilogue tile
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == sk.nseg - 1;
+      if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const int ktt = p.Kpad / GBK;
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int row = erow0 + u * RPI;
+      if (row >= BM) continue;
+      f32x4 acc4 = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int sg = 0; sg < sk.nseg; ++sg) {
+        if (sg == sk.seg) {
+          acc4 += *(const f32x4*)(epi + row * EPI_LD + ecc * 4);
+        } else {
+          const int off = (f32_sk_slot(sk.g_first + sg, tile, ktt, p.sk_iters) * BM * BN + row * BN + ecc * 4) * 4;
+          acc4 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wsr, off, 0, F32_CPOL_SC1));
+        }
+      }
+      *(f32x4*)(epi + row * EPI_LD + ecc * 4) = acc4;           // each thread re-reads only its own chunks
+    }
+  }
   if (en >= p.N) return;
   if (p.ksplit > 1) {
-    float* slab = p.ws + (size_t)blockIdx.y * p.M * p.N;
+    float* slab = p.ws + (size_t)split_idx * p.M * p.N;
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
       const int row = erow0 + u * RPI, m = m0 + row;
@@ -300,6 +358,45 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
   }
 }
 
+// One launch = (a) data-parallel tiles x split-K slices (p.ksplit >= 1), or (b)
+// stream-K (p.ksplit < 0): the tiles x K-tiles iteration space is cut into equal
+// contiguous ranges of p.sk_iters, one per block (256 x -ksplit blocks), so a
+// ~200-tile layer keeps every CU busy instead of leaving a quarter of the chip
+// idle: at 1/16 of the bf16 rate every fp32 conv is matrix-bound, and the
+// partial-tile traffic is small beside its MFMA time.
+template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, int KG>
+__global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32Params p,
+                                                                         const float* __restrict__ zero) {
+  using S = F32gShape<BM, BN, STAGES>;
+  __shared__ __attribute__((aligned(16))) char smem[S::LDS_BYTES + 16];
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int kt = p.Kpad / GBK;
+  if (p.ksplit >= 1) {
+    const int tile = xcd_remap(blockIdx.x, tiles);
+    const int kper = (kt + p.ksplit - 1) / p.ksplit;
+    const int kt0 = blockIdx.y * kper, kt1 = min(kt, kt0 + kper);
+    f32g_tile<BM, BN, WM, WN, STAGES, PURE, KG>(p, zero, smem, tile, kt0, kt1, blockIdx.y, F32Seg{-1, 1, 0, 0});
+    return;
+  }
+  const int g = blockIdx.x, iters = p.sk_iters;
+  const int total = tiles * kt;
+  int it = g * iters;
+  const int it_end = min(total, it + iters);
+  while (it < it_end) {
+    const int tile = it / kt;
+    const int kbeg = it - tile * kt;
+    const int kend = min(kt, kbeg + (it_end - it));
+    F32Seg sk{-1, 1, 0, 0};
+    if (kbeg != 0 || kend != kt) {
+      const int g_first = (tile * kt) / iters, g_last = ((tile + 1) * kt - 1) / iters;
+      sk = F32Seg{f32_sk_slot(g, tile, kt, iters), g_last - g_first + 1, g - g_first, g_first};
+    }
+    f32g_tile<BM, BN, WM, WN, STAGES, PURE, KG>(p, zero, smem, tile, kbeg, kend, 0, sk);
+    it += kend - kbeg;
+    __syncthreads();   // the next segment's DMA reuses the epilogue's LDS
+  }
+}
+
 // 16-byte aligned zero page that out-of-range lanes fetch from
 __device__ __attribute__((aligned(64))) float g_zero_page_f32[64];
 
@@ -312,12 +409,29 @@ hipError_t launch_f32g(const ConvF32Params& p, bool pure, hipStream_t s) {
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   dim3 grid(tiles, p.ksplit), block(WM * WN * KG * 64);
+  if (p.ksplit < 0) {
+    int g, iters;
+    conv_f32g_sk_plan(tiles, p.Kpad / GBK, -p.ksplit, &g, &iters);
+    if (!p.counters || !p.ws || iters != p.sk_iters) return hipErrorInvalidValue;
+    grid = dim3(g, 1);
+  }
   if (pure) hipLaunchKernelGGL((conv_f32g_kernel<BM, BN, WM, WN, STAGES, true, KG>), grid, block, 0, s, p, zero);
   else hipLaunchKernelGGL((conv_f32g_kernel<BM, BN, WM, WN, STAGES, false, KG>), grid, block, 0, s, p, zero);
   return hipGetLastError();
 }
 
 }  // namespace
+
+// stream-K grid of the v2 fp32 kernels: `mult` x 256 blocks, each taking ceil(total / G)
+// consecutive (tile, K-tile) iterations
+void conv_f32g_sk_plan(int tiles, int kt, int mult, int* grid, int* iters) {
+  const long long total = (long long)tiles * kt;
+  long long G = 256LL * (mult > 0 ? mult : 1);
+  if (G > total) G = total;
+  const long long it = (total + G - 1) / G;
+  *iters = (int)it;
+  *grid = (int)((total + it - 1) / it);
+}
 
 // v2 fp32 tile configs: id -> BM, BN, WM, WN, STAGES, KG (ops/conv.py F32_TILES mirrors the tile sizes)
 #define ADAPT_F32G_CFGS(X)         \
@@ -332,7 +446,7 @@ hipError_t launch_f32g(const ConvF32Params& p, bool pure, hipStream_t s) {
   X(18, 64, 64, 2, 2, 4, 2)        \
   X(19, 128, 64, 2, 2, 4, 2)       \
   X(20, 64, 128, 2, 2, 4, 2)       \
-  X(21, 256, 64, 4, 2, 4, 1)
+  X(21, 256, 64, 4, 2, 3, 1)
 
 // cfg in the v2 family and the problem on its path (tap-major walk: Cin % 32 == 0; 16-byte output
 // chunks: N % 4 == 0)
@@ -340,6 +454,15 @@ bool conv_f32g_ok(int cfg, int Cin, int N) {
   if (Cin % GBK || N % 4) return false;
   switch (cfg) {
 #define X(id, BM_, BN_, WM_, WN_, S_, KG_) case id: return true;
+    ADAPT_F32G_CFGS(X)
+#undef X
+  }
+  return false;
+}
+
+bool conv_f32g_cfg_tile(int cfg, int* bm, int* bn) {
+  switch (cfg) {
+#define X(id, BM_, BN_, WM_, WN_, S_, KG_) case id: *bm = BM_; *bn = BN_; return true;
     ADAPT_F32G_CFGS(X)
 #undef X
   }

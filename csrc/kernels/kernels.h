@@ -111,8 +111,12 @@ struct ConvF32Params {
   int KH, KW, stride, pad_t, pad_l;
   int M, K, Kpad;
   int relu;
-  int ksplit;
+  int ksplit;       // >= 1: split-K slabs + reduce; < 0 (v2 configs): stream-K over -ksplit x 256 blocks
+  int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
+  int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_f32g_sk_plan)
 };
+void conv_f32g_sk_plan(int tiles, int kt, int mult, int* grid, int* iters);
+bool conv_f32g_cfg_tile(int cfg, int* bm, int* bn);
 // fp32 stem (stem_f32.hip): 7x7/s2 conv (+BN, ReLU) + 3x3/s2 max-pool, weights [64][176] fp32
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                             int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s);
@@ -122,7 +126,7 @@ hipError_t conv_f32g_launch(const ConvF32Params& p, int cfg, bool pure, hipStrea
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,
-                            hipStream_t s);
+                            hipStream_t s, int* counters = nullptr);
 hipError_t maxpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
                        int pad_l, int pad_zero, hipStream_t s);
 hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);

@@ -125,7 +125,9 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
     const int nr = first ? 3 : 2;
     // the next step's 4 input rows, in flight during this step's MFMAs
     const bool more = t + 1 < t1;
-    const int nxt_lo = 2 * (2 * (t + 1) - pool_pad + 1) - pad_t + 3;   // rows 4(t+1)-... not yet staged
+    // step t+1 computes conv rows ra' = 2(t+1) - pp + 1 and ra' + 1, which need input rows
+    // 2ra' - pad_t .. 2ra' - pad_t + 8; rows up to 2ra' - pad_t + 4 are staged already
+    const int nxt_lo = 2 * (2 * (t + 1) - pool_pad + 1) - pad_t + 5;
     f32x4 pv[MAXC];
     if (more) get_rows(pv, nxt_lo, 4);
     const int units = nr * tpr;                                 // pixel tiles this step (x 4 channel tiles)

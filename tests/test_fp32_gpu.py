@@ -44,8 +44,9 @@ SHAPES = [  # (B, H, W, Cin, Cout, k, stride, pad, residual, relu)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("ksplit", [1, 4])
+@pytest.mark.parametrize("ksplit", [1, 4, -1, -2])
 def test_conv_f32_matches_fp64(shape, ksplit):
+    """Every fp32 tile config; ksplit > 1 split-K slabs, ksplit < 0 stream-K (v2 configs)."""
     B, H, W, Cin, Cout, k, s, pad, has_res, relu = shape
     rng = np.random.default_rng(hash(shape) % 2**32)
     x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
@@ -58,12 +59,20 @@ def test_conv_f32_matches_fp64(shape, ksplit):
     want = _ref_conv(x, kern, bias, s, pads, res, relu)
     pc = C.pack_conv_f32(kern, bias, s, pads, "cuda")
     out = torch.empty((B, OH, OW, Cout), dtype=torch.float32, device="cuda")
+    M = B * OH * OW
     for cfg in C.F32_TILES:
-        if not C.f32_cfg_supported(cfg, Cin, Cout):
+        if not C.f32_cfg_supported(cfg, Cin, Cout) or (ksplit < 0 and cfg not in C.F32G_CFGS):
             continue
+        ctr = None
+        if ksplit < 0:
+            ctr = torch.zeros(C.f32_sk_plan(M, Cout, pc.Kpad, cfg, -ksplit)[0], dtype=torch.int32, device="cuda")
         out.fill_(float("nan"))
-        C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out, None if res is None else torch.from_numpy(res).cuda(),
-                           relu=relu, cfg=cfg, ksplit=ksplit)
+        for _rep in range(2 if ksplit < 0 else 1):       # stream-K counters must come back zeroed
+            C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out,
+                               None if res is None else torch.from_numpy(res).cuda(),
+                               relu=relu, cfg=cfg, ksplit=ksplit, counters=ctr)
+        if ctr is not None:
+            assert int(ctr.abs().sum()) == 0, f"cfg {cfg}: stream-K counters not reset"
         got = out.cpu().numpy()
         err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
         assert err < 2e-5, f"cfg {cfg} ksplit {ksplit}: rel err {err}"

@@ -11,6 +11,7 @@
 #   rehearse  bench.py --gpus 2 --backend gloo (the multi-GPU record, ranks sharing one GPU)
 #   prof      rocprofv3 kernel trace + stats of the fp32 and bf16 benches
 #   fp32t     the fp32 kernel / model tests only
+#   models    model numerics + multi-GPU link twins + DEFER GPU tests
 #   peak      fp32 MFMA ceiling under full load (tools/mfma_f32_peak.hip, prebuilt .bin)
 #   tune32    fp32 conv autotune of ResNet-50 bs=32 (entries to gpurun_out/<outdir>/tune_f32.json)
 #   fault     4-stage SIGKILL recovery bench (device links)
@@ -35,6 +36,7 @@ for p in "${P[@]}"; do
     prof)     steps+=("240|$out/prof_fp32|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_fp32 -o run -- python3 bench.py --no-bf16 --steps 30 --warmup 5")
               steps+=("240|$out/prof_bf16|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_bf16 -o run -- python3 bench.py --dtype bf16 --steps 50 --warmup 10") ;;
     fp32t)    steps+=("400|$out/pytest_fp32|python -u -m pytest tests/test_fp32_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread") ;;
+    models)   steps+=("600|$out/pytest_models|python -u -m pytest tests/test_model_gpu.py tests/test_multigpu_links.py tests/test_defer_gpu.py -m gpu -v --timeout 300 --timeout-method thread") ;;
     peak)     steps+=("60|$out/mfma_f32_peak|./tools/mfma_f32_peak.bin") ;;
     tune32)   steps+=("600|$out/tune_f32|python -u tools/tune_f32.py --models resnet50 --batch 32 --out gpurun_out/$out/tune_f32.json") ;;
     fault)    steps+=("300|$out/fault4_dev|python -u tools/fault_bench.py --workers 4 --device cuda:0 --model resnet50 --image 224 --batch 32 --duration 25 --kill-at 10 --links dev --inflight 8 --json gpurun_out/$out/fault_r50_4w_dev.json") ;;
