@@ -67,6 +67,8 @@ def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
         return pure and pw_supported(pc)
     if cfg in RR3_CFGS:
         return rr3_supported(pc)
+    if cfg in CS3_CFGS:
+        return cs3_supported(pc)
     if cfg in V1_CFGS:
         return True
     if cfg in HALO_PATCH:
@@ -226,6 +228,11 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
         if ksplit != 1 or ns or out_f32 or residual is not None or (H, W) != (28, 28) or OH != H or OW != W:
             raise ValueError(f"3x3 config {cfg}: 28x28 stride-1 bf16 output, no residual / split-K")
         rr3_forward(x, pc, out.view(x.shape[0], OH, OW, N), relu=int(relu), kg=RR3_CFGS[cfg], stream=stream)
+        return out
+    if cfg in CS3_CFGS:                    # channel-split register-resident 3x3 (conv3x3_cs.hip)
+        if ksplit != 1 or ns or out_f32 or residual is not None or OH != H or OW != W:
+            raise ValueError(f"3x3 config {cfg}: stride-1 bf16 output, no residual / split-K")
+        cs3_forward(x, pc, out.view(x.shape[0], OH, OW, N), relu=int(relu), stream=stream)
         return out
     if cfg in PW_CFGS:                     # persistent pointwise kernel (pw_wide.hip)
         if ksplit != 1 or ns or out_f32 or OH != H or OW != W:
@@ -550,6 +557,32 @@ def rr3_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, relu: int 
             raise ValueError("rr3 conv: contiguous bf16 NHWC tensors")
     kernels().conv3x3_rr_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(out), int(x.shape[0]), 28, 28,
                                  128, int(relu), int(kg), stream_handle(stream))
+    return out
+
+
+# channel-split register-resident 3x3 (conv3x3_cs.hip): a block holds a 64- (stage 4) or
+# 32-channel (stage 5) slice of the filter in VGPRs and walks pixel tiles staged in LDS
+CS3_CFGS = {73: 0}
+CS3_SHAPES = {(256, 14, 14), (512, 7, 7)}       # (C, H, W): ResNet stages 4 and 5
+
+
+def cs3_supported(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (3, 3, 1, 1, 1, 1, 1)
+            and pc.cin == pc.cout and pc.cin in (256, 512) and pc.Kpad == 9 * pc.cin and not pc.n_split)
+
+
+def cs3_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, relu: int = 1, stream=None) -> torch.Tensor:
+    if not cs3_supported(pc):
+        raise ValueError("cs3 conv: needs a 3x3 / s1 / p1 conv 256 -> 256 or 512 -> 512")
+    if x.dim() != 4 or (x.shape[3], x.shape[1], x.shape[2]) not in CS3_SHAPES or x.shape[3] != pc.cin \
+            or tuple(out.shape) != tuple(x.shape):
+        raise ValueError(f"cs3 conv: x {tuple(x.shape)} out {tuple(out.shape)} (needs B x 14 x 14 x 256 or B x 7 x 7 x 512)")
+    for t in (x, out):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise ValueError("cs3 conv: contiguous bf16 NHWC tensors")
+    B, H, W, C = (int(v) for v in x.shape)
+    kernels().conv3x3_cs_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(out), B, H, W, C, int(relu),
+                                 stream_handle(stream))
     return out
 
 

@@ -338,6 +338,11 @@ PYBIND11_MODULE(_C, m) {
     adapt::Conv3x3RRParams p{P<const bf16>(x), P<const bf16>(wfrag), P<const float>(bias), P<bf16>(out), B, relu};
     check(adapt::conv3x3_rr_forward(p, C, H, W, kg, S(s)), "conv3x3_rr_forward");
   });
+  m.def("conv3x3_cs_forward", [](u64 x, u64 wfrag, u64 bias, u64 out, int B, int H, int W, int C, int relu, u64 s) {
+    adapt::Conv3x3RRParams p{P<const bf16>(x), P<const bf16>(wfrag), P<const float>(bias), P<bf16>(out), B, relu};
+    check(adapt::conv3x3_cs_forward(p, C, H, W, S(s)), "conv3x3_cs_forward");
+  });
+  m.def("conv3x3_cs_supported", [](int C, int H, int W) { return adapt::conv3x3_cs_supported(C, H, W); });
   m.def("pw_pair_supported", [](int cin, int co, int cm, int bm) { return adapt::pw_pair_supported(cin, co, cm, bm); });
   m.def("ingest_u8", [](u64 x, u64 y, size_t n, int C, int reverse, std::vector<float> scale,
                         std::vector<float> shift, u64 s) {

@@ -191,6 +191,9 @@ struct Conv3x3RRParams {
 };
 bool conv3x3_rr_supported(int C, int H, int W);
 hipError_t conv3x3_rr_forward(const Conv3x3RRParams& p, int C, int H, int W, int kg, hipStream_t s);
+// channel-split register-resident 3x3 (conv3x3_cs.hip): stage 4 (256, 14x14) and stage 5 (512, 7x7)
+bool conv3x3_cs_supported(int C, int H, int W);
+hipError_t conv3x3_cs_forward(const Conv3x3RRParams& p, int C, int H, int W, hipStream_t s);
 hipError_t pw_pair_forward(const PwPairParams& p, int cin, int co, int cm, int bm, hipStream_t s);
 // persistent pointwise conv, weights register-resident per wave (pw_wide.hip):
 // out[m][n] = act(x[m] . W[n] + bias[n] (+ res[m][n])), x [M][K], W in MFMA fragment order

@@ -15,6 +15,9 @@
 #   peak      fp32 MFMA ceiling under full load (tools/mfma_f32_peak.hip, prebuilt .bin)
 #   tune32    fp32 conv autotune of ResNet-50 bs=32 (entries to gpurun_out/<outdir>/tune_f32.json)
 #   fault     4-stage SIGKILL recovery bench (device links)
+#   pmc32     two rocprofv3 PMC passes over the fp32 bench (tools/pmc_summary.py reads them)
+#   hang      4-stage wedged-stage (alive, no progress) recovery bench (device links)
+#   cs3       channel-split 3x3 (stage 4/5) numerics, isolated timings vs the tile kernels, whole-model A/B
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -39,7 +42,12 @@ for p in "${P[@]}"; do
     models)   steps+=("600|$out/pytest_models|python -u -m pytest tests/test_model_gpu.py tests/test_multigpu_links.py tests/test_defer_gpu.py -m gpu -v --timeout 300 --timeout-method thread") ;;
     peak)     steps+=("60|$out/mfma_f32_peak|./tools/mfma_f32_peak.bin") ;;
     tune32)   steps+=("600|$out/tune_f32|python -u tools/tune_f32.py --models resnet50 --batch 32 --out gpurun_out/$out/tune_f32.json") ;;
+    pmc32)    steps+=("500|$out/pmc32|bash tools/pmc_run.sh gpurun_out/$out/pmc32 bench.py --no-bf16 --steps 2 --warmup 1") ;;
+    hang)     steps+=("300|$out/hang4_dev|python -u tools/fault_bench.py --workers 4 --device cuda:0 --model resnet50 --image 224 --batch 32 --duration 25 --kill-at 10 --links dev --inflight 8 --fault hang --json gpurun_out/$out/hang_r50_4w_dev.json") ;;
     fault)    steps+=("300|$out/fault4_dev|python -u tools/fault_bench.py --workers 4 --device cuda:0 --model resnet50 --image 224 --batch 32 --duration 25 --kill-at 10 --links dev --inflight 8 --json gpurun_out/$out/fault_r50_4w_dev.json") ;;
+    cs3)      steps+=("300|$out/pytest_cs3|python -u -m pytest tests/test_cs3_gpu.py tests/test_rr3_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread")
+              steps+=("240|$out/cs3_bench|python -u tools/conv_bench.py --shape 32,14,14,256,256,3,1,1 --shape 32,7,7,512,512,3,1,1 --only 73,0,1,2,3,4,5,6,7,8,9 --ks 1,2,4,-1")
+              steps+=("240|$out/cs3_ab|python -u tools/ab_cfg.py --model resnet50 --set 32x14x14x256,3x3s1p1111@73@1 --set 32x7x7x512,3x3s1p1111@73@1 --json gpurun_out/$out/cs3_ab.json") ;;
     *) echo "unknown preset $p"; exit 2 ;;
   esac
 done
