@@ -133,7 +133,7 @@ class DEFER:
     def __init__(self, computeNodes: Optional[Sequence[str]] = None, *, membership: Optional[Tuple[str, int]] = None,
                  membership_port: int = 2379, result_port: int = RESULT_PORT, chunk_size: int = 512 * 1000,
                  batch: int = 1, codec: str = "none", weight_codec: str = "zfp+lz4", max_inflight: int = 8,
-                 task_timeout: float = 30.0, worker_wait: float = 5.0, elastic: bool = False,
+                 task_timeout: float = 10.0, worker_wait: float = 5.0, elastic: bool = False,
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
                  transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,

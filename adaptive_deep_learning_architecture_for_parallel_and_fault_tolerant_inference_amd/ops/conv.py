@@ -370,13 +370,16 @@ def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pa
 # ------------------------------------------------------------------ fp32 path
 # The reference's precision (Keras float32, `src/node.py:177`): conv / GEMM on
 # the fp32 matrix cores.  Tiles (BM, BN) per cfg id: 0-5 mirror ADAPT_F32_CFGS
-# (csrc/kernels/conv_f32.hip, register-staged, any Cin), 10-21 ADAPT_F32G_CFGS
+# (csrc/kernels/conv_f32.hip, register-staged, any Cin), 10-41 ADAPT_F32G_CFGS
 # (csrc/kernels/conv_f32g.hip, LDS-DMA ring, Cin % 32 == 0); K tiles are 32 floats.
 F32_BK = 32
 F32_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (256, 64), 5: (64, 256),
              10: (128, 128), 11: (128, 128), 12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (256, 128),
              16: (128, 256), 17: (128, 128), 18: (64, 64), 19: (128, 64), 20: (64, 128), 21: (256, 64)}
-F32G_CFGS = frozenset(range(10, 22))
+# 30-41: the software-pipelined twins of 10-21 (next tile's fragments read between the two
+# MFMA halves of the current one); 35 / 36 would spill and do not exist
+F32_TILES.update({c + 20: F32_TILES[c] for c in range(10, 22) if c not in (15, 16)})
+F32G_CFGS = frozenset(list(range(10, 22)) + [c + 20 for c in range(10, 22) if c not in (15, 16)])
 
 
 def f32_sk_plan(M: int, N: int, Kpad: int, cfg: int, mult: int = 1):

@@ -51,7 +51,7 @@ def make_store_server(host: str = "0.0.0.0", port: int = 0) -> dist.TCPStore:
 class EpochGroup:
     def __init__(self, backend: str, store_host: str, store_port: int, epoch: int, rank: int, world: int,
                  device: Optional[torch.device] = None, timeout_s: float = 30.0, ctl: bool = False,
-                 stall_s: float = 10.0, op_timeout_s: float = 7 * 86400.0):
+                 stall_s: float = 5.0, op_timeout_s: float = 7 * 86400.0):
         self.backend = backend
         self.rank, self.world, self.epoch = rank, world, epoch
         self.device = device

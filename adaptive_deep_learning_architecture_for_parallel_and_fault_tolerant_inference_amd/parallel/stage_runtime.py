@@ -257,7 +257,7 @@ class CollectiveStageRuntime:
         try:
             self.group = EpochGroup(cc["backend"], cc["store_host"], int(cc["store_port"]), self.epoch, self.stage,
                                     self.stages, self.dev if self.gpu else None, float(cc.get("timeout", 30)),
-                                    ctl=self.link_codec != "none", stall_s=float(cc.get("stall_s", 10.0)))
+                                    ctl=self.link_codec != "none", stall_s=float(cc.get("stall_s", 5.0)))
             self._handshake(self.group)
         except Exception as e:  # noqa: BLE001 - rendezvous failed (a member died): epoch is dead
             self._fail("rendezvous", e)

@@ -47,7 +47,7 @@ class AdaptConfig:
     lease_ttl: float = 1.0
     # flow control / fault handling
     max_inflight: int = 8
-    task_timeout: float = 30.0
+    task_timeout: float = 10.0
     worker_wait: float = 5.0
     ordered: bool = False
     # worker

@@ -30,6 +30,8 @@
 //   residual (prefetched before the K loop when it fits the registers), ReLU.
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace adapt {
 
 typedef __attribute__((address_space(3))) void lds_void_f32;
@@ -71,7 +73,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_ws_rsrc(const float* base)
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, int KG>
+template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, int KG, bool PIPE>
 __device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* __restrict__ zero, char* smem,
                                           int tile, int kt0, int kt1, int split_idx, const F32Seg& sk) {
   using S = F32gShape<BM, BN, STAGES>;
@@ -86,7 +88,7 @@ __device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* _
   constexpr int TILE_A = BM * 128, STAGE_BYTES = S::STAGE_BYTES, EPI_LD = S::EPI_LD;
   static_assert(A_INS * 8 * NWA == BM && B_INS * 8 * NWA == BN, "waves / tile split");
   static_assert(STAGES >= 2 && S::LDS_BYTES <= 160 * 1024, "stages");
-  static_assert((STAGES - 2) * LPW <= 63, "vmcnt range");
+  static_assert((STAGES - (PIPE ? 1 : 2)) * LPW <= 63, "vmcnt range");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -206,18 +208,10 @@ __device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* _
     }
   }
 
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) issue(s);
-
-  for (int t = 0; t < nk; ++t) {
-    fwait_vm<(STAGES - 2) * LPW>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int nslot = (t + STAGES - 1) % STAGES;
-    const char* sa = smem + (t % STAGES) * STAGE_BYTES;
+  constexpr int MT = NH * 4 * FM * FN;         // MFMAs per wave per K tile
+  auto read_frags = [&](int slot, f32x4 (&af)[NH][FM], f32x4 (&bfr)[NH][FN]) {
+    const char* sa = smem + slot * STAGE_BYTES;
     const char* sb = sa + TILE_A;
-    f32x4 af[NH][FM], bfr[NH][FN];
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int kq = (h + kg) * 4 + fq;       // this lane's 16-byte chunk of half h + kg
@@ -226,26 +220,82 @@ __device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* _
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[h][j] = *(const f32x4*)(sb + fswz2(wn * TN + j * 16 + fr, kq));
     }
-    issue(nslot);
+  };
+  // MFMA steps [S0, S1) of the NH * 4 (half, k) steps of one K tile
+  auto mfma_steps = [&](const f32x4 (&af)[NH][FM], const f32x4 (&bfr)[NH][FN], auto s0c, auto s1c) {
+    constexpr int S0 = decltype(s0c)::value, S1 = decltype(s1c)::value;
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+    for (int st = S0; st < S1; ++st)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[st / 4][i][st % 4], bfr[st / 4][j][st % 4], acc[i][j],
+                                                           0, 0, 0);
+  };
+
+  if constexpr (!PIPE) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[h][i][s], bfr[h][j][s], acc[i][j], 0, 0, 0);
-    // LDS-DMA pieces of tile t+STAGES-1 spread between this tile's MFMAs
-    constexpr int MT = NH * 4 * FM * FN;
-    constexpr int MPP = MT / LPW > 0 ? MT / LPW : 1;
-    __builtin_amdgcn_sched_group_barrier(0x100, NH * (FM + FN), 0);   // ds_read
+    for (int s = 0; s < STAGES - 1; ++s) issue(s);
+
+    for (int t = 0; t < nk; ++t) {
+      fwait_vm<(STAGES - 2) * LPW>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int nslot = (t + STAGES - 1) % STAGES;
+      f32x4 af[NH][FM], bfr[NH][FN];
+      read_frags(t % STAGES, af, bfr);
+      issue(nslot);
+      mfma_steps(af, bfr, std::integral_constant<int, 0>{}, std::integral_constant<int, NH * 4>{});
+      // LDS-DMA pieces of tile t+STAGES-1 spread between this tile's MFMAs
+      constexpr int MPP = MT / LPW > 0 ? MT / LPW : 1;
+      __builtin_amdgcn_sched_group_barrier(0x100, NH * (FM + FN), 0);   // ds_read
 #pragma unroll
-    for (int q = 0; q < LPW; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, MPP, 0);            // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);              // VMEM (LDS-DMA piece)
+      for (int q = 0; q < LPW; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MPP, 0);            // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);              // VMEM (LDS-DMA piece)
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, MT, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, MT, 0);
+  } else {
+    // Software-pipelined: the fragments of tile t+1 are read from LDS (and tile
+    // t+STAGES is put in flight) between the two halves of tile t's MFMAs, so
+    // the matrix pipe never waits out a barrier + ds_read round trip.  Slot
+    // t % STAGES is refilled right after the mid-tile barrier of tile t: every
+    // wave has its tile-t fragments in registers by then (lgkmcnt(0)).
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s) issue(s);
+    fwait_vm<(STAGES - 1) * LPW>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    f32x4 fa0[NH][FM], fb0[NH][FN], fa1[NH][FM], fb1[NH][FN];
+    read_frags(0, fa0, fb0);
+    constexpr int HALF = NH * 2;
+    constexpr int MH = MT / 2;
+    constexpr int MPP = MH / LPW > 0 ? MH / LPW : 1;
+    auto step = [&](int t, const f32x4 (&ca)[NH][FM], const f32x4 (&cb)[NH][FN], f32x4 (&na)[NH][FM],
+                    f32x4 (&nb)[NH][FN]) {
+      mfma_steps(ca, cb, std::integral_constant<int, 0>{}, std::integral_constant<int, HALF>{});
+      fwait_vm<(STAGES - 2) * LPW>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read_frags((t + 1) % STAGES, na, nb);
+      issue(t % STAGES);
+      mfma_steps(ca, cb, std::integral_constant<int, HALF>{}, std::integral_constant<int, NH * 4>{});
+      __builtin_amdgcn_sched_group_barrier(0x100, NH * (FM + FN), 0);   // ds_read (next tile)
+#pragma unroll
+      for (int q = 0; q < LPW; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MPP, 0);            // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);              // VMEM (LDS-DMA piece)
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, MH, 0);
+    };
+    for (int t = 0; t < nk; t += 2) {
+      step(t, fa0, fb0, fa1, fb1);
+      if (t + 1 < nk) step(t + 1, fa1, fb1, fa0, fb0);
+    }
   }
   fwait_vm<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -364,7 +414,7 @@ __device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* _
 // ~200-tile layer keeps every CU busy instead of leaving a quarter of the chip
 // idle: at 1/16 of the bf16 rate every fp32 conv is matrix-bound, and the
 // partial-tile traffic is small beside its MFMA time.
-template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, int KG>
+template <int BM, int BN, int WM, int WN, int STAGES, bool PURE, int KG, bool PIPE>
 __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32Params p,
                                                                          const float* __restrict__ zero) {
   using S = F32gShape<BM, BN, STAGES>;
@@ -375,7 +425,7 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
     const int tile = xcd_remap(blockIdx.x, tiles);
     const int kper = (kt + p.ksplit - 1) / p.ksplit;
     const int kt0 = blockIdx.y * kper, kt1 = min(kt, kt0 + kper);
-    f32g_tile<BM, BN, WM, WN, STAGES, PURE, KG>(p, zero, smem, tile, kt0, kt1, blockIdx.y, F32Seg{-1, 1, 0, 0});
+    f32g_tile<BM, BN, WM, WN, STAGES, PURE, KG, PIPE>(p, zero, smem, tile, kt0, kt1, blockIdx.y, F32Seg{-1, 1, 0, 0});
     return;
   }
   const int g = blockIdx.x, iters = p.sk_iters;
@@ -391,7 +441,7 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
       const int g_first = (tile * kt) / iters, g_last = ((tile + 1) * kt - 1) / iters;
       sk = F32Seg{f32_sk_slot(g, tile, kt, iters), g_last - g_first + 1, g - g_first, g_first};
     }
-    f32g_tile<BM, BN, WM, WN, STAGES, PURE, KG>(p, zero, smem, tile, kbeg, kend, 0, sk);
+    f32g_tile<BM, BN, WM, WN, STAGES, PURE, KG, PIPE>(p, zero, smem, tile, kbeg, kend, 0, sk);
     it += kend - kbeg;
     __syncthreads();   // the next segment's DMA reuses the epilogue's LDS
   }
@@ -400,7 +450,7 @@ __global__ __launch_bounds__(WM * WN * KG * 64, 1) void conv_f32g_kernel(ConvF32
 // 16-byte aligned zero page that out-of-range lanes fetch from
 __device__ __attribute__((aligned(64))) float g_zero_page_f32[64];
 
-template <int BM, int BN, int WM, int WN, int STAGES, int KG>
+template <int BM, int BN, int WM, int WN, int STAGES, int KG, bool PIPE>
 hipError_t launch_f32g(const ConvF32Params& p, bool pure, hipStream_t s) {
   static float* zero = nullptr;
   if (!zero) {
@@ -415,8 +465,8 @@ hipError_t launch_f32g(const ConvF32Params& p, bool pure, hipStream_t s) {
     if (!p.counters || !p.ws || iters != p.sk_iters) return hipErrorInvalidValue;
     grid = dim3(g, 1);
   }
-  if (pure) hipLaunchKernelGGL((conv_f32g_kernel<BM, BN, WM, WN, STAGES, true, KG>), grid, block, 0, s, p, zero);
-  else hipLaunchKernelGGL((conv_f32g_kernel<BM, BN, WM, WN, STAGES, false, KG>), grid, block, 0, s, p, zero);
+  if (pure) hipLaunchKernelGGL((conv_f32g_kernel<BM, BN, WM, WN, STAGES, true, KG, PIPE>), grid, block, 0, s, p, zero);
+  else hipLaunchKernelGGL((conv_f32g_kernel<BM, BN, WM, WN, STAGES, false, KG, PIPE>), grid, block, 0, s, p, zero);
   return hipGetLastError();
 }
 
@@ -433,27 +483,39 @@ void conv_f32g_sk_plan(int tiles, int kt, int mult, int* grid, int* iters) {
   *grid = (int)((total + it - 1) / it);
 }
 
-// v2 fp32 tile configs: id -> BM, BN, WM, WN, STAGES, KG (ops/conv.py F32_TILES mirrors the tile sizes)
-#define ADAPT_F32G_CFGS(X)         \
-  X(10, 128, 128, 2, 2, 4, 1)      \
-  X(11, 128, 128, 2, 2, 3, 2)      \
-  X(12, 128, 64, 2, 2, 4, 1)       \
-  X(13, 64, 128, 2, 2, 4, 1)       \
-  X(14, 64, 64, 2, 2, 4, 1)        \
-  X(15, 256, 128, 4, 2, 3, 1)      \
-  X(16, 128, 256, 2, 4, 3, 1)      \
-  X(17, 128, 128, 4, 2, 4, 1)      \
-  X(18, 64, 64, 2, 2, 4, 2)        \
-  X(19, 128, 64, 2, 2, 4, 2)       \
-  X(20, 64, 128, 2, 2, 4, 2)       \
-  X(21, 256, 64, 4, 2, 3, 1)
+// v2 fp32 tile configs: id -> BM, BN, WM, WN, STAGES, KG, PIPE (ops/conv.py F32_TILES mirrors the
+// tile sizes); 30-41 are the software-pipelined twins of 10-21 (no 35 / 36: their two fragment sets
+// spill at 256 x 128 / 128 x 256)
+#define ADAPT_F32G_CFGS(X)            \
+  X(10, 128, 128, 2, 2, 4, 1, false)  \
+  X(11, 128, 128, 2, 2, 3, 2, false)  \
+  X(12, 128, 64, 2, 2, 4, 1, false)   \
+  X(13, 64, 128, 2, 2, 4, 1, false)   \
+  X(14, 64, 64, 2, 2, 4, 1, false)    \
+  X(15, 256, 128, 4, 2, 3, 1, false)  \
+  X(16, 128, 256, 2, 4, 3, 1, false)  \
+  X(17, 128, 128, 4, 2, 4, 1, false)  \
+  X(18, 64, 64, 2, 2, 4, 2, false)    \
+  X(19, 128, 64, 2, 2, 4, 2, false)   \
+  X(20, 64, 128, 2, 2, 4, 2, false)   \
+  X(21, 256, 64, 4, 2, 3, 1, false)   \
+  X(30, 128, 128, 2, 2, 4, 1, true)   \
+  X(31, 128, 128, 2, 2, 3, 2, true)   \
+  X(32, 128, 64, 2, 2, 4, 1, true)    \
+  X(33, 64, 128, 2, 2, 4, 1, true)    \
+  X(34, 64, 64, 2, 2, 4, 1, true)     \
+  X(37, 128, 128, 4, 2, 4, 1, true)   \
+  X(38, 64, 64, 2, 2, 4, 2, true)     \
+  X(39, 128, 64, 2, 2, 4, 2, true)    \
+  X(40, 64, 128, 2, 2, 4, 2, true)    \
+  X(41, 256, 64, 4, 2, 3, 1, true)
 
 // cfg in the v2 family and the problem on its path (tap-major walk: Cin % 32 == 0; 16-byte output
 // chunks: N % 4 == 0)
 bool conv_f32g_ok(int cfg, int Cin, int N) {
   if (Cin % GBK || N % 4) return false;
   switch (cfg) {
-#define X(id, BM_, BN_, WM_, WN_, S_, KG_) case id: return true;
+#define X(id, BM_, BN_, WM_, WN_, S_, KG_, P_) case id: return true;
     ADAPT_F32G_CFGS(X)
 #undef X
   }
@@ -462,7 +524,7 @@ bool conv_f32g_ok(int cfg, int Cin, int N) {
 
 bool conv_f32g_cfg_tile(int cfg, int* bm, int* bn) {
   switch (cfg) {
-#define X(id, BM_, BN_, WM_, WN_, S_, KG_) case id: *bm = BM_; *bn = BN_; return true;
+#define X(id, BM_, BN_, WM_, WN_, S_, KG_, P_) case id: *bm = BM_; *bn = BN_; return true;
     ADAPT_F32G_CFGS(X)
 #undef X
   }
@@ -471,7 +533,7 @@ bool conv_f32g_cfg_tile(int cfg, int* bm, int* bn) {
 
 hipError_t conv_f32g_launch(const ConvF32Params& p, int cfg, bool pure, hipStream_t s) {
   switch (cfg) {
-#define X(id, BM_, BN_, WM_, WN_, S_, KG_) case id: return launch_f32g<BM_, BN_, WM_, WN_, S_, KG_>(p, pure, s);
+#define X(id, BM_, BN_, WM_, WN_, S_, KG_, P_) case id: return launch_f32g<BM_, BN_, WM_, WN_, S_, KG_, P_>(p, pure, s);
     ADAPT_F32G_CFGS(X)
 #undef X
   }

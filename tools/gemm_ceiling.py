@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
-"""Library ceiling for the ResNet-50 bs=32 conv GEMM shapes: plain bf16
+"""Library ceiling for the ResNet-50 bs=32 conv GEMM shapes: plain
 torch.matmul (hipBLASLt on ROCm) on the implicit-GEMM dims M x N x K, timed by
-hipGraph replay.  A reference point for our fused implicit-GEMM kernels only."""
+hipGraph replay.  A reference point for our fused implicit-GEMM kernels only.
+    python tools/gemm_ceiling.py [--dtype bf16|fp32]
+(fp32 runs with TF32 off: true fp32 matrix math, as the fp32 conv kernels do)."""
+import argparse
+
 import torch
 
 SHAPES = [  # name, M, N, K
@@ -14,11 +18,16 @@ SHAPES = [  # name, M, N, K
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    dt = torch.bfloat16 if ap.parse_args().dtype == "bf16" else torch.float32
+    torch.backends.cuda.matmul.allow_tf32 = False
     dev = "cuda"
-    for name, M, N, K in SHAPES:
-        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
-        b = torch.randn(K, N, device=dev).to(torch.bfloat16)
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    shapes = SHAPES + ([("square 8192", 8192, 8192, 8192)] if dt == torch.float32 else [])
+    for name, M, N, K in shapes:
+        a = torch.randn(M, K, device=dev).to(dt)
+        b = torch.randn(K, N, device=dev).to(dt)
+        out = torch.empty(M, N, device=dev, dtype=dt)
         torch.matmul(a, b, out=out)
         torch.cuda.synchronize()
         reps = 20

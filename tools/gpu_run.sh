@@ -17,6 +17,7 @@
 #   fault     4-stage SIGKILL recovery bench (device links)
 #   pmc32     two rocprofv3 PMC passes over the fp32 bench (tools/pmc_summary.py reads them)
 #   hang      4-stage wedged-stage (alive, no progress) recovery bench (device links)
+#   roof32    per-layer fp32 roofline table (two PMC passes over tools/roofline_r50.py --dtype fp32)
 #   cs3       channel-split 3x3 (stage 4/5) numerics, isolated timings vs the tile kernels, whole-model A/B
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -48,6 +49,8 @@ for p in "${P[@]}"; do
     cs3)      steps+=("300|$out/pytest_cs3|python -u -m pytest tests/test_cs3_gpu.py tests/test_rr3_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread")
               steps+=("240|$out/cs3_bench|python -u tools/conv_bench.py --shape 32,14,14,256,256,3,1,1 --shape 32,7,7,512,512,3,1,1 --only 73,0,1,2,3,4,5,6,7,8,9 --ks 1,2,4,-1")
               steps+=("240|$out/cs3_ab|python -u tools/ab_cfg.py --model resnet50 --set 32x14x14x256,3x3s1p1111@73@1 --set 32x7x7x512,3x3s1p1111@73@1 --json gpurun_out/$out/cs3_ab.json") ;;
+    roof32)   steps+=("400|$out/roof32_pmc|bash tools/pmc_groups.sh gpurun_out/$out/roof32 'SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT' 'TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum' -- tools/roofline_r50.py --run --dtype fp32 --meta gpurun_out/$out/roof32/meta.json")
+              steps+=("60|$out/roof32_table|python tools/roofline_r50.py --table gpurun_out/$out/roof32 --meta gpurun_out/$out/roof32/meta.json --json gpurun_out/$out/roof32/roofline_fp32.json") ;;
     *) echo "unknown preset $p"; exit 2 ;;
   esac
 done

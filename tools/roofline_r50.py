@@ -13,8 +13,9 @@ Two halves:
   write the table: achieved TFLOP/s, L2<->fabric bytes (TCC_EA0_RDREQ x 128 B
   -- gfx950 tallies a 128-B request at 64 B, MI355X_MICROARCH.md "HBM" --
   plus TCC_EA0_WRREQ x 64 B), compulsory bytes, MFMA busy share and the
-  roofline floor max(flop / 2.5 PF, compulsory bytes / 6.3 TB/s) next to the
-  measured time.
+  roofline floor max(flop / peak, compulsory bytes / 6.3 TB/s) next to the
+  measured time (peak: 2.5 PF bf16, or the measured 150 TF fp32 matrix ceiling
+  with ``--dtype fp32``).
 
 The fabric counters include Infinity-Cache hits (the whole bs=32 ResNet-50
 working set fits in the 256 MiB MALL), so "fabric bytes" is an upper bound on
@@ -35,6 +36,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 PEAK_BF16 = 2.5e15         # dense bf16 MFMA (no sparsity)
+PEAK_FP32 = 1.50e14        # v_mfma_f32_16x16x4_f32 under full load, measured (profiles/r3/mfma_f32_peak.txt)
 HBM_BW = 6.3e12            # achievable HBM3E stream (MI355X_MICROARCH.md "HBM")
 SEP_NAME = "FillFunctor"   # torch fill_ kernel used as the separator
 REPS = 10
@@ -71,7 +73,7 @@ def run(a):
         SliceExecutor
     g = build_model(a.model)
     w = init_weights(g, 0)
-    ex = SliceExecutor(g, w, a.batch)
+    ex = SliceExecutor(g, w, a.batch, precision=a.dtype)
     ex.input_buf(g.input).copy_(torch.randn(ex.input_buf(g.input).shape, device="cuda"))
     sep = torch.zeros(1, device="cuda")
     for _ in range(3):
@@ -98,10 +100,12 @@ def run(a):
         outs = [st.out] + ([st.p["out2"]] if st.p.get("out2") else [])
         act = sum(_bytes_of(ex, g, n, a.batch) for n in list(st.ins) + outs)
         meta.append({"i": i, "kind": st.kind, "out": st.out, "ms": t_ms, "flop": step_flop(g, st, a.batch),
-                     "act_bytes": act, "weight_bytes": _weight_bytes(g, st), "cfg": ex.cfg.get(i)})
+                     "act_bytes": act, "weight_bytes": _weight_bytes(g, st, 4 if a.dtype == "fp32" else 2),
+                     "cfg": ex.cfg.get(i)})
     if a.meta:
         with open(a.meta, "w") as f:
-            json.dump({"model": a.model, "batch": a.batch, "reps": REPS, "steps": meta}, f, indent=1)
+            json.dump({"model": a.model, "batch": a.batch, "reps": REPS, "dtype": a.dtype, "steps": meta}, f,
+                      indent=1)
 
 
 def _read_counters(d):
@@ -137,6 +141,7 @@ def _segments(disp, n_steps):
 def table(a):
     meta = json.load(open(a.meta))
     steps = meta["steps"]
+    peak = PEAK_FP32 if meta.get("dtype") == "fp32" else PEAK_BF16
     reps = meta["reps"]
     merged = [dict() for _ in steps]
     kernels = [None] * len(steps)
@@ -160,7 +165,7 @@ def table(a):
             fabric = rd * 128 + wbytes
         comp = st["act_bytes"] + st["weight_bytes"]
         t = st["ms"] * 1e-3 if st["ms"] else None
-        floor = max(st["flop"] / PEAK_BF16, comp / HBM_BW)      # compulsory traffic only
+        floor = max(st["flop"] / peak, comp / HBM_BW)           # compulsory traffic only
         row = {"i": st["i"], "kind": st["kind"], "out": st["out"], "cfg": st["cfg"], "ms": st["ms"],
                "gflop": round(st["flop"] / 1e9, 3),
                "tflops": round(st["flop"] / t / 1e12, 1) if t and st["flop"] else None,
@@ -168,8 +173,8 @@ def table(a):
                "fabric_MB": round(fabric / 1e6, 2) if fabric is not None else None,
                "fabric_TBps": round(fabric / t / 1e12, 2) if (fabric and t) else None,
                "floor_ms": round(floor * 1e3, 4),
-               "bound": "compute" if st["flop"] / PEAK_BF16 >= comp / HBM_BW else "memory",
-               "mfma_util": round(st["flop"] / t / PEAK_BF16, 3) if t and st["flop"] else None,
+               "bound": "compute" if st["flop"] / peak >= comp / HBM_BW else "memory",
+               "mfma_util": round(st["flop"] / t / peak, 3) if t and st["flop"] else None,
                "of_floor": round(t / floor, 2) if t and floor else None}
         gui = c.get("GRBM_GUI_ACTIVE")
         mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
@@ -195,11 +200,14 @@ def table(a):
         print(f"{r['i']:3d} {r['kind']:10} {r['out'][:24]:24} {r['ms'] or 0:7.4f} {str(r['tflops']):>6} "
               f"{r['compulsory_MB']:7.2f} {str(r['fabric_MB']):>7} {str(r['fabric_TBps']):>5} {r['floor_ms']:7.4f} "
               f"{str(r['of_floor']):>5} {str(r.get('mfma_busy')):>5} {r['bound']}")
+    floor_sum = sum(r["floor_ms"] for r in rows)
     print(f"sum: {tot['ms']:.4f} ms, {tot['flop'] / 1e9:.1f} GFLOP, fabric {tot['fabric'] / 1e6:.1f} MB, "
-          f"compulsory {tot['compulsory'] / 1e6:.1f} MB")
+          f"compulsory {tot['compulsory'] / 1e6:.1f} MB, floors {floor_sum:.4f} ms "
+          f"(peak {peak / 1e12:.0f} TF/s, {HBM_BW / 1e12:.1f} TB/s)")
     if a.json:
         with open(a.json, "w") as f:
-            json.dump({"model": meta["model"], "batch": meta["batch"], "peak_bf16": PEAK_BF16, "hbm_bw": HBM_BW,
+            json.dump({"model": meta["model"], "batch": meta["batch"], "dtype": meta.get("dtype", "bf16"),
+                       "peak_flops": peak, "hbm_bw": HBM_BW,
                        "rows": rows, "total": tot}, f, indent=1)
 
 
@@ -211,6 +219,7 @@ def main():
     ap.add_argument("--meta", default="")
     ap.add_argument("--table", default="", help="directory holding the g1, g2 ... rocprofv3 output dirs")
     ap.add_argument("--json", default="")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args()
     if a.run:
         run(a)
