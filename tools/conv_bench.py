@@ -50,7 +50,9 @@ def bench(shape, only=None, reps=20, ks_list=(1, 2, 3, 4, 6, 8, -1, -2)):
                 continue
             if ks < 0 and cfg in C.V1_CFGS:
                 continue
-            need = C.workspace_elems(M, N, pc.Kpad, cfg, ks)
+            if ks != 1 and cfg not in C.CFG_TILES:      # register-resident / persistent kernels: whole K only
+                continue
+            need = C.workspace_elems(M, N, pc.Kpad, cfg, ks) if cfg in C.CFG_TILES else 0
             ws = torch.empty(need, device=dev, dtype=torch.float32) if need else None
             ctr = torch.zeros(C.sk_plan(M, N, pc.Kpad, cfg, -ks)[0], device=dev, dtype=torch.int32) if ks < 0 else None
             try:
