@@ -104,6 +104,7 @@ class PackedConv:
     pad_b: int
     pad_r: int
     n_split: int = 0         # > 0: two sibling convs packed along N (outputs [0, n_split) and [n_split, cout))
+    wino: Optional[torch.Tensor] = None   # fp32 3x3/s1/p1: Winograd-transformed weights (pack_wino_f32)
 
     @property
     def K(self) -> int:
@@ -399,8 +400,38 @@ def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int
     return 0
 
 
-def f32_cfg_supported(cfg: int, cin: int, cout: int) -> bool:
-    """Whether fp32 tile config `cfg` runs a conv with `cin` input / `cout` output channels."""
+# fp32 Winograd F(2x2, 3x3) configs (csrc/kernels/conv_wino_f32.hip ADAPT_WINO_CFGS): id -> (waves of 16
+# tiles per block, 16-channel output fragments per wave); 3x3 / stride 1 / pad 1 convs only, split-K >= 1
+WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85: (2, 1)}
+# B^T (input), G (weights) and A^T (output) of F(2x2, 3x3) (Lavin & Gray 2016)
+WINO_BT = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
+WINO_G = np.array([[1, 0, 0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0, 0, 1]], np.float64)
+WINO_AT = np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64)
+
+
+def wino_supported(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (3, 3, 1, 1, 1, 1, 1)
+            and pc.cin % 16 == 0 and pc.cout % 16 == 0)
+
+
+def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
+    """U_p = (G g G^T)_p of every (cin, cout) filter in fp64, rounded to fp32, in the MFMA fragment
+    order conv_wino_f32.hip streams: [C/16][N/16][16 positions][64 lanes][4], lane l = 16 q + n'
+    holding U_p[16 kc + 4 q + s][16 nf + n'] for s = 0..3."""
+    kh, kw, C, N = kernel_hwio.shape
+    if (kh, kw) != (3, 3) or C % 16 or N % 16:
+        raise ValueError(f"Winograd F(2x2,3x3) packs 3x3 filters with C, N % 16 == 0 (got {kernel_hwio.shape})")
+    U = np.einsum("ai,ijcn,bj->abcn", WINO_G, np.asarray(kernel_hwio, np.float64), WINO_G)   # [4][4][C][N]
+    U = U.reshape(16, C // 16, 4, 4, N // 16, 16)          # p, kc, q, s, nf, n'
+    return np.ascontiguousarray(U.transpose(1, 4, 0, 2, 5, 3).reshape(C // 16, N // 16, 16, 64, 4).astype(np.float32))
+
+
+def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] = None) -> bool:
+    """Whether fp32 tile config `cfg` runs a conv with `cin` input / `cout` output channels
+    (Winograd configs also need the conv itself: 3x3 / s1 / p1 with its transformed weights)."""
+    if cfg in WINO_F32_CFGS:
+        return (pc is not None and pc.wino is not None and wino_supported(pc)
+                and cout % (16 * WINO_F32_CFGS[cfg][1]) == 0)
     if cfg in F32G_CFGS:
         return cin % F32_BK == 0 and cout % 4 == 0
     return cfg in F32_TILES
@@ -416,9 +447,12 @@ def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, 
     wt = np.zeros((Npad, Kpad), np.float32)
     wt[:cout, :K] = np.asarray(kernel_hwio, np.float32).transpose(3, 0, 1, 2).reshape(cout, K)
     (pt, pb), (pl, pr) = pads
-    return PackedConv(w=torch.from_numpy(wt).to(device=device).contiguous(),
-                      bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),
-                      kh=kh, kw=kw, cin=cin, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
+    pc = PackedConv(w=torch.from_numpy(wt).to(device=device).contiguous(),
+                    bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),
+                    kh=kh, kw=kw, cin=cin, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
+    if wino_supported(pc):
+        pc.wino = torch.from_numpy(wino_pack_np(kernel_hwio)).to(device=device).contiguous()
+    return pc
 
 
 def choose_cfg_f32(M: int, N: int, Kpad: int, occupancy: int = 2):
@@ -477,6 +511,25 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         raise ValueError("conv epilogue activation must be 0 (none), 1 (ReLU) or 2 (ReLU6)")
     if cfg is None:
         cfg, ksplit = choose_cfg_f32(M, N, pc.Kpad)
+    if cfg in WINO_F32_CFGS:
+        ksplit = int(ksplit) or 1
+        if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or ksplit < 1:
+            raise ValueError(f"Winograd config {cfg}: 3x3/s1/p1 conv with transformed weights, C % 16 == 0, "
+                             f"N % {16 * WINO_F32_CFGS[cfg][1]} == 0, split-K >= 1")
+        if ksplit > (C // 16):
+            raise ValueError(f"Winograd split-K {ksplit} exceeds the {C // 16} channel chunks")
+        ws_ptr = 0
+        if ksplit > 1:
+            need = ksplit * M * N
+            if workspace is None:
+                workspace = torch.empty(need, dtype=torch.float32, device=x.device)
+            if workspace.numel() < need or workspace.dtype != torch.float32:
+                raise ValueError(f"Winograd split-K {ksplit} needs an fp32 workspace of {need} elements")
+            ws_ptr = ptr(workspace)
+        kernels().conv_f32_forward(ptr(x), ptr(pc.wino), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C,
+                                   OH, OW, N, 3, 3, 1, 1, 1, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),
+                                   stream_handle(stream), 0)
+        return out
     if cfg not in F32_TILES:
         raise ValueError(f"unknown fp32 tile config {cfg}")
     bm, bn = F32_TILES[cfg]

@@ -540,15 +540,21 @@ class SliceExecutor:
             out = torch.empty(M * N, dtype=torch.float32, device=self.device)
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
-            for cfg in conv_ops.F32_TILES:
-                if not conv_ops.f32_cfg_supported(cfg, C, pc.cout):
+            for cfg in list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS):
+                if not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc):
                     continue
-                bm, bn = conv_ops.F32_TILES[cfg]
-                tiles = math.ceil(M / bm) * math.ceil(N / bn)
-                sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
+                if cfg in conv_ops.WINO_F32_CFGS:         # Winograd F(2x2,3x3): split-K over 16-channel chunks
+                    nwm, fn = conv_ops.WINO_F32_CFGS[cfg]
+                    tiles = math.ceil(B * ((OH + 1) // 2) * ((OW + 1) // 2) / (16 * nwm)) * (N // (16 * fn))
+                    kts, sks = C // 16, ()
+                else:
+                    bm, bn = conv_ops.F32_TILES[cfg]
+                    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+                    kts = ktiles
+                    sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
                 for ks in (1, 2, 4, 8, 16) + sks:
                     # split-K / stream-K only where the tiles alone leave CUs idle
-                    if ks > 1 and (ktiles // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
+                    if ks > 1 and (kts // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue
                     if ks < 0 and tiles >= 4 * conv_ops.NUM_CUS:
                         continue

@@ -285,6 +285,16 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
     ADAPT_F32_CFGS(X)
 #undef X
     default:
+      if (cfg >= 80) {
+        // Winograd F(2x2, 3x3) (conv_wino_f32.hip): w is the transformed, fragment-packed weight tensor
+        if (KH != 3 || KW != 3 || stride != 1 || pad_t != 1 || pad_l != 1 || OH != H || OW != W || p.ksplit < 1 ||
+            !conv_wino_f32_ok(cfg, Cin, N))
+          return hipErrorInvalidValue;
+        const int th = (H + 1) / 2, tw = (W + 1) / 2;
+        WinoF32Params wp{x, w, bias, res, out, ws, B, H, W, Cin, N, th, tw, B * th * tw, relu, p.ksplit};
+        e = conv_wino_f32_launch(wp, cfg, s);
+        break;
+      }
       // v2: LDS-DMA ring (conv_f32g.hip); tap-major walk needs Cin % 32 == 0
       if (!conv_f32g_ok(cfg, Cin, N)) return hipErrorInvalidValue;
       e = conv_f32g_launch(p, cfg, pure, s);

@@ -123,6 +123,21 @@ hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, f
 // v2 fp32 kernel family (conv_f32g.hip, cfg ids >= 10): LDS-DMA ring
 bool conv_f32g_ok(int cfg, int Cin, int N);
 hipError_t conv_f32g_launch(const ConvF32Params& p, int cfg, bool pure, hipStream_t s);
+// fp32 Winograd F(2x2, 3x3) 3x3/s1/p1 conv (conv_wino_f32.hip, cfg ids 80-85): u = transformed weights
+// in MFMA fragment order [C/16][N/16][16 positions][64 lanes][4] (ops/conv.py pack_wino_f32)
+struct WinoF32Params {
+  const float* x;
+  const float* u;
+  const float* bias;
+  const float* res;
+  float* out;
+  float* ws;          // ksplit > 1: fp32 slabs [ksplit][B*H*W][N] (splitk_reduce_f32 adds bias / ReLU)
+  int B, H, W, C, N;
+  int TH, TW, T;      // 2x2 output tiles per column / row of an image, B * TH * TW
+  int relu, ksplit;
+};
+bool conv_wino_f32_ok(int cfg, int C, int N);
+hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,

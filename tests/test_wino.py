@@ -1,0 +1,77 @@
+"""CPU checks of the fp32 Winograd F(2x2, 3x3) conv path (csrc/kernels/conv_wino_f32.hip):
+the host weight transform + fragment packing (ops/conv.py wino_pack_np), unpacked with the exact
+lane / element indexing the kernel uses, and the input / output transforms, reproduce a direct
+3x3 / stride-1 / pad-1 convolution (even and odd maps: ResNet stages 2-4 and stage 5's 7x7)."""
+import numpy as np
+import pytest
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C
+
+
+def direct_conv(x, k):
+    B, H, W, Ci = x.shape
+    xp = np.pad(x, ((0, 0), (1, 1), (1, 1), (0, 0)))
+    y = np.zeros((B, H, W, k.shape[3]))
+    for i in range(3):
+        for j in range(3):
+            y += np.einsum("bhwc,cn->bhwn", xp[:, i:i + H, j:j + W], k[i, j])
+    return y
+
+
+def kernel_emulation(x, packed):
+    """The kernel's arithmetic in fp64: U_p[c][n] read as lane l = 16 q + n', element s of piece
+    (kc, nf, p); V = B^T d B per 4x4 patch; y = A^T (sum_c V U) A, cropped to the map."""
+    B, H, W, Ci = x.shape
+    KC, NF = packed.shape[0], packed.shape[1]
+    N = NF * 16
+    U = np.zeros((16, Ci, N))
+    for kc in range(KC):
+        for nf in range(NF):
+            for p in range(16):
+                for lane in range(64):
+                    q, n_ = lane >> 4, lane & 15
+                    for s in range(4):
+                        U[p, 16 * kc + 4 * q + s, 16 * nf + n_] = packed[kc, nf, p, lane, s]
+    TH, TW = (H + 1) // 2, (W + 1) // 2
+    xp = np.zeros((B, 2 * TH + 2, 2 * TW + 2, Ci))
+    xp[:, 1:H + 1, 1:W + 1] = x
+    y = np.zeros((B, 2 * TH, 2 * TW, N))
+    BT, AT = C.WINO_BT, C.WINO_AT
+    for ty in range(TH):
+        for tx in range(TW):
+            d = xp[:, 2 * ty:2 * ty + 4, 2 * tx:2 * tx + 4]                  # [B][4][4][C]
+            V = np.einsum("ai,bijc,dj->badc", BT, d, BT).reshape(B, 16, Ci)  # p = 4a + b
+            M = np.einsum("bpc,pcn->bpn", V, U).reshape(B, 4, 4, N)
+            y[:, 2 * ty:2 * ty + 2, 2 * tx:2 * tx + 2] = np.einsum("ai,bijn,dj->badn", AT, M, AT)
+    return y[:, :H, :W]
+
+
+@pytest.mark.parametrize("H,W,Ci,N", [(8, 8, 32, 16), (7, 7, 16, 32), (6, 10, 16, 16)])
+def test_wino_packing_and_transforms_match_direct_conv(H, W, Ci, N):
+    rng = np.random.default_rng(H * 100 + Ci)
+    x = rng.standard_normal((2, H, W, Ci))
+    k = rng.standard_normal((3, 3, Ci, N)) / np.sqrt(9 * Ci)
+    packed = C.wino_pack_np(k)
+    assert packed.shape == (Ci // 16, N // 16, 16, 64, 4) and packed.dtype == np.float32
+    got = kernel_emulation(x, packed.astype(np.float64))
+    want = direct_conv(x, k)
+    # the packed weights are fp32: agreement to fp32 rounding of U
+    assert np.abs(got - want).max() / np.abs(want).max() < 2e-6
+
+
+def test_wino_pack_rejects_other_filters():
+    with pytest.raises(ValueError):
+        C.wino_pack_np(np.zeros((1, 1, 16, 16), np.float32))
+    with pytest.raises(ValueError):
+        C.wino_pack_np(np.zeros((3, 3, 8, 16), np.float32))
+
+
+def test_pack_conv_f32_attaches_wino_only_to_3x3_s1_p1():
+    k3 = np.random.default_rng(0).standard_normal((3, 3, 32, 64)).astype(np.float32)
+    pc = C.pack_conv_f32(k3, np.zeros(64, np.float32), 1, ((1, 1), (1, 1)), "cpu")
+    assert pc.wino is not None and tuple(pc.wino.shape) == (2, 4, 16, 64, 4)
+    assert C.f32_cfg_supported(80, 32, 64, pc) and not C.f32_cfg_supported(84, 32, 64, pc)   # 64 % 48
+    pc2 = C.pack_conv_f32(k3, np.zeros(64, np.float32), 2, ((0, 1), (0, 1)), "cpu")
+    assert pc2.wino is None and not C.f32_cfg_supported(80, 32, 64, pc2)
+    k1 = np.zeros((1, 1, 32, 64), np.float32)
+    assert C.pack_conv_f32(k1, np.zeros(64, np.float32), 1, ((0, 0), (0, 0)), "cpu").wino is None
