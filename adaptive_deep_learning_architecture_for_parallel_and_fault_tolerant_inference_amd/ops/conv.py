@@ -402,7 +402,19 @@ def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int
 
 # fp32 Winograd F(2x2, 3x3) configs (csrc/kernels/conv_wino_f32.hip ADAPT_WINO_CFGS): id -> (waves of 16
 # tiles per block, 16-channel output fragments per wave); 3x3 / stride 1 / pad 1 convs only, split-K >= 1
-WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85: (2, 1)}
+WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85: (2, 1),
+                 86: (4, 2), 87: (4, 3), 88: (8, 1),          # 86-88: the next chunk's patch prefetched
+                 100: (8, 2), 101: (8, 1), 102: (4, 1)}       # v2: input patches staged in LDS by LDS-DMA
+WINO_V2_CFGS = frozenset((100, 101, 102))
+
+
+def wino_map_ok(cfg: int, H: int, W: int) -> bool:
+    """v2 configs stage a wave's 16 tiles as <= 4 tile-row segments: 2x2-tile rows of >= 4 tiles."""
+    return cfg not in WINO_V2_CFGS or (W + 1) // 2 >= 4
+
+
+# cfg 80 with ablation switches (conv_wino_f32.hip ABL = id - 90): tools/conv_bench_f32.py only, never tuned
+WINO_F32_ABLATE = {90 + a: (4, 2) for a in (1, 2, 4, 5, 8, 9)}
 # B^T (input), G (weights) and A^T (output) of F(2x2, 3x3) (Lavin & Gray 2016)
 WINO_BT = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
 WINO_G = np.array([[1, 0, 0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0, 0, 1]], np.float64)
@@ -429,9 +441,9 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] = None) -> bool:
     """Whether fp32 tile config `cfg` runs a conv with `cin` input / `cout` output channels
     (Winograd configs also need the conv itself: 3x3 / s1 / p1 with its transformed weights)."""
-    if cfg in WINO_F32_CFGS:
-        return (pc is not None and pc.wino is not None and wino_supported(pc)
-                and cout % (16 * WINO_F32_CFGS[cfg][1]) == 0)
+    if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
+        fn = {**WINO_F32_CFGS, **WINO_F32_ABLATE}[cfg][1]
+        return pc is not None and pc.wino is not None and wino_supported(pc) and cout % (16 * fn) == 0
     if cfg in F32G_CFGS:
         return cin % F32_BK == 0 and cout % 4 == 0
     return cfg in F32_TILES
@@ -511,11 +523,12 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         raise ValueError("conv epilogue activation must be 0 (none), 1 (ReLU) or 2 (ReLU6)")
     if cfg is None:
         cfg, ksplit = choose_cfg_f32(M, N, pc.Kpad)
-    if cfg in WINO_F32_CFGS:
+    if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         ksplit = int(ksplit) or 1
-        if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or ksplit < 1:
+        if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or ksplit < 1 \
+                or not wino_map_ok(cfg, H, W):
             raise ValueError(f"Winograd config {cfg}: 3x3/s1/p1 conv with transformed weights, C % 16 == 0, "
-                             f"N % {16 * WINO_F32_CFGS[cfg][1]} == 0, split-K >= 1")
+                             f"N % 16 * fragments == 0, split-K >= 1")
         if ksplit > (C // 16):
             raise ValueError(f"Winograd split-K {ksplit} exceeds the {C // 16} channel chunks")
         ws_ptr = 0

@@ -41,12 +41,72 @@ typedef __attribute__((address_space(3))) void lds_void_w;
 
 __device__ __attribute__((aligned(64))) float g_wino_zero[64];
 
-// two waves per SIMD (<= 256 VGPRs) up to FN = 2; FN = 3 keeps one (its 192 accumulators)
-template <int NWM, int FN>
-constexpr int wino_min_blocks() { return FN <= 2 ? (8 / NWM > 0 ? 8 / NWM : 1) : (4 / NWM > 0 ? 4 / NWM : 1); }
+// output transform A^T M A (lane-local) + bias / residual / ReLU, or a split-K slab (blockIdx.z);
+// acc[p][j][i] = M_p[tile tw0 + 4q + i][channel 16 (nf0 + j) + r]
+template <int FN, int ABL>
+__device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x4 (&acc)[16][FN], int tw0, int r,
+                                              int q, int nf0) {
+  const bool split = p.ksplit > 1;
+  float* dst = split ? p.ws + (size_t)blockIdx.z * p.B * p.H * p.W * p.N : p.out;
+  const int tpi = p.TH * p.TW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tt = tw0 + 4 * q + i;
+    if (tt >= p.T) continue;
+    const int im = tt / tpi, rr = tt - im * tpi;
+    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = (nf0 + j) * 16 + r;
+      float m[4][4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) m[a][b] = acc[a * 4 + b][j][i];
+      float w0[4], w1[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        w0[b] = m[0][b] + m[1][b] + m[2][b];
+        w1[b] = m[1][b] - m[2][b] - m[3][b];
+      }
+      float y[2][2];
+      y[0][0] = w0[0] + w0[1] + w0[2];
+      y[0][1] = w0[1] - w0[2] - w0[3];
+      y[1][0] = w1[0] + w1[1] + w1[2];
+      y[1][1] = w1[1] - w1[2] - w1[3];
+      const float bn = split ? 0.f : p.bias[n];
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          if (oy + dy >= p.H || ox + dx >= p.W) continue;
+          const size_t o = (((size_t)im * p.H + oy + dy) * p.W + ox + dx) * p.N + n;
+          float v = y[dy][dx] + bn;
+          if (!split) {
+            if (p.res) v += p.res[o];
+            v = act_relu(v, p.relu);
+          }
+          if constexpr (ABL & 4) asm volatile("" ::"v"(v));
+          else dst[o] = v;
+        }
+    }
+  }
+}
 
-template <int NWM, int FN, int STAGES>
-__global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN>())) void conv_wino_f32_kernel(WinoF32Params p) {
+// two waves per SIMD (<= 256 VGPRs) up to FN = 2 without prefetch; FN = 3 (192 accumulators) or the
+// register prefetch of the next chunk's patch (64 more VGPRs) keep one
+template <int NWM, int FN, bool PF>
+constexpr int wino_min_blocks() {
+  return (FN <= 2 && !PF) ? (8 / NWM > 0 ? 8 / NWM : 1) : (4 / NWM > 0 ? 4 / NWM : 1);
+}
+
+// ABL: ablation switches for the cfg 90+ twins of cfg 80 (tools/conv_bench_f32.py; 0 in production):
+// 1 = every patch load from one address (no scattered loads), 2 = no MFMA, 4 = no output stores,
+// 8 = no weight DMA
+// PF: the next chunk's patch loads are issued into a second register set right after the chunk's
+// barrier, so they are in flight under the chunk's MFMAs instead of exposed at the next chunk's start.
+template <int NWM, int FN, int STAGES, bool PF, int ABL = 0>
+__global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void conv_wino_f32_kernel(WinoF32Params p) {
   constexpr int NT = NWM * 64;
   constexpr int BT = 16 * NWM;                       // tiles per block
   constexpr int PIECES = 16 * FN;                    // 1 KiB weight pieces per chunk
@@ -100,22 +160,36 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN>())) void conv_w
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (kc0 < kc1) issue_w(kc0, 0);
-  for (int kc = kc0; kc < kc1; ++kc) {
-    const int slot = (kc - kc0) % STAGES;
-    // this lane's patch, channels 16kc + 4q .. +3 (zero outside the image)
-    f32x4 d[4][4];
+  // this lane's patch, channels 16kc + 4q .. +3 (zero outside the image)
+  auto load_patch = [&](f32x4 (&dd)[4][4], int kc) {
 #pragma unroll
     for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 4; ++dx) {
-        const float* src = ((ok >> (4 * dy + dx)) & 1u) ? xb + dy * rstride + dx * p.C + kc * 16 : g_wino_zero;
-        d[dy][dx] = *(const f32x4*)src;
+        const float* src = (!(ABL & 1) && (!PF || kc < kc1) && ((ok >> (4 * dy + dx)) & 1u))
+                               ? xb + dy * rstride + dx * p.C + kc * 16 : g_wino_zero;
+        dd[dy][dx] = *(const f32x4*)src;
       }
+  };
+  f32x4 dn[PF ? 4 : 1][PF ? 4 : 1];
+  if (!(ABL & 8) && kc0 < kc1) issue_w(kc0, 0);
+  if constexpr (PF) load_patch(dn, kc0);
+  for (int kc = kc0; kc < kc1; ++kc) {
+    const int slot = (kc - kc0) % STAGES;
+    f32x4 d[4][4];
+    if constexpr (PF) {
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx) d[dy][dx] = dn[dy][dx];
+    } else {
+      load_patch(d, kc);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                    // every wave's pieces of chunk kc are in; slot kc+1 is free
     asm volatile("" ::: "memory");
-    if (kc + 1 < kc1) issue_w(kc + 1, (slot + 1) % STAGES);
+    if (!(ABL & 8) && kc + 1 < kc1) issue_w(kc + 1, (slot + 1) % STAGES);
+    if constexpr (PF) load_patch(dn, kc + 1);
 
     // B^T d: rows
 #pragma unroll
@@ -135,91 +209,237 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN>())) void conv_w
       v[1] = d[pa][1] + d[pa][2];
       v[2] = d[pa][2] - d[pa][1];
       v[3] = d[pa][1] - d[pa][3];
-      f32x4 u[4][FN];
 #pragma unroll
-      for (int pb = 0; pb < 4; ++pb)
+      for (int pb = 0; pb < 4; ++pb) {
+        f32x4 u[FN];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) u[pb][j] = *(const f32x4*)(sl + ((j * 16 + pa * 4 + pb) * 64 + lane) * 16);
+        for (int j = 0; j < FN; ++j) u[j] = *(const f32x4*)(sl + ((j * 16 + pa * 4 + pb) * 64 + lane) * 16);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int pb = 0; pb < 4; ++pb)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[pa * 4 + pb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[pb][s], u[pb][j][s], acc[pa * 4 + pb][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (ABL & 2) acc[pa * 4 + pb][j][s] += v[pb][s] * u[j][s];
+            else acc[pa * 4 + pb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[pb][s], u[j][s], acc[pa * 4 + pb][j], 0, 0, 0);
+          }
+      }
     }
   }
 
-  // ---- output transform A^T M A (lane-local) + bias / ReLU, or a split-K slab
-  // acc[p][j][i] = M_p[tile 4q + i of the wave][channel 16 (nf0 + j) + r]
-  const bool split = p.ksplit > 1;
-  float* dst = split ? p.ws + (size_t)blockIdx.z * p.B * p.H * p.W * p.N : p.out;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tt = blockIdx.x * BT + wave * 16 + 4 * q + i;
-    if (tt >= p.T) continue;
-    const int im = tt / tpi, rr = tt - im * tpi;
-    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = (nf0 + j) * 16 + r;
-      float m[4][4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) m[a][b] = acc[a * 4 + b][j][i];
-      float w0[4], w1[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        w0[b] = m[0][b] + m[1][b] + m[2][b];
-        w1[b] = m[1][b] - m[2][b] - m[3][b];
-      }
-      float y[2][2];
-      y[0][0] = w0[0] + w0[1] + w0[2];
-      y[0][1] = w0[1] - w0[2] - w0[3];
-      y[1][0] = w1[0] + w1[1] + w1[2];
-      y[1][1] = w1[1] - w1[2] - w1[3];
-      const float bn = split ? 0.f : p.bias[n];
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          if (oy + dy >= p.H || ox + dx >= p.W) continue;
-          const size_t o = (((size_t)im * p.H + oy + dy) * p.W + ox + dx) * p.N + n;
-          float v = y[dy][dx] + bn;
-          if (!split) {
-            if (p.res) v += p.res[o];
-            v = act_relu(v, p.relu);
-          }
-          dst[o] = v;
-        }
-    }
-  }
+  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0);
 }
 
-template <int NWM, int FN, int STAGES>
+// ---------------------------------------------------------------------------
+// v2: the wave's input patches staged in LDS by LDS-DMA (cfg 100+).
+//
+// The v1 ablation (tools/conv_bench_f32.py, cfgs 90-99) put the cost in the
+// per-lane patch loads: 16 scattered float4 loads per lane per chunk, waited on
+// right away (stage-3 3x3: 65 us, 41 us without them).  Here a wave's 16 tiles
+// (16 consecutive tiles in (image, tile row, tile column) order, as in v1) form
+// at most four row segments; a segment of `len` tiles needs 4 input rows x
+// (2 len + 2) pixels, so the wave's input is <= 160 pixels instead of 256, and
+// it is fetched as whole 64-byte pixel chunks (16 channels) by LDS-DMA into the
+// wave's own LDS image.  Each lane then reads its 16 patch pixels with
+// ds_read_b128 at the start of the chunk and the wave immediately refills the
+// same image with the next chunk (only this wave reads it, so no barrier is
+// needed), which keeps the next chunk's input in flight under this chunk's
+// MFMAs without a second register set.  The weight ring is as in v1.
+template <int NW, int FN>
+__global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
+  constexpr int PMAX = 10;                           // 1 KiB input pieces per wave (<= 160 pixels)
+  constexpr int PIECES = 16 * FN;
+  constexpr int PPW = (PIECES + NW - 1) / NW;
+  constexpr int SLOT = PIECES * 1024;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + NW * PMAX * 1024];
+  char* ring = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  char* pimg = smem + 2 * SLOT + wave * PMAX * 1024;
+  const int nf0 = blockIdx.y * FN;
+  const int NF = p.N / 16;
+  const int KC = p.C / 16;
+  const int kper = (KC + p.ksplit - 1) / p.ksplit;
+  const int kc0 = blockIdx.z * kper, kc1 = min(KC, kc0 + kper);
+  const int TR = p.B * p.TH;                         // tile rows over the batch
+
+  // ---- the wave's row segments (wave-uniform)
+  const int tw0 = (blockIdx.x * NW + wave) * 16;
+  const int tlast = min(tw0 + 15, p.T - 1);
+  const int R0 = tw0 / p.TW;
+  const int nseg = tw0 < p.T ? tlast / p.TW - R0 + 1 : 0;
+  int seg_lo[4], seg_w[4], seg_b[5];
+  seg_b[0] = 0;
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {
+    const int lo = sg == 0 ? tw0 - R0 * p.TW : 0;
+    const int hi = sg == nseg - 1 ? tlast - (R0 + sg) * p.TW : p.TW - 1;
+    seg_lo[sg] = lo;
+    seg_w[sg] = sg < nseg ? 2 * (hi - lo + 1) + 2 : 0;
+    seg_b[sg + 1] = seg_b[sg] + 4 * seg_w[sg];
+  }
+
+  // ---- LDS-DMA sources: piece i, lane l -> image pixel (element offset), chunk-invariant
+  int src_off[PMAX];
+  unsigned src_ok = 0;
+#pragma unroll
+  for (int i = 0; i < PMAX; ++i) {
+    const int pix = i * 16 + (lane >> 2), qq = lane & 3;
+    int sg = 0;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) sg += pix >= seg_b[k] ? 1 : 0;
+    const int wdt = sg == 0 ? seg_w[0] : sg == 1 ? seg_w[1] : sg == 2 ? seg_w[2] : seg_w[3];
+    const int lo = sg == 0 ? seg_lo[0] : 0;
+    const int bb = sg == 0 ? seg_b[0] : sg == 1 ? seg_b[1] : sg == 2 ? seg_b[2] : seg_b[3];
+    const int lp = pix - bb;
+    const int prow = wdt ? lp / wdt : 0, pcol = lp - prow * wdt;
+    const int R = R0 + sg;
+    const int img = R / p.TH, ty = R - img * p.TH;
+    const int iy = 2 * ty - 1 + prow, ix = 2 * lo - 1 + pcol;
+    const bool in = pix < seg_b[4] && R < TR && (unsigned)iy < (unsigned)p.H &&
+                    (unsigned)ix < (unsigned)p.W;
+    src_off[i] = in ? ((img * p.H + iy) * p.W + ix) * p.C + 4 * qq : 0;
+    src_ok |= in ? 1u << i : 0u;
+  }
+  auto issue_x = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < PMAX; ++i) {
+      const float* src = ((src_ok >> i) & 1u) ? p.x + src_off[i] + kc * 16 : g_wino_zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- this lane's patch in the wave image: pixel index of (dy, dx) = prow0 + dy * pw + dx
+  const int t = tw0 + r;
+  const int tsg = t < p.T ? t / p.TW - R0 : 0;
+  const int pw = tsg == 0 ? seg_w[0] : tsg == 1 ? seg_w[1] : tsg == 2 ? seg_w[2] : seg_w[3];
+  const int pb0 = tsg == 0 ? seg_b[0] : tsg == 1 ? seg_b[1] : tsg == 2 ? seg_b[2] : seg_b[3];
+  const int plo = tsg == 0 ? seg_lo[0] : 0;
+  const int prow0 = t < p.T ? pb0 + 2 * (t - (R0 + tsg) * p.TW - plo) : 0;
+  const char* prd = pimg + (prow0 * 4 + q) * 16;
+  const int pws = pw * 64;                           // bytes per patch-row step
+
+  const float* ub = p.u + (size_t)nf0 * 16 * 256;
+  const size_t uchunk = (size_t)NF * 16 * 256;
+  auto issue_w = [&](int kc, int slot) {
+    const float* src = ub + (size_t)kc * uchunk;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;
+      if (PIECES % NW == 0 || pc < PIECES)
+        __builtin_amdgcn_global_load_lds((const void*)(src + pc * 256 + lane * 4),
+                                         (lds_void_w*)(ring + slot * SLOT + pc * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[16][FN];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (kc0 < kc1) {
+    issue_w(kc0, 0);
+    issue_x(kc0);
+  }
+  for (int kc = kc0; kc < kc1; ++kc) {
+    const int slot = (kc - kc0) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                    // all weight pieces of chunk kc in; the other slot is free
+    asm volatile("" ::: "memory");
+    if (kc + 1 < kc1) issue_w(kc + 1, slot ^ 1);
+    f32x4 d[4][4];
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) d[dy][dx] = *(const f32x4*)(prd + dy * pws + dx * 64);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kc + 1 < kc1) issue_x(kc + 1);               // this wave's image is free again: refill it
+
+#pragma unroll
+    for (int dx = 0; dx < 4; ++dx) {
+      const f32x4 a0 = d[0][dx], a1 = d[1][dx], a2 = d[2][dx], a3 = d[3][dx];
+      d[0][dx] = a0 - a2;
+      d[1][dx] = a1 + a2;
+      d[2][dx] = a2 - a1;
+      d[3][dx] = a1 - a3;
+    }
+    const char* sl = ring + slot * SLOT;
+#pragma unroll
+    for (int pa = 0; pa < 4; ++pa) {
+      f32x4 v[4];
+      v[0] = d[pa][0] - d[pa][2];
+      v[1] = d[pa][1] + d[pa][2];
+      v[2] = d[pa][2] - d[pa][1];
+      v[3] = d[pa][1] - d[pa][3];
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        f32x4 u[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) u[j] = *(const f32x4*)(sl + ((j * 16 + pa * 4 + pb) * 64 + lane) * 16);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[pa * 4 + pb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[pb][s], u[j][s], acc[pa * 4 + pb][j], 0, 0, 0);
+      }
+    }
+  }
+  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0);
+}
+
+// v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
+bool wino_v2_shape_ok(int TW) { return TW >= 5 || TW == 4; }
+
+template <int NW, int FN>
+hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
+  if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW)) return hipErrorInvalidValue;
+  const dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
+  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN>), grid, block, 0, s, p);
+  return hipGetLastError();
+}
+
+template <int NWM, int FN, int STAGES, bool PF, int ABL>
 hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN)) return hipErrorInvalidValue;
   const dim3 grid((p.T + 16 * NWM - 1) / (16 * NWM), p.N / (16 * FN), p.ksplit), block(NWM * 64);
-  hipLaunchKernelGGL((conv_wino_f32_kernel<NWM, FN, STAGES>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((conv_wino_f32_kernel<NWM, FN, STAGES, PF, ABL>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
 }  // namespace
 
 // Winograd cfg ids (ops/conv.py WINO_F32_CFGS mirrors them): id -> waves (16 tiles each), 16-channel
-// output fragments per wave, LDS ring stages
-#define ADAPT_WINO_CFGS(X) \
-  X(80, 4, 2, 2)           \
-  X(81, 4, 1, 2)           \
-  X(82, 2, 2, 2)           \
-  X(83, 8, 2, 2)           \
-  X(84, 4, 3, 2)           \
-  X(85, 2, 1, 2)
+// output fragments per wave, LDS ring stages, patch prefetch, ablation
+// (90-99: cfg 80 with ablation switches ABL = id - 90, measurement only)
+#define ADAPT_WINO_CFGS(X)  \
+  X(80, 4, 2, 2, false, 0) \
+  X(81, 4, 1, 2, false, 0) \
+  X(82, 2, 2, 2, false, 0) \
+  X(83, 8, 2, 2, false, 0) \
+  X(84, 4, 3, 2, false, 0) \
+  X(85, 2, 1, 2, false, 0) \
+  X(86, 4, 2, 2, true, 0)  \
+  X(87, 4, 3, 2, true, 0)  \
+  X(88, 8, 1, 2, true, 0)  \
+  X(91, 4, 2, 2, false, 1) \
+  X(92, 4, 2, 2, false, 2) \
+  X(94, 4, 2, 2, false, 4) \
+  X(95, 4, 2, 2, false, 5) \
+  X(98, 4, 2, 2, false, 8) \
+  X(99, 4, 2, 2, false, 9)
+// v2 (input patches staged by LDS-DMA): id -> waves, 16-channel output fragments per wave
+#define ADAPT_WINO2_CFGS(X) \
+  X(100, 8, 2)              \
+  X(101, 8, 1)              \
+  X(102, 4, 1)
 
 bool conv_wino_f32_ok(int cfg, int C, int N) {
   switch (cfg) {
-#define X(id, NWM_, FN_, S_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
+#define X(id, NW_, FN_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
+    ADAPT_WINO2_CFGS(X)
+#undef X
+#define X(id, NWM_, FN_, S_, PF_, A_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
     ADAPT_WINO_CFGS(X)
 #undef X
   }
@@ -230,7 +450,10 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) 
   if (p.C % 16 || p.ksplit < 1 || p.T != p.B * p.TH * p.TW) return hipErrorInvalidValue;
   if (p.ksplit > 1 && !p.ws) return hipErrorInvalidValue;
   switch (cfg) {
-#define X(id, NWM_, FN_, S_) case id: return launch_wino<NWM_, FN_, S_>(p, s);
+#define X(id, NW_, FN_) case id: return launch_wino_v2<NW_, FN_>(p, s);
+    ADAPT_WINO2_CFGS(X)
+#undef X
+#define X(id, NWM_, FN_, S_, PF_, A_) case id: return launch_wino<NWM_, FN_, S_, PF_, A_>(p, s);
     ADAPT_WINO_CFGS(X)
 #undef X
   }

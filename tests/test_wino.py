@@ -75,3 +75,64 @@ def test_pack_conv_f32_attaches_wino_only_to_3x3_s1_p1():
     assert pc2.wino is None and not C.f32_cfg_supported(80, 32, 64, pc2)
     k1 = np.zeros((1, 1, 32, 64), np.float32)
     assert C.pack_conv_f32(k1, np.zeros(64, np.float32), 1, ((0, 0), (0, 0)), "cpu").wino is None
+
+
+def _v2_lane_maps(tw0, T, TW, TH, H, W):
+    """conv_wino_f32_v2_kernel's wave-image bookkeeping, transcribed: the LDS-DMA source of every
+    (piece, lane) slot and every lane's patch pixel index; returns (dma, reads) for checking."""
+    TR_ = T // TW
+    tlast = min(tw0 + 15, T - 1)
+    R0 = tw0 // TW
+    nseg = tlast // TW - R0 + 1 if tw0 < T else 0
+    seg_lo, seg_w, seg_b = [], [], [0]
+    for sg in range(4):
+        lo = tw0 - R0 * TW if sg == 0 else 0
+        hi = tlast - (R0 + sg) * TW if sg == nseg - 1 else TW - 1
+        seg_lo.append(lo)
+        seg_w.append(2 * (hi - lo + 1) + 2 if sg < nseg else 0)
+        seg_b.append(seg_b[-1] + 4 * seg_w[-1])
+    dma = {}
+    for i in range(10):
+        for lane in range(64):
+            pix, qq = i * 16 + (lane >> 2), lane & 3
+            sg = sum(1 for k in (1, 2, 3) if pix >= seg_b[k])
+            wdt, lo, bb = seg_w[sg], (seg_lo[0] if sg == 0 else 0), seg_b[sg]
+            lp = pix - bb
+            prow = lp // wdt if wdt else 0
+            pcol = lp - prow * wdt
+            R = R0 + sg
+            img, ty = R // TH, R % TH
+            iy, ix = 2 * ty - 1 + prow, 2 * lo - 1 + pcol
+            inside = pix < seg_b[4] and R < TR_ and 0 <= iy < H and 0 <= ix < W
+            dma[pix * 4 + qq] = (img, iy, ix) if inside else None
+    reads = {}
+    for r in range(16):
+        t = tw0 + r
+        if t >= T:
+            continue
+        tsg = t // TW - R0
+        prow0 = seg_b[tsg] + 2 * (t - (R0 + tsg) * TW - (seg_lo[0] if tsg == 0 else 0))
+        for dy in range(4):
+            for dx in range(4):
+                reads[(r, dy, dx)] = prow0 + dy * seg_w[tsg] + dx
+    return dma, reads, seg_b[4]
+
+
+@pytest.mark.parametrize("B,H,W", [(3, 56, 56), (2, 28, 28), (3, 14, 14), (5, 7, 7), (2, 9, 13), (2, 8, 8)])
+def test_wino_v2_wave_image_bookkeeping(B, H, W):
+    """Every lane's 16 patch pixels come from the LDS slots that the wave's LDS-DMA filled with exactly
+    that image pixel (or zeros outside the image), within the 10 KiB wave image, for every wave."""
+    TH, TW = (H + 1) // 2, (W + 1) // 2
+    T = B * TH * TW
+    for tw0 in range(0, T, 16):
+        dma, reads, total = _v2_lane_maps(tw0, T, TW, TH, H, W)
+        assert total <= 160
+        for (r, dy, dx), pix in reads.items():
+            assert 0 <= pix < 160
+            t = tw0 + r
+            img, rem = divmod(t, TH * TW)
+            ty, tx = divmod(rem, TW)
+            iy, ix = 2 * ty - 1 + dy, 2 * tx - 1 + dx
+            want = (img, iy, ix) if 0 <= iy < H and 0 <= ix < W else None
+            for qq in range(4):
+                assert dma[pix * 4 + qq] == want, (tw0, r, dy, dx)

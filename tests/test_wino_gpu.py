@@ -24,6 +24,8 @@ SHAPES = [  # (B, H, W, Cin, Cout, residual, relu)
 @pytest.mark.parametrize("ksplit", [1, 2, 4])
 def test_wino_f32_matches_fp64(shape, ksplit):
     B, H, W, Cin, Cout, has_res, relu = shape
+    if ksplit > Cin // 16:
+        pytest.skip("split-K beyond the 16-channel chunks")
     rng = np.random.default_rng(hash(shape) % 2**32)
     x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
     kern = (rng.standard_normal((3, 3, Cin, Cout)) / np.sqrt(9 * Cin)).astype(np.float32)
@@ -38,7 +40,7 @@ def test_wino_f32_matches_fp64(shape, ksplit):
     out = torch.empty((B, H, W, Cout), dtype=torch.float32, device="cuda")
     ran = 0
     for cfg in C.WINO_F32_CFGS:
-        if not C.f32_cfg_supported(cfg, Cin, Cout, pc) or ksplit > Cin // 16:
+        if not C.f32_cfg_supported(cfg, Cin, Cout, pc) or not C.wino_map_ok(cfg, H, W):
             continue
         out.fill_(float("nan"))
         C.conv_forward_f32(xd, pc, out, rd, relu=relu, cfg=cfg, ksplit=ksplit)
