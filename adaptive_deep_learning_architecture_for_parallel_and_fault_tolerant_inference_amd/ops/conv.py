@@ -392,20 +392,42 @@ def f32_sk_plan(M: int, N: int, Kpad: int, cfg: int, mult: int = 1):
 
 
 def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int:
-    """fp32 workspace a launch needs: split-K slabs or stream-K partial slots."""
+    """fp32 workspace a launch needs: split-K slabs or stream-K partial slots
+    (Winograd ksplit < 0: -ksplit slabs, the fixup fused into the kernel)."""
     if ksplit > 1:
         return ksplit * M * N
     if ksplit < 0:
+        if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
+            return -ksplit * M * N
         return f32_sk_plan(M, N, Kpad, cfg, -ksplit)[3]
     return 0
+
+
+def wino_blocks(cfg: int, B: int, H: int, W: int, N: int) -> int:
+    """Blocks per split of a Winograd launch (tile groups x channel groups): the fused split-K
+    arrival counters it needs."""
+    nwm, fn = {**WINO_F32_CFGS, **WINO_F32_ABLATE}[cfg]
+    return math.ceil(B * ((H + 1) // 2) * ((W + 1) // 2) / (16 * nwm)) * (N // (16 * fn))
+
+
+def f32_counter_elems(cfg: int, ksplit: int, B: int, H: int, W: int, OH: int, OW: int, N: int, Kpad: int) -> int:
+    """int32 arrival counters an fp32 launch needs: stream-K tiles (v2 GEMM configs) or fused
+    Winograd split-K blocks; 0 for plain launches."""
+    if ksplit >= 0:
+        return 0
+    if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
+        return wino_blocks(cfg, B, H, W, N)
+    return f32_sk_plan(B * OH * OW, N, Kpad, cfg, -ksplit)[0]
 
 
 # fp32 Winograd F(2x2, 3x3) configs (csrc/kernels/conv_wino_f32.hip ADAPT_WINO_CFGS): id -> (waves of 16
 # tiles per block, 16-channel output fragments per wave); 3x3 / stride 1 / pad 1 convs only, split-K >= 1
 WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85: (2, 1),
                  86: (4, 2), 87: (4, 3), 88: (8, 1),          # 86-88: the next chunk's patch prefetched
-                 100: (8, 2), 101: (8, 1), 102: (4, 1)}       # v2: input patches staged in LDS by LDS-DMA
-WINO_V2_CFGS = frozenset((100, 101, 102))
+                 100: (8, 2), 101: (8, 1), 102: (4, 1),       # v2: input patches staged in LDS by LDS-DMA
+                 103: (8, 2), 104: (8, 1), 105: (4, 1),       # v2 with the bank-swizzled wave image
+                 106: (8, 2), 107: (8, 1), 108: (4, 1)}       # ... and the next patch read before the barrier
+WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108))
 
 
 def wino_map_ok(cfg: int, H: int, W: int) -> bool:
@@ -524,24 +546,33 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
     if cfg is None:
         cfg, ksplit = choose_cfg_f32(M, N, pc.Kpad)
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
+        # ksplit > 1: slabs + splitk_reduce_f32; ksplit <= -2: -ksplit slabs, the last split of
+        # each block adds them in split order inside the kernel (needs `counters`)
         ksplit = int(ksplit) or 1
-        if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or ksplit < 1 \
+        if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or ksplit == -1 \
                 or not wino_map_ok(cfg, H, W):
             raise ValueError(f"Winograd config {cfg}: 3x3/s1/p1 conv with transformed weights, C % 16 == 0, "
-                             f"N % 16 * fragments == 0, split-K >= 1")
-        if ksplit > (C // 16):
-            raise ValueError(f"Winograd split-K {ksplit} exceeds the {C // 16} channel chunks")
-        ws_ptr = 0
-        if ksplit > 1:
-            need = ksplit * M * N
+                             f"N % 16 * fragments == 0, split-K >= 1 or fused split-K <= -2")
+        if abs(ksplit) > (C // 16) or ksplit < -4:
+            raise ValueError(f"Winograd split-K {ksplit} exceeds the {C // 16} channel chunks (fused: <= 4 splits)")
+        ws_ptr = ctr_ptr = 0
+        if ksplit != 1:
+            need = abs(ksplit) * M * N
+            if need * 4 > 0x7fffffff:
+                raise ValueError("Winograd split-K slabs beyond 2 GiB")
             if workspace is None:
                 workspace = torch.empty(need, dtype=torch.float32, device=x.device)
             if workspace.numel() < need or workspace.dtype != torch.float32:
                 raise ValueError(f"Winograd split-K {ksplit} needs an fp32 workspace of {need} elements")
             ws_ptr = ptr(workspace)
+        if ksplit < 0:
+            nb = wino_blocks(cfg, B, H, W, N)
+            if counters is None or counters.numel() < nb or counters.dtype != torch.int32:
+                raise ValueError(f"Winograd fused split-K needs {nb} int32 arrival counters (zeroed)")
+            ctr_ptr = ptr(counters)
         kernels().conv_f32_forward(ptr(x), ptr(pc.wino), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C,
                                    OH, OW, N, 3, 3, 1, 1, 1, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),
-                                   stream_handle(stream), 0)
+                                   stream_handle(stream), ctr_ptr)
         return out
     if cfg not in F32_TILES:
         raise ValueError(f"unknown fp32 tile config {cfg}")

@@ -461,8 +461,7 @@ class SliceExecutor:
                 if ks != 1:
                     B, H, W, C, OH, OW, pc = self._conv_geom(i)
                     need = max(need, conv_ops.workspace_elems_f32(B * OH * OW, pc.cout, pc.Kpad, cfg, ks))
-                    if ks < 0:
-                        ctr = max(ctr, conv_ops.f32_sk_plan(B * OH * OW, pc.cout, pc.Kpad, cfg, -ks)[0])
+                    ctr = max(ctr, conv_ops.f32_counter_elems(cfg, ks, B, H, W, OH, OW, pc.cout, pc.Kpad))
                 continue
             if ks != 1:
                 B, H, W, C, OH, OW, pc = self._conv_geom(i)
@@ -546,7 +545,7 @@ class SliceExecutor:
                 if cfg in conv_ops.WINO_F32_CFGS:         # Winograd F(2x2,3x3): split-K over 16-channel chunks
                     nwm, fn = conv_ops.WINO_F32_CFGS[cfg]
                     tiles = math.ceil(B * ((OH + 1) // 2) * ((OW + 1) // 2) / (16 * nwm)) * (N // (16 * fn))
-                    kts, sks = C // 16, ()
+                    kts, sks = C // 16, (-2, -4)          # fused split-K (fixup in the kernel, <= 4 splits)
                 else:
                     bm, bn = conv_ops.F32_TILES[cfg]
                     tiles = math.ceil(M / bm) * math.ceil(N / bn)
@@ -558,10 +557,12 @@ class SliceExecutor:
                         continue
                     if ks < 0 and tiles >= 4 * conv_ops.NUM_CUS:
                         continue
+                    if ks < 0 and cfg in conv_ops.WINO_F32_CFGS and (kts // -ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
+                        continue
                     nws = conv_ops.workspace_elems_f32(M, N, pc.Kpad, cfg, ks)
                     ws = torch.empty(nws, dtype=torch.float32, device=self.device) if nws else None
-                    ctr = (torch.zeros(conv_ops.f32_sk_plan(M, N, pc.Kpad, cfg, -ks)[0], dtype=torch.int32,
-                                       device=self.device) if ks < 0 else None)
+                    nctr = conv_ops.f32_counter_elems(cfg, ks, B, H, W, OH, OW, N, pc.Kpad)
+                    ctr = torch.zeros(nctr, dtype=torch.int32, device=self.device) if nctr else None
                     try:
                         t = self._time_graph(lambda: conv_ops.conv_forward_f32(x, pc, out, cfg=cfg, ksplit=ks,
                                                                                workspace=ws, counters=ctr), reps)

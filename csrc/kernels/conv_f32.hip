@@ -268,7 +268,7 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
   ConvF32Params p{x, w, bias, res, out, ws, B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
                   B * OH * OW, K, Kpad, relu, ksplit == 0 ? 1 : ksplit, counters, 0};
   if (Kpad % FBK || (p.ksplit > 1 && ws == nullptr)) return hipErrorInvalidValue;
-  if (p.ksplit < 0) {
+  if (p.ksplit < 0 && cfg < 80) {
     // stream-K: v2 configs only
     int bm, bn, g;
     if (!conv_f32g_ok(cfg, Cin, N) || !conv_f32g_cfg_tile(cfg, &bm, &bn) || !ws || !counters)
@@ -287,11 +287,14 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
     default:
       if (cfg >= 80) {
         // Winograd F(2x2, 3x3) (conv_wino_f32.hip): w is the transformed, fragment-packed weight tensor
-        if (KH != 3 || KW != 3 || stride != 1 || pad_t != 1 || pad_l != 1 || OH != H || OW != W || p.ksplit < 1 ||
-            !conv_wino_f32_ok(cfg, Cin, N))
+        // ksplit < 0: split -ksplit ways with the fixup fused into the kernel (needs ws + counters)
+        if (KH != 3 || KW != 3 || stride != 1 || pad_t != 1 || pad_l != 1 || OH != H || OW != W ||
+            p.ksplit == 0 || p.ksplit == -1 || !conv_wino_f32_ok(cfg, Cin, N) ||
+            (p.ksplit < 0 && (!ws || !counters)))
           return hipErrorInvalidValue;
         const int th = (H + 1) / 2, tw = (W + 1) / 2;
-        WinoF32Params wp{x, w, bias, res, out, ws, B, H, W, Cin, N, th, tw, B * th * tw, relu, p.ksplit};
+        WinoF32Params wp{x, w, bias, res, out, ws, B, H, W, Cin, N, th, tw, B * th * tw, relu,
+                         p.ksplit < 0 ? -p.ksplit : p.ksplit, p.ksplit < 0 ? counters : nullptr};
         e = conv_wino_f32_launch(wp, cfg, s);
         break;
       }

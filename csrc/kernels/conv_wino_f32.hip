@@ -30,7 +30,8 @@
 // The accumulator layout puts all 16 positions of (tile, channel) in one lane,
 // so the output transform is lane-local: no shuffle, no LDS round trip.
 // Split-K (gridDim.z) writes the transformed partial outputs to fp32 slabs
-// (linear, so A^T (sum M) A = sum A^T M A); splitk_reduce_f32 adds bias / ReLU.
+// (linear, so A^T (sum M) A = sum A^T M A); splitk_reduce_f32 adds bias / ReLU,
+// or (fused split-K, p.counters) the last split of each output tile does.
 #include "kernels.h"
 
 namespace adapt {
@@ -41,20 +42,95 @@ typedef __attribute__((address_space(3))) void lds_void_w;
 
 __device__ __attribute__((aligned(64))) float g_wino_zero[64];
 
-// output transform A^T M A (lane-local) + bias / residual / ReLU, or a split-K slab (blockIdx.z);
-// acc[p][j][i] = M_p[tile tw0 + 4q + i][channel 16 (nf0 + j) + r]
-template <int FN, int ABL>
-__device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x4 (&acc)[16][FN], int tw0, int r,
-                                              int q, int nf0) {
-  const bool split = p.ksplit > 1;
-  float* dst = split ? p.ws + (size_t)blockIdx.z * p.B * p.H * p.W * p.N : p.out;
+constexpr int WINO_CPOL_SC1 = 16;   // gfx950 cache policy: sc1 (write-through L2, bypass L1)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+
+// fused split-K, last split of a block: out = act(sum_z slab_z + bias (+ res)) in split order, with
+// this split's own partials from registers; all (S - 1) x 4 x FN x 4 slab loads issue before the sum
+template <int FN, int S>
+__device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (&yk)[4][FN][4], const int (&ok)[4],
+                                           int tw0, int r, int q, int nf0, __amdgpu_buffer_rsrc_t wsr, int MN) {
   const int tpi = p.TH * p.TW;
+  const int zs = blockIdx.z;
+  float ld[S][4][FN][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int tt = tw0 + 4 * q + i;
+    const int rr = tt - (tt / tpi) * tpi;
+    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int dy = k >> 1, dx = k & 1;
+        const bool in = ok[i] >= 0 && oy + dy < p.H && ox + dx < p.W;
+        const int o = ok[i] + (dy * p.W + dx) * p.N + (nf0 + j) * 16 + r;
+#pragma unroll
+        for (int z = 0; z < S; ++z)
+          ld[z][i][j][k] = (in && z < p.ksplit && z != zs)
+                               ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                               wsr, (z * MN + o) * 4, 0, WINO_CPOL_SC1))
+                               : 0.f;
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (ok[i] < 0) continue;
+    const int tt = tw0 + 4 * q + i;
+    const int rr = tt - (tt / tpi) * tpi;
+    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = (nf0 + j) * 16 + r;
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int dy = k >> 1, dx = k & 1;
+        if (oy + dy >= p.H || ox + dx >= p.W) continue;
+        const int o = ok[i] + (dy * p.W + dx) * p.N + n;
+        float v = 0.f;
+#pragma unroll
+        for (int z = 0; z < S; ++z)
+          if (z < p.ksplit) v += z == zs ? yk[i][j][k] : ld[z][i][j][k];
+        v += bn;
+        if (p.res) v += p.res[o];
+        p.out[o] = act_relu(v, p.relu);
+      }
+    }
+  }
+}
+
+// output transform A^T M A (lane-local) + bias / residual / ReLU, or a split-K slab (blockIdx.z);
+// acc[p][j][i] = M_p[tile tw0 + 4q + i][channel 16 (nf0 + j) + r]
+//
+// Fused split-K (p.counters set, cfgs with ksplit < 0 on the host): every split stores its
+// transformed partial outputs to its slab with sc1 stores, one lane counts the arrival of the
+// (tile group, channel group), and the last split to arrive re-reads the others' slabs (sc1) in
+// split order -- deterministic, whoever is last -- and runs the epilogue: no splitk_reduce_f32
+// launch.  Nobody waits on anybody, so the grid never needs to be co-resident.
+template <int FN, int ABL>
+__device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x4 (&acc)[16][FN], int tw0, int r,
+                                              int q, int nf0, int* flag) {
+  const bool split = p.ksplit > 1;
+  const bool fused = split && p.counters != nullptr;
+  float* dst = split ? p.ws + (size_t)blockIdx.z * p.B * p.H * p.W * p.N : p.out;
+  const int tpi = p.TH * p.TW;
+  const int MN = p.B * p.H * p.W * p.N;
+  const __amdgpu_buffer_rsrc_t wsr = wino_ws_rsrc(p.ws);
+  float yk[4][FN][4];                                 // fused: this split's partial outputs
+  int ok[4];                                          // their NHWC offsets at channel 0 (-1: outside)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tt = tw0 + 4 * q + i;
+    ok[i] = -1;
     if (tt >= p.T) continue;
     const int im = tt / tpi, rr = tt - im * tpi;
     const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+    ok[i] = ((im * p.H + oy) * p.W + ox) * p.N;
+    const bool iny = oy + 1 < p.H, inx = ox + 1 < p.W;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = (nf0 + j) * 16 + r;
@@ -79,17 +155,39 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
       for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
-          if (oy + dy >= p.H || ox + dx >= p.W) continue;
-          const size_t o = (((size_t)im * p.H + oy + dy) * p.W + ox + dx) * p.N + n;
+          if ((dy && !iny) || (dx && !inx)) continue;
+          const int o = ok[i] + (dy * p.W + dx) * p.N + n;
           float v = y[dy][dx] + bn;
+          if (fused) {
+            yk[i][j][dy * 2 + dx] = v;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), wsr,
+                                                  (int)((blockIdx.z * (size_t)MN + o) * 4), 0, WINO_CPOL_SC1);
+            continue;
+          }
           if (!split) {
             if (p.res) v += p.res[o];
             v = act_relu(v, p.relu);
           }
           if constexpr (ABL & 4) asm volatile("" ::"v"(v));
-          else dst[o] = v;
+          else dst[(size_t)o] = v;
         }
     }
+  }
+  if (!fused) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* ctr = p.counters + blockIdx.x + gridDim.x * blockIdx.y;
+    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == p.ksplit - 1;
+    if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  switch (p.ksplit) {                                 // every other slab's loads in flight together
+    case 2: wino_fixup<FN, 2>(p, yk, ok, tw0, r, q, nf0, wsr, MN); break;
+    default: wino_fixup<FN, 4>(p, yk, ok, tw0, r, q, nf0, wsr, MN); break;   // 3 or 4
   }
 }
 
@@ -113,6 +211,7 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void co
   constexpr int PPW = (PIECES + NWM - 1) / NWM;      // pieces per wave
   constexpr int SLOT = PIECES * 1024;
   __shared__ __attribute__((aligned(16))) char ring[STAGES * SLOT];
+  __shared__ int last_flag;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -225,7 +324,7 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void co
     }
   }
 
-  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0);
+  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0, &last_flag);
 }
 
 // ---------------------------------------------------------------------------
@@ -243,13 +342,32 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void co
 // same image with the next chunk (only this wave reads it, so no barrier is
 // needed), which keeps the next chunk's input in flight under this chunk's
 // MFMAs without a second register set.  The weight ring is as in v1.
-template <int NW, int FN>
+//
+// SW (cfgs 103-105): the wave image is bank-swizzled.  Unswizzled, quad q of
+// pixel P sits in 16-B slot 4P + q, i.e. at position 4(P & 3) + q of its 256-B
+// bank row; consecutive tiles are 2 pixels apart, so a ds_read_b128 lane group
+// ({0-3,12-15,20-27}, ...) lands on 4 positions: 4-way conflicts, 256 LDS cycles
+// per wave per chunk for the 16 patch reads (329 at stage 4).  With SW the
+// position is XORed with h(row) = (2 row + 8 (row >> 2)) & 15, row = slot >> 4
+// (a bijection inside each bank row; the LDS-DMA lanes fetch the inverse-mapped
+// pixel / quad, since a DMA piece lands lane-linear): 73 / 110 / 142 / 64 cycles
+// for stages 2-5 (tools/wino_swizzle_search.py, exhaustive over that family).
+__device__ __forceinline__ int wino_sw(int slot) {
+  const int row = slot >> 4;
+  return slot ^ ((2 * row + 8 * (row >> 2)) & 15);
+}
+
+// EP (cfgs 106-108): each wave reads the next chunk's patch from its image right after its own
+// MFMAs of this chunk (its LDS-DMA has had the whole chunk to land), before the chunk barrier,
+// instead of every wave reading its patch right after the barrier while no MFMA runs.
+template <int NW, int FN, bool SW = false, bool EP = false>
 __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
   constexpr int PMAX = 10;                           // 1 KiB input pieces per wave (<= 160 pixels)
   constexpr int PIECES = 16 * FN;
   constexpr int PPW = (PIECES + NW - 1) / NW;
   constexpr int SLOT = PIECES * 1024;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + NW * PMAX * 1024];
+  __shared__ int last_flag;
   char* ring = smem;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -284,7 +402,8 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
   unsigned src_ok = 0;
 #pragma unroll
   for (int i = 0; i < PMAX; ++i) {
-    const int pix = i * 16 + (lane >> 2), qq = lane & 3;
+    const int sl = SW ? wino_sw(i * 64 + lane) : i * 64 + lane;   // the slot this lane's DMA fills holds
+    const int pix = sl >> 2, qq = sl & 3;                          // (pixel, quad); wino_sw is an involution
     int sg = 0;
 #pragma unroll
     for (int k = 1; k < 4; ++k) sg += pix >= seg_b[k] ? 1 : 0;
@@ -316,7 +435,8 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
   const int pb0 = tsg == 0 ? seg_b[0] : tsg == 1 ? seg_b[1] : tsg == 2 ? seg_b[2] : seg_b[3];
   const int plo = tsg == 0 ? seg_lo[0] : 0;
   const int prow0 = t < p.T ? pb0 + 2 * (t - (R0 + tsg) * p.TW - plo) : 0;
-  const char* prd = pimg + (prow0 * 4 + q) * 16;
+  const int ps0 = prow0 * 4 + q;                     // slot of patch pixel (0, 0)
+  const char* prd = pimg + ps0 * 16;
   const int pws = pw * 64;                           // bytes per patch-row step
 
   const float* ub = p.u + (size_t)nf0 * 16 * 256;
@@ -338,22 +458,35 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (kc0 < kc1) {
-    issue_w(kc0, 0);
-    issue_x(kc0);
-  }
-  for (int kc = kc0; kc < kc1; ++kc) {
-    const int slot = (kc - kc0) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                    // all weight pieces of chunk kc in; the other slot is free
-    asm volatile("" ::: "memory");
-    if (kc + 1 < kc1) issue_w(kc + 1, slot ^ 1);
-    f32x4 d[4][4];
+  f32x4 d[4][4];
+  auto read_patch = [&]() {
 #pragma unroll
     for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
-      for (int dx = 0; dx < 4; ++dx) d[dy][dx] = *(const f32x4*)(prd + dy * pws + dx * 64);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int dx = 0; dx < 4; ++dx) {
+        if constexpr (SW) d[dy][dx] = *(const f32x4*)(pimg + wino_sw(ps0 + dy * pw * 4 + dx * 4) * 16);
+        else d[dy][dx] = *(const f32x4*)(prd + dy * pws + dx * 64);
+      }
+  };
+  if (kc0 < kc1) {
+    issue_w(kc0, 0);
+    issue_x(kc0);
+    if constexpr (EP) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      read_patch();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  for (int kc = kc0; kc < kc1; ++kc) {
+    const int slot = (kc - kc0) & 1;
+    if constexpr (!EP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                    // all weight pieces of chunk kc in; the other slot is free
+    asm volatile("" ::: "memory");
+    if (kc + 1 < kc1) issue_w(kc + 1, slot ^ 1);
+    if constexpr (!EP) {
+      read_patch();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     if (kc + 1 < kc1) issue_x(kc + 1);               // this wave's image is free again: refill it
 
 #pragma unroll
@@ -384,18 +517,27 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
             acc[pa * 4 + pb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[pb][s], u[j][s], acc[pa * 4 + pb][j], 0, 0, 0);
       }
     }
+    if constexpr (EP) {
+      // the next chunk's patch, read while the other waves still run this chunk's MFMAs: the
+      // barrier no longer releases every wave into the same LDS burst
+      if (kc + 1 < kc1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        read_patch();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
   }
-  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0);
+  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, &last_flag);
 }
 
 // v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
 bool wino_v2_shape_ok(int TW) { return TW >= 5 || TW == 4; }
 
-template <int NW, int FN>
+template <int NW, int FN, bool SW, bool EP>
 hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW)) return hipErrorInvalidValue;
   const dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
-  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
@@ -428,15 +570,22 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(95, 4, 2, 2, false, 5) \
   X(98, 4, 2, 2, false, 8) \
   X(99, 4, 2, 2, false, 9)
-// v2 (input patches staged by LDS-DMA): id -> waves, 16-channel output fragments per wave
-#define ADAPT_WINO2_CFGS(X) \
-  X(100, 8, 2)              \
-  X(101, 8, 1)              \
-  X(102, 4, 1)
+// v2 (input patches staged by LDS-DMA): id -> waves, 16-channel output fragments per wave, swizzled image,
+// early patch read
+#define ADAPT_WINO2_CFGS(X)      \
+  X(100, 8, 2, false, false)     \
+  X(101, 8, 1, false, false)     \
+  X(102, 4, 1, false, false)     \
+  X(103, 8, 2, true, false)      \
+  X(104, 8, 1, true, false)      \
+  X(105, 4, 1, true, false)      \
+  X(106, 8, 2, true, true)       \
+  X(107, 8, 1, true, true)       \
+  X(108, 4, 1, true, true)
 
 bool conv_wino_f32_ok(int cfg, int C, int N) {
   switch (cfg) {
-#define X(id, NW_, FN_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
+#define X(id, NW_, FN_, SW_, EP_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
@@ -449,8 +598,10 @@ bool conv_wino_f32_ok(int cfg, int C, int N) {
 hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) {
   if (p.C % 16 || p.ksplit < 1 || p.T != p.B * p.TH * p.TW) return hipErrorInvalidValue;
   if (p.ksplit > 1 && !p.ws) return hipErrorInvalidValue;
+  if (p.counters && (p.ksplit < 2 || p.ksplit > 4 || (size_t)p.ksplit * p.B * p.H * p.W * p.N * 4 > 0x7fffffffu))
+    return hipErrorInvalidValue;                     // fused split-K: 32-bit slab offsets
   switch (cfg) {
-#define X(id, NW_, FN_) case id: return launch_wino_v2<NW_, FN_>(p, s);
+#define X(id, NW_, FN_, SW_, EP_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_>(p, s);
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return launch_wino<NWM_, FN_, S_, PF_, A_>(p, s);

@@ -135,6 +135,8 @@ struct WinoF32Params {
   int B, H, W, C, N;
   int TH, TW, T;      // 2x2 output tiles per column / row of an image, B * TH * TW
   int relu, ksplit;
+  int* counters;      // fused split-K: one arrival counter per (tile group, channel group) block, zero
+                      // before the launch, left zero after it (no splitk_reduce_f32 launch)
 };
 bool conv_wino_f32_ok(int cfg, int C, int N);
 hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);

@@ -77,9 +77,16 @@ def test_pack_conv_f32_attaches_wino_only_to_3x3_s1_p1():
     assert C.pack_conv_f32(k1, np.zeros(64, np.float32), 1, ((0, 0), (0, 0)), "cpu").wino is None
 
 
-def _v2_lane_maps(tw0, T, TW, TH, H, W):
+def _wino_sw(slot):
+    """conv_wino_f32.hip wino_sw: the bank swizzle of the v2 wave image (cfgs 103-105)."""
+    row = slot >> 4
+    return slot ^ ((2 * row + 8 * (row >> 2)) & 15)
+
+
+def _v2_lane_maps(tw0, T, TW, TH, H, W, sw=False):
     """conv_wino_f32_v2_kernel's wave-image bookkeeping, transcribed: the LDS-DMA source of every
-    (piece, lane) slot and every lane's patch pixel index; returns (dma, reads) for checking."""
+    (piece, lane) slot and every lane's patch pixel index; returns (dma, reads) for checking.
+    With `sw` the DMA of LDS slot S fetches logical slot wino_sw(S), and dma is keyed by LDS slot."""
     TR_ = T // TW
     tlast = min(tw0 + 15, T - 1)
     R0 = tw0 // TW
@@ -94,7 +101,8 @@ def _v2_lane_maps(tw0, T, TW, TH, H, W):
     dma = {}
     for i in range(10):
         for lane in range(64):
-            pix, qq = i * 16 + (lane >> 2), lane & 3
+            sl = _wino_sw(i * 64 + lane) if sw else i * 64 + lane
+            pix, qq = sl >> 2, sl & 3
             sg = sum(1 for k in (1, 2, 3) if pix >= seg_b[k])
             wdt, lo, bb = seg_w[sg], (seg_lo[0] if sg == 0 else 0), seg_b[sg]
             lp = pix - bb
@@ -104,7 +112,7 @@ def _v2_lane_maps(tw0, T, TW, TH, H, W):
             img, ty = R // TH, R % TH
             iy, ix = 2 * ty - 1 + prow, 2 * lo - 1 + pcol
             inside = pix < seg_b[4] and R < TR_ and 0 <= iy < H and 0 <= ix < W
-            dma[pix * 4 + qq] = (img, iy, ix) if inside else None
+            dma[i * 64 + lane] = (img, iy, ix) if inside else None
     reads = {}
     for r in range(16):
         t = tw0 + r
@@ -118,14 +126,15 @@ def _v2_lane_maps(tw0, T, TW, TH, H, W):
     return dma, reads, seg_b[4]
 
 
+@pytest.mark.parametrize("sw", [False, True])
 @pytest.mark.parametrize("B,H,W", [(3, 56, 56), (2, 28, 28), (3, 14, 14), (5, 7, 7), (2, 9, 13), (2, 8, 8)])
-def test_wino_v2_wave_image_bookkeeping(B, H, W):
+def test_wino_v2_wave_image_bookkeeping(B, H, W, sw):
     """Every lane's 16 patch pixels come from the LDS slots that the wave's LDS-DMA filled with exactly
     that image pixel (or zeros outside the image), within the 10 KiB wave image, for every wave."""
     TH, TW = (H + 1) // 2, (W + 1) // 2
     T = B * TH * TW
     for tw0 in range(0, T, 16):
-        dma, reads, total = _v2_lane_maps(tw0, T, TW, TH, H, W)
+        dma, reads, total = _v2_lane_maps(tw0, T, TW, TH, H, W, sw)
         assert total <= 160
         for (r, dy, dx), pix in reads.items():
             assert 0 <= pix < 160
@@ -135,4 +144,11 @@ def test_wino_v2_wave_image_bookkeeping(B, H, W):
             iy, ix = 2 * ty - 1 + dy, 2 * tx - 1 + dx
             want = (img, iy, ix) if 0 <= iy < H and 0 <= ix < W else None
             for qq in range(4):
-                assert dma[pix * 4 + qq] == want, (tw0, r, dy, dx)
+                slot = pix * 4 + qq
+                assert dma[_wino_sw(slot) if sw else slot] == want, (tw0, r, dy, dx)
+
+
+def test_wino_v2_swizzle_is_a_bank_row_involution():
+    for s in range(640):
+        t = _wino_sw(s)
+        assert t >> 4 == s >> 4 and _wino_sw(t) == s

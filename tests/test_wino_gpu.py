@@ -21,10 +21,12 @@ SHAPES = [  # (B, H, W, Cin, Cout, residual, relu)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("ksplit", [1, 2, 4])
+@pytest.mark.parametrize("ksplit", [1, 2, 4, -2, -4])
 def test_wino_f32_matches_fp64(shape, ksplit):
+    """ksplit < 0: fused split-K (the last split of each block adds the slabs in the kernel); run
+    twice so the second launch also checks that the first left its arrival counters zero."""
     B, H, W, Cin, Cout, has_res, relu = shape
-    if ksplit > Cin // 16:
+    if abs(ksplit) > Cin // 16:
         pytest.skip("split-K beyond the 16-channel chunks")
     rng = np.random.default_rng(hash(shape) % 2**32)
     x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
@@ -42,13 +44,35 @@ def test_wino_f32_matches_fp64(shape, ksplit):
     for cfg in C.WINO_F32_CFGS:
         if not C.f32_cfg_supported(cfg, Cin, Cout, pc) or not C.wino_map_ok(cfg, H, W):
             continue
-        out.fill_(float("nan"))
-        C.conv_forward_f32(xd, pc, out, rd, relu=relu, cfg=cfg, ksplit=ksplit)
-        got = out.cpu().numpy()
-        err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
-        assert np.isfinite(got).all() and err < 2e-5, f"cfg {cfg} ksplit {ksplit}: rel err {err}"
+        ctr = None
+        if ksplit < 0:
+            ctr = torch.zeros(C.wino_blocks(cfg, B, H, W, Cout), dtype=torch.int32, device="cuda")
+        for rep in range(2 if ksplit < 0 else 1):
+            out.fill_(float("nan"))
+            C.conv_forward_f32(xd, pc, out, rd, relu=relu, cfg=cfg, ksplit=ksplit, counters=ctr)
+            got = out.cpu().numpy()
+            err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
+            assert np.isfinite(got).all() and err < 2e-5, f"cfg {cfg} ksplit {ksplit} rep {rep}: rel err {err}"
+        if ctr is not None:
+            assert int(ctr.abs().sum()) == 0, "fused split-K left arrival counters non-zero"
         ran += 1
     assert ran > 0
+
+
+def test_wino_f32_fused_split_matches_slab_split():
+    """Fused split-K sums the same slabs in the same (split) order as splitk_reduce_f32."""
+    B, H, W, Cin, Cout = 4, 14, 14, 256, 256
+    rng = np.random.default_rng(7)
+    kern = (rng.standard_normal((3, 3, Cin, Cout)) / np.sqrt(9 * Cin)).astype(np.float32)
+    pc = C.pack_conv_f32(kern, rng.standard_normal(Cout).astype(np.float32), 1, ((1, 1), (1, 1)), "cuda")
+    xd = torch.from_numpy(rng.standard_normal((B, H, W, Cin)).astype(np.float32)).cuda()
+    a = torch.empty((B, H, W, Cout), device="cuda")
+    b = torch.empty_like(a)
+    for cfg in (103, 105):
+        ctr = torch.zeros(C.wino_blocks(cfg, B, H, W, Cout), dtype=torch.int32, device="cuda")
+        C.conv_forward_f32(xd, pc, a, relu=1, cfg=cfg, ksplit=4)
+        C.conv_forward_f32(xd, pc, b, relu=1, cfg=cfg, ksplit=-4, counters=ctr)
+        assert torch.equal(a, b), f"cfg {cfg}: fused and slab split-K differ"
 
 
 def test_wino_f32_rejects_other_convs():

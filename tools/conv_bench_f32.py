@@ -35,14 +35,14 @@ def bench(shape, only=None, ks_list=(1, 2, 4, -1, -2), reps=10, top=20):
             continue
         wino = cfg in C.WINO_F32_CFGS or cfg in C.WINO_F32_ABLATE
         for ks in ks_list:
-            if ks > 1 and (Cin // 16 if wino else pc.Kpad // C.F32_BK) // ks < 2:
+            if abs(ks) > 1 and (wino or ks > 0) and (Cin // 16 if wino else pc.Kpad // C.F32_BK) // abs(ks) < 2:
                 continue
-            if ks < 0 and cfg not in C.F32G_CFGS:
+            if ks < 0 and cfg not in C.F32G_CFGS and not (wino and ks <= -2):
                 continue
             nws = C.workspace_elems_f32(M, N, pc.Kpad, cfg, ks)
             ws = torch.empty(nws, device=dev) if nws else None
-            ctr = (torch.zeros(C.f32_sk_plan(M, N, pc.Kpad, cfg, -ks)[0], device=dev, dtype=torch.int32)
-                   if ks < 0 else None)
+            nctr = C.f32_counter_elems(cfg, ks, B, H, W, OH, OW, N, pc.Kpad)
+            ctr = torch.zeros(nctr, device=dev, dtype=torch.int32) if nctr else None
             try:
                 def run():
                     C.conv_forward_f32(x, pc, out, residual=res, relu=1, cfg=cfg, ksplit=ks, workspace=ws,

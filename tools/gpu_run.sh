@@ -19,6 +19,9 @@
 #   hang      4-stage wedged-stage (alive, no progress) recovery bench (device links)
 #   roof32    per-layer fp32 roofline table (two PMC passes over tools/roofline_r50.py --dtype fp32)
 #   cs3       channel-split 3x3 (stage 4/5) numerics, isolated timings vs the tile kernels, whole-model A/B
+#   wino      fp32 Winograd numerics + isolated timings of the v2 configs on the four ResNet-50 3x3 shapes
+#   pmcw      PMC passes over the fp32 Winograd kernel (tools/pmc_f32.sh), stage 2-5 shapes
+#   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -51,6 +54,10 @@ for p in "${P[@]}"; do
               steps+=("240|$out/cs3_ab|python -u tools/ab_cfg.py --model resnet50 --set 32x14x14x256,3x3s1p1111@73@1 --set 32x7x7x512,3x3s1p1111@73@1 --json gpurun_out/$out/cs3_ab.json") ;;
     roof32)   steps+=("400|$out/roof32_pmc|bash tools/pmc_groups.sh gpurun_out/$out/roof32 'SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT' 'TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum' -- tools/roofline_r50.py --run --dtype fp32 --meta $PWD/gpurun_out/$out/roof32/meta.json")
               steps+=("60|$out/roof32_table|python tools/roofline_r50.py --table gpurun_out/$out/roof32 --meta gpurun_out/$out/roof32/meta.json --json gpurun_out/$out/roof32/roofline_fp32.json") ;;
+    wino)     steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py tests/test_wino.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108 --ks 1,2,4,-2,-4") ;;
+    pmcw)     steps+=("500|$out/pmcw|bash tools/pmc_f32.sh gpurun_out/$out/pmcw 32,56,56,64,64,3,1,1,0:106:1 32,56,56,64,64,3,1,1,0:103:1 32,28,28,128,128,3,1,1,0:106:1 32,28,28,128,128,3,1,1,0:103:1 32,14,14,256,256,3,1,1,0:108:1 32,14,14,256,256,3,1,1,0:105:1") ;;
+    pmc1x1)   steps+=("500|$out/pmc1x1|bash tools/pmc_f32.sh gpurun_out/$out/pmc1x1 32,14,14,1024,256,1,1,0,0:18:-2 32,14,14,256,1024,1,1,0,1:38:1 32,56,56,64,256,1,1,0,1:3:1 32,28,28,512,1024,1,2,0,0:20:-1") ;;
     *) echo "unknown preset $p"; exit 2 ;;
   esac
 done
