@@ -211,7 +211,6 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void co
   constexpr int PPW = (PIECES + NWM - 1) / NWM;      // pieces per wave
   constexpr int SLOT = PIECES * 1024;
   __shared__ __attribute__((aligned(16))) char ring[STAGES * SLOT];
-  __shared__ int last_flag;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -324,7 +323,7 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void co
     }
   }
 
-  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0, &last_flag);
+  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0, (int*)ring);
 }
 
 // ---------------------------------------------------------------------------
@@ -367,7 +366,6 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
   constexpr int PPW = (PIECES + NW - 1) / NW;
   constexpr int SLOT = PIECES * 1024;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + NW * PMAX * 1024];
-  __shared__ int last_flag;
   char* ring = smem;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -527,7 +525,10 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
       }
     }
   }
-  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, &last_flag);
+  // the fused split-K arrival flag lives in the ring (dead after the loop): a second __shared__ object
+  // makes the compiler's LDS-DMA alias tracking put a vmcnt(0) between every chunk's weight DMA issue
+  // and the patch reads, which serialises the whole prefetch
+  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem);
 }
 
 // v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
