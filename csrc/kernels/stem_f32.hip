@@ -139,16 +139,30 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
       const int ow = min(c0 + fr, OW - 1);                      // ragged last tile: clamp the read, skip the store
       const int ihb = 2 * r - pad_t;                            // input row of filter row 0
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int h = 0; h < SF_KH; ++h) {
+      // ring row of filter row s: (ihb + s) mod 16 with ihb + s + 64 > 0, so a mask, not a signed %
+      const unsigned rb = (unsigned)(ihb + 4 * SF_RING);
+      const float* pcol = patch + SF_OFF + 6 * ow;
+      auto bop = [&](int h) {
         const int s = koff[h] >> 16, j = koff[h] & 0xffff;
-        const float* src = patch + ((ihb + s + 4 * SF_RING) % SF_RING) * SF_ROWLEN + SF_OFF + 6 * ow + j;
+        const float* src = pcol + ((rb + s) & (SF_RING - 1)) * SF_ROWLEN + j;
         const f32x2 lo = *(const f32x2*)src, hi = *(const f32x2*)(src + 2);
-        const f32x4 pb = {lo[0], lo[1], hi[0], hi[1]};
+        return (f32x4){lo[0], lo[1], hi[0], hi[1]};
+      };
+      // the even / odd K halves alternate MFMA by MFMA: two independent chains back to back
+      // instead of runs of four dependent MFMAs (40-cycle dependent latency vs 32-cycle issue)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (h & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb[e], acc1, 0, 0, 0);
-          else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb[e], acc0, 0, 0, 0);
+      for (int h = 0; h < SF_KH; h += 2) {
+        const f32x4 pb0 = bop(h);
+        if (h + 1 < SF_KH) {
+          const f32x4 pb1 = bop(h + 1);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb0[e], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], pb1[e], acc1, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb0[e], acc0, 0, 0, 0);
         }
       }
       // C^T fragment: channel = 16ct + 4fq + e, pixel = c0 + fr
