@@ -398,9 +398,14 @@ def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int
         return ksplit * M * N
     if ksplit < 0:
         if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
-            return -ksplit * M * N
+            return (4 if ksplit <= WINO_SK_BASE else -ksplit) * M * N    # stream-K: <= 4 partials per unit
         return f32_sk_plan(M, N, Kpad, cfg, -ksplit)[3]
     return 0
+
+
+def wino_sk_plan(cfg: int, B: int, H: int, W: int, N: int, C: int, ksplit: int):
+    """(grid, iterations per block, most partials of one unit) of a stream-K Winograd launch."""
+    return tuple(kernels().conv_wino_sk_plan(wino_blocks(cfg, B, H, W, N), C // 16, WINO_SK_BASE - ksplit))
 
 
 def wino_blocks(cfg: int, B: int, H: int, W: int, N: int) -> int:
@@ -426,8 +431,12 @@ WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85:
                  86: (4, 2), 87: (4, 3), 88: (8, 1),          # 86-88: the next chunk's patch prefetched
                  100: (8, 2), 101: (8, 1), 102: (4, 1),       # v2: input patches staged in LDS by LDS-DMA
                  103: (8, 2), 104: (8, 1), 105: (4, 1),       # v2 with the bank-swizzled wave image
-                 106: (8, 2), 107: (8, 1), 108: (4, 1)}       # ... and the next patch read before the barrier
-WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108))
+                 106: (8, 2), 107: (8, 1), 108: (4, 1),       # ... and the next patch read before the barrier
+                 110: (8, 2), 111: (8, 2), 112: (4, 1), 113: (4, 1), 114: (8, 1)}   # stream-K twins
+WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114))
+# stream-K Winograd configs: ksplit <= -100 means (-ksplit - 100) x 256 blocks over the (unit, chunk) space
+WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114))
+WINO_SK_BASE = -100
 
 
 def wino_map_ok(cfg: int, H: int, W: int) -> bool:
@@ -548,16 +557,21 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         # ksplit > 1: slabs + splitk_reduce_f32; ksplit <= -2: -ksplit slabs, the last split of
         # each block adds them in split order inside the kernel (needs `counters`)
+        # ksplit <= -100 (stream-K configs only): (-ksplit - 100) x 256 blocks over the (unit, chunk) space
         ksplit = int(ksplit) or 1
+        sk = ksplit <= WINO_SK_BASE
         if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or ksplit == -1 \
-                or not wino_map_ok(cfg, H, W):
+                or not wino_map_ok(cfg, H, W) or sk != (cfg in WINO_SK_CFGS):
             raise ValueError(f"Winograd config {cfg}: 3x3/s1/p1 conv with transformed weights, C % 16 == 0, "
-                             f"N % 16 * fragments == 0, split-K >= 1 or fused split-K <= -2")
-        if abs(ksplit) > (C // 16) or ksplit < -4:
+                             f"N % 16 * fragments == 0, split-K >= 1 or fused split-K <= -2; stream-K configs "
+                             f"{sorted(WINO_SK_CFGS)} take ksplit <= {WINO_SK_BASE}")
+        if not sk and (abs(ksplit) > (C // 16) or ksplit < -4):
             raise ValueError(f"Winograd split-K {ksplit} exceeds the {C // 16} channel chunks (fused: <= 4 splits)")
+        if sk and wino_sk_plan(cfg, B, H, W, N, C, ksplit)[2] > 4:
+            raise ValueError("Winograd stream-K would cut a unit into more than 4 partials")
         ws_ptr = ctr_ptr = 0
         if ksplit != 1:
-            need = abs(ksplit) * M * N
+            need = workspace_elems_f32(M, N, pc.Kpad, cfg, ksplit)
             if need * 4 > 0x7fffffff:
                 raise ValueError("Winograd split-K slabs beyond 2 GiB")
             if workspace is None:
@@ -568,7 +582,7 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         if ksplit < 0:
             nb = wino_blocks(cfg, B, H, W, N)
             if counters is None or counters.numel() < nb or counters.dtype != torch.int32:
-                raise ValueError(f"Winograd fused split-K needs {nb} int32 arrival counters (zeroed)")
+                raise ValueError(f"Winograd fused split-K / stream-K needs {nb} int32 arrival counters (zeroed)")
             ctr_ptr = ptr(counters)
         kernels().conv_f32_forward(ptr(x), ptr(pc.wino), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C,
                                    OH, OW, N, 3, 3, 1, 1, 1, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),

@@ -546,18 +546,20 @@ class SliceExecutor:
                     nwm, fn = conv_ops.WINO_F32_CFGS[cfg]
                     tiles = math.ceil(B * ((OH + 1) // 2) * ((OW + 1) // 2) / (16 * nwm)) * (N // (16 * fn))
                     kts, sks = C // 16, (-2, -4)          # fused split-K (fixup in the kernel, <= 4 splits)
+                    if cfg in conv_ops.WINO_SK_CFGS:       # stream-K twins: 1 or 2 x 256 blocks only
+                        kts, sks = C // 16, (conv_ops.WINO_SK_BASE - 1, conv_ops.WINO_SK_BASE - 2)
                 else:
                     bm, bn = conv_ops.F32_TILES[cfg]
                     tiles = math.ceil(M / bm) * math.ceil(N / bn)
                     kts = ktiles
                     sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
-                for ks in (1, 2, 4, 8, 16) + sks:
+                for ks in ((1, 2, 4, 8, 16) if cfg not in conv_ops.WINO_SK_CFGS else ()) + sks:
                     # split-K / stream-K only where the tiles alone leave CUs idle
                     if ks > 1 and (kts // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue
                     if ks < 0 and tiles >= 4 * conv_ops.NUM_CUS:
                         continue
-                    if ks < 0 and cfg in conv_ops.WINO_F32_CFGS and (kts // -ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
+                    if -100 < ks < 0 and cfg in conv_ops.WINO_F32_CFGS and (kts // -ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue
                     nws = conv_ops.workspace_elems_f32(M, N, pc.Kpad, cfg, ks)
                     ws = torch.empty(nws, dtype=torch.float32, device=self.device) if nws else None

@@ -194,6 +194,11 @@ PYBIND11_MODULE(_C, m) {
      py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("N"), py::arg("KH"),
      py::arg("KW"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("K"), py::arg("Kpad"),
      py::arg("relu"), py::arg("ksplit"), py::arg("cfg"), py::arg("s"), py::arg("counters") = 0);
+  m.def("conv_wino_sk_plan", [](int units, int kc, int mult) {
+    int g, it, smax;
+    adapt::conv_wino_sk_plan(units, kc, mult, &g, &it, &smax);
+    return py::make_tuple(g, it, smax);
+  });
   m.def("conv_f32g_sk_plan", [](int tiles, int kt, int mult) {
     int g = 0, it = 0;
     adapt::conv_f32g_sk_plan(tiles, kt, mult, &g, &it);

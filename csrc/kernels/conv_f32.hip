@@ -287,14 +287,25 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
     default:
       if (cfg >= 80) {
         // Winograd F(2x2, 3x3) (conv_wino_f32.hip): w is the transformed, fragment-packed weight tensor
-        // ksplit < 0: split -ksplit ways with the fixup fused into the kernel (needs ws + counters)
+        // ksplit <= -100: stream-K over (-ksplit - 100) x 256 blocks; -100 < ksplit < 0: split -ksplit
+        // ways with the fixup fused into the kernel; both need ws + counters
         if (KH != 3 || KW != 3 || stride != 1 || pad_t != 1 || pad_l != 1 || OH != H || OW != W ||
             p.ksplit == 0 || p.ksplit == -1 || !conv_wino_f32_ok(cfg, Cin, N) ||
             (p.ksplit < 0 && (!ws || !counters)))
           return hipErrorInvalidValue;
         const int th = (H + 1) / 2, tw = (W + 1) / 2;
+        const bool sk = p.ksplit <= -100;
         WinoF32Params wp{x, w, bias, res, out, ws, B, H, W, Cin, N, th, tw, B * th * tw, relu,
-                         p.ksplit < 0 ? -p.ksplit : p.ksplit, p.ksplit < 0 ? counters : nullptr};
+                         sk ? 1 : (p.ksplit < 0 ? -p.ksplit : p.ksplit), p.ksplit < 0 ? counters : nullptr, 0,
+                         sk ? -p.ksplit - 100 : 0};
+        if (sk) {
+          int nw = 0, fn = 0;
+          if (!conv_wino_f32_cfg(cfg, &nw, &fn)) return hipErrorInvalidValue;
+          int G, iters, smax;
+          conv_wino_sk_plan(((wp.T + 16 * nw - 1) / (16 * nw)) * (N / (16 * fn)), Cin / 16, wp.sk_mult, &G, &iters,
+                            &smax);
+          wp.sk_iters = iters;
+        }
         e = conv_wino_f32_launch(wp, cfg, s);
         break;
       }

@@ -52,9 +52,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_ws_rsrc(const float* base
 // this split's own partials from registers; all (S - 1) x 4 x FN x 4 slab loads issue before the sum
 template <int FN, int S>
 __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (&yk)[4][FN][4], const int (&ok)[4],
-                                           int tw0, int r, int q, int nf0, __amdgpu_buffer_rsrc_t wsr, int MN) {
+                                           int tw0, int r, int q, int nf0, __amdgpu_buffer_rsrc_t wsr, int MN, int zs,
+                                           int ns) {
   const int tpi = p.TH * p.TW;
-  const int zs = blockIdx.z;
   float ld[S][4][FN][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -70,7 +70,7 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
         const int o = ok[i] + (dy * p.W + dx) * p.N + (nf0 + j) * 16 + r;
 #pragma unroll
         for (int z = 0; z < S; ++z)
-          ld[z][i][j][k] = (in && z < p.ksplit && z != zs)
+          ld[z][i][j][k] = (in && z < ns && z != zs)
                                ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                                wsr, (z * MN + o) * 4, 0, WINO_CPOL_SC1))
                                : 0.f;
@@ -94,7 +94,7 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
         float v = 0.f;
 #pragma unroll
         for (int z = 0; z < S; ++z)
-          if (z < p.ksplit) v += z == zs ? yk[i][j][k] : ld[z][i][j][k];
+          if (z < ns) v += z == zs ? yk[i][j][k] : ld[z][i][j][k];
         v += bn;
         if (p.res) v += p.res[o];
         p.out[o] = act_relu(v, p.relu);
@@ -113,10 +113,12 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
 // launch.  Nobody waits on anybody, so the grid never needs to be co-resident.
 template <int FN, int ABL>
 __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x4 (&acc)[16][FN], int tw0, int r,
-                                              int q, int nf0, int* flag) {
-  const bool split = p.ksplit > 1;
+                                              int q, int nf0, int* flag, int zs, int ns, int ctr_idx) {
+  // zs / ns: this partial's slab index / the partials of its output block (ns == 1: whole K);
+  // fused fixup when the host passed arrival counters, else slab ws[zs] for splitk_reduce_f32
+  const bool split = ns > 1;
   const bool fused = split && p.counters != nullptr;
-  float* dst = split ? p.ws + (size_t)blockIdx.z * p.B * p.H * p.W * p.N : p.out;
+  float* dst = split ? p.ws + (size_t)zs * p.B * p.H * p.W * p.N : p.out;
   const int tpi = p.TH * p.TW;
   const int MN = p.B * p.H * p.W * p.N;
   const __amdgpu_buffer_rsrc_t wsr = wino_ws_rsrc(p.ws);
@@ -161,7 +163,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
           if (fused) {
             yk[i][j][dy * 2 + dx] = v;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), wsr,
-                                                  (int)((blockIdx.z * (size_t)MN + o) * 4), 0, WINO_CPOL_SC1);
+                                                  (int)((zs * (size_t)MN + o) * 4), 0, WINO_CPOL_SC1);
             continue;
           }
           if (!split) {
@@ -177,18 +179,17 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    int* ctr = p.counters + blockIdx.x + gridDim.x * blockIdx.y;
+    int* ctr = p.counters + ctr_idx;
     const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == p.ksplit - 1;
+    const int last = old == ns - 1;
     if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = last;
   }
   __syncthreads();
-  if (!*flag) return;
-  switch (p.ksplit) {                                 // every other slab's loads in flight together
-    case 2: wino_fixup<FN, 2>(p, yk, ok, tw0, r, q, nf0, wsr, MN); break;
-    default: wino_fixup<FN, 4>(p, yk, ok, tw0, r, q, nf0, wsr, MN); break;   // 3 or 4
-  }
+  if (!*flag) return;                                // (a stream-K block's next segment starts with a barrier
+                                                      // before its DMA can reuse the flag's LDS word)
+  if (ns == 2) wino_fixup<FN, 2>(p, yk, ok, tw0, r, q, nf0, wsr, MN, zs, ns);   // other slabs' loads in flight
+  else wino_fixup<FN, 4>(p, yk, ok, tw0, r, q, nf0, wsr, MN, zs, ns);           // together (3 or 4)
 }
 
 // two waves per SIMD (<= 256 VGPRs) up to FN = 2 without prefetch; FN = 3 (192 accumulators) or the
@@ -323,7 +324,8 @@ __global__ __launch_bounds__(NWM * 64, (wino_min_blocks<NWM, FN, PF>())) void co
     }
   }
 
-  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0, (int*)ring);
+  wino_epilogue<FN, ABL>(p, acc, blockIdx.x * BT + wave * 16, r, q, nf0, (int*)ring, blockIdx.z, p.ksplit,
+                        blockIdx.x + gridDim.x * blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -359,28 +361,33 @@ __device__ __forceinline__ int wino_sw(int slot) {
 // EP (cfgs 106-108): each wave reads the next chunk's patch from its image right after its own
 // MFMAs of this chunk (its LDS-DMA has had the whole chunk to land), before the chunk barrier,
 // instead of every wave reading its patch right after the barrier while no MFMA runs.
-template <int NW, int FN, bool SW = false, bool EP = false>
-__global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
-  constexpr int PMAX = 10;                           // 1 KiB input pieces per wave (<= 160 pixels)
-  constexpr int PIECES = 16 * FN;
-  constexpr int PPW = (PIECES + NW - 1) / NW;
-  constexpr int SLOT = PIECES * 1024;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + NW * PMAX * 1024];
-  char* ring = smem;
+template <int NW, int FN>
+struct WinoV2Shape {
+  static constexpr int PMAX = 10;                    // 1 KiB input pieces per wave (<= 160 pixels)
+  static constexpr int PIECES = 16 * FN;
+  static constexpr int PPW = (PIECES + NW - 1) / NW;
+  static constexpr int SLOT = PIECES * 1024;
+  static constexpr int LDS = 2 * SLOT + NW * PMAX * 1024;
+};
 
+// one (tile group tg, channel group cg, K chunks [kc0, kc1)) unit of work; zs / ns / ctr_idx: its partial's
+// slab, the partials of its output block and their arrival counter (ns == 1: whole K, plain epilogue)
+template <int NW, int FN, bool SW, bool EP>
+__device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem, int tg, int cg, int kc0, int kc1,
+                                             int zs, int ns, int ctr_idx) {
+  using S = WinoV2Shape<NW, FN>;
+  constexpr int PMAX = S::PMAX, PIECES = S::PIECES, PPW = S::PPW, SLOT = S::SLOT;
+  char* ring = smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
   char* pimg = smem + 2 * SLOT + wave * PMAX * 1024;
-  const int nf0 = blockIdx.y * FN;
+  const int nf0 = cg * FN;
   const int NF = p.N / 16;
-  const int KC = p.C / 16;
-  const int kper = (KC + p.ksplit - 1) / p.ksplit;
-  const int kc0 = blockIdx.z * kper, kc1 = min(KC, kc0 + kper);
   const int TR = p.B * p.TH;                         // tile rows over the batch
 
   // ---- the wave's row segments (wave-uniform)
-  const int tw0 = (blockIdx.x * NW + wave) * 16;
+  const int tw0 = (tg * NW + wave) * 16;
   const int tlast = min(tw0 + 15, p.T - 1);
   const int R0 = tw0 / p.TW;
   const int nseg = tw0 < p.T ? tlast / p.TW - R0 + 1 : 0;
@@ -528,17 +535,76 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
   // the fused split-K arrival flag lives in the ring (dead after the loop): a second __shared__ object
   // makes the compiler's LDS-DMA alias tracking put a vmcnt(0) between every chunk's weight DMA issue
   // and the patch reads, which serialises the whole prefetch
-  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem);
+  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx);
+}
+
+// Stream-K (p.sk_iters > 0, cfgs 103-108 with ksplit <= -100 on the host): a 1-D grid of about
+// (-ksplit - 100) x 256 blocks, each taking sk_iters consecutive (unit, K-chunk) iterations of the
+// units x KC space (unit = channel group major, tile group minor).  A ResNet 3x3 has 196-400 units of
+// 4-16 chunks, i.e. 0.77-1.53 rounds of the 256 CUs: the last partial round idled 23-50 % of the chip.
+// Partial units meet through the fused fixup (deterministic, segment order).
+template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false>
+__global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[WinoV2Shape<NW, FN>::LDS];
+  const int KC = p.C / 16;
+  if constexpr (!SK) {
+    const int kper = (KC + p.ksplit - 1) / p.ksplit;
+    const int kc0 = blockIdx.z * kper;
+    wino_v2_unit<NW, FN, SW, EP>(p, smem, blockIdx.x, blockIdx.y, kc0, min(KC, kc0 + kper), blockIdx.z, p.ksplit,
+                                 blockIdx.x + gridDim.x * blockIdx.y);
+    return;
+  }
+  const bool sk = SK;
+  const int gx = (p.T + 16 * NW - 1) / (16 * NW);
+  const int iters = p.sk_iters;
+  int it = sk ? blockIdx.x * iters : 0;
+  const int it_end = sk ? min(gx * (p.N / (16 * FN)) * KC, it + iters) : 1;
+  while (it < it_end) {                              // one pass in grid mode: a single call site
+    int tg, cg, kb, ke, zs, ns, ctr;
+    if (!sk) {
+      const int kper = (KC + p.ksplit - 1) / p.ksplit;
+      tg = blockIdx.x;
+      cg = blockIdx.y;
+      kb = blockIdx.z * kper;
+      ke = min(KC, kb + kper);
+      zs = blockIdx.z;
+      ns = p.ksplit;
+      ctr = blockIdx.x + gridDim.x * blockIdx.y;
+    } else {
+      const int u = it / KC;
+      kb = it - u * KC;
+      ke = min(KC, kb + (it_end - it));
+      tg = u % gx;
+      cg = u / gx;
+      ctr = u;
+      zs = 0;
+      ns = 1;
+      if (kb != 0 || ke != KC) {
+        const int g_first = (u * KC) / iters, g_last = ((u + 1) * KC - 1) / iters;
+        zs = blockIdx.x - g_first;
+        ns = g_last - g_first + 1;
+      }
+      __syncthreads();                               // the previous segment's ring / flag / images are dead
+    }
+    wino_v2_unit<NW, FN, SW, EP>(p, smem, tg, cg, kb, ke, zs, ns, ctr);
+    it = sk ? it + (ke - kb) : it_end;
+  }
 }
 
 // v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
 bool wino_v2_shape_ok(int TW) { return TW >= 5 || TW == 4; }
 
-template <int NW, int FN, bool SW, bool EP>
+template <int NW, int FN, bool SW, bool EP, bool SK>
 hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
-  if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW)) return hipErrorInvalidValue;
-  const dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
-  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP>), grid, block, 0, s, p);
+  if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || SK != (p.sk_iters > 0)) return hipErrorInvalidValue;
+  dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
+  if (SK) {
+    int G, iters, smax;
+    conv_wino_sk_plan(grid.x * grid.y, p.C / 16, p.sk_mult, &G, &iters, &smax);
+    if (iters != p.sk_iters || smax > 4 || !p.counters || !p.ws) return hipErrorInvalidValue;
+    grid = dim3(G, 1, 1);
+  }
+  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP, SK>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
@@ -572,21 +638,55 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(98, 4, 2, 2, false, 8) \
   X(99, 4, 2, 2, false, 9)
 // v2 (input patches staged by LDS-DMA): id -> waves, 16-channel output fragments per wave, swizzled image,
-// early patch read
-#define ADAPT_WINO2_CFGS(X)      \
-  X(100, 8, 2, false, false)     \
-  X(101, 8, 1, false, false)     \
-  X(102, 4, 1, false, false)     \
-  X(103, 8, 2, true, false)      \
-  X(104, 8, 1, true, false)      \
-  X(105, 4, 1, true, false)      \
-  X(106, 8, 2, true, true)       \
-  X(107, 8, 1, true, true)       \
-  X(108, 4, 1, true, true)
+// early patch read, stream-K (110-114: the host passes ksplit <= -100)
+#define ADAPT_WINO2_CFGS(X)          \
+  X(100, 8, 2, false, false, false)  \
+  X(101, 8, 1, false, false, false)  \
+  X(102, 4, 1, false, false, false)  \
+  X(103, 8, 2, true, false, false)   \
+  X(104, 8, 1, true, false, false)   \
+  X(105, 4, 1, true, false, false)   \
+  X(106, 8, 2, true, true, false)    \
+  X(107, 8, 1, true, true, false)    \
+  X(108, 4, 1, true, true, false)    \
+  X(110, 8, 2, true, true, true)     \
+  X(111, 8, 2, true, false, true)    \
+  X(112, 4, 1, true, true, true)     \
+  X(113, 4, 1, true, false, true)    \
+  X(114, 8, 1, true, true, true)
+
+// stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
+// smax = the most partials one unit is cut into (the fused fixup takes <= 4)
+void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* smax) {
+  const long long total = (long long)units * kc;
+  long long G = 256LL * (mult > 0 ? mult : 1);
+  if (G > total) G = total;
+  const long long it = (total + G - 1) / G;
+  *iters = (int)it;
+  *grid = (int)((total + it - 1) / it);
+  int m = 1;
+  for (int u = 0; u < units; ++u) {
+    const long long g0 = ((long long)u * kc) / it, g1 = ((long long)(u + 1) * kc - 1) / it;
+    if (g1 - g0 + 1 > m) m = (int)(g1 - g0 + 1);
+  }
+  *smax = m;
+}
+
+bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
+  switch (cfg) {
+#define X(id, NW_, FN_, SW_, EP_, SK_) case id: *nw = NW_; *fn = FN_; return true;
+    ADAPT_WINO2_CFGS(X)
+#undef X
+#define X(id, NWM_, FN_, S_, PF_, A_) case id: *nw = NWM_; *fn = FN_; return true;
+    ADAPT_WINO_CFGS(X)
+#undef X
+  }
+  return false;
+}
 
 bool conv_wino_f32_ok(int cfg, int C, int N) {
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
+#define X(id, NW_, FN_, SW_, EP_, SK_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
@@ -599,10 +699,13 @@ bool conv_wino_f32_ok(int cfg, int C, int N) {
 hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) {
   if (p.C % 16 || p.ksplit < 1 || p.T != p.B * p.TH * p.TW) return hipErrorInvalidValue;
   if (p.ksplit > 1 && !p.ws) return hipErrorInvalidValue;
-  if (p.counters && (p.ksplit < 2 || p.ksplit > 4 || (size_t)p.ksplit * p.B * p.H * p.W * p.N * 4 > 0x7fffffffu))
+  if (p.sk_iters > 0) {                              // stream-K: v2 configs, <= 4 slabs, 32-bit slab offsets
+    if (cfg < 110 || p.ksplit != 1 || (size_t)4 * p.B * p.H * p.W * p.N * 4 > 0x7fffffffu) return hipErrorInvalidValue;
+  } else if (p.counters && (p.ksplit < 2 || p.ksplit > 4 || (size_t)p.ksplit * p.B * p.H * p.W * p.N * 4 > 0x7fffffffu)) {
     return hipErrorInvalidValue;                     // fused split-K: 32-bit slab offsets
+  }
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_>(p, s);
+#define X(id, NW_, FN_, SW_, EP_, SK_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_, SK_>(p, s);
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return launch_wino<NWM_, FN_, S_, PF_, A_>(p, s);

@@ -137,8 +137,12 @@ struct WinoF32Params {
   int relu, ksplit;
   int* counters;      // fused split-K: one arrival counter per (tile group, channel group) block, zero
                       // before the launch, left zero after it (no splitk_reduce_f32 launch)
+  int sk_iters;       // > 0: stream-K, (unit, chunk) iterations per block (conv_wino_sk_plan), ksplit 1
+  int sk_mult;        // stream-K grid: about sk_mult x 256 blocks
 };
+void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* smax);
 bool conv_wino_f32_ok(int cfg, int C, int N);
+bool conv_wino_f32_cfg(int cfg, int* nw, int* fn);
 hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,

@@ -152,3 +152,60 @@ def test_wino_v2_swizzle_is_a_bank_row_involution():
     for s in range(640):
         t = _wino_sw(s)
         assert t >> 4 == s >> 4 and _wino_sw(t) == s
+
+
+def _sk_plan(units, kc, mult):
+    """conv_wino_f32.hip conv_wino_sk_plan, transcribed."""
+    total = units * kc
+    G = min(256 * max(mult, 1), total)
+    it = -(-total // G)
+    G = -(-total // it)
+    smax = max(((u + 1) * kc - 1) // it - (u * kc) // it + 1 for u in range(units))
+    return G, it, smax
+
+
+def _sk_segments(units, kc, G, it):
+    """Every block's (unit, chunk range, partial index, partials) as the stream-K kernel walks them."""
+    segs = []
+    for b in range(G):
+        i, end = b * it, min(units * kc, (b + 1) * it)
+        while i < end:
+            u, kb = divmod(i, kc)
+            ke = min(kc, kb + end - i)
+            zs, ns = 0, 1
+            if kb or ke != kc:
+                g0, g1 = (u * kc) // it, ((u + 1) * kc - 1) // it
+                zs, ns = b - g0, g1 - g0 + 1
+            segs.append((u, kb, ke, zs, ns))
+            i += ke - kb
+    return segs
+
+
+@pytest.mark.parametrize("cfg_nw_fn", [(110, 8, 2), (112, 4, 1), (114, 8, 1)])
+@pytest.mark.parametrize("B,H,C,N", [(32, 56, 64, 64), (32, 28, 128, 128), (32, 14, 256, 256), (32, 7, 512, 512),
+                                     (2, 56, 64, 64), (3, 14, 256, 96)])
+@pytest.mark.parametrize("mult", [1, 2])
+def test_wino_stream_k_plan_partitions_every_unit(cfg_nw_fn, B, H, C, N, mult):
+    """The stream-K walk covers each unit's K chunks exactly once, its partials are numbered 0..ns-1
+    in chunk order with one agreed ns, and the ResNet-50 bs=32 shapes need <= 4 partials at 256
+    blocks (the fused fixup's limit; the host refuses more)."""
+    _, nw, fn = cfg_nw_fn
+    if N % (16 * fn):
+        pytest.skip("channels")
+    T = B * ((H + 1) // 2) ** 2
+    units = -(-T // (16 * nw)) * (N // (16 * fn))
+    kc = C // 16
+    G, it, smax = _sk_plan(units, kc, mult)
+    cover = {}
+    for u, kb, ke, zs, ns in _sk_segments(units, kc, G, it):
+        cover.setdefault(u, []).append((kb, ke, zs, ns))
+    assert sorted(cover) == list(range(units))
+    for u, parts in cover.items():
+        parts.sort()
+        assert parts[0][0] == 0 and parts[-1][1] == kc
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        assert [p[2] for p in parts] == list(range(len(parts)))
+        assert all(p[3] == len(parts) for p in parts)
+        assert len(parts) <= smax
+    if B == 32 and mult == 1:
+        assert smax <= 4

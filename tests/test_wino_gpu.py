@@ -21,12 +21,13 @@ SHAPES = [  # (B, H, W, Cin, Cout, residual, relu)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("ksplit", [1, 2, 4, -2, -4])
+@pytest.mark.parametrize("ksplit", [1, 2, 4, -2, -4, -101, -102])
 def test_wino_f32_matches_fp64(shape, ksplit):
-    """ksplit < 0: fused split-K (the last split of each block adds the slabs in the kernel); run
-    twice so the second launch also checks that the first left its arrival counters zero."""
+    """ksplit < 0: fused split-K (the last split of each block adds the slabs in the kernel); ksplit
+    <= -100: stream-K configs over (-ksplit - 100) x 256 blocks; run twice so the second launch also
+    checks that the first left its arrival counters zero."""
     B, H, W, Cin, Cout, has_res, relu = shape
-    if abs(ksplit) > Cin // 16:
+    if -100 < ksplit and abs(ksplit) > Cin // 16:
         pytest.skip("split-K beyond the 16-channel chunks")
     rng = np.random.default_rng(hash(shape) % 2**32)
     x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
@@ -44,6 +45,10 @@ def test_wino_f32_matches_fp64(shape, ksplit):
     for cfg in C.WINO_F32_CFGS:
         if not C.f32_cfg_supported(cfg, Cin, Cout, pc) or not C.wino_map_ok(cfg, H, W):
             continue
+        if (ksplit <= C.WINO_SK_BASE) != (cfg in C.WINO_SK_CFGS):
+            continue
+        if ksplit <= C.WINO_SK_BASE and C.wino_sk_plan(cfg, B, H, W, Cout, Cin, ksplit)[2] > 4:
+            continue
         ctr = None
         if ksplit < 0:
             ctr = torch.zeros(C.wino_blocks(cfg, B, H, W, Cout), dtype=torch.int32, device="cuda")
@@ -56,6 +61,8 @@ def test_wino_f32_matches_fp64(shape, ksplit):
         if ctr is not None:
             assert int(ctr.abs().sum()) == 0, "fused split-K left arrival counters non-zero"
         ran += 1
+    if ran == 0 and ksplit <= C.WINO_SK_BASE:
+        pytest.skip("no stream-K config maps this shape")
     assert ran > 0
 
 

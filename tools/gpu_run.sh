@@ -52,7 +52,8 @@ for p in "${P[@]}"; do
     cs3)      steps+=("300|$out/pytest_cs3|python -u -m pytest tests/test_cs3_gpu.py tests/test_rr3_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread")
               steps+=("240|$out/cs3_bench|python -u tools/conv_bench.py --shape 32,14,14,256,256,3,1,1 --shape 32,7,7,512,512,3,1,1 --only 73,0,1,2,3,4,5,6,7,8,9 --ks 1,2,4,-1")
               steps+=("240|$out/cs3_ab|python -u tools/ab_cfg.py --model resnet50 --set 32x14x14x256,3x3s1p1111@73@1 --set 32x7x7x512,3x3s1p1111@73@1 --json gpurun_out/$out/cs3_ab.json") ;;
-    roof32)   steps+=("400|$out/roof32_pmc|bash tools/pmc_groups.sh gpurun_out/$out/roof32 'SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT' 'TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum' -- tools/roofline_r50.py --run --dtype fp32 --meta $PWD/gpurun_out/$out/roof32/meta.json")
+    roof32)   steps+=("200|$out/roof32_meta|mkdir -p gpurun_out/$out/roof32 && python -u tools/roofline_r50.py --run --dtype fp32 --meta gpurun_out/$out/roof32/meta.json")
+              steps+=("400|$out/roof32_pmc|bash tools/pmc_groups.sh gpurun_out/$out/roof32 'SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT' 'TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum' -- tools/roofline_r50.py --run --dtype fp32")
               steps+=("60|$out/roof32_table|python tools/roofline_r50.py --table gpurun_out/$out/roof32 --meta gpurun_out/$out/roof32/meta.json --json gpurun_out/$out/roof32/roofline_fp32.json") ;;
     wino)     steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py tests/test_wino.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108 --ks 1,2,4,-2,-4") ;;

@@ -4,10 +4,12 @@
 Two halves:
 
 * ``--run`` (under ``rocprofv3 --pmc ...``): warm the executor, then for every
-  plan step launch a one-element separator kernel (``torch.Tensor.fill_``)
-  followed by REPS eager launches of that step alone; ``--meta`` writes the
-  step list (flops, compulsory bytes, measured ms from a graph-timed pass);
-  a closing separator follows the REPS launches.
+  plan step launch a separator kernel (``torch.cuda._sleep``, a name no plan
+  step uses) followed by REPS eager launches of that step alone; a closing
+  separator follows the REPS launches.  ``--meta`` writes the step list (flops,
+  compulsory bytes, measured ms from a graph-timed pass): run it once WITHOUT
+  the profiler (counter collection serialises dispatches and inflates times),
+  and the PMC passes without ``--meta``.
 * ``--table``: read the rocprofv3 counter CSVs, split the dispatch stream at
   the separators, average each step's counters over its REPS and print /
   write the table: achieved TFLOP/s, L2<->fabric bytes (TCC_EA0_RDREQ x 128 B
@@ -38,7 +40,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 PEAK_BF16 = 2.5e15         # dense bf16 MFMA (no sparsity)
 PEAK_FP32 = 1.50e14        # v_mfma_f32_16x16x4_f32 under full load, measured (profiles/r3/mfma_f32_peak.txt)
 HBM_BW = 6.3e12            # achievable HBM3E stream (MI355X_MICROARCH.md "HBM")
-SEP_NAME = "FillFunctor"   # torch fill_ kernel used as the separator
+SEP_NAME = "spin_kernel"   # torch.cuda._sleep: a kernel no plan step launches (fill_ is also used by steps)
 REPS = 10
 
 
@@ -92,10 +94,10 @@ def run(a):
                         ex._launch(0)
                 t_ms = time_fn(lambda: gg.replay(), reps=5, warm=2) / 20
             torch.cuda.synchronize()
-            sep.fill_(float(i))                 # opening separator
+            torch.cuda._sleep(64)               # opening separator
             for _ in range(REPS):
                 ex._launch(0)
-            sep.fill_(-1.0)                     # closing separator
+            torch.cuda._sleep(64)               # closing separator
             torch.cuda.synchronize()
         outs = [st.out] + ([st.p["out2"]] if st.p.get("out2") else [])
         act = sum(_bytes_of(ex, g, n, a.batch) for n in list(st.ins) + outs)
