@@ -527,11 +527,14 @@ def choose_cfg_f32(M: int, N: int, Kpad: int, occupancy: int = 2):
 def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: Optional[torch.Tensor] = None,
                      relu: int = 0, cfg: Optional[int] = None, ksplit: int = 1,
                      workspace: Optional[torch.Tensor] = None, stream=None,
-                     counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     counters: Optional[torch.Tensor] = None, out2: Optional[torch.Tensor] = None,
+                     relu2: int = 0) -> torch.Tensor:
     """fp32 conv / GEMM: x [B,H,W,Cin] (or [M,K]) fp32 -> out [B,OH,OW,Cout] fp32, with
     act(conv + bias (+ residual)) fused.  ksplit > 1: split-K, needs `workspace`
     (ksplit*M*N fp32); ksplit < 0 (v2 configs): stream-K over -ksplit x 256 blocks,
-    needs `workspace` (workspace_elems_f32) and `counters` (int32 zeros, one per tile)."""
+    needs `workspace` (workspace_elems_f32) and `counters` (int32 zeros, one per tile).
+    Dual output (``pc.n_split > 0``, two sibling 1x1 convs packed along N, no residual):
+    channels [0, n_split) go to `out` (activation `relu`), the rest to `out2` (`relu2`)."""
     if x.dim() == 2:
         B, H, W, C = x.shape[0], 1, 1, x.shape[1]
     else:
@@ -545,7 +548,16 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         raise ValueError("fp32 conv needs weights packed by pack_conv_f32")
     OH, OW = pc.out_hw(H, W)
     M, N = B * OH * OW, pc.cout
-    if out.numel() != M * N:
+    ns = pc.n_split
+    if ns:
+        if out2 is None or residual is not None or ns % 4:
+            raise ValueError("dual-output fp32 conv needs out2 and no residual")
+        if out.numel() != M * ns or out2.numel() != M * (N - ns) or out2.dtype != torch.float32 \
+                or not out2.is_contiguous():
+            raise ValueError("dual-output fp32 conv: out / out2 sizes")
+    elif out2 is not None:
+        raise ValueError("out2 given for a single-output conv")
+    elif out.numel() != M * N:
         raise ValueError(f"conv output buffer has {out.numel()} elements, need {M * N}")
     if residual is not None and (residual.numel() != M * N or residual.dtype != torch.float32
                                  or not residual.is_contiguous()):
@@ -611,7 +623,7 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         ws_ptr = ptr(workspace)
     kernels().conv_f32_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W, C, OH, OW,
                                N, pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.K, pc.Kpad, int(relu),
-                               ksplit, int(cfg), stream_handle(stream), ctr_ptr)
+                               ksplit, int(cfg), stream_handle(stream), ctr_ptr, ptr(out2), int(ns), int(relu2))
     return out
 
 

@@ -235,7 +235,13 @@ class SliceExecutor:
         for i, st in enumerate(self.steps):
             if st.kind == "conv":
                 kf, bf = self._folded(weights, st.p)
+                n_split = 0
+                if st.p.get("sibling"):                # merged sibling 1x1 convs: one GEMM, N = N0 + N1
+                    k2, b2 = self._folded(weights, st.p["sibling"])
+                    n_split = kf.shape[-1]
+                    kf, bf = np.concatenate([kf, k2], axis=-1), np.concatenate([bf, b2])
                 self.packed[i] = conv_ops.pack_conv_f32(kf, bf, st.p["stride"], st.p["pads"], dev)
+                self.packed[i].n_split = n_split
             elif st.kind == "stem_f32":
                 kf, bf = self._folded(weights, st.p)
                 self.packed[i] = conv_ops.pack_stem_f32(kf, bf, st.p["pads"], dev)
@@ -536,7 +542,9 @@ class SliceExecutor:
                 self.cfg[i] = done[key]
                 continue
             x = torch.randn(self.bufs(0)[st.ins[0]].shape, device=self.device)
-            out = torch.empty(M * N, dtype=torch.float32, device=self.device)
+            ns = pc.n_split                       # merged sibling convs write two outputs
+            out = torch.empty(M * (ns or N), dtype=torch.float32, device=self.device)
+            out2 = torch.empty(M * (N - ns), dtype=torch.float32, device=self.device) if ns else None
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
             for cfg in list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS):
@@ -567,7 +575,8 @@ class SliceExecutor:
                     ctr = torch.zeros(nctr, dtype=torch.int32, device=self.device) if nctr else None
                     try:
                         t = self._time_graph(lambda: conv_ops.conv_forward_f32(x, pc, out, cfg=cfg, ksplit=ks,
-                                                                               workspace=ws, counters=ctr), reps)
+                                                                               workspace=ws, counters=ctr,
+                                                                               out2=out2), reps)
                     except (RuntimeError, ValueError):
                         continue
                     if best is None or t < best[0]:
@@ -863,8 +872,10 @@ class SliceExecutor:
         if k == "conv":
             cfg, ks = self.cfg[i]
             res = b[st.ins[1]] if len(st.ins) > 1 else None
+            out2 = b[st.p["out2"]] if st.p.get("out2") else None
             conv_ops.conv_forward_f32(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
-                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr)
+                                      cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr,
+                                      out2=out2, relu2=st.p.get("relu2", 0))
         elif k == "dense":
             cfg, ks = self.cfg[i]
             x = b[st.ins[0]].reshape(self.batch, -1)

@@ -318,6 +318,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
     if fp32:
         if os.environ.get("ADAPT_NO_STEM", "0") != "1":
             steps = _fuse_stem_f32(g, steps, outset)
+        if os.environ.get("ADAPT_NO_SIBLINGS", "0") != "1":
+            steps = merge_siblings(steps)
         return steps
     if os.environ.get("ADAPT_FUSED_BOTTLENECK", "1") == "1":
         steps = fuse_bottlenecks(g, steps, outset)

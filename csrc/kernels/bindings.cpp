@@ -184,16 +184,18 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_f32_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, u64 ws, int B, int H, int W, int Cin,
                                int OH, int OW, int N, int KH, int KW, int stride, int pad_t, int pad_l, int K,
-                               int Kpad, int relu, int ksplit, int cfg, u64 s, u64 counters) {
+                               int Kpad, int relu, int ksplit, int cfg, u64 s, u64 counters, u64 out2, int n_split,
+                               int relu2) {
     py::gil_scoped_release nogil;
     check(adapt::conv_f32_forward(P<const float>(x), P<const float>(w), P<const float>(bias), P<const float>(res),
                                   P<float>(out), P<float>(ws), B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
-                                  K, Kpad, relu, ksplit, cfg, S(s), P<int>(counters)),
+                                  K, Kpad, relu, ksplit, cfg, S(s), P<int>(counters), P<float>(out2), n_split, relu2),
           "conv_f32_forward");
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("out"), py::arg("ws"), py::arg("B"),
      py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("N"), py::arg("KH"),
      py::arg("KW"), py::arg("stride"), py::arg("pad_t"), py::arg("pad_l"), py::arg("K"), py::arg("Kpad"),
-     py::arg("relu"), py::arg("ksplit"), py::arg("cfg"), py::arg("s"), py::arg("counters") = 0);
+     py::arg("relu"), py::arg("ksplit"), py::arg("cfg"), py::arg("s"), py::arg("counters") = 0,
+     py::arg("out2") = 0, py::arg("n_split") = 0, py::arg("relu2") = 0);
   m.def("conv_wino_sk_plan", [](int units, int kc, int mult) {
     int g, it, smax;
     adapt::conv_wino_sk_plan(units, kc, mult, &g, &it, &smax);

@@ -208,6 +208,7 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
     const int n = n0 + wn * TN + j * 16 + fr;
     if (n >= p.N) continue;
     const float b = (slab == nullptr && p.bias) ? p.bias[n] : 0.f;
+    const F32Dst d = f32_dst(p, n);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(FNT, 2) void conv_f32_kernel(ConvF32Params p) {
         }
         v += b;
         if (pre_res) v += rres[i][j][r];
-        p.out[o] = act_relu(v, p.relu);
+        d.base[(size_t)m * d.ld + d.col] = act_relu(v, d.relu);
       }
   }
 }
@@ -235,7 +236,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_f32(ConvF32Params p) {
     const int n = (int)(o % p.N);
     if (p.bias) v += p.bias[n];
     if (p.res) v += p.res[o];
-    p.out[o] = act_relu(v, p.relu);
+    const F32Dst d = f32_dst(p, n);
+    d.base[(o / p.N) * d.ld + d.col] = act_relu(v, d.relu);
   }
 }
 
@@ -264,10 +266,11 @@ hipError_t launch_f32(const ConvF32Params& p, bool pure, bool vec, hipStream_t s
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,
-                            hipStream_t s, int* counters) {
+                            hipStream_t s, int* counters, float* out2, int n_split, int relu2) {
   ConvF32Params p{x, w, bias, res, out, ws, B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
-                  B * OH * OW, K, Kpad, relu, ksplit == 0 ? 1 : ksplit, counters, 0};
+                  B * OH * OW, K, Kpad, relu, ksplit == 0 ? 1 : ksplit, counters, 0, out2, n_split, relu2};
   if (Kpad % FBK || (p.ksplit > 1 && ws == nullptr)) return hipErrorInvalidValue;
+  if (n_split && (n_split % 4 || n_split >= N || !out2 || res || cfg >= 80)) return hipErrorInvalidValue;
   if (p.ksplit < 0 && cfg < 80) {
     // stream-K: v2 configs only
     int bm, bn, g;

@@ -401,9 +401,10 @@ __device__ __forceinline__ void f32g_tile(const ConvF32Params& p, const float* _
       const int row = erow0 + (g + u) * RPI, m = m0 + row;
       if (g + u >= IT || row >= BM || m >= p.M) continue;
       f32x4 v = *(const f32x4*)(epi + row * EPI_LD + ecc * 4) + b + r[u];
-      v[0] = act_relu(v[0], p.relu); v[1] = act_relu(v[1], p.relu);
-      v[2] = act_relu(v[2], p.relu); v[3] = act_relu(v[3], p.relu);
-      *(f32x4*)(p.out + (size_t)m * p.N + en) = v;
+      const F32Dst d = f32_dst(p, en);
+      v[0] = act_relu(v[0], d.relu); v[1] = act_relu(v[1], d.relu);
+      v[2] = act_relu(v[2], d.relu); v[3] = act_relu(v[3], d.relu);
+      *(f32x4*)(d.base + (size_t)m * d.ld + d.col) = v;
     }
   }
 }

@@ -114,8 +114,20 @@ struct ConvF32Params {
   int ksplit;       // >= 1: split-K slabs + reduce; < 0 (v2 configs): stream-K over -ksplit x 256 blocks
   int* counters;    // stream-K: one arrival counter per output tile (zeroed, self-resetting)
   int sk_iters;     // stream-K: (tile, K-tile) iterations per block (conv_f32g_sk_plan)
+  float* out2;      // n_split > 0: two sibling 1x1 convs packed along N; columns >= n_split go to out2
+  int n_split;      // (row stride N - n_split, activation relu2), columns < n_split to out (row stride n_split)
+  int relu2;
 };
 void conv_f32g_sk_plan(int tiles, int kt, int mult, int* grid, int* iters);
+struct F32Dst {
+  float* base;
+  int col, ld, relu;
+};
+// destination of output column n of an fp32 conv (dual output: merged sibling convs, n_split % 4 == 0)
+__device__ __forceinline__ F32Dst f32_dst(const ConvF32Params& p, int n) {
+  if (p.n_split > 0 && n >= p.n_split) return F32Dst{p.out2, n - p.n_split, p.N - p.n_split, p.relu2};
+  return F32Dst{p.out, n, p.n_split > 0 ? p.n_split : p.N, p.relu};
+}
 bool conv_f32g_cfg_tile(int cfg, int* bm, int* bn);
 // fp32 stem (stem_f32.hip): 7x7/s2 conv (+BN, ReLU) + 3x3/s2 max-pool, weights [64][176] fp32
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
@@ -147,7 +159,8 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,
-                            hipStream_t s, int* counters = nullptr);
+                            hipStream_t s, int* counters = nullptr, float* out2 = nullptr, int n_split = 0,
+                            int relu2 = 0);
 hipError_t maxpool_f32(const float* x, float* y, int B, int H, int W, int C, int OH, int OW, int K, int S, int pad_t,
                        int pad_l, int pad_zero, hipStream_t s);
 hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
