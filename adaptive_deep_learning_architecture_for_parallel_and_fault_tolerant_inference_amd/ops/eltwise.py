@@ -187,6 +187,29 @@ def dense_small(x: torch.Tensor, pc, part: torch.Tensor, logits: Optional[torch.
                           stream_handle(stream))
 
 
+def dense_small_f32_scratch(M: int, N: int, Kpad: int) -> int:
+    """fp32 elements of the split-K scratch `dense_small_f32` needs."""
+    return kernels().dense_small_f32_kslices(Kpad) * M * N
+
+
+def dense_small_f32(x: torch.Tensor, pc, part: torch.Tensor, logits: Optional[torch.Tensor] = None,
+                    probs: Optional[torch.Tensor] = None, stream=None) -> None:
+    """fp32 classifier GEMM for M <= 32 rows (csrc/kernels/head.hip dense_partial_f32_kernel + finish):
+    x [M][K] fp32, weights packed by ops.conv.pack_conv_f32, fp32 logits and/or softmax probs."""
+    _chk(x, torch.float32, "x")
+    M, K = x.shape[0], x.numel() // x.shape[0]
+    N = pc.cout
+    if M > 32 or K != pc.K or pc.w.dtype != torch.float32:
+        raise ValueError(f"dense_small_f32: M={M} (<= 32), K={K} (== {pc.K}) and fp32 weights required")
+    if part.dtype != torch.float32 or part.numel() < dense_small_f32_scratch(M, N, pc.Kpad):
+        raise ValueError("dense_small_f32: scratch too small")
+    for t in (logits, probs):
+        if t is not None and (t.dtype != torch.float32 or t.numel() != M * N or not t.is_contiguous()):
+            raise ValueError("dense_small_f32: outputs must be contiguous fp32 [M][N]")
+    kernels().dense_small_f32(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(part), ptr(logits), ptr(probs), M, N, K,
+                              pc.Kpad, stream_handle(stream))
+
+
 def softmax_rows(x: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
     _chk(x, torch.float32, "x"); _chk(out, torch.float32, "out")
     rows, n = x.shape

@@ -380,6 +380,12 @@ class SliceExecutor:
                 pc = self.packed[i]
                 n = E.dense_small_scratch(self.batch, pc.cout, pc.K)
                 self._dense_part[i] = torch.empty(n, dtype=torch.float32, device=dev)
+            elif (st.kind == "dense" and self.batch <= 32 and not st.p.get("relu") and self.fp32
+                  and self.device.type == "cuda" and os.environ.get("ADAPT_F32_HEAD", "1") == "1"):
+                # fp32 small-M head (head.hip dense_partial_f32_kernel + finish): logits + softmax in 2 launches
+                pc = self.packed[i]
+                self._dense_part[i] = torch.empty(E.dense_small_f32_scratch(self.batch, pc.cout, pc.Kpad),
+                                                  dtype=torch.float32, device=dev)
             if st.kind == "dense" and st.p["softmax"]:
                 # pre-softmax logits stay readable (`logits()`): numerics checks compare them
                 self._logits[i] = torch.empty((self.batch, st.p["units"]), dtype=torch.float32, device=dev)
@@ -876,6 +882,13 @@ class SliceExecutor:
             conv_ops.conv_forward_f32(b[st.ins[0]], self.packed[i], b[st.out], residual=res, relu=st.p["relu"],
                                       cfg=cfg, ksplit=ks, workspace=ws, stream=stream, counters=ctr,
                                       out2=out2, relu2=st.p.get("relu2", 0))
+        elif k == "dense" and i in self._dense_part:
+            x = b[st.ins[0]].reshape(self.batch, -1)
+            if st.p["softmax"]:
+                E.dense_small_f32(x, self.packed[i], self._dense_part[i], logits=self._logits[i], probs=b[st.out],
+                                  stream=stream)
+            else:
+                E.dense_small_f32(x, self.packed[i], self._dense_part[i], logits=b[st.out], stream=stream)
         elif k == "dense":
             cfg, ks = self.cfg[i]
             x = b[st.ins[0]].reshape(self.batch, -1)

@@ -170,6 +170,13 @@ PYBIND11_MODULE(_C, m) {
                              P<float>(logits), P<float>(probs), M, N, K, Kpad, S(s)),
           "dense_small");
   });
+  m.def("dense_small_f32_kslices", &adapt::dense_small_f32_kslices);
+  m.def("dense_small_f32", [](u64 x, u64 w, u64 bias, u64 part, u64 logits, u64 probs, int M, int N, int K,
+                              int Kpad, u64 s) {
+    check(adapt::dense_small_f32(P<const float>(x), P<const float>(w), P<const float>(bias), P<float>(part),
+                                 P<float>(logits), P<float>(probs), M, N, K, Kpad, S(s)),
+          "dense_small_f32");
+  });
   m.def("gap", [](u64 x, u64 y, u64 y32, int B, int HW, int C, u64 s) {
     check(adapt::gap(P<const bf16>(x), P<bf16>(y), P<float>(y32), B, HW, C, S(s)), "gap");
   });

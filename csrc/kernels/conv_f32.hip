@@ -361,17 +361,32 @@ __global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restric
 }
 
 // y[b][c] = mean over HW of x[b][hw][c]; one thread per (b, 4 channels)
-__global__ __launch_bounds__(256) void gap_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
-                                                      int HW, int C) {
+// GAP over small maps (ResNet's 7x7x2048 head): one thread per (image, float4 channel chunk)
+// walking all HW pixels made 64 blocks of 49 dependent loads (14 us at bs=32).  Here a block
+// owns 64 float4 channel chunks of one image with GP = 4 threads per chunk: thread (g, c) sums
+// pixels g, g + GP, ... of chunk c (independent loads), and the GP partials meet in LDS.
+constexpr int GAP_CC = 64;                   // float4 channel chunks per block
+constexpr int GAP_GP = 4;                    // pixel groups per chunk
+__global__ __launch_bounds__(GAP_CC * GAP_GP) void gap_f32_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                                   int B, int HW, int C) {
+  __shared__ f32x4 red[GAP_GP][GAP_CC];
   const int C4 = C / 4;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C4) return;
-  const int b = i / C4, c4 = i - b * C4;
+  const int cblocks = (C4 + GAP_CC - 1) / GAP_CC;
+  const int b = blockIdx.x / cblocks, c4 = (blockIdx.x - b * cblocks) * GAP_CC + (threadIdx.x % GAP_CC);
+  const int g = threadIdx.x / GAP_CC;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  const float* p = x + (size_t)b * HW * C + c4 * 4;
-  for (int t = 0; t < HW; ++t) s += *(const f32x4*)(p + (size_t)t * C);
-  const float inv = 1.f / (float)HW;
-  *(f32x4*)(y + (size_t)b * C + c4 * 4) = s * inv;
+  if (c4 < C4) {
+    const float* p = x + (size_t)b * HW * C + c4 * 4;
+#pragma unroll 4
+    for (int t = g; t < HW; t += GAP_GP) s += *(const f32x4*)(p + (size_t)t * C);
+  }
+  red[g][threadIdx.x % GAP_CC] = s;
+  __syncthreads();
+  if (g == 0 && c4 < C4) {
+#pragma unroll
+    for (int k = 1; k < GAP_GP; ++k) s += red[k][threadIdx.x];
+    *(f32x4*)(y + (size_t)b * C + c4 * 4) = s * (1.f / (float)HW);
+  }
 }
 
 // GAP over large maps (the squeeze-excite pools of EfficientNet run over up to
@@ -709,7 +724,8 @@ hipError_t maxpool_f32(const float* x, float* y, int B, int H, int W, int C, int
 
 hipError_t gap_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {
   if (C % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gap_f32_kernel, dim3((B * C / 4 + 255) / 256), dim3(256), 0, s, x, y, B, HW, C);
+  const int cblocks = (C / 4 + GAP_CC - 1) / GAP_CC;
+  hipLaunchKernelGGL(gap_f32_kernel, dim3(B * cblocks), dim3(GAP_CC * GAP_GP), 0, s, x, y, B, HW, C);
   return hipGetLastError();
 }
 

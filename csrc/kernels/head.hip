@@ -218,6 +218,66 @@ __global__ __launch_bounds__(256) void dense_finish_reg_kernel(const float* __re
     if (ok[j]) probs[(size_t)row * N + tid + 256 * j] = v[j] * inv;
 }
 
+// fp32 classifier GEMM for M <= 32 rows (ResNet's 2048 -> 1000 head at the reference's precision): the
+// generic fp32 conv GEMM ran it as 64x64 tiles split-K 8 plus a reduce and a softmax launch (~22 us at
+// bs=32).  Here block (column group, K slice): 4 waves x 16 columns, both 16-row M fragments, the K
+// slice in steps of 16 on v_mfma_f32_16x16x4_f32 (lane group q supplies k = 16h + 4q + s to step s for
+// both operands, one float4 load each); fp32 partials [KS][M][N] go to the finish kernels above
+// (bias, logits, softmax).  w: pack_conv_f32 layout [Npad][Kpad], zero-padded.
+constexpr int DHF_KSL = 128;                 // K per slice
+__global__ __launch_bounds__(256) void dense_partial_f32_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ w, float* __restrict__ part,
+                                                                int M, int N, int K, int Kpad) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int n = blockIdx.x * 64 + wv * 16 + r;
+  const int k0 = blockIdx.y * DHF_KSL, k1 = min(Kpad, k0 + DHF_KSL);
+  const float* wr = w + (size_t)n * Kpad + 4 * q;
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 4
+  for (int k = k0; k < k1; k += 16) {
+    const f32x4 b = *(const f32x4*)(wr + k);
+    f32x4 a[2];
+#pragma unroll
+    for (int mf = 0; mf < 2; ++mf) {
+      const int row = mf * 16 + r;
+      a[mf] = (row < M && k + 4 * q < K) ? *(const f32x4*)(x + (size_t)row * K + k + 4 * q)
+                                         : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) acc[mf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][s4], b[s4], acc[mf], 0, 0, 0);
+  }
+  // acc[mf][e] = C[row mf*16 + 4q + e][column n]
+  if (n >= N) return;
+  float* pr = part + (size_t)blockIdx.y * M * N;
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = mf * 16 + 4 * q + e;
+      if (row < M) pr[(size_t)row * N + n] = acc[mf][e];
+    }
+}
+
+int dense_small_f32_kslices(int Kpad) { return (Kpad + DHF_KSL - 1) / DHF_KSL; }
+
+hipError_t dense_small_f32(const float* x, const float* w, const float* bias, float* part, float* logits,
+                           float* probs, int M, int N, int K, int Kpad, hipStream_t s) {
+  if (M < 1 || M > 32 || K % 4 || Kpad % 16 || Kpad < K || N < 1) return hipErrorInvalidValue;
+  const int ks = dense_small_f32_kslices(Kpad);
+  hipLaunchKernelGGL(dense_partial_f32_kernel, dim3((N + 63) / 64, ks), dim3(256), 0, s, x, w, part, M, N, K, Kpad);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (N <= 1024)
+    hipLaunchKernelGGL(dense_finish_reg_kernel, dim3(M), dim3(256), 0, s, part, bias, logits, probs, M, N, ks);
+  else
+    hipLaunchKernelGGL(dense_finish_kernel, dim3(M), dim3(256), (size_t)N * sizeof(float), s, part, bias, logits,
+                       probs, M, N, ks);
+  return hipGetLastError();
+}
+
 hipError_t dense_small(const bf16* x, const bf16* w, const float* bias, float* part, float* logits, float* probs,
                        int M, int N, int K, int Kpad, hipStream_t s) {
   if (M < 1 || M > 32 || K % 8 || N < 1) return hipErrorInvalidValue;

@@ -87,6 +87,9 @@ hipError_t maxpool(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, i
 hipError_t gap(const bf16* x, bf16* y, float* y32, int B, int HW, int C, hipStream_t s);
 int dense_small_kslices(int K);
 // M <= 32 rows: out = x[M][K] . w^T + bias -> logits and/or softmax(probs); part = [kslices][M][N] fp32 scratch
+int dense_small_f32_kslices(int Kpad);
+hipError_t dense_small_f32(const float* x, const float* w, const float* bias, float* part, float* logits,
+                           float* probs, int M, int N, int K, int Kpad, hipStream_t s);
 hipError_t dense_small(const bf16* x, const bf16* w, const float* bias, float* part, float* logits, float* probs,
                        int M, int N, int K, int Kpad, hipStream_t s);
 hipError_t softmax_rows(const float* x, float* y, int rows, int N, int ldx, hipStream_t s);

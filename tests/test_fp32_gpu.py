@@ -90,6 +90,27 @@ def test_dense_f32_split_k():
     assert np.abs(out.cpu().numpy() - want).max() / np.abs(want).max() < 2e-5
 
 
+@pytest.mark.parametrize("M,K,N", [(32, 2048, 1000), (1, 2048, 1000), (5, 1280, 1000), (17, 4096, 10), (32, 96, 130)])
+def test_dense_small_f32_head(M, K, N):
+    """fp32 small-M head (head.hip dense_partial_f32_kernel + finish): logits against fp64, softmax
+    probabilities of those logits."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import eltwise as E
+    rng = np.random.default_rng(M * 7 + K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    w = (rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    pc = C.pack_conv_f32(w.reshape(1, 1, K, N), b, 1, ((0, 0), (0, 0)), "cuda")
+    part = torch.empty(E.dense_small_f32_scratch(M, N, pc.Kpad), dtype=torch.float32, device="cuda")
+    logits = torch.full((M, N), float("nan"), device="cuda")
+    probs = torch.full((M, N), float("nan"), device="cuda")
+    E.dense_small_f32(torch.from_numpy(x).cuda(), pc, part, logits=logits, probs=probs)
+    want = x.astype(np.float64) @ w.astype(np.float64) + b
+    got = logits.cpu().numpy()
+    assert np.abs(got - want).max() / np.abs(want).max() < 2e-5
+    e = np.exp(want - want.max(1, keepdims=True))
+    assert np.abs(probs.cpu().numpy() - e / e.sum(1, keepdims=True)).max() < 1e-5
+
+
 def test_f32_layers():
     rng = np.random.default_rng(1)
     x = torch.from_numpy(rng.standard_normal((2, 15, 15, 64)).astype(np.float32))
