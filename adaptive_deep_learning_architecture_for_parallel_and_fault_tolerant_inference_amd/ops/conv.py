@@ -821,6 +821,61 @@ def pack_pair(k3, b3, k1, b1, device="cuda") -> PackedPair:
                       cin=k3.shape[2], co=k3.shape[3], cm=k1.shape[3], bm=pair_bm(k3.shape[2]))
 
 
+# fp32 fused 1x1 pair (csrc/kernels/pw_pair_f32.hip): ResNet stage 2 only (64 -> 256 -> 64); the
+# weights of wider pairs do not fit one block's registers at fp32
+PAIR_F32_SHAPES = frozenset({(64, 256, 64)})
+PAIR_F32_BM = (16, 32)
+
+
+def pair_f32_supported(cin: int, co: int, cm: int) -> bool:
+    return (cin, co, cm) in PAIR_F32_SHAPES
+
+
+def pair_f32_bm() -> int:
+    bm = int(os.environ.get("ADAPT_PAIR_F32_BM", "32"))
+    if bm not in PAIR_F32_BM:
+        raise ValueError(f"ADAPT_PAIR_F32_BM must be one of {PAIR_F32_BM}")
+    return bm
+
+
+def pack_pair_f32(k3, b3, k1, b1, device="cuda") -> PackedPair:
+    """HWIO kernels (BN folded, fp64 / fp32) of the two 1x1 convs, packed in the fragment order
+    pw_pair_f32.hip keeps in registers: W3 [16 channel frags][4 k halves][64 lanes][4] with lane
+    16q + r holding W3[16h + 4q + s][16 cf + r]; W1 [2 K halves x 4 channel frags][8 halves][64][4]
+    holding W1[128 kh + 16h + 4q + s][16 c2 + r] (wave = 4 kh + c2)."""
+    if k3.shape[:2] != (1, 1) or k1.shape[:2] != (1, 1) or k1.shape[2] != k3.shape[3]:
+        raise ValueError(f"fused 1x1 pair: shapes {k3.shape} -> {k1.shape}")
+    cin, co, cm = k3.shape[2], k3.shape[3], k1.shape[3]
+    if not pair_f32_supported(cin, co, cm):
+        raise ValueError(f"fp32 fused 1x1 pair: no kernel for {cin}->{co}->{cm}")
+    w3 = np.asarray(k3[0, 0], np.float64).reshape(4, 4, 4, 16, 16)          # h, q, s, cf, r
+    w3 = w3.transpose(3, 0, 1, 4, 2).reshape(16, 4, 64, 4)
+    w1 = np.asarray(k1[0, 0], np.float64).reshape(2, 8, 4, 4, 4, 16)        # kh, h, q, s, c2, r
+    w1 = w1.transpose(0, 4, 1, 2, 5, 3).reshape(8, 8, 64, 4)
+
+    def dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device=device).contiguous()
+    return PackedPair(w3=dev(w3), b3=dev(b3), w1=dev(w1), b1=dev(b1), cin=cin, co=co, cm=cm, bm=pair_f32_bm())
+
+
+def pair_f32_forward(x: torch.Tensor, res: torch.Tensor, pp: PackedPair, y: torch.Tensor, z: torch.Tensor,
+                     bm: Optional[int] = None, grid: int = 0, stream=None):
+    """y = relu(x . W3 + b3 + res), z = relu(y . W1 + b1) in one fp32 launch (pw_pair_f32.hip)."""
+    bm = (pp.bm or pair_f32_bm()) if bm is None else bm
+    for t in (x, res, y, z):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != x.device:
+            raise ValueError("fp32 fused 1x1 pair: contiguous fp32 tensors on one device")
+    M = x.numel() // pp.cin
+    if x.shape[-1] != pp.cin or res.numel() != M * pp.co or y.numel() != M * pp.co or z.numel() != M * pp.cm:
+        raise ValueError(f"fp32 fused 1x1 pair: x {tuple(x.shape)} res {tuple(res.shape)} y {tuple(y.shape)} "
+                         f"z {tuple(z.shape)} for {pp.cin}->{pp.co}->{pp.cm}")
+    if not kernels().pw_pair_f32_supported(pp.cin, pp.co, pp.cm, bm):
+        raise ValueError(f"fp32 fused 1x1 pair: no kernel for {pp.cin}->{pp.co}->{pp.cm} at {bm} pixels per tile")
+    kernels().pw_pair_f32_forward(ptr(x), ptr(pp.w3), ptr(pp.b3), ptr(res), ptr(pp.w1), ptr(pp.b1), ptr(y), ptr(z),
+                                  M, pp.cin, pp.co, pp.cm, bm, int(grid), stream_handle(stream))
+    return y, z
+
+
 def pair_forward(x: torch.Tensor, res: torch.Tensor, pp: PackedPair, y: torch.Tensor, z: torch.Tensor,
                  bm: Optional[int] = None, stream=None):
     bm = (pp.bm or pair_bm(pp.cin)) if bm is None else bm

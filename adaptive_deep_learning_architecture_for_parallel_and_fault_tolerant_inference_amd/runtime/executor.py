@@ -245,6 +245,10 @@ class SliceExecutor:
             elif st.kind == "stem_f32":
                 kf, bf = self._folded(weights, st.p)
                 self.packed[i] = conv_ops.pack_stem_f32(kf, bf, st.p["pads"], dev)
+            elif st.kind == "pair":
+                k3, b3 = self._folded(weights, st.p["c3"])
+                k1, b1 = self._folded(weights, st.p["c1"])
+                self.packed[i] = conv_ops.pack_pair_f32(k3, b3, k1, b1, device=dev)
             elif st.kind == "dense":
                 name = st.p.get("layer", st.out)
                 k = weights[f"{name}/kernel"]
@@ -899,6 +903,9 @@ class SliceExecutor:
                 E.softmax_rows(dst, b[st.out], stream=stream)
         elif k == "stem_f32":
             conv_ops.stem_f32_forward(b[st.ins[0]], self.packed[i], b[st.out], pool_pad=st.p["pool_pad"],
+                                      stream=stream)
+        elif k == "pair":
+            conv_ops.pair_f32_forward(b[st.ins[0]], b[st.ins[1]], self.packed[i], b[st.out], b[st.p["out2"]],
                                       stream=stream)
         elif k == "maxpool":
             (pt, _), (pl, _) = st.p["pads"]

@@ -318,6 +318,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
     if fp32:
         if os.environ.get("ADAPT_NO_STEM", "0") != "1":
             steps = _fuse_stem_f32(g, steps, outset)
+        if os.environ.get("ADAPT_FUSED_PAIR_F32", "1") == "1":
+            steps = fuse_pairs(g, steps, outset, fp32=True)
         if os.environ.get("ADAPT_NO_SIBLINGS", "0") != "1":
             steps = merge_siblings(steps)
         return steps
@@ -391,14 +393,15 @@ def fuse_bottlenecks(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step
     return [repl.get(j, st) for j, st in enumerate(steps) if j not in drop]
 
 
-def fuse_pairs(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
+def fuse_pairs(g: Graph, steps: List[Step], outset: Set[str], fp32: bool = False) -> List[Step]:
     """1x1 (CIN -> CO) + BN + residual + ReLU (block k's ``_out``) followed by the
     1x1 (CO -> CM) + BN + ReLU that is the next block's ``_1`` ==> one ``pair``
     step with two outputs (csrc/kernels/pw_pair.hip): y is still written (it is
     the next residual) but the second GEMM reads it from LDS, and the pair is
     one launch.  Only the stride-1 pairs inside a ResNet stage qualify.  Both
-    outputs land in their own named buffers, so either may be a slice frontier."""
-    from ..ops.conv import pair_supported   # static shape table, no device needed
+    outputs land in their own named buffers, so either may be a slice frontier.
+    fp32: csrc/kernels/pw_pair_f32.hip, ResNet stage 2 (64 -> 256 -> 64) only."""
+    from ..ops.conv import pair_f32_supported, pair_supported   # static shape tables, no device needed
 
     def conv1x1(st: Step, relu: int, res: bool) -> bool:
         p = st.p
@@ -422,7 +425,7 @@ def fuse_pairs(g: Graph, steps: List[Step], outset: Set[str]) -> List[Step]:
         if len(xl.out_shape) != 3:
             continue
         cin, co, cm = xl.out_shape[2], a.p["filters"], b.p["filters"]
-        if not pair_supported(cin, co, cm):
+        if not (pair_f32_supported(cin, co, cm) if fp32 else pair_supported(cin, co, cm)):
             continue
         p = {"c3": a.p, "c1": b.p, "out2": b.out, "cin": cin, "co": co, "cm": cm}
         repl[ja] = Step("pair", a.out, list(a.ins), a.covers + b.covers, p)

@@ -170,6 +170,13 @@ PYBIND11_MODULE(_C, m) {
                              P<float>(logits), P<float>(probs), M, N, K, Kpad, S(s)),
           "dense_small");
   });
+  m.def("pw_pair_f32_supported", &adapt::pw_pair_f32_supported);
+  m.def("pw_pair_f32_forward", [](u64 x, u64 w3, u64 b3, u64 res, u64 w1, u64 b1, u64 y, u64 z, int M, int cin,
+                                  int co, int cm, int bm, int grid, u64 s) {
+    adapt::PwPairF32Params p{P<const float>(x), P<const float>(w3), P<const float>(b3), P<const float>(res),
+                             P<const float>(w1), P<const float>(b1), P<float>(y), P<float>(z), M};
+    check(adapt::pw_pair_f32_forward(p, cin, co, cm, bm, grid, S(s)), "pw_pair_f32_forward");
+  });
   m.def("dense_small_f32_kslices", &adapt::dense_small_f32_kslices);
   m.def("dense_small_f32", [](u64 x, u64 w, u64 bias, u64 part, u64 logits, u64 probs, int M, int N, int K,
                               int Kpad, u64 s) {

@@ -217,6 +217,20 @@ struct PwPairParams {
   int M;
 };
 bool pw_pair_supported(int cin, int co, int cm, int bm);
+// fp32 fused 1x1 pair (pw_pair_f32.hip): ResNet stage 2, 64 -> 256 -> 64
+struct PwPairF32Params {
+  const float* x;
+  const float* w3;
+  const float* b3;
+  const float* res;
+  const float* w1;
+  const float* b1;
+  float* y;
+  float* z;
+  int M;
+};
+bool pw_pair_f32_supported(int cin, int co, int cm, int bm);
+hipError_t pw_pair_f32_forward(const PwPairF32Params& p, int cin, int co, int cm, int bm, int grid, hipStream_t s);
 // 3x3 / s1 / p1 conv with the filter resident in VGPRs (conv3x3_rr.hip): out = act(conv(x) + bias)
 struct Conv3x3RRParams {
   const bf16* x;

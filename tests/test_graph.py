@@ -198,3 +198,20 @@ def test_fp32_plan_fuses_stem_and_pool():
     assert steps[0].kind == "stem_f32" and steps[0].out == "pool1_pool"
     assert "conv1_conv" in steps[0].covers and "pool1_pool" in steps[0].covers
     assert not any(s.kind == "maxpool" for s in steps)
+
+
+def test_fp32_plan_fuses_stage2_pairs_and_merges_siblings():
+    """fp32 ResNet-50 plan: the two stride-1 stage-2 1x1 pairs (block k `_out` + block k+1 `_1`) become
+    fp32 pair steps (pw_pair_f32.hip), and each stage's projection shortcut shares one GEMM with that
+    block's `_1` conv (dual output)."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.plan import compile_plan
+    g = build_resnet("resnet50")
+    steps = compile_plan(g, fp32=True)
+    pairs = [s for s in steps if s.kind == "pair"]
+    assert [s.out for s in pairs] == ["conv2_block1_out", "conv2_block2_out"]
+    assert [s.p["out2"] for s in pairs] == ["conv2_block2_1_relu", "conv2_block3_1_relu"]
+    merged = [s for s in steps if s.kind == "conv" and s.p.get("out2")]
+    assert len(merged) == 4 and all(s.p["kernel"] == (1, 1) for s in merged)
+    covered = [c for s in steps for c in s.covers]
+    assert len(covered) == len(set(covered))
