@@ -77,7 +77,7 @@ def _nbytes(shape, dtype) -> int:
 class SliceExecutor:
     """Runs one (sub)graph for a fixed batch on one device with our HIP kernels."""
 
-    FP32_KINDS = ("conv", "dense", "maxpool", "gap", "softmax", "add", "bn", "relu", "pad", "copy",
+    FP32_KINDS = ("conv", "pair", "dense", "maxpool", "gap", "softmax", "add", "bn", "relu", "pad", "copy",
                   "dwconv", "avgpool", "concat", "act", "binary", "affine", "stem_f32")
 
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device="cuda",
