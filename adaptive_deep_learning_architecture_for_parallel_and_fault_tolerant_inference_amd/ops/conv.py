@@ -105,6 +105,7 @@ class PackedConv:
     pad_r: int
     n_split: int = 0         # > 0: two sibling convs packed along N (outputs [0, n_split) and [n_split, cout))
     wino: Optional[torch.Tensor] = None   # fp32 3x3/s1/p1: Winograd-transformed weights (pack_wino_f32)
+    pwf: Optional[torch.Tensor] = None    # fp32 1x1/s1: fragment-packed weights of pw_f32.hip (pack_pw_f32)
 
     @property
     def K(self) -> int:
@@ -469,9 +470,32 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(U.transpose(1, 4, 0, 2, 5, 3).reshape(C // 16, N // 16, 16, 64, 4).astype(np.float32))
 
 
+# fp32 persistent pointwise configs (csrc/kernels/pw_f32.hip): id -> pixels per tile; 1x1 / s1 / p0 convs
+# with K in {64, 128, 256, 512} and N a multiple of the slice (FPW x 128 channels), ksplit 1
+PW_F32_CFGS = {120: 16, 121: 32}
+PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1}
+PW_F32_BMS = {64: (32,), 128: (16, 32), 256: (16, 32), 512: (16, 32)}
+
+
+def pw_f32_shape_ok(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 1, 0, 0, 0, 0)
+            and pc.cin in PW_F32_FPW and pc.cout % (PW_F32_FPW[pc.cin] * 128) == 0 and not pc.n_split)
+
+
+def pack_pw_f32(kernel_hwio: np.ndarray) -> np.ndarray:
+    """[N/16][K/16][64 lanes][4] fp32: lane 16q + r of fragment gf, half h holds W[16h + 4q + s][16 gf + r]."""
+    K, N = kernel_hwio.shape[2], kernel_hwio.shape[3]
+    w = np.asarray(kernel_hwio[0, 0], np.float64).reshape(K // 16, 4, 4, N // 16, 16)    # h, q, s, gf, r
+    return np.ascontiguousarray(w.transpose(3, 0, 1, 4, 2).reshape(N // 16, K // 16, 64, 4).astype(np.float32))
+
+
 def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] = None) -> bool:
     """Whether fp32 tile config `cfg` runs a conv with `cin` input / `cout` output channels
-    (Winograd configs also need the conv itself: 3x3 / s1 / p1 with its transformed weights)."""
+    (Winograd configs also need the conv itself: 3x3 / s1 / p1 with its transformed weights;
+    the pointwise configs a 1x1 / s1 conv with its fragment-packed weights)."""
+    if cfg in PW_F32_CFGS:
+        return (pc is not None and pc.pwf is not None and pw_f32_shape_ok(pc)
+                and PW_F32_CFGS[cfg] in PW_F32_BMS[pc.cin])
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         fn = {**WINO_F32_CFGS, **WINO_F32_ABLATE}[cfg][1]
         return pc is not None and pc.wino is not None and wino_supported(pc) and cout % (16 * fn) == 0
@@ -495,6 +519,8 @@ def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, 
                     kh=kh, kw=kw, cin=cin, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
     if wino_supported(pc):
         pc.wino = torch.from_numpy(wino_pack_np(kernel_hwio)).to(device=device).contiguous()
+    if pw_f32_shape_ok(pc):
+        pc.pwf = torch.from_numpy(pack_pw_f32(kernel_hwio)).to(device=device).contiguous()
     return pc
 
 
@@ -566,6 +592,13 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         raise ValueError("conv epilogue activation must be 0 (none), 1 (ReLU) or 2 (ReLU6)")
     if cfg is None:
         cfg, ksplit = choose_cfg_f32(M, N, pc.Kpad)
+    if cfg in PW_F32_CFGS:
+        if not f32_cfg_supported(cfg, C, N, pc) or int(ksplit or 1) != 1 or (OH, OW) != (H, W) or out2 is not None:
+            raise ValueError(f"pointwise fp32 config {cfg}: 1x1 / s1 conv, K in {sorted(PW_F32_FPW)}, "
+                             f"N % slice == 0, ksplit 1, single output")
+        kernels().pw_f32_forward(ptr(x), ptr(pc.pwf), ptr(pc.bias), ptr(residual), ptr(out), M, C, N, int(relu),
+                                 PW_F32_CFGS[cfg], stream_handle(stream))
+        return out
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         # ksplit > 1: slabs + splitk_reduce_f32; ksplit <= -2: -ksplit slabs, the last split of
         # each block adds them in split order inside the kernel (needs `counters`)

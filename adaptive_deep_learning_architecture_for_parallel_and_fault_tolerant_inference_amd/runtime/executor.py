@@ -557,10 +557,12 @@ class SliceExecutor:
             out2 = torch.empty(M * (N - ns), dtype=torch.float32, device=self.device) if ns else None
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
-            for cfg in list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS):
+            for cfg in list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.PW_F32_CFGS):
                 if not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc):
                     continue
-                if cfg in conv_ops.WINO_F32_CFGS:         # Winograd F(2x2,3x3): split-K over 16-channel chunks
+                if cfg in conv_ops.PW_F32_CFGS:            # persistent pointwise: whole K, one launch
+                    tiles, kts, sks = 0, 1, ()
+                elif cfg in conv_ops.WINO_F32_CFGS:         # Winograd F(2x2,3x3): split-K over 16-channel chunks
                     nwm, fn = conv_ops.WINO_F32_CFGS[cfg]
                     tiles = math.ceil(B * ((OH + 1) // 2) * ((OW + 1) // 2) / (16 * nwm)) * (N // (16 * fn))
                     kts, sks = C // 16, (-2, -4)          # fused split-K (fixup in the kernel, <= 4 splits)
@@ -571,7 +573,8 @@ class SliceExecutor:
                     tiles = math.ceil(M / bm) * math.ceil(N / bn)
                     kts = ktiles
                     sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
-                for ks in ((1, 2, 4, 8, 16) if cfg not in conv_ops.WINO_SK_CFGS else ()) + sks:
+                for ks in ((1,) if cfg in conv_ops.PW_F32_CFGS else
+                           (1, 2, 4, 8, 16) if cfg not in conv_ops.WINO_SK_CFGS else ()) + sks:
                     # split-K / stream-K only where the tiles alone leave CUs idle
                     if ks > 1 and (kts // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue

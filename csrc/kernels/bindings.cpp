@@ -170,6 +170,12 @@ PYBIND11_MODULE(_C, m) {
                              P<float>(logits), P<float>(probs), M, N, K, Kpad, S(s)),
           "dense_small");
   });
+  m.def("pw_f32_supported", &adapt::pw_f32_supported);
+  m.def("pw_f32_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, int M, int K, int N, int relu, int bm, u64 s) {
+    adapt::PwF32Params p{P<const float>(x), P<const float>(w), P<const float>(bias), P<const float>(res), P<float>(out),
+                         M, K, N, relu};
+    check(adapt::pw_f32_forward(p, bm, S(s)), "pw_f32_forward");
+  });
   m.def("pw_pair_f32_supported", &adapt::pw_pair_f32_supported);
   m.def("pw_pair_f32_forward", [](u64 x, u64 w3, u64 b3, u64 res, u64 w1, u64 b1, u64 y, u64 z, int M, int cin,
                                   int co, int cm, int bm, int grid, u64 s) {

@@ -182,7 +182,23 @@ __global__ __launch_bounds__(256) void dense_finish_reg_kernel(const float* __re
     ok[j] = i < N;
     v[j] = (ok[j] && bias) ? bias[i] : 0.f;
   }
-  for (int sl = 0; sl < KS; ++sl) {
+  // four slices' loads in flight per round (the fp32 head has 16 slices; a loop of dependent
+  // rounds left the finish latency-bound at 8 us)
+  int sl = 0;
+  for (; sl + 4 <= KS; sl += 4) {
+    float t[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* pr = part + ((size_t)(sl + u) * M + row) * N;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[u][j] = ok[j] ? pr[tid + 256 * j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += t[u][j];
+  }
+  for (; sl < KS; ++sl) {
     const float* pr = part + ((size_t)sl * M + row) * N;
     float t[4];
 #pragma unroll

@@ -230,6 +230,18 @@ struct PwPairF32Params {
   int M;
 };
 bool pw_pair_f32_supported(int cin, int co, int cm, int bm);
+// fp32 persistent pointwise conv, filter slice register-resident (pw_f32.hip)
+struct PwF32Params {
+  const float* x;
+  const float* w;      // fragment-packed [N/16][K/16][64 lanes][4]
+  const float* bias;
+  const float* res;
+  float* out;
+  int M, K, N, relu;
+};
+int pw_f32_fpw(int K);
+bool pw_f32_supported(int K, int N, int bm);
+hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s);
 hipError_t pw_pair_f32_forward(const PwPairF32Params& p, int cin, int co, int cm, int bm, int grid, hipStream_t s);
 // 3x3 / s1 / p1 conv with the filter resident in VGPRs (conv3x3_rr.hip): out = act(conv(x) + bias)
 struct Conv3x3RRParams {

@@ -1,0 +1,167 @@
+// Persistent fp32 pointwise (1x1 / stride 1) conv with the filter slice resident in registers:
+//
+//   out = act(x . W + bias (+ res))      x [M][K], W [K][N], K in {64, 128, 256, 512}
+//
+// The fp32 tile GEMMs (conv_f32.hip / conv_f32g.hip) run ResNet's 1x1 convs at 43-51 % MFMA busy
+// (profiles/r3/pmc/pmc_gemm1x1_f32.txt): at K = 128-512 a 64x64 tile has only 4-16 K steps, so every
+// tile pays its ring fill, barriers and epilogue.  Here a block owns an N slice of NS = FPW x 128
+// output channels for the whole launch: each of its 8 waves keeps FPW 16-channel fragments x all of
+// K in VGPRs (FPW x K / 4 = 128 registers), and the block walks BM-pixel tiles of its slice, so the
+// weights cross L2 -> VGPR once per block and the only per-tile traffic is the activation rows in
+// (16-byte row-contiguous loads, prefetched one tile ahead into registers and staged in a swizzled
+// LDS double buffer) and the outputs / residual (16 bytes per lane, straight from the accumulators).
+// One barrier per tile.
+//
+// Transposed MFMA as in pw_pair_f32.hip: A = weight fragment, B = activation fragment
+// (ds_read_b128 of a pixel row, lane group q supplying k = 16h + 4q + s to step s), D =
+// [channel][pixel], so a lane's accumulator is 4 consecutive channels of one pixel.
+#include "kernels.h"
+
+namespace adapt {
+
+namespace {
+
+template <int NCH>
+__device__ __forceinline__ int pswz32(int r, int c) {   // 16-byte chunk c of row r (NCH chunks per row)
+  return r * (NCH * 16) + (((c & ~15) | ((c ^ r) & 15)) << 4);
+}
+
+}  // namespace
+
+template <int K, int FPW, int BM>
+__global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
+  constexpr int NT = 512, NS = FPW * 128;
+  constexpr int KH = K / 16;                          // 16-wide K halves
+  constexpr int XCH = K / 4;                          // 16-byte chunks per pixel row
+  constexpr int PF = BM / 16;
+  constexpr int AB = BM * K * 4;
+  constexpr int XIT = (BM * XCH + NT - 1) / NT;
+  static_assert(FPW * K <= 512 && BM % 16 == 0 && 2 * AB <= 160 * 1024, "pw shape");
+  __shared__ __attribute__((aligned(16))) char abuf[2 * AB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nsl = p.N / NS;
+  const int ntiles = (p.M + BM - 1) / BM;
+  // slice-major block order: a slice's blocks are consecutive (one XCD shares its weights in L2)
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = gridDim.x / nsl;                    // blocks per slice (host: gridDim.x % nsl == 0)
+  const int slice = logical / per, b0 = logical - slice * per;
+  if (b0 >= ntiles) return;
+
+  f32x4 wr[FPW][KH];
+  f32x4 bias[FPW];
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    const int gf = (slice * 8 + wave) * FPW + j;      // global 16-channel fragment
+#pragma unroll
+    for (int h = 0; h < KH; ++h) wr[j][h] = *(const f32x4*)(p.w + ((size_t)(gf * KH + h) * 64 + lane) * 4);
+    bias[j] = *(const f32x4*)(p.bias + gf * 16 + fq * 4);
+  }
+
+  f32x4 rx[XIT];
+  auto load_next = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int i = tid + it * NT;
+      const int px = i / XCH, c = i - px * XCH;
+      const int m = min(t * BM + px, p.M - 1);
+      if (XIT * NT == BM * XCH || i < BM * XCH) rx[it] = *(const f32x4*)(p.x + (size_t)m * K + c * 4);
+    }
+  };
+  auto stage_next = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int i = tid + it * NT;
+      if (XIT * NT == BM * XCH || i < BM * XCH) *(f32x4*)(abuf + b * AB + pswz32<XCH>(i / XCH, i % XCH)) = rx[it];
+    }
+  };
+
+  int t = b0;
+  load_next(t);
+  stage_next(0);
+  __syncthreads();
+  int buf = 0;
+  for (; t < ntiles; t += per) {
+    const int tn = t + per;
+    const bool more = tn < ntiles;
+    const int m0 = t * BM;
+    if (more) load_next(tn);                          // in flight under this tile's MFMAs
+    const char* a = abuf + buf * AB;
+    f32x4 acc[FPW][PF];
+#pragma unroll
+    for (int j = 0; j < FPW; ++j)
+#pragma unroll
+      for (int i = 0; i < PF; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < KH; ++h)
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        const f32x4 xf = *(const f32x4*)(a + pswz32<XCH>(i * 16 + fr, h * 4 + fq));
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int j = 0; j < FPW; ++j)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][h][s], xf[s], acc[j][i], 0, 0, 0);
+      }
+    // epilogue: acc[j][i][e] = out[pixel m0 + 16 i + fr][channel 16 gf + 4 fq + e]
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int m = m0 + i * 16 + fr;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < FPW; ++j) {
+        const int ch = ((slice * 8 + wave) * FPW + j) * 16 + fq * 4;
+        f32x4 v = acc[j][i] + bias[j];
+        if (p.res) v += *(const f32x4*)(p.res + (size_t)m * p.N + ch);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], p.relu);
+        *(f32x4*)(p.out + (size_t)m * p.N + ch) = v;
+      }
+    }
+    if (more) stage_next(buf ^ 1);
+    __syncthreads();                                  // next tile staged; this buffer's reads done
+    buf ^= 1;
+  }
+}
+
+// (K, FPW, BM) instances: FPW x K = 512 resident weight floats per lane (128 VGPRs)
+#define ADAPT_PW_F32_CFGS(X) \
+  X(64, 2, 32)               \
+  X(128, 4, 16)              \
+  X(128, 4, 32)              \
+  X(256, 2, 16)              \
+  X(256, 2, 32)              \
+  X(512, 1, 16)              \
+  X(512, 1, 32)
+
+int pw_f32_fpw(int K) { return K == 64 ? 2 : K == 128 ? 4 : K == 256 ? 2 : K == 512 ? 1 : 0; }
+
+bool pw_f32_supported(int K, int N, int bm) {
+  const int fpw = pw_f32_fpw(K);
+  if (!fpw || N % (fpw * 128)) return false;
+#define X(K_, F_, B_) if (K == K_ && bm == B_) return true;
+  ADAPT_PW_F32_CFGS(X)
+#undef X
+  return false;
+}
+
+hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s) {
+  if (!pw_f32_supported(p.K, p.N, bm) || p.M < 1) return hipErrorInvalidValue;
+  const int nsl = p.N / (pw_f32_fpw(p.K) * 128);
+  const int ntiles = (p.M + bm - 1) / bm;
+  int per = 256 / nsl;                                // ~one block per CU over all slices
+  if (per < 1) per = 1;
+  if (per > ntiles) per = ntiles;
+#define X(K_, F_, B_)                                                                                  \
+  if (p.K == K_ && bm == B_) {                                                                         \
+    hipLaunchKernelGGL((pw_f32_kernel<K_, F_, B_>), dim3(per * nsl), dim3(512), 0, s, p);              \
+    return hipGetLastError();                                                                          \
+  }
+  ADAPT_PW_F32_CFGS(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace adapt

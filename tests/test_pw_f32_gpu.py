@@ -1,0 +1,44 @@
+"""fp32 persistent pointwise conv (csrc/kernels/pw_f32.hip, cfgs 120 / 121: filter slice register-resident,
+persistent pixel tiles) against a float64 CPU reference: the ResNet-50 `_out` shapes with residual + ReLU,
+a pixel count that is not a tile multiple, and no-residual / no-activation."""
+import numpy as np
+import pytest
+import torch
+
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # B, H, W, K, N, residual, relu
+    (2, 14, 14, 256, 1024, True, 1),
+    (2, 28, 28, 128, 512, True, 1),
+    (2, 7, 7, 512, 2048, True, 1),
+    (2, 56, 56, 64, 256, True, 1),
+    (1, 5, 3, 256, 512, False, 0),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("cfg", sorted(C.PW_F32_CFGS))
+def test_pw_f32_matches_fp64(shape, cfg):
+    B, H, W, K, N, has_res, relu = shape
+    rng = np.random.default_rng(K + N + cfg)
+    x = rng.standard_normal((B, H, W, K)).astype(np.float32)
+    kern = (rng.standard_normal((1, 1, K, N)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    res = rng.standard_normal((B, H, W, N)).astype(np.float32) if has_res else None
+    pc = C.pack_conv_f32(kern, bias, 1, ((0, 0), (0, 0)), "cuda")
+    if not C.f32_cfg_supported(cfg, K, N, pc):
+        pytest.skip("tile size not built for this K")
+    out = torch.full((B, H, W, N), float("nan"), device="cuda")
+    C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out, None if res is None else torch.from_numpy(res).cuda(),
+                       relu=relu, cfg=cfg)
+    want = x.astype(np.float64) @ kern[0, 0].astype(np.float64) + bias
+    if res is not None:
+        want = want + res
+    if relu:
+        want = np.maximum(want, 0)
+    got = out.cpu().numpy()
+    assert np.isfinite(got).all()
+    err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
+    assert err < 2e-5, f"cfg {cfg}: rel err {err}"
