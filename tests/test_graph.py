@@ -215,3 +215,20 @@ def test_fp32_plan_fuses_stage2_pairs_and_merges_siblings():
     assert len(merged) == 4 and all(s.p["kernel"] == (1, 1) for s in merged)
     covered = [c for s in steps for c in s.covers]
     assert len(covered) == len(set(covered))
+
+
+@pytest.mark.parametrize("cut", ["conv2_block1_out", "conv2_block2_1_relu", "conv2_block2_out",
+                                 "conv3_block1_1_conv", "conv4_block1_out"])
+def test_fp32_plan_slices_cover_every_layer_once(cut):
+    """fp32 plans of a 2-stage cut (including cuts that expose one output of a stage-2 pair, or the
+    block-1 conv of a merged sibling GEMM) still compute every layer exactly once across the slices."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.models.resnet import build_resnet
+    g = build_resnet("resnet50")
+    s = partition(g, [cut])
+    covered = []
+    for sl in s:
+        sg = subgraph(g, sl)
+        for st in compile_plan(sg, fp32=True):
+            covered += [c for c in st.covers if sg.layers[c].op != "input"]
+    layers = [n for n in g.order if g.layers[n].op != "input"]
+    assert sorted(covered) == sorted(layers)
