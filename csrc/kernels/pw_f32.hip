@@ -9,7 +9,8 @@
 // K in VGPRs (FPW x K / 4 = 128 registers), and the block walks BM-pixel tiles of its slice, so the
 // weights cross L2 -> VGPR once per block and the only per-tile traffic is the activation rows in
 // (16-byte row-contiguous loads, prefetched one tile ahead into registers and staged in a swizzled
-// LDS double buffer) and the outputs / residual (16 bytes per lane, straight from the accumulators).
+// LDS double buffer), the residual (16 bytes per lane, also a tile ahead, in registers) and the
+// outputs (16 bytes per lane, straight from the accumulators).
 // One barrier per tile.
 //
 // Transposed MFMA as in pw_pair_f32.hip: A = weight fragment, B = activation fragment
@@ -61,6 +62,8 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
   }
 
   f32x4 rx[XIT];
+  f32x4 rres[FPW][PF], nres[FPW][PF];                 // this tile's / the next tile's residual fragments
+  const bool has_res = p.res != nullptr;
   auto load_next = [&](int t) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
@@ -68,6 +71,15 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
       const int px = i / XCH, c = i - px * XCH;
       const int m = min(t * BM + px, p.M - 1);
       if (XIT * NT == BM * XCH || i < BM * XCH) rx[it] = *(const f32x4*)(p.x + (size_t)m * K + c * 4);
+    }
+    if (has_res) {                                    // the epilogue's residual, a tile ahead like x
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        const int m = min(t * BM + i * 16 + fr, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < FPW; ++j)
+          nres[j][i] = *(const f32x4*)(p.res + (size_t)m * p.N + ((slice * 8 + wave) * FPW + j) * 16 + fq * 4);
+      }
     }
   };
   auto stage_next = [&](int b) __attribute__((always_inline)) {
@@ -87,6 +99,12 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
     const int tn = t + per;
     const bool more = tn < ntiles;
     const int m0 = t * BM;
+    if (has_res) {
+#pragma unroll
+      for (int j = 0; j < FPW; ++j)
+#pragma unroll
+        for (int i = 0; i < PF; ++i) rres[j][i] = nres[j][i];
+    }
     if (more) load_next(tn);                          // in flight under this tile's MFMAs
     const char* a = abuf + buf * AB;
     f32x4 acc[FPW][PF];
@@ -114,7 +132,7 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
       for (int j = 0; j < FPW; ++j) {
         const int ch = ((slice * 8 + wave) * FPW + j) * 16 + fq * 4;
         f32x4 v = acc[j][i] + bias[j];
-        if (p.res) v += *(const f32x4*)(p.res + (size_t)m * p.N + ch);
+        if (has_res) v += rres[j][i];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], p.relu);
         *(f32x4*)(p.out + (size_t)m * p.N + ch) = v;

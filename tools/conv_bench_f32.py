@@ -71,7 +71,7 @@ def bench(shape, only=None, ks_list=(1, 2, 4, -1, -2), reps=10, top=20):
     print(f"\n== fp32 B{B} {H}x{W}x{Cin} -> {Cout} k{k} s{s} res{has_res}  M={M} N={N} K={pc.K}  "
           f"{flop / 1e9:.2f} GFLOP  (floor {flop / 150e12 * 1e6:.1f} us at 150 TF/s)", flush=True)
     for t, cfg, ks in rows[:top]:
-        print(f"  cfg {cfg:2d} {str(C.F32_TILES.get(cfg, ('wino',) + {**C.WINO_F32_CFGS, **C.WINO_F32_ABLATE}.get(cfg, ()))):10s} ks {ks:2d}  {t:7.2f} us  {flop / t / 1e6:6.1f} TF/s",
+        print(f"  cfg {cfg:2d} {str(C.F32_TILES.get(cfg, (('pw', C.PW_F32_CFGS[cfg]) if cfg in C.PW_F32_CFGS else ('wino',) + {**C.WINO_F32_CFGS, **C.WINO_F32_ABLATE}.get(cfg, ())))):10s} ks {ks:2d}  {t:7.2f} us  {flop / t / 1e6:6.1f} TF/s",
               flush=True)
     return rows
 
