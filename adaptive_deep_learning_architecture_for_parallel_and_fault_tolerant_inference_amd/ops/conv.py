@@ -473,13 +473,19 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 # fp32 persistent pointwise configs (csrc/kernels/pw_f32.hip): id -> pixels per tile; 1x1 / s1 / p0 convs
 # with K in {64, 128, 256, 512} and N a multiple of the slice (FPW x 128 channels), ksplit 1
 PW_F32_CFGS = {120: 16, 121: 32}
-PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1}
-PW_F32_BMS = {64: (32,), 128: (16, 32), 256: (16, 32), 512: (16, 32)}
+PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1, 1024: 1}     # 16-channel fragments per wave
+PW_F32_KG = {1024: 2}                                       # K groups of waves (partials meet in LDS)
+PW_F32_BMS = {64: (32,), 128: (16, 32), 256: (16, 32), 512: (16, 32), 1024: (16,)}
+
+
+def pw_f32_slice(K: int) -> int:
+    """Output channels per block of the pointwise kernel (FPW x 16 x waves per K group)."""
+    return PW_F32_FPW[K] * 16 * (8 // PW_F32_KG.get(K, 1))
 
 
 def pw_f32_shape_ok(pc: "PackedConv") -> bool:
     return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 1, 0, 0, 0, 0)
-            and pc.cin in PW_F32_FPW and pc.cout % (PW_F32_FPW[pc.cin] * 128) == 0 and not pc.n_split)
+            and pc.cin in PW_F32_FPW and pc.cout % pw_f32_slice(pc.cin) == 0 and not pc.n_split)
 
 
 def pack_pw_f32(kernel_hwio: np.ndarray) -> np.ndarray:

@@ -29,19 +29,25 @@ __device__ __forceinline__ int pswz32(int r, int c) {   // 16-byte chunk c of ro
 
 }  // namespace
 
-template <int K, int FPW, int BM>
+// KG > 1 (K = 1024): the 8 waves form KG groups that each hold the same channels over 1/KG of K;
+// groups 1.. leave their partial sums in LDS and group 0 adds them in its epilogue.
+template <int K, int FPW, int BM, int KG = 1>
 __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
-  constexpr int NT = 512, NS = FPW * 128;
+  constexpr int NT = 512, NWG = 8 / KG, NS = FPW * 16 * NWG;
   constexpr int KH = K / 16;                          // 16-wide K halves
+  constexpr int KHG = KH / KG;                        // halves per K group
   constexpr int XCH = K / 4;                          // 16-byte chunks per pixel row
   constexpr int PF = BM / 16;
   constexpr int AB = BM * K * 4;
+  constexpr int RED = (KG - 1) * BM * NS * 4;
   constexpr int XIT = (BM * XCH + NT - 1) / NT;
-  static_assert(FPW * K <= 512 && BM % 16 == 0 && 2 * AB <= 160 * 1024, "pw shape");
-  __shared__ __attribute__((aligned(16))) char abuf[2 * AB];
+  static_assert(FPW * K / KG <= 512 && BM % 16 == 0 && 2 * AB + RED <= 160 * 1024 && KH % KG == 0, "pw shape");
+  __shared__ __attribute__((aligned(16))) char abuf[2 * AB + (RED > 0 ? RED : 16)];
+  float* const red = (float*)(abuf + 2 * AB);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kgi = wave / NWG, wg = wave - kgi * NWG;  // K group, wave within the group
   const int fr = lane & 15, fq = lane >> 4;
   const int nsl = p.N / NS;
   const int ntiles = (p.M + BM - 1) / BM;
@@ -51,13 +57,14 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
   const int slice = logical / per, b0 = logical - slice * per;
   if (b0 >= ntiles) return;
 
-  f32x4 wr[FPW][KH];
+  f32x4 wr[FPW][KHG];
   f32x4 bias[FPW];
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
-    const int gf = (slice * 8 + wave) * FPW + j;      // global 16-channel fragment
+    const int gf = (slice * NWG + wg) * FPW + j;      // global 16-channel fragment
 #pragma unroll
-    for (int h = 0; h < KH; ++h) wr[j][h] = *(const f32x4*)(p.w + ((size_t)(gf * KH + h) * 64 + lane) * 4);
+    for (int h = 0; h < KHG; ++h)
+      wr[j][h] = *(const f32x4*)(p.w + ((size_t)(gf * KH + kgi * KHG + h) * 64 + lane) * 4);
     bias[j] = *(const f32x4*)(p.bias + gf * 16 + fq * 4);
   }
 
@@ -72,13 +79,13 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
       const int m = min(t * BM + px, p.M - 1);
       if (XIT * NT == BM * XCH || i < BM * XCH) rx[it] = *(const f32x4*)(p.x + (size_t)m * K + c * 4);
     }
-    if (has_res) {                                    // the epilogue's residual, a tile ahead like x
+    if (has_res && kgi == 0) {                        // the epilogue's residual, a tile ahead like x
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
         const int m = min(t * BM + i * 16 + fr, p.M - 1);
 #pragma unroll
         for (int j = 0; j < FPW; ++j)
-          nres[j][i] = *(const f32x4*)(p.res + (size_t)m * p.N + ((slice * 8 + wave) * FPW + j) * 16 + fq * 4);
+          nres[j][i] = *(const f32x4*)(p.res + (size_t)m * p.N + ((slice * NWG + wg) * FPW + j) * 16 + fq * 4);
       }
     }
   };
@@ -113,24 +120,43 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
 #pragma unroll
       for (int i = 0; i < PF; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int h = 0; h < KH; ++h)
+    for (int h = 0; h < KHG; ++h)
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
-        const f32x4 xf = *(const f32x4*)(a + pswz32<XCH>(i * 16 + fr, h * 4 + fq));
+        const f32x4 xf = *(const f32x4*)(a + pswz32<XCH>(i * 16 + fr, (kgi * KHG + h) * 4 + fq));
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int j = 0; j < FPW; ++j)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][h][s], xf[s], acc[j][i], 0, 0, 0);
       }
-    // epilogue: acc[j][i][e] = out[pixel m0 + 16 i + fr][channel 16 gf + 4 fq + e]
+    if constexpr (KG > 1) {                           // K groups 1.. -> LDS -> group 0
+      if (kgi > 0) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i)
+#pragma unroll
+          for (int j = 0; j < FPW; ++j)
+            *(f32x4*)(red + (((kgi - 1) * BM + i * 16 + fr) * NS + (wg * FPW + j) * 16 + fq * 4)) = acc[j][i];
+      }
+      __syncthreads();
+      if (kgi == 0) {
+#pragma unroll
+        for (int g = 1; g < KG; ++g)
+#pragma unroll
+          for (int i = 0; i < PF; ++i)
+#pragma unroll
+            for (int j = 0; j < FPW; ++j)
+              acc[j][i] += *(const f32x4*)(red + (((g - 1) * BM + i * 16 + fr) * NS + (wg * FPW + j) * 16 + fq * 4));
+      }
+    }
+    // epilogue (K group 0): acc[j][i][e] = out[pixel m0 + 16 i + fr][channel 16 gf + 4 fq + e]
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
       const int m = m0 + i * 16 + fr;
-      if (m >= p.M) continue;
+      if (m >= p.M || kgi > 0) continue;
 #pragma unroll
       for (int j = 0; j < FPW; ++j) {
-        const int ch = ((slice * 8 + wave) * FPW + j) * 16 + fq * 4;
+        const int ch = ((slice * NWG + wg) * FPW + j) * 16 + fq * 4;
         f32x4 v = acc[j][i] + bias[j];
         if (has_res) v += rres[j][i];
 #pragma unroll
@@ -144,22 +170,25 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
   }
 }
 
-// (K, FPW, BM) instances: FPW x K = 512 resident weight floats per lane (128 VGPRs)
+// (K, FPW, BM, KG) instances: FPW x K / KG = 512 resident weight floats per lane (128 VGPRs)
 #define ADAPT_PW_F32_CFGS(X) \
-  X(64, 2, 32)               \
-  X(128, 4, 16)              \
-  X(128, 4, 32)              \
-  X(256, 2, 16)              \
-  X(256, 2, 32)              \
-  X(512, 1, 16)              \
-  X(512, 1, 32)
+  X(64, 2, 32, 1)            \
+  X(128, 4, 16, 1)           \
+  X(128, 4, 32, 1)           \
+  X(256, 2, 16, 1)           \
+  X(256, 2, 32, 1)           \
+  X(512, 1, 16, 1)           \
+  X(512, 1, 32, 1)           \
+  X(1024, 1, 16, 2)
 
-int pw_f32_fpw(int K) { return K == 64 ? 2 : K == 128 ? 4 : K == 256 ? 2 : K == 512 ? 1 : 0; }
+int pw_f32_fpw(int K) { return K == 64 ? 2 : K == 128 ? 4 : K == 256 ? 2 : K == 512 ? 1 : K == 1024 ? 1 : 0; }
+static int pw_f32_kg(int K) { return K == 1024 ? 2 : 1; }
+static int pw_f32_ns(int K) { return pw_f32_fpw(K) * 16 * (8 / pw_f32_kg(K)); }   // channels per block slice
 
 bool pw_f32_supported(int K, int N, int bm) {
   const int fpw = pw_f32_fpw(K);
-  if (!fpw || N % (fpw * 128)) return false;
-#define X(K_, F_, B_) if (K == K_ && bm == B_) return true;
+  if (!fpw || N % pw_f32_ns(K)) return false;
+#define X(K_, F_, B_, G_) if (K == K_ && bm == B_) return true;
   ADAPT_PW_F32_CFGS(X)
 #undef X
   return false;
@@ -167,14 +196,14 @@ bool pw_f32_supported(int K, int N, int bm) {
 
 hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s) {
   if (!pw_f32_supported(p.K, p.N, bm) || p.M < 1) return hipErrorInvalidValue;
-  const int nsl = p.N / (pw_f32_fpw(p.K) * 128);
+  const int nsl = p.N / pw_f32_ns(p.K);
   const int ntiles = (p.M + bm - 1) / bm;
   int per = 256 / nsl;                                // ~one block per CU over all slices
   if (per < 1) per = 1;
   if (per > ntiles) per = ntiles;
-#define X(K_, F_, B_)                                                                                  \
+#define X(K_, F_, B_, G_)                                                                              \
   if (p.K == K_ && bm == B_) {                                                                         \
-    hipLaunchKernelGGL((pw_f32_kernel<K_, F_, B_>), dim3(per * nsl), dim3(512), 0, s, p);              \
+    hipLaunchKernelGGL((pw_f32_kernel<K_, F_, B_, G_>), dim3(per * nsl), dim3(512), 0, s, p);          \
     return hipGetLastError();                                                                          \
   }
   ADAPT_PW_F32_CFGS(X)

@@ -15,6 +15,8 @@ SHAPES = [  # B, H, W, K, N, residual, relu
     (2, 7, 7, 512, 2048, True, 1),
     (2, 56, 56, 64, 256, True, 1),
     (1, 5, 3, 256, 512, False, 0),
+    (2, 14, 14, 1024, 256, False, 1),          # K groups (partials meet in LDS)
+    (1, 3, 5, 1024, 192, True, 0),
 ]
 
 
