@@ -483,9 +483,15 @@ def pw_f32_slice(K: int) -> int:
     return PW_F32_FPW[K] * 16 * (8 // PW_F32_KG.get(K, 1))
 
 
-def pw_f32_shape_ok(pc: "PackedConv") -> bool:
-    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 1, 0, 0, 0, 0)
-            and pc.cin in PW_F32_FPW and pc.cout % pw_f32_slice(pc.cin) == 0 and not pc.n_split)
+def pw_f32_packable(pc: "PackedConv") -> bool:
+    """1x1, no padding, stride 1 or 2, K one the pointwise kernel is built for."""
+    return ((pc.kh, pc.kw, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 0, 0, 0, 0) and pc.stride in (1, 2)
+            and pc.cin in PW_F32_FPW)
+
+
+def pw_f32_shape_ok(pc: "PackedConv", bm: int = 16) -> bool:
+    """Packable and some built instance's channel slice divides N (and the dual-output split)."""
+    return pw_f32_packable(pc) and kernels().pw_f32_fpw(pc.cin, pc.cout, int(pc.n_split), bm) > 0
 
 
 def pack_pw_f32(kernel_hwio: np.ndarray) -> np.ndarray:
@@ -500,8 +506,8 @@ def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] 
     (Winograd configs also need the conv itself: 3x3 / s1 / p1 with its transformed weights;
     the pointwise configs a 1x1 / s1 conv with its fragment-packed weights)."""
     if cfg in PW_F32_CFGS:
-        return (pc is not None and pc.pwf is not None and pw_f32_shape_ok(pc)
-                and PW_F32_CFGS[cfg] in PW_F32_BMS[pc.cin])
+        return (pc is not None and pc.pwf is not None and PW_F32_CFGS[cfg] in PW_F32_BMS[pc.cin]
+                and pw_f32_shape_ok(pc, PW_F32_CFGS[cfg]))
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         fn = {**WINO_F32_CFGS, **WINO_F32_ABLATE}[cfg][1]
         return pc is not None and pc.wino is not None and wino_supported(pc) and cout % (16 * fn) == 0
@@ -525,7 +531,7 @@ def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, 
                     kh=kh, kw=kw, cin=cin, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
     if wino_supported(pc):
         pc.wino = torch.from_numpy(wino_pack_np(kernel_hwio)).to(device=device).contiguous()
-    if pw_f32_shape_ok(pc):
+    if pw_f32_packable(pc) and cout % 16 == 0:
         pc.pwf = torch.from_numpy(pack_pw_f32(kernel_hwio)).to(device=device).contiguous()
     return pc
 
@@ -599,11 +605,12 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
     if cfg is None:
         cfg, ksplit = choose_cfg_f32(M, N, pc.Kpad)
     if cfg in PW_F32_CFGS:
-        if not f32_cfg_supported(cfg, C, N, pc) or int(ksplit or 1) != 1 or (OH, OW) != (H, W) or out2 is not None:
-            raise ValueError(f"pointwise fp32 config {cfg}: 1x1 / s1 conv, K in {sorted(PW_F32_FPW)}, "
-                             f"N % slice == 0, ksplit 1, single output")
+        if not f32_cfg_supported(cfg, C, N, pc) or int(ksplit or 1) != 1 or x.dim() != 4:
+            raise ValueError(f"pointwise fp32 config {cfg}: 1x1 / s1-2 conv, K in {sorted(PW_F32_FPW)}, "
+                             f"N (and the dual-output split) a multiple of the slice, ksplit 1")
         kernels().pw_f32_forward(ptr(x), ptr(pc.pwf), ptr(pc.bias), ptr(residual), ptr(out), M, C, N, int(relu),
-                                 PW_F32_CFGS[cfg], stream_handle(stream))
+                                 PW_F32_CFGS[cfg], stream_handle(stream), B, H, W, OH, OW, pc.stride, ptr(out2),
+                                 int(ns), int(relu2))
         return out
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         # ksplit > 1: slabs + splitk_reduce_f32; ksplit <= -2: -ksplit slabs, the last split of

@@ -1,6 +1,9 @@
 // Persistent fp32 pointwise (1x1 / stride 1) conv with the filter slice resident in registers:
 //
-//   out = act(x . W + bias (+ res))      x [M][K], W [K][N], K in {64, 128, 256, 512}
+//   out = act(x . W + bias (+ res))      x [M][K], W [K][N], K in {64, 128, 256, 512, 1024}
+//
+// (also stride-s 1x1 convs, the input row of output pixel m being pixel (s oh, s ow), and merged
+// sibling convs with a dual output split at a slice boundary)
 //
 // The fp32 tile GEMMs (conv_f32.hip / conv_f32g.hip) run ResNet's 1x1 convs at 43-51 % MFMA busy
 // (profiles/r3/pmc/pmc_gemm1x1_f32.txt): at K = 128-512 a 64x64 tile has only 4-16 K steps, so every
@@ -68,6 +71,19 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
     bias[j] = *(const f32x4*)(p.bias + gf * 16 + fq * 4);
   }
 
+  // input row of output pixel m (stride-s 1x1: pixel (img, s oh, s ow) of the H x W input)
+  const int ohw = p.OH * p.OW;
+  auto xrow = [&](int m) __attribute__((always_inline)) {
+    if (p.stride == 1) return m;
+    const int img = m / ohw, r = m - img * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+    return (img * p.H + oh * p.stride) * p.W + ow * p.stride;
+  };
+  // dual output (merged sibling convs, n_split a multiple of the slice): one destination per block
+  const bool second = p.n_split > 0 && slice * NS >= p.n_split;
+  float* const dst = second ? p.out2 : p.out;
+  const int ldo = p.n_split > 0 ? (second ? p.N - p.n_split : p.n_split) : p.N;
+  const int cof = second ? p.n_split : 0;
+  const int relu = second ? p.relu2 : p.relu;
   f32x4 rx[XIT];
   f32x4 rres[FPW][PF], nres[FPW][PF];                 // this tile's / the next tile's residual fragments
   const bool has_res = p.res != nullptr;
@@ -77,7 +93,7 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
       const int i = tid + it * NT;
       const int px = i / XCH, c = i - px * XCH;
       const int m = min(t * BM + px, p.M - 1);
-      if (XIT * NT == BM * XCH || i < BM * XCH) rx[it] = *(const f32x4*)(p.x + (size_t)m * K + c * 4);
+      if (XIT * NT == BM * XCH || i < BM * XCH) rx[it] = *(const f32x4*)(p.x + (size_t)xrow(m) * K + c * 4);
     }
     if (has_res && kgi == 0) {                        // the epilogue's residual, a tile ahead like x
 #pragma unroll
@@ -160,8 +176,8 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
         f32x4 v = acc[j][i] + bias[j];
         if (has_res) v += rres[j][i];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], p.relu);
-        *(f32x4*)(p.out + (size_t)m * p.N + ch) = v;
+        for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
+        *(f32x4*)(dst + (size_t)m * ldo + ch - cof) = v;
       }
     }
     if (more) stage_next(buf ^ 1);
@@ -170,39 +186,50 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
   }
 }
 
-// (K, FPW, BM, KG) instances: FPW x K / KG = 512 resident weight floats per lane (128 VGPRs)
+// (K, FPW, BM, KG) instances: FPW x K / KG <= 512 resident weight floats per lane (<= 128 VGPRs)
 #define ADAPT_PW_F32_CFGS(X) \
   X(64, 2, 32, 1)            \
   X(128, 4, 16, 1)           \
   X(128, 4, 32, 1)           \
   X(256, 2, 16, 1)           \
   X(256, 2, 32, 1)           \
+  X(256, 1, 16, 1)           \
   X(512, 1, 16, 1)           \
   X(512, 1, 32, 1)           \
   X(1024, 1, 16, 2)
 
-int pw_f32_fpw(int K) { return K == 64 ? 2 : K == 128 ? 4 : K == 256 ? 2 : K == 512 ? 1 : K == 1024 ? 1 : 0; }
 static int pw_f32_kg(int K) { return K == 1024 ? 2 : 1; }
-static int pw_f32_ns(int K) { return pw_f32_fpw(K) * 16 * (8 / pw_f32_kg(K)); }   // channels per block slice
-
-bool pw_f32_supported(int K, int N, int bm) {
-  const int fpw = pw_f32_fpw(K);
-  if (!fpw || N % pw_f32_ns(K)) return false;
-#define X(K_, F_, B_, G_) if (K == K_ && bm == B_) return true;
+static bool pw_f32_has(int K, int fpw, int bm) {
+#define X(K_, F_, B_, G_) if (K == K_ && fpw == F_ && bm == B_) return true;
   ADAPT_PW_F32_CFGS(X)
 #undef X
   return false;
 }
+// fragments per wave for (K, N, bm): the widest built instance whose slice (FPW x 16 x waves per
+// K group channels) divides N, and (dual output) the first output's width; 0: none
+static int pw_f32_pick(int K, int N, int n_split, int bm) {
+  for (int fpw = 4; fpw >= 1; fpw >>= 1) {
+    const int ns = fpw * 16 * (8 / pw_f32_kg(K));
+    if (pw_f32_has(K, fpw, bm) && N % ns == 0 && n_split % ns == 0) return fpw;
+  }
+  return 0;
+}
+int pw_f32_fpw(int K, int N, int n_split, int bm) { return pw_f32_pick(K, N, n_split, bm); }
+
+bool pw_f32_supported(int K, int N, int bm) { return pw_f32_pick(K, N, 0, bm) > 0; }
 
 hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s) {
-  if (!pw_f32_supported(p.K, p.N, bm) || p.M < 1) return hipErrorInvalidValue;
-  const int nsl = p.N / pw_f32_ns(p.K);
+  const int fpw = pw_f32_pick(p.K, p.N, p.n_split, bm);
+  if (!fpw || p.M < 1 || p.stride < 1 || (p.n_split && (!p.out2 || p.res)) ||
+      p.M != p.B * p.OH * p.OW || (p.stride == 1 && (p.H != p.OH || p.W != p.OW)))
+    return hipErrorInvalidValue;
+  const int nsl = p.N / (fpw * 16 * (8 / pw_f32_kg(p.K)));
   const int ntiles = (p.M + bm - 1) / bm;
   int per = 256 / nsl;                                // ~one block per CU over all slices
   if (per < 1) per = 1;
   if (per > ntiles) per = ntiles;
 #define X(K_, F_, B_, G_)                                                                              \
-  if (p.K == K_ && bm == B_) {                                                                         \
+  if (p.K == K_ && fpw == F_ && bm == B_) {                                                            \
     hipLaunchKernelGGL((pw_f32_kernel<K_, F_, B_, G_>), dim3(per * nsl), dim3(512), 0, s, p);          \
     return hipGetLastError();                                                                          \
   }

@@ -44,3 +44,27 @@ def test_pw_f32_matches_fp64(shape, cfg):
     assert np.isfinite(got).all()
     err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
     assert err < 2e-5, f"cfg {cfg}: rel err {err}"
+
+
+@pytest.mark.parametrize("cfg", [120])
+@pytest.mark.parametrize("B,H,K,N0,N1", [(2, 56, 256, 512, 128), (2, 28, 512, 1024, 256), (1, 9, 256, 512, 128)])
+def test_pw_f32_strided_dual_output(cfg, B, H, K, N0, N1):
+    """Merged sibling stride-2 1x1 convs (the ResNet projection shortcut + block-1 `_1` conv): one pointwise
+    launch, columns >= N0 to the second output with their own activation."""
+    rng = np.random.default_rng(B + H + K)
+    x = rng.standard_normal((B, H, H, K)).astype(np.float32)
+    kern = (rng.standard_normal((1, 1, K, N0 + N1)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal(N0 + N1).astype(np.float32)
+    pc = C.pack_conv_f32(kern, bias, 2, ((0, 0), (0, 0)), "cuda")
+    pc.n_split = N0
+    if not C.f32_cfg_supported(cfg, K, N0 + N1, pc):
+        pytest.skip("no pointwise instance for this split")
+    OH = (H - 1) // 2 + 1
+    out = torch.full((B, OH, OH, N0), float("nan"), device="cuda")
+    out2 = torch.full((B, OH, OH, N1), float("nan"), device="cuda")
+    C.conv_forward_f32(torch.from_numpy(x).cuda(), pc, out, relu=0, cfg=cfg, out2=out2, relu2=1)
+    want = x[:, ::2, ::2, :].astype(np.float64) @ kern[0, 0].astype(np.float64) + bias
+    for got, w in ((out, want[..., :N0]), (out2, np.maximum(want[..., N0:], 0))):
+        g = got.cpu().numpy()
+        assert np.isfinite(g).all()
+        assert np.abs(g - w).max() / max(1.0, np.abs(w).max()) < 2e-5
