@@ -288,3 +288,11 @@ def test_resnet50_fp32_plan_uses_fused_stem_and_v2_convs():
     assert kinds[0] == "stem_f32" and "maxpool" not in kinds
     v2 = [c for i, (c, _) in ex.cfg.items() if c in C.F32G_CFGS]
     print(f"fp32 plan: {len(ex.steps)} steps, {len(v2)} of {len(ex.cfg)} GEMMs on the v2 LDS-DMA kernel")
+    # the round-3 kernels are on the tuned bs=32 plan, not silently replaced by a generic path
+    assert kinds.count("pair") == 2                                    # pw_pair_f32.hip, stage 2
+    assert sum(1 for st in ex.steps if st.kind == "conv" and st.p.get("out2")) == 4     # merged siblings
+    cfgs = {c for c, _ in ex.cfg.values()}
+    assert cfgs & set(C.WINO_F32_CFGS), "no Winograd config on the fp32 3x3 convs"
+    assert cfgs & set(C.PW_F32_CFGS), "no persistent pointwise config on the fp32 1x1 convs"
+    wino3x3 = [i for i, st in enumerate(ex.steps) if st.kind == "conv" and st.p.get("kernel") == (3, 3)]
+    assert wino3x3 and all(ex.cfg[i][0] in C.WINO_F32_CFGS for i in wino3x3)
