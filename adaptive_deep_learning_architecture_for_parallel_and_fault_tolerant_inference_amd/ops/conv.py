@@ -475,7 +475,7 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 PW_F32_CFGS = {120: 16, 121: 32}
 PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1, 1024: 1}     # 16-channel fragments per wave
 PW_F32_KG = {1024: 2}                                       # K groups of waves (partials meet in LDS)
-PW_F32_BMS = {64: (32,), 128: (16, 32), 256: (16, 32), 512: (16, 32), 1024: (16,)}
+PW_F32_BMS = {64: (16, 32), 128: (16, 32), 256: (16, 32), 512: (16, 32), 1024: (16,)}
 
 
 def pw_f32_slice(K: int) -> int:

@@ -188,6 +188,7 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
 
 // (K, FPW, BM, KG) instances: FPW x K / KG <= 512 resident weight floats per lane (<= 128 VGPRs)
 #define ADAPT_PW_F32_CFGS(X) \
+  X(64, 2, 16, 1)            \
   X(64, 2, 32, 1)            \
   X(128, 4, 16, 1)           \
   X(128, 4, 32, 1)           \
