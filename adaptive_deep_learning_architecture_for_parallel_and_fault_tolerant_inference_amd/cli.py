@@ -96,7 +96,8 @@ def cmd_serve(argv):
     ap.add_argument("--uint8", action="store_true", help="send uint8 images (4x fewer bytes), preprocessed on the GPU")
     ap.add_argument("--preprocess", default="none", choices=["none", "caffe", "tf", "torch"],
                     help="Keras preprocess_input mode applied by stage 0 to uint8 requests")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="worker compute precision")
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="worker compute precision (fp32 = the reference's Keras float32)")
     a = ap.parse_args(argv)
     cfg = _cfg(a, transport=a.transport, codec=a.codec, replicas=a.replicas)
     from .dispatcher import DEFER

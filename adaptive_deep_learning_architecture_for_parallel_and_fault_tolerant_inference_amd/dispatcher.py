@@ -133,11 +133,11 @@ class DEFER:
     def __init__(self, computeNodes: Optional[Sequence[str]] = None, *, membership: Optional[Tuple[str, int]] = None,
                  membership_port: int = 2379, result_port: int = RESULT_PORT, chunk_size: int = 512 * 1000,
                  batch: int = 1, codec: str = "none", weight_codec: str = "zfp+lz4", max_inflight: int = 8,
-                 task_timeout: float = 10.0, worker_wait: float = 5.0, elastic: bool = False,
+                 task_timeout: Optional[float] = None, worker_wait: float = 5.0, elastic: bool = False,
                  ordered: bool = False, device_graph: bool = True, min_workers: int = 1,
-                 transport: str = "tcp", link_codec: str = "none", replicas: Union[int, str] = "auto",
+                 transport: str = "auto", link_codec: str = "none", replicas: Union[int, str] = "auto",
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
-                 quarantine_s: float = 30.0, hb_timeout: float = 0.25, precision: str = "bf16",
+                 quarantine_s: float = 30.0, hb_timeout: float = 0.25, precision: str = "fp32",
                  ingest: str = "auto", preprocess: str = "none", links: str = "auto",
                  hang_factor: float = 20.0, hang_min_s: float = 0.2) -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
@@ -146,7 +146,10 @@ class DEFER:
         the collective stage-to-stage links ("none", "lz4", "zvc"; codec/wire.py,
         on a side stream).  transport: stage-to-stage links — "tcp" (framed,
         codec; any host), "rccl" (RCCL p2p over xGMI between GPU workers),
-        "gloo" (CPU workers).  replicas: "auto" = as many k-stage pipelines as
+        "gloo" (CPU workers), "auto" (default: per epoch, "rccl" when every
+        stage of the replica is a GPU worker on its own device of one host —
+        the north star's stage-per-MI355X chain — else "tcp"; see
+        `epoch_transport`).  replicas: "auto" = as many k-stage pipelines as
         the live workers fill, or a maximum count.  resident: keep the whole
         model on every worker after its first slice so re-plans push nothing.
         ingest: "auto" = requests go through same-host shared memory to a local
@@ -164,10 +167,15 @@ class DEFER:
         tolerates a heartbeat thread delayed on a loaded host).  hang_factor /
         hang_min_s: a stage whose progress counter stands still for
         max(hang_factor x micro-batch period, hang_min_s) while its replica
-        holds work is hung."""
+        holds work is hung.  task_timeout: age (from submission) at which an
+        in-flight request marks its replica failed; None (default) = per
+        replica, max(10 s for an all-GPU replica / 30 s when any stage runs
+        on a CPU, 4 x max_inflight x the replica's measured micro-batch
+        period), so requests queued behind a full window on slow edge stages
+        are not mistaken for a failure."""
         if links not in ("auto", "dev", "shm", "tcp"):
             raise ValueError(f"unknown links mode {links!r}")
-        if transport not in ("tcp", "rccl", "gloo"):
+        if transport not in ("tcp", "rccl", "gloo", "auto"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
         self.link_codec = link_codec
@@ -184,6 +192,7 @@ class DEFER:
         self.codec = codec
         self.weight_codec = weight_codec
         self.task_timeout = task_timeout
+        self.max_inflight = max_inflight
         self.worker_wait = worker_wait
         self.elastic = elastic
         self.ordered = ordered
@@ -254,6 +263,7 @@ class DEFER:
         self._epoch_results: Dict[int, int] = {}    # epoch -> results received from its last stage
         self._epoch_t0: Dict[int, float] = {}       # epoch -> when it was installed
         self._hung_epochs: set = set()
+        self._prog_hist: Dict[Tuple[str, int], List[Tuple[int, float]]] = {}   # (worker, epoch) -> [(count, t)]
         try:
             from .native import runtime
             self._hb = runtime().hb_monitor_start(0)
@@ -487,6 +497,29 @@ class DEFER:
         t = stage_s if stage_s > 0 else ent[1]
         return max(self.hang_factor * t, self.hang_min_s)
 
+    def _note_counters(self, prog: Dict[str, Tuple[int, float, float, int]], now: float) -> None:
+        """Remember when each stage's progress counter reached each value it was
+        seen at: (count, time it advanced), per (worker, epoch).  A counter
+        observed jumping from 3 to 5 records (5, t): the time it passed 4 is at
+        most t, so later lookups can only under-estimate a stall."""
+        for wid, (n, age, _st, ep) in prog.items():
+            h = self._prog_hist.setdefault((wid, ep), [])
+            if n > 0 and (not h or n > h[-1][0]):
+                h.append((n, now - age))
+                if len(h) > 256:
+                    del h[:len(h) - 256]
+        if len(self._prog_hist) > 8 * max(1, len(prog)) + 16:
+            with self._rep_lock:
+                live = {p.epoch for p in self.replicas.values()}
+            for key in [k for k in self._prog_hist if k[1] not in live]:
+                del self._prog_hist[key]
+
+    def _reached_at(self, wid: str, epoch: int, count: int) -> Optional[float]:
+        for c, t in self._prog_hist.get((wid, epoch), ()):
+            if c >= count:
+                return t
+        return None
+
     def _hang_check(self, prog: Dict[str, Tuple[int, float, float, int]]) -> None:
         """Find the stage the oldest request of a replica is stuck in and call it
         hung once it has made no progress for its threshold.
@@ -495,8 +528,16 @@ class DEFER:
         of epoch e came back, every stage that completed more than C micro-batches
         of e has passed the oldest unfinished one; the first stage that completed
         at most C holds it (or it is in transfer to it).  Starved stages further
-        down and back-pressured ones further up are never blamed."""
+        down and back-pressured ones further up are never blamed.
+
+        The holding stage's stall clock starts at the later of its own last
+        progress and the moment request C+1 could have reached it: when the
+        upstream stage's counter passed C (stage 0: the request's submission).
+        A fast stage that sat idle while a slow upstream stage worked on the
+        request is therefore not blamed for the upstream time (an idle gap, or
+        an unbalanced cut under low-rate traffic)."""
         now = time.time()
+        self._note_counters(prog, now)
         with self._rep_lock:
             reps = list(self.replicas.values())
         for p in reps:
@@ -510,6 +551,7 @@ class DEFER:
                 continue
             done = self._epoch_results.get(p.epoch, 0)
             t0 = self._epoch_t0.get(p.epoch, now)
+            arrived = now - oldest_task                  # request done+1 reached stage 0 when it was submitted
             for idx, wid in enumerate(p.workers):
                 ent = prog.get(wid)
                 if ent is None:
@@ -517,19 +559,22 @@ class DEFER:
                 n, age, stage_s, ep = ent
                 if ep != p.epoch:
                     n, age = 0, now - t0                 # nothing completed in this epoch yet
-                age = min(age, now - t0)
                 if n > done:
-                    continue                             # passed the oldest request
+                    # passed the oldest request: it reached the next stage once this counter passed `done`
+                    t_pass = self._reached_at(wid, p.epoch, done + 1)
+                    arrived = t_pass if t_pass is not None else now
+                    continue
+                stalled = now - max(now - age, arrived, t0)
                 thr = self.hang_threshold(p.replica, p.epoch, stage_s)
-                if age > thr and oldest_task > thr:
+                if stalled > thr and oldest_task > thr:
                     self.hangs.append({"t": now, "worker": wid, "stage": idx, "replica": p.replica,
-                                       "epoch": p.epoch, "stalled_ms": round(age * 1e3, 1),
+                                       "epoch": p.epoch, "stalled_ms": round(stalled * 1e3, 1),
                                        "threshold_ms": round(thr * 1e3, 1), "completed": n, "results": done})
                     METRICS.inc("stages_hung")
                     self._hung_epochs.add(p.epoch)
                     self._quarantine[wid] = now + self.quarantine_s
                     self._mark_dirty(p.replica, f"worker {wid} (stage {idx}) hung: no progress for "
-                                                f"{age * 1e3:.0f} ms (threshold {thr * 1e3:.0f} ms) holding "
+                                                f"{stalled * 1e3:.0f} ms (threshold {thr * 1e3:.0f} ms) holding "
                                                 f"request #{done + 1} of epoch {p.epoch}", epoch=p.epoch)
                 break
 
@@ -636,16 +681,40 @@ class DEFER:
         self._sent_slices.setdefault(wid, set()).add(key)
         return wid
 
+    def epoch_transport(self, recs: Sequence[dict]) -> str:
+        """The stage -> stage transport of one replica's epoch.  An explicit
+        `transport` is used as given.  "auto" picks RCCL p2p (xGMI) when the
+        replica has more than one stage and every stage is a GPU worker on a
+        distinct device of one host (one process per MI355X); any
+        CPU stage, two stages sharing a GPU (RCCL refuses duplicate devices) or
+        stages on different hosts fall back to "tcp" (with same-host device /
+        shared-memory links, `links`)."""
+        if self.transport != "auto":
+            return self.transport
+        if len(recs) < 2:
+            return "tcp"
+        devs = []
+        for r in recs:
+            d = str(r.get("device", ""))
+            if not d.startswith("cuda"):
+                return "tcp"
+            idx = int(d.split(":", 1)[1]) if ":" in d else 0
+            devs.append((r.get("shm_domain") or r.get("host"), idx))
+        if len({h for h, _ in devs}) != 1 or len(set(devs)) != len(devs):
+            return "tcp"
+        return "rccl"
+
     def _stage_cfg(self, epoch: int, st: int, k: int, cuts: List[str], recs: List[dict], rid: int) -> dict:
         rec = recs[st]
+        transport = self.epoch_transport(recs)
         nxt = None
         if st < k - 1:
             nxt = {"host": recs[st + 1]["host"], "port": int(recs[st + 1]["data_port"])}
         cfg = {"cmd": "configure", "epoch": epoch, "stage": st, "stages": k, "batch": self.batch,
                "next": nxt, "result_addr": [self._result_host(rec), self.result_port], "part_at": list(cuts),
-               "codec": self.codec, "graph": self.device_graph, "transport": self.transport, "replica": rid,
+               "codec": self.codec, "graph": self.device_graph, "transport": transport, "replica": rid,
                "precision": self.precision, "preprocess": self.preprocess}
-        if (nxt is not None and self.transport == "tcp" and self.links in ("auto", "dev", "shm")
+        if (nxt is not None and transport == "tcp" and self.links in ("auto", "dev", "shm")
                 and rec.get("shm_domain") and rec.get("shm_domain") == recs[st + 1].get("shm_domain")):
             # same host: device link when both stages are GPU workers (IPC, device to device), else host slots
             both_gpu = all(str(r.get("device", "")).startswith("cuda") for r in (rec, recs[st + 1]))
@@ -658,9 +727,9 @@ class DEFER:
                 peers = [r for r in self.workers.values()
                          if r.get("shm_domain") == rec.get("shm_domain") and r.get("device") == rec.get("device")]
             cfg["stage_streams"] = 1 if len(peers) > 1 else 2
-        if self.transport != "tcp":
+        if transport != "tcp":
             cfg["link_codec"] = self.link_codec
-            cfg["collective"] = {"backend": "nccl" if self.transport == "rccl" else "gloo",
+            cfg["collective"] = {"backend": "nccl" if transport == "rccl" else "gloo",
                                  "store_host": self._result_host(rec), "store_port": self._store_port,
                                  "timeout": 30}
         return cfg
@@ -684,7 +753,7 @@ class DEFER:
             try:
                 cfg = self._stage_cfg(epoch, st, k, cuts, recs, rid)
                 if st < k - 1:
-                    hops[st] = cfg.get("link", self.transport)
+                    hops[st] = cfg.get("link", cfg["transport"])
                 ok[st] = self._acquire_and_configure_worker(st + 1, members[st], cfg) is not None
             except BaseException as e:  # noqa: BLE001 - reported below
                 errs.append(e)
@@ -705,6 +774,7 @@ class DEFER:
             self._ensure_session(w)
         p = Pipeline(epoch, list(cuts), list(members), recs, s0, replica=rid)
         self._log(f"epoch {epoch}: replica {rid}, {k} stages on {members} cuts={cuts} "
+                  f"transport={self.epoch_transport(recs)} "
                   f"({(time.time() - t0) * 1e3:.0f} ms)" + (f" links={','.join(hops)}" if hops else ""))
         return p
 
@@ -1163,12 +1233,28 @@ class DEFER:
         return int(METRICS.counters.get("results_duplicate_dropped", 0))
 
     # ----------------------------------------------------- fault handling
+    def task_timeout_for(self, rid: int) -> float:
+        """The watchdog's age limit for requests of replica `rid` (see `task_timeout`)."""
+        if self.task_timeout is not None:
+            return float(self.task_timeout)
+        with self._rep_lock:
+            p = self.replicas.get(rid)
+        recs = p.records if p is not None else []
+        gpu = bool(recs) and all(str(r.get("device", "")).startswith("cuda") for r in recs)
+        base = 10.0 if gpu else 30.0
+        ent = self._rep_period.get(rid)
+        period = ent[1] if ent is not None and p is not None and ent[0] == p.epoch else 0.0
+        return max(base, 4.0 * self.max_inflight * period)
+
     def _task_watchdog(self) -> None:
         while not self._shutdown_event.wait(0.02):
             now = time.time()
             with self.inflight_lock:
+                tasks = [t for t in self.inflight_tasks.values() if t["replica"] is not None]
+            limits = {rid: self.task_timeout_for(rid) for rid in {t["replica"] for t in tasks}}
+            with self.inflight_lock:
                 stale = {t["replica"] for t in self.inflight_tasks.values()
-                         if now - t["start_time"] > self.task_timeout and t["replica"] is not None}
+                         if t["replica"] is not None and now - t["start_time"] > limits.get(t["replica"], 10.0)}
                 unsent = any(t["epoch"] is None for t in self.inflight_tasks.values()
                              if now - t["start_time"] > 0.5)
             for rid in stale:

@@ -82,7 +82,7 @@ class Model:
 
     # ------------------------------------------------------------ compute
     def predict(self, x: np.ndarray, device: Optional[str] = None, batch: Optional[int] = None,
-                precision: str = "bf16") -> np.ndarray:
+                precision: str = "fp32") -> np.ndarray:
         """Single-device inference (`test/local_infer.py:22`): our HIP runtime on
         a GPU (precision "bf16" or "fp32", the reference's Keras float32), the
         fp32 oracle on CPU.  Inputs are NHWC float32 images."""

@@ -365,8 +365,8 @@ class StageRuntime:
                 except queue.Empty:
                     continue
                 self.node.state.state = StateEnum.BUSY
-                self.node.fault_point(self.stop)
-                t_c = time.perf_counter()
+                slept = self.node.fault_point(self.stop)
+                t_c = time.perf_counter() - slept     # an injected delay counts as compute
                 with self._busy:
                     if self.stop.is_set():
                         break
@@ -514,6 +514,7 @@ class Node:
         self._hb_handles: set = set()
         self._hb_lock = threading.Lock()
         self._hang = threading.Event()                   # fault injection: "hang"
+        self._delay_s = 0.0                              # fault injection: "delay:<s>"
         self._retired_pools: list = []                   # device link pools of the last torn-down epoch
 
     # ---------------------------------------------------------- lifecycle
@@ -601,17 +602,29 @@ class Node:
         """Fault injection (tests, tools/fault_bench.py): ``"hang"`` wedges this
         worker's compute loops at their next micro-batch while every other
         thread (heartbeat, sessions, config server) keeps running - the
-        failure a heartbeat alone cannot see; ``"clear"`` releases them."""
+        failure a heartbeat alone cannot see; ``"delay:<s>"`` makes every
+        micro-batch take <s> seconds longer (a slow but healthy stage: its
+        progress counter and reported stage time include the delay);
+        ``"clear"`` releases both."""
         if kind == "hang":
             self._hang.set()
+        elif kind.startswith("delay:"):
+            self._delay_s = max(0.0, float(kind.split(":", 1)[1]))
         elif kind == "clear":
             self._hang.clear()
+            self._delay_s = 0.0
         else:
             raise ValueError(f"unknown fault {kind!r}")
 
-    def fault_point(self, stop: threading.Event) -> None:
+    def fault_point(self, stop: threading.Event) -> float:
+        """Called by the compute loops before each micro-batch; returns the
+        injected delay it slept (the caller counts it as compute time)."""
         while self._hang.is_set() and not stop.is_set() and not self._stop.is_set():
             time.sleep(0.005)
+        d = self._delay_s
+        if d > 0:
+            stop.wait(d)
+        return d
 
     def retire_link_pool(self, pool) -> None:
         """Keep a torn-down epoch's device link pool alive until the next one is
@@ -692,7 +705,7 @@ class Node:
         key = cfg.get("cache_key")
         if not key:
             return None
-        return (key, int(cfg["batch"]), cfg.get("precision", "bf16"), cfg.get("preprocess", "none")) + \
+        return (key, int(cfg["batch"]), cfg.get("precision", "fp32"), cfg.get("preprocess", "none")) + \
             self.compute_shape(cfg, self.device)
 
     def stage_compute(self, cfg: Dict, g, weights: Dict[str, np.ndarray], capture_mode: str = "global"):
@@ -714,7 +727,7 @@ class Node:
         try:
             c = StageCompute(g, weights, int(cfg["batch"]), self.device, graph_capture=graph, num_sets=num_sets,
                              host_ring=host_ring, capture_mode=capture_mode, streams=streams,
-                             precision=cfg.get("precision", "bf16"), preprocess=cfg.get("preprocess", "none"))
+                             precision=cfg.get("precision", "fp32"), preprocess=cfg.get("preprocess", "none"))
         finally:
             if key is not None:
                 with self._computes_lock:

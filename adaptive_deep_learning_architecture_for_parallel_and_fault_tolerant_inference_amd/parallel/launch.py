@@ -26,6 +26,11 @@ import time
 from typing import Dict, List, Optional, Sequence
 
 RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+# set by a torchrun agent for *its* job; a job started from inside one of its ranks
+# (bench.py's sub-runs) must not inherit them: with TORCHELASTIC_USE_AGENT_STORE
+# the new job's rank 0 would join the agent's store instead of hosting its own
+AGENT_ENV = ("GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE",
+             "LOCAL_WORLD_SIZE", "TORCH_NCCL_ASYNC_ERROR_HANDLING_DISABLED")
 
 
 def free_port(host: str = "127.0.0.1") -> int:
@@ -47,6 +52,9 @@ def rank_envs(nprocs: int, port: int, base: Optional[Dict[str, str]] = None,
     if nprocs < 1:
         raise ValueError(f"need at least one rank, got {nprocs}")
     base = dict(os.environ if base is None else base)
+    for k in list(base):
+        if k.startswith("TORCHELASTIC_") or k in AGENT_ENV:
+            del base[k]
     out = []
     for r in range(nprocs):
         e = dict(base)
@@ -59,19 +67,23 @@ def rank_envs(nprocs: int, port: int, base: Optional[Dict[str, str]] = None,
 
 
 def launch_local(argv: Sequence[str], nprocs: int, script: Optional[str] = None, timeout_s: Optional[float] = None,
-                 port: Optional[int] = None, poll_s: float = 0.05, module: Optional[str] = None) -> int:
+                 port: Optional[int] = None, poll_s: float = 0.05, module: Optional[str] = None,
+                 stdout=None) -> int:
     """Run `python <script> <argv>` (or `python -m <module> <argv>`) as `nprocs`
-    ranks; returns the job's exit code.
+    ranks; returns the job's exit code (124 on timeout).
 
-    Ranks inherit stdout/stderr (rank 0 prints the bench line).  When any rank
-    exits non-zero, or `timeout_s` passes, the rest of the job is terminated."""
+    Ranks inherit stdout/stderr (rank 0 prints the bench line) unless `stdout`
+    redirects them (bench.py's sub-runs send theirs to stderr, so the only
+    JSON line on stdout is the record).  When any rank exits non-zero, or
+    `timeout_s` passes, the rest of the job is terminated."""
     target = ["-m", module] if module else [script or sys.argv[0]]
     port = port or free_port()
     envs = rank_envs(nprocs, port)
     procs: List[subprocess.Popen] = []
     for e in envs:
         # each rank leads its own process group so a kill reaches its helpers too
-        procs.append(subprocess.Popen([sys.executable, *target, *argv], env=e, start_new_session=True))
+        procs.append(subprocess.Popen([sys.executable, *target, *argv], env=e, start_new_session=True,
+                                      stdout=stdout))
     t0 = time.monotonic()
     rc = 0
     try:

@@ -197,13 +197,27 @@ class RcclComm:
         """ncclCommAbort (any thread); returns its latency in ms."""
         return self._c.abort()
 
-    def destroy(self) -> None:
-        """Tear down after the link stream has drained.  ncclCommAbort rather than
-        ncclCommFinalize + ncclCommDestroy: the caller synchronised, so nothing is
-        left to flush, and abort never waits on the peer (a finalize on RCCL 2.26
-        was seen to block for good after an earlier failed group in the process)."""
-        self.stream.synchronize()
+    def destroy(self, timeout_s: float = 10.0) -> bool:
+        """Tear down once the link stream has drained; returns whether it did.
+        The drain is polled, never a blocking stream sync: a peer that died with
+        a send or receive still pending on this stream would keep that sync from
+        returning, and the abort that releases it would never run.  So the wait
+        ends early when the communicator failed or was aborted, and at
+        `timeout_s` at the latest.  ncclCommAbort rather than ncclCommFinalize +
+        ncclCommDestroy: nothing is left to flush, and abort never waits on the
+        peer (a finalize on RCCL 2.26 was seen to block for good after an
+        earlier failed group in the process)."""
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        t0 = time.monotonic()
+        drained = True
+        while not ev.query():
+            if self.failed or self.aborted or time.monotonic() - t0 > timeout_s:
+                drained = False
+                break
+            time.sleep(1e-4)
         self._c.abort()
+        return drained
 
 
 def _check_dev(t: torch.Tensor, dev: torch.device) -> None:
@@ -228,18 +242,24 @@ class PairLinks:
         self.abort_flag = threading.Event()
         self.inp: Optional[RcclComm] = None
         self.out: Optional[RcclComm] = None
-        # the out-link first: this rank publishes that pair's unique id, so the
-        # next stage never waits on our own upstream rendezvous
-        if next is not None:
-            self.out = RcclComm(store, f"{prefix}/link{rank}-{next}", 2, 0, device, wait=False, timeout_s=timeout_s,
-                                watch_us=watch_us)
-        if prev is not None:
-            self.inp = RcclComm(store, f"{prefix}/link{prev}-{rank}", 2, 1, device, wait=False, timeout_s=timeout_s,
-                                watch_us=watch_us)
         t0 = time.perf_counter()
-        for c in (self.inp, self.out):
-            if c is not None:
-                c.wait_ready(timeout_s)
+        try:
+            # the out-link first: this rank publishes that pair's unique id, so the
+            # next stage never waits on our own upstream rendezvous
+            if next is not None:
+                self.out = RcclComm(store, f"{prefix}/link{rank}-{next}", 2, 0, device, wait=False,
+                                    timeout_s=timeout_s, watch_us=watch_us)
+            if prev is not None:
+                self.inp = RcclComm(store, f"{prefix}/link{prev}-{rank}", 2, 1, device, wait=False,
+                                    timeout_s=timeout_s, watch_us=watch_us)
+            for c in (self.inp, self.out):
+                if c is not None:
+                    c.wait_ready(timeout_s)
+        except BaseException:
+            # a half-built pair (e.g. the upstream peer never arrived) must not keep its
+            # communicator, watch thread and RCCL resources alive until garbage collection
+            self.abort()
+            raise
         self.init_ms = (time.perf_counter() - t0) * 1e3
 
     def comms(self) -> List[RcclComm]:
@@ -262,6 +282,10 @@ class PairLinks:
         for c in self.comms():
             c.abort()
 
-    def destroy(self) -> None:
+    def destroy(self, timeout_s: float = 10.0) -> bool:
+        """Bounded teardown of both links (see `RcclComm.destroy`); False when a
+        link had to be aborted with work still pending."""
+        ok = True
         for c in self.comms():
-            c.destroy()
+            ok = c.destroy(timeout_s) and ok
+        return ok

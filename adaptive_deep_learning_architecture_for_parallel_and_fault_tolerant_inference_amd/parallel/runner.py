@@ -33,7 +33,7 @@ class DPJob:
     per-layer GEMMs of different micro-batches fill CUs the other leaves idle."""
 
     def __init__(self, g, weights, world: int, rank: int, device, batch: int, graph: bool = True, tune: bool = False,
-                 streams: int = 1, precision: str = "bf16"):
+                 streams: int = 1, precision: str = "fp32"):
         self.device = torch.device(device)
         self.exs = [SliceExecutor(g, weights, batch, device=device, tune=tune and i == 0, precision=precision)
                     for i in range(streams)]
@@ -84,7 +84,7 @@ class PipelineJob:
 
     def __init__(self, g, weights, world: int, rank: int, device, batch: int, stages: int,
                  part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False, nsets: int = 2,
-                 host_staged: bool = False, codec: str = "none", precision: str = "bf16"):
+                 host_staged: bool = False, codec: str = "none", precision: str = "fp32"):
         if world % stages:
             raise ValueError(f"world {world} not divisible by stages {stages}")
         self.stages = stages
@@ -154,17 +154,29 @@ class PipelineJob:
     def finish(self) -> None:
         self.link.drain()
 
-    def close(self) -> None:
-        """Orderly teardown of the RCCL links (every rank of the pipeline calls it)."""
+    def close(self, timeout_s: float = 10.0) -> bool:
+        """Teardown of the RCCL links (every rank of the pipeline calls it).  The
+        link streams are drained with a bounded poll, then the communicators
+        aborted; only then is the device synchronised, so a peer that died with
+        a transfer pending cannot block this rank for good.  Returns whether
+        the links drained cleanly."""
+        ok = True
         if self.links is not None:
-            torch.cuda.synchronize(self.ex.device)
-            self.links.destroy()
+            ok = self.links.destroy(timeout_s)
             self.links = None
+        torch.cuda.synchronize(self.ex.device)
+        return ok
+
+    def abort(self) -> None:
+        """Abort the RCCL links from any thread (failure isolation in bench.py):
+        RCCL kernels waiting on a peer return, pending host waits raise."""
+        if self.links is not None:
+            self.links.abort()
 
 
 def build_job(g, weights, mode: str, world: int, rank: int, device, batch: int = 32, stages: int = 0,
               part_at: Optional[List[str]] = None, graph: bool = True, tune: bool = False,
-              host_staged: bool = False, streams: int = 1, codec: str = "none", precision: str = "bf16"):
+              host_staged: bool = False, streams: int = 1, codec: str = "none", precision: str = "fp32"):
     if mode == "dp" or world == 1 and not part_at:
         return DPJob(g, weights, world, rank, device, batch, graph=graph, tune=tune, streams=streams,
                      precision=precision)

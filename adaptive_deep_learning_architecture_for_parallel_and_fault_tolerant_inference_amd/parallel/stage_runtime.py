@@ -325,8 +325,8 @@ class CollectiveStageRuntime:
                 for w in send_w[j] or []:
                     G.wait(w)
                 send_w[j] = None
-                self.node.fault_point(self.stop)
-                t_c = time.perf_counter()
+                slept = self.node.fault_point(self.stop)
+                t_c = time.perf_counter() - slept     # an injected delay counts as compute
                 self._compute(j)
                 if self.gpu:
                     ev = torch.cuda.Event()
@@ -443,8 +443,8 @@ class CollectiveStageRuntime:
                     raise Aborted("stopped")
             if self.gpu and self.enc is not None and self.enc[j]:
                 torch.cuda.current_stream(self.dev).wait_event(self.enc[j][-1].done)
-            self.node.fault_point(self.stop)
-            t_c = time.perf_counter()
+            slept = self.node.fault_point(self.stop)
+            t_c = time.perf_counter() - slept     # an injected delay counts as compute
             self._compute(j)
             if self.gpu:
                 ev = torch.cuda.Event()

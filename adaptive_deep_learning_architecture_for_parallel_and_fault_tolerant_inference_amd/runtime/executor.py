@@ -82,7 +82,7 @@ class SliceExecutor:
 
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device="cuda",
                  outputs: Optional[Sequence[str]] = None, tune: bool = False, num_sets: int = 1,
-                 precision: str = "bf16", private_sets: bool = False):
+                 precision: str = "fp32", private_sets: bool = False):
         """precision: "bf16" (bf16 activations / weights, fp32 accumulation: the
         fast path) or "fp32" (fp32 activations and weights on the fp32 matrix
         cores: the reference's Keras float32 numerics, csrc/kernels/conv_f32.hip).

@@ -72,7 +72,7 @@ def to_numpy(t: torch.Tensor) -> Tuple[np.ndarray, bool]:
 class StageCompute:
     def __init__(self, g: Graph, weights: Dict[str, np.ndarray], batch: int, device: str = "cpu",
                  outputs: Optional[Sequence[str]] = None, graph_capture: bool = True, num_sets: int = 1,
-                 host_ring: int = 8, capture_mode: str = "global", precision: str = "bf16",
+                 host_ring: int = 8, capture_mode: str = "global", precision: str = "fp32",
                  preprocess: str = "none", streams: int = 2):
         self.g = g
         self.preprocess = preprocess          # uint8 image inputs: Keras preprocess_input mode (ops/eltwise.py)

@@ -33,7 +33,7 @@ class AdaptConfig:
     elastic: bool = False                    # rebalance on worker join, not only on leave
     replicas: Union[int, str] = "auto"       # PP x DP: pipeline replicas ("auto" = live // stages)
     # data plane
-    transport: str = "tcp"                   # tcp | rccl | gloo
+    transport: str = "auto"                  # auto | tcp | rccl | gloo (auto: rccl between distinct local GPUs)
     codec: str = "none"                      # activations on TCP links: none|lz4|zvc|zfp+lz4 (host LZ4 of
                                              # activations: ratio ~1.02 at 0.2 GB/s, so off by default)
     weight_codec: str = "zfp+lz4"            # slice push (reference: zfp+lz4)
@@ -47,7 +47,7 @@ class AdaptConfig:
     lease_ttl: float = 1.0
     # flow control / fault handling
     max_inflight: int = 8
-    task_timeout: float = 10.0
+    task_timeout: Optional[float] = None       # None: per replica, 10 s GPU / 30 s CPU, scaled by the period
     worker_wait: float = 5.0
     ordered: bool = False
     # worker
@@ -112,8 +112,10 @@ def _coerce(s: str, like: Any):
     if isinstance(like, list):
         return [x for x in s.split(",") if x]
     if like is None:
-        try:
-            return int(s)
-        except ValueError:
-            return s
+        for conv in (int, float):
+            try:
+                return conv(s)
+            except ValueError:
+                pass
+        return s
     return s

@@ -23,11 +23,28 @@ A step = one bs=32 batch per pipeline replica slot: dp processes 32*N images
 per step, pp keeps N micro-batches in flight and completes N per step, so
 per-GPU work is fixed as N grows (weak scaling) in every mode.
 
-With N > 1 the same invocation then times the reference's own topology, an
-N-stage pipeline over the native RCCL p2p layer (`parallel/rccl.py`), checks
-the last stage's logits against an unsliced forward of the same input, and
-measures the stage-0 -> stage-1 p2p rate; that lands in the ``pp`` sub-object
-(and the rate in `tuning/gfx950_links.json` for the planner).
+Control traffic (barriers, the max over ranks, result agreement) always runs
+on a host (gloo) process group; activations move over the native RCCL p2p
+layer (`parallel/rccl.py`), so no eager ProcessGroupNCCL stream competes with
+the pipeline's compute and link streams for the 4 hardware queues.
+
+With N > 1 (dp mode) the same invocation then measures BASELINE.json's other
+configs as *sub-runs*: after the headline ranks are done, rank 0 starts each
+one as a fresh job of its own (`parallel/launch.py`, one process per GPU, a
+time limit each, stdout to stderr), so a failing or hanging sub-run is killed
+and recorded as ``{"ok": false, "error": ...}`` while the headline line is
+always printed:
+
+  pp       every N: the reference's layer-partitioned chain as an N-stage
+           pipeline over RCCL p2p, logits checked against the unsliced forward,
+           stage0 -> stage1 p2p rate; N == 2 uses config 2's
+           part_at=['conv3_block1_1_conv'] (a multi-tensor frontier), N == 8
+           config 3's lz4 activation compression on a side stream (wire_ratio)
+  pp_r152  N == 4: config 5, ResNet-152 as a 4-stage bf16 pipeline
+  fault    N >= 2: config 4, a DEFER serving run at its defaults (fp32,
+           transport auto = RCCL p2p with one stage per GPU, 0.25 s heartbeat)
+           whose middle stage is SIGKILLed: recovery_ms, detect_ms,
+           exactly_once (`parallel/fault_run.py`)
 """
 from __future__ import annotations
 
@@ -71,6 +88,14 @@ def parse(argv=None):
                     help="precision of the pipeline sub-benchmark (default: --dtype)")
     ap.add_argument("--codec", default="none", choices=["none", "lz4", "zvc"],
                     help="pp/ppdp: compress stage-boundary activations on a side stream (BASELINE config 3)")
+    ap.add_argument("--no-fault", action="store_true", help="N > 1: skip the kill/recovery sub-run (config 4)")
+    ap.add_argument("--no-subruns", action="store_true", help="N > 1: headline only")
+    ap.add_argument("--sub-budget", type=float, default=420.0,
+                    help="seconds all sub-runs together may take (each also has its own limit)")
+    ap.add_argument("--fault-duration", type=float, default=10.0)
+    # internal: this process is one rank of a sub-run job started by the headline's rank 0
+    ap.add_argument("--sub", default="", choices=["", "pp"], help=argparse.SUPPRESS)
+    ap.add_argument("--out", default="", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -84,7 +109,7 @@ PP_LOGIT_RTOL = {"bf16": 5e-2, "fp32": 1e-3}
 
 
 def make_record(args, world: int, n_gpus: int, backend: str, value: float, elapsed: float, image, job,
-                bf16: dict = None, pp: dict = None) -> dict:
+                bf16: dict = None, pp: dict = None, subs: dict = None) -> dict:
     """The one JSON line rank 0 prints (the driver's contract)."""
     rec = {
         "metric": f"images/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} bs={args.batch}",
@@ -102,7 +127,8 @@ def make_record(args, world: int, n_gpus: int, backend: str, value: float, elaps
         "config": {"model": args.model, "global_batch": job["global_batch"], "seq_len": None,
                    "image": list(image), "parallelism": job["parallelism"], "part_at": job["part_at"],
                    "micro_batch": args.batch, "hipgraph": not args.no_graph,
-                   "ranks": world, "backend": backend if world > 1 else None},
+                   "ranks": world, "backend": backend if world > 1 else None,
+                   "control": "gloo" if world > 1 else None},
     }
     if job.get("codec"):
         rec["config"]["codec"] = job["codec"]
@@ -112,6 +138,8 @@ def make_record(args, world: int, n_gpus: int, backend: str, value: float, elaps
         rec["ms_per_step_bf16"] = round(bf16["elapsed"] / args.steps * 1e3, 4)
     if pp is not None:
         rec["pp"] = pp
+    for k, v in (subs or {}).items():
+        rec[k] = v
     return rec
 
 
@@ -125,16 +153,16 @@ def make_pp_record(value: float, elapsed: float, steps: int, stages: int, part_a
             "backend": backend}
 
 
-def _max_over_ranks(x: float, world: int, dev, backend: str) -> float:
+def _max_over_ranks(x: float, world: int) -> float:
+    """MAX over ranks on the host (gloo) control group."""
     if world == 1:
         return x
     t = torch.tensor([x], dtype=torch.float64)
-    t = t.to(dev) if backend == "nccl" else t
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
 
 
-def timed(job, steps: int, warmup: int, dev, world: int, backend: str) -> float:
+def timed(job, steps: int, warmup: int, dev, world: int) -> float:
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize;
     returns the slowest rank's seconds."""
     if hasattr(job, "set_total_steps"):
@@ -155,7 +183,7 @@ def timed(job, steps: int, warmup: int, dev, world: int, backend: str) -> float:
     elapsed = time.perf_counter() - t0
     if hasattr(job, "finish"):
         job.finish()
-    return _max_over_ranks(elapsed, world, dev, backend)
+    return _max_over_ranks(elapsed, world)
 
 
 def _p2p_rate(job, dev, world: int, backend: str, mib: int = 64, reps: int = 10):
@@ -164,40 +192,42 @@ def _p2p_rate(job, dev, world: int, backend: str, mib: int = 64, reps: int = 10)
     buf = torch.empty(n, dtype=torch.uint8, device=dev)
     links = getattr(job, "links", None)
     role = job.stage if job.replica == 0 and job.stage < 2 else None
+    dt = 0.0
     for it in range(2):                                 # warm-up round, then the timed round
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
         if role is not None:
+            w = None
             for _ in range(reps):
                 if links is not None:
                     w = links.isend([buf]) if role == 0 else links.irecv([buf])
                 elif role == 0:
-                    dist.send(buf.cpu() if backend != "nccl" else buf, job.next)
+                    dist.send(buf.cpu(), job.next)
                 else:
-                    tmp = buf.cpu() if backend != "nccl" else buf
+                    tmp = buf.cpu()
                     dist.recv(tmp, job.prev)
-                    if tmp is not buf:
-                        buf.copy_(tmp)
-            if links is not None:
+                    buf.copy_(tmp)
+            if w is not None:
                 w.wait_host(timeout_s=60)
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0 if role is not None else 0.0
-    dt = _max_over_ranks(dt, world, dev, backend)
+    dt = _max_over_ranks(dt, world)
     return n * reps / dt if dt > 0 else None
 
 
-def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, resnet, runner, executor):
+def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, executor, part_at) -> dict:
     """The reference's layer-partitioned chain over RCCL, verified against an unsliced forward."""
     dtype = args.pp_dtype or args.dtype
-    part_at = [s for s in args.part_at.split(",") if s] if args.mode == "pp" else []
+    t_build = time.perf_counter()
     job = runner.build_job(g, weights, mode="pp", world=world, rank=rank, device=dev, batch=args.batch,
                            part_at=part_at, graph=not args.no_graph, host_staged=(backend != "nccl"),
                            codec=args.codec, precision=dtype)
+    build_s = time.perf_counter() - t_build
     image = tuple(g.layers[g.input].out_shape)
     x = torch.randn((args.batch,) + image, generator=torch.Generator().manual_seed(4321)).to(dev)
     job.set_synthetic_input(x)
-    elapsed = timed(job, args.steps, args.warmup, dev, world, backend)
+    elapsed = timed(job, args.steps, args.warmup, dev, world)
     value = job.images_per_step * args.steps / elapsed
     rate = _p2p_rate(job, dev, world, backend)
     ok, rel, top1 = 1, None, None
@@ -212,10 +242,8 @@ def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, resnet, r
         del full
     flag = torch.tensor([ok, rel if rel is not None else 0.0, top1 if top1 is not None else 1.0],
                         dtype=torch.float64)
-    flag = flag.to(dev) if backend == "nccl" else flag
-    # MIN over ok/top1 and MAX over rel: gather everything
     flags = [torch.zeros_like(flag) for _ in range(world)]
-    dist.all_gather(flags, flag)
+    dist.all_gather(flags, flag)                # host control group
     oks = [int(f[0].item()) for f in flags]
     last = flags[world - 1] if job.replicas == 1 else max(flags, key=lambda f: f[1].item())
     native = getattr(job, "links", None) is not None
@@ -230,13 +258,156 @@ def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, resnet, r
     rec = make_pp_record(value, elapsed, args.steps, job.stages, job.part_at, dtype, min(oks) == 1,
                          last[1].item(), last[2].item(), rate / 1e9 if rate else None,
                          world if native else 0, "rccl-native" if native else backend)
+    rec["model"] = args.model
+    rec["build_s"] = round(build_s, 2)
+    link = getattr(job, "link", None)
+    if args.codec != "none":
+        ratio = getattr(link, "ratio", None)
+        rec["codec"] = args.codec
+        rec["wire_ratio"] = round(ratio, 4) if ratio else None
     if hasattr(job, "close"):
-        job.close()
+        rec["links_drained"] = bool(job.close())
     return rec
+
+
+# ---------------------------------------------------------------- sub-runs
+SUB_LIMIT_S = {"pp": 180.0, "pp_r152": 200.0, "fault": 240.0}
+
+
+def plan_subruns(args, world: int, backend: str) -> list:
+    """(name, kind, argv, nprocs, limit_s, label) of the BASELINE.json configs a
+    `--gpus N` dp run measures after its headline."""
+    if args.no_subruns or args.mode != "dp" or world < 2:
+        return []
+    common = ["--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch),
+              "--backend", backend, "--seed", str(args.seed)] + (["--no-graph"] if args.no_graph else [])
+    subs = []
+    if not args.no_pp:
+        pp = ["--sub", "pp", "--model", args.model, "--pp-dtype", args.pp_dtype or args.dtype] + common
+        label = f"{world}-stage pipeline, planner cuts"
+        if args.part_at:
+            pp += ["--part-at", args.part_at]
+            label = f"{world}-stage pipeline, part_at={args.part_at}"
+        elif world == 2 and args.model == "resnet50":
+            pp += ["--part-at", "conv3_block1_1_conv"]
+            label = "BASELINE config 2: 2-stage, part_at=['conv3_block1_1_conv'] (multi-tensor frontier)"
+        if args.codec != "none":
+            pp += ["--codec", args.codec]
+        elif world == 8:
+            pp += ["--codec", "lz4"]
+            label = "BASELINE config 3: 8-stage pipeline, lz4 activation compression on a side stream"
+        subs.append(("pp", "bench", pp, world, SUB_LIMIT_S["pp"], label))
+        if world == 4:
+            r152 = ["--sub", "pp", "--model", "resnet152", "--pp-dtype", "bf16"] + common
+            subs.append(("pp_r152", "bench", r152, 4, SUB_LIMIT_S["pp_r152"],
+                         "BASELINE config 5: ResNet-152 4-stage bf16"))
+    if not args.no_fault:
+        image = "224"
+        fault = ["--workers", str(world), "--devices", "each", "--model", args.model, "--image", image,
+                 "--batch", str(args.batch), "--duration", str(args.fault_duration),
+                 "--kill-at", str(max(2.0, 0.4 * args.fault_duration))]
+        subs.append(("fault", "fault", fault, 1, SUB_LIMIT_S["fault"],
+                     f"BASELINE config 4: {world}-stage DEFER, middle worker SIGKILLed, DEFER defaults"))
+    return subs
+
+
+def run_subrun(name: str, kind: str, argv: list, nprocs: int, limit_s: float, label: str, launch) -> dict:
+    """One sub-run as a fresh job (a process per rank, its own time limit);
+    returns its record, or {"ok": false, "error": ...}.  Never raises."""
+    import glob
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"bench_{name}_{os.getpid()}_{int(time.time() * 1e3)}.json")
+    t0 = time.monotonic()
+    print(f"bench: sub-run {name} ({label}): {nprocs} process(es), limit {limit_s:.0f} s", file=sys.stderr,
+          flush=True)
+    try:
+        if kind == "bench":
+            rc = launch.launch_local(argv + ["--out", out], nprocs, script=os.path.abspath(__file__),
+                                     timeout_s=limit_s, stdout=sys.stderr)
+        else:
+            rc = launch.launch_local(argv + ["--json", out], 1, module=f"{PKG}.parallel.fault_run",
+                                     timeout_s=limit_s, stdout=sys.stderr)
+    except Exception as e:  # noqa: BLE001 - a sub-run never takes the headline down
+        rc = -1
+        err = f"{type(e).__name__}: {e}"
+    else:
+        err = None
+    wall = time.monotonic() - t0
+    rec = None
+    try:
+        with open(out) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        pass
+    errs = []
+    for p in sorted(glob.glob(out + ".rank*.err")):
+        try:
+            with open(p) as f:
+                errs.append(f.read().strip()[-600:])
+        except OSError:
+            pass
+        os.unlink(p)
+    if os.path.exists(out):
+        os.unlink(out)
+    if rec is None or rc != 0:
+        why = err or (errs[0] if errs else ("time limit reached" if rc == 124 else f"exit code {rc}"))
+        rec = dict(rec or {}, ok=False, error=why, rc=rc)
+    rec.setdefault("ok", True)
+    rec["label"] = label
+    rec["wall_s"] = round(wall, 1)
+    print(f"bench: sub-run {name} done in {wall:.1f} s, ok={rec['ok']}", file=sys.stderr, flush=True)
+    return rec
+
+
+def sub_main(args) -> int:
+    """One rank of a `--sub pp` job: a pipeline over RCCL p2p (or the gloo
+    rehearsal), result to ``--out`` (rank 0), errors to ``--out.rank<r>.err``."""
+    from importlib import import_module
+    import datetime
+    import traceback
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    try:
+        ndev = torch.cuda.device_count()
+        dev_idx = local % max(1, ndev)
+        torch.cuda.set_device(dev_idx)
+        dev = torch.device("cuda", dev_idx)
+        backend = "gloo" if (args.backend == "nccl" and world > ndev) else args.backend
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=150))
+        zoo = import_module(f"{PKG}.models.zoo")
+        resnet = import_module(f"{PKG}.models.resnet")
+        runner = import_module(f"{PKG}.parallel.runner")
+        executor = import_module(f"{PKG}.runtime.executor")
+        g = zoo.build_model(args.model)
+        weights = resnet.init_weights(g, seed=args.seed)
+        part_at = [c for c in args.part_at.split(",") if c]
+        rec = run_pp(args, g, weights, world, rank, dev, backend, runner, executor, part_at)
+        if rank == 0 and args.out:
+            with open(args.out + ".tmp", "w") as f:
+                json.dump(rec, f)
+            os.replace(args.out + ".tmp", args.out)
+        dist.barrier()
+        dist.destroy_process_group()
+        return 0
+    except BaseException as e:  # noqa: BLE001 - reported to the parent, which records ok: false
+        if args.out:
+            try:
+                with open(f"{args.out}.rank{rank}.err", "w") as f:
+                    f.write(f"rank {rank}: {type(e).__name__}: {e}\n" + traceback.format_exc()[-400:])
+            except OSError:
+                pass
+        traceback.print_exc()
+        return 3             # the launcher then ends the other ranks (blocked on this one's links)
 
 
 def main(argv=None):
     args = parse(argv)
+    if args.sub:
+        sys.stdout.flush()
+        rc = sub_main(args)
+        sys.stderr.flush()
+        os._exit(rc)          # RCCL / gloo threads of an aborted job must not block interpreter exit
     from importlib import import_module
     launch = import_module(f"{PKG}.parallel.launch")
     if args.gpus > 1 and not launch.launched_by_torchrun():
@@ -259,15 +430,13 @@ def main(argv=None):
                   f"(host-staged rehearsal)", file=sys.stderr)
         backend = "gloo"
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        # host control group only: the data plane is the native RCCL layer
+        import datetime
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
 
     resnet = import_module(f"{PKG}.models.resnet")
     zoo = import_module(f"{PKG}.models.zoo")
     runner = import_module(f"{PKG}.parallel.runner")
-    executor = import_module(f"{PKG}.runtime.executor")
 
     g = zoo.build_model(args.model)
     weights = resnet.init_weights(g, seed=args.seed)
@@ -282,7 +451,7 @@ def main(argv=None):
         # synthetic input, resident on device (data="synthetic")
         gen = torch.Generator(device=dev).manual_seed(1234 + rank)
         job.set_synthetic_input(torch.randn((args.batch,) + image, generator=gen, device=dev))
-        elapsed = timed(job, args.steps, args.warmup, dev, world, backend)
+        elapsed = timed(job, args.steps, args.warmup, dev, world)
         info = {"global_batch": job.global_batch, "parallelism": job.parallelism, "part_at": job.part_at}
         link = getattr(job, "link", None)
         if args.codec != "none" and link is not None:
@@ -300,9 +469,6 @@ def main(argv=None):
     if args.dtype == "fp32" and not args.no_bf16:
         v16, e16, _ = headline("bf16")
         bf16 = {"value": v16, "elapsed": e16}
-    pp = None
-    if world > 1 and not args.no_pp and args.mode == "dp":
-        pp = run_pp(args, g, weights, world, rank, dev, backend, resnet, runner, executor)
 
     n_gpus = 1
     if world > 1:
@@ -310,12 +476,24 @@ def main(argv=None):
         devs = [None] * world
         dist.all_gather_object(devs, (socket.gethostname(), dev_idx))
         n_gpus = launch.distinct_devices(devs)
-    if rank == 0:
-        print(json.dumps(make_record(args, world, n_gpus, backend, value, elapsed, image, info, bf16, pp)),
-              flush=True)
-    if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rank != 0:
+        return
+    # BASELINE configs 2-5: fresh jobs, one at a time, each with a time limit; rank 0 does
+    # not touch its GPU meanwhile (its executors are freed) and the other ranks have exited
+    del weights
+    torch.cuda.empty_cache()
+    subs = {}
+    budget_end = time.monotonic() + args.sub_budget
+    for name, kind, sargv, nprocs, limit, label in plan_subruns(args, world, backend):
+        left = budget_end - time.monotonic()
+        if left < 30:
+            subs[name] = {"ok": False, "error": f"sub-run budget ({args.sub_budget:.0f} s) spent", "label": label}
+            continue
+        subs[name] = run_subrun(name, kind, sargv, nprocs, min(limit, left), label, launch)
+    print(json.dumps(make_record(args, world, n_gpus, backend, value, elapsed, image, info, bf16, subs=subs)),
+          flush=True)
 
 
 if __name__ == "__main__":

@@ -116,6 +116,9 @@ PYBIND11_MODULE(_C, m) {
                               OH, OW, pad_t, pad_l, pool, PH, PW, pool_pad, S(s)),
           "stem_forward");
   });
+  m.def("spin_flag", [](u64 flag, u64 out, double timeout_ms, u64 s) {
+    check(adapt::spin_flag(P<const int>(flag), P<int>(out), timeout_ms, S(s)), "spin_flag");
+  });
   m.def("input_pack", [](u64 x, u64 y, size_t pixels, int C, int Cp, u64 s) {
     check(adapt::input_pack(P<const float>(x), P<bf16>(y), pixels, C, Cp, S(s)), "input_pack");
   });

@@ -63,6 +63,8 @@ hipError_t conv_glds_launch(const ConvParams& p, int cfg, hipStream_t s, bool pu
 bool conv_glds_cfg_tile(int cfg, int* bm, int* bn);
 int conv_num_cfgs();
 void conv_cfg_tile(int cfg, int* bm, int* bn);
+// diagnostic: occupy stream `s` until *flag != 0 (host-written) or timeout_ms; *out = 1 (flag) / 2 (timeout)
+hipError_t spin_flag(const int* flag, int* out, double timeout_ms, hipStream_t s);
 hipError_t input_pack(const float* x, bf16* y, size_t pixels, int C, int Cp, hipStream_t s);
 hipError_t bn_act(const bf16* x, bf16* y, const float* scale, const float* shift, size_t elems, int C, int relu,
                   hipStream_t s);

@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--part-at", default="", help="comma-separated cut layers, or auto:K")
     ap.add_argument("--task-size", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="worker precision: fp32 = the reference's Keras float32 (`src/node.py:177`)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "tcp", "rccl", "gloo"],
+                    help="stage -> stage hops; auto = RCCL p2p when every stage has its own GPU")
     a = ap.parse_args()
     devices = [d for d in a.devices.split(",") if d]
     image = (32, 32, 3) if a.model == "resnet_tiny" else (224, 224, 3)
@@ -42,7 +46,7 @@ def main():
     model = resnet(a.model, seed=0, **kw)
     part_at = [c for c in a.part_at.split(",") if c]
     defer = DEFER(membership_port=0, result_port=0, batch=a.batch, min_workers=len(devices), worker_wait=60,
-                  ordered=True)
+                  ordered=True, precision=a.dtype, transport=a.transport)
     defer.membership_server.start()
     nodes = [Node(membership_port=defer.membership_port, data_port=0, config_port=0, device=d, node_id=f"w{i}")
              for i, d in enumerate(devices)]

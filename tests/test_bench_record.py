@@ -54,3 +54,108 @@ def test_record_single_gpu_has_no_pp():
 def test_pp_tolerances():
     b = _bench()
     assert b.PP_LOGIT_RTOL["bf16"] == 5e-2 and b.PP_LOGIT_RTOL["fp32"] <= 1e-3
+
+
+def _names(subs):
+    return {s[0]: s for s in subs}
+
+
+def test_subrun_plan_covers_every_baseline_config():
+    """N=2: config 2's multi-tensor cut; N=4: config 5 (R152 4-stage bf16);
+    N=8: config 3 (lz4 on the links); N>=2: config 4 (kill + recovery)."""
+    b = _bench()
+    a = b.parse(["--steps", "20", "--warmup", "5"])
+    assert b.plan_subruns(a, 1, "nccl") == []
+    s2 = _names(b.plan_subruns(a, 2, "nccl"))
+    assert set(s2) == {"pp", "fault"}
+    pp = s2["pp"][2]
+    assert pp[pp.index("--part-at") + 1] == "conv3_block1_1_conv" and "--codec" not in pp
+    assert s2["pp"][3] == 2 and "config 2" in s2["pp"][5]
+    s4 = _names(b.plan_subruns(a, 4, "nccl"))
+    assert set(s4) == {"pp", "pp_r152", "fault"}
+    r152 = s4["pp_r152"][2]
+    assert r152[r152.index("--model") + 1] == "resnet152" and r152[r152.index("--pp-dtype") + 1] == "bf16"
+    assert s4["pp_r152"][3] == 4
+    s8 = _names(b.plan_subruns(a, 8, "nccl"))
+    pp8 = s8["pp"][2]
+    assert pp8[pp8.index("--codec") + 1] == "lz4" and "--part-at" not in pp8 and s8["pp"][3] == 8
+    f = s8["fault"][2]
+    assert f[f.index("--workers") + 1] == "8" and f[f.index("--devices") + 1] == "each"
+    assert "--hb-timeout" not in f and "--precision" not in f and "--transport" not in f   # DEFER defaults
+    assert s8["fault"][1] == "fault" and s8["fault"][3] == 1
+    # the steps / warmup / backend of the headline reach the pipeline sub-runs
+    assert pp8[pp8.index("--steps") + 1] == "20" and pp8[pp8.index("--backend") + 1] == "nccl"
+    assert b.plan_subruns(b.parse(["--no-subruns"]), 8, "nccl") == []
+    assert set(_names(b.plan_subruns(b.parse(["--no-fault"]), 8, "nccl"))) == {"pp"}
+    assert b.plan_subruns(b.parse(["--mode", "pp"]), 8, "nccl") == []
+
+
+def test_subrun_time_limits_fit_the_driver():
+    """Worst case (every sub-run of N=4 hits its limit) stays under the budget."""
+    b = _bench()
+    a = b.parse([])
+    assert a.sub_budget <= 420
+    assert all(v <= a.sub_budget for v in b.SUB_LIMIT_S.values())
+
+
+class _FakeLaunch:
+    def __init__(self, rc, write=None, sleep=0.0):
+        self.rc, self.write, self.sleep = rc, write, sleep
+        self.calls = []
+
+    def launch_local(self, argv, nprocs, script=None, timeout_s=None, stdout=None, module=None):
+        import time
+        self.calls.append((list(argv), nprocs, script, module, timeout_s))
+        out = argv[argv.index("--out" if "--out" in argv else "--json") + 1]
+        if self.write is not None:
+            with open(out, "w") as f:
+                json.dump(self.write, f)
+        if self.rc not in (0, 124):
+            with open(out + ".rank1.err", "w") as f:
+                f.write("rank 1: LinkError: pp8/job1/link1-2: communicator aborted")
+        time.sleep(self.sleep)
+        return self.rc
+
+
+def test_subrun_failure_is_recorded_not_raised():
+    b = _bench()
+    ok = b.run_subrun("pp", "bench", ["--sub", "pp"], 2, 60, "x", _FakeLaunch(0, write={"value": 5.0, "ok": True}))
+    assert ok["ok"] is True and ok["value"] == 5.0 and ok["label"] == "x" and "wall_s" in ok
+    bad = b.run_subrun("pp", "bench", ["--sub", "pp"], 8, 60, "x", _FakeLaunch(3))
+    assert bad["ok"] is False and "LinkError" in bad["error"] and bad["rc"] == 3
+    hung = b.run_subrun("fault", "fault", ["--workers", "8"], 1, 60, "y", _FakeLaunch(124))
+    assert hung["ok"] is False and hung["error"] == "time limit reached"
+    # a record written before the job failed keeps its fields but is marked failed
+    part = b.run_subrun("pp", "bench", [], 2, 60, "z", _FakeLaunch(3, write={"value": 1.0}))
+    assert part["ok"] is False and part["value"] == 1.0
+
+    class Boom:
+        def launch_local(self, *a, **k):
+            raise OSError("fork failed")
+    boom = b.run_subrun("pp", "bench", [], 2, 60, "w", Boom())
+    assert boom["ok"] is False and "fork failed" in boom["error"]
+
+
+def test_headline_record_carries_failed_subruns():
+    b = _bench()
+    a = b.parse(["--steps", "20", "--warmup", "5"])
+    subs = {"pp": {"ok": False, "error": "time limit reached"}, "fault": {"ok": True, "value": 150.0}}
+    rec = b.make_record(a, world=8, n_gpus=8, backend="nccl", value=100000.0, elapsed=0.6, image=(224, 224, 3),
+                        job={"global_batch": 256, "parallelism": "dp8", "part_at": []}, subs=subs)
+    line = json.loads(json.dumps(rec))
+    assert line["value"] == 100000.0 and line["pp"]["ok"] is False and line["fault"]["value"] == 150.0
+    assert line["config"]["control"] == "gloo"
+
+
+def test_subrun_of_a_real_job_fails_cleanly_without_gpu(tmp_path):
+    """The real launcher + `bench.py --sub pp` on a machine without a GPU: every
+    rank fails at device selection, and the parent records ok: false with the
+    rank's error instead of raising."""
+    import torch
+    if torch.cuda.is_available():
+        import pytest
+        pytest.skip("needs a GPU-less host")
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel import launch
+    b = _bench()
+    rec = b.run_subrun("pp", "bench", ["--sub", "pp", "--steps", "1", "--warmup", "0"], 2, 120, "cpu", launch)
+    assert rec["ok"] is False and rec["rc"] != 0 and "rank" in rec["error"]

@@ -52,13 +52,13 @@ def test_resnet50_fused_vs_unfused():
     g = R.build_resnet("resnet50")
     w = R.init_weights(g, seed=0)
     x = torch.randn(8, 224, 224, 3, device="cuda")
-    fused = SliceExecutor(g, w, batch=8, device="cuda")
+    fused = SliceExecutor(g, w, batch=8, device="cuda", precision="bf16")
     assert sum(st.kind == "bottleneck" for st in fused.steps) == 3
     fused(x)
     lf = fused.logits().clone()
     os.environ["ADAPT_FUSED_BOTTLENECK"] = "0"
     try:
-        plain = SliceExecutor(g, w, batch=8, device="cuda")
+        plain = SliceExecutor(g, w, batch=8, device="cuda", precision="bf16")
     finally:
         os.environ.pop("ADAPT_FUSED_BOTTLENECK")
     assert not any(st.kind == "bottleneck" for st in plain.steps)

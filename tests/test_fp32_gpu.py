@@ -217,7 +217,7 @@ def test_resnet50_bf16_logits_and_top1():
     g = R.build_resnet("resnet50")
     w = R.init_weights(g, seed=0)
     x = np.random.default_rng(3).standard_normal((8, 224, 224, 3)).astype(np.float32)
-    ex = SliceExecutor(g, w, batch=8, device="cuda:0")
+    ex = SliceExecutor(g, w, batch=8, device="cuda:0", precision="bf16")
     ex(torch.from_numpy(x).cuda())
     logits = ex.logits().double().cpu().numpy()
     want = _oracle_logits(g, w, x)

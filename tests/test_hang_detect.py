@@ -132,3 +132,47 @@ def test_hung_stage_detected_and_replayed_exactly_once(tiny, transport):
             except ProcessLookupError:
                 pass
             p.wait(timeout=10)
+
+
+def test_slow_upstream_after_idle_is_not_a_hang(tiny):
+    """An unbalanced 3-stage cut under low-rate traffic: stage 0 takes 0.3 s per
+    micro-batch, stages 1 and 2 a few ms (their hang threshold is the 0.2 s
+    floor).  After an idle gap each request spends 0.3 s in stage 0 while the
+    downstream stages sit idle; their stall clock must start when the request
+    can reach them, not at their own last progress, so no stage is called hung
+    (a fast downstream stage was quarantined the moment a request
+    that waited longer than its threshold upstream arrived)."""
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=1, max_inflight=4, weight_codec="lz4",
+              min_workers=3, replicas=1, task_timeout=30, transport="tcp", hang_min_s=0.2, hang_factor=10)
+    d.membership_server.start()
+    procs = [_spawn_worker(d.membership_port, f"s{i}") for i in range(3)]
+    try:
+        inq, outq = queue.Queue(8), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, ["conv3_block1_out", "conv4_block1_out"], inq, outq),
+                         daemon=True).start()
+        x = np.random.default_rng(4).standard_normal((1, 32, 32, 3)).astype(np.float32)
+        t_end = time.time() + 120
+        while d.pipeline is None and time.time() < t_end:
+            time.sleep(0.05)
+        assert d.pipeline is not None and len(d.pipeline.workers) == 3
+        d.inject_fault(d.pipeline.workers[0], "delay:0.3")
+        for _ in range(6):                               # overlapping requests: the replica period is measured
+            inq.put(x)
+        for _ in range(6):
+            outq.get(timeout=120)
+        assert d.hang_threshold(d.pipeline.replica, d.pipeline.epoch) is not None
+        time.sleep(1.0)                                  # idle gap
+        for _ in range(5):                               # low-rate traffic: one request at a time
+            inq.put(x)
+            outq.get(timeout=120)
+            time.sleep(0.3)
+        assert not d.hangs, d.hangs
+        assert not d.recoveries and len(d.pipeline.workers) == 3, d.events[-5:]
+    finally:
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait(timeout=10)

@@ -100,3 +100,15 @@ def test_bench_self_launches_without_torchrun(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     for k in range(2):
         assert (tmp_path / f"rank{k}").read_text() == "2 --gpus 2 --steps 1"
+
+
+def test_rank_envs_drop_torchrun_agent_vars():
+    """A job started from inside a torchrun rank (bench.py's sub-runs) must host
+    its own store, not join the agent's."""
+    base = {"TORCHELASTIC_USE_AGENT_STORE": "True", "TORCHELASTIC_RUN_ID": "x", "GROUP_WORLD_SIZE": "1",
+            "ROLE_WORLD_SIZE": "8", "RANK": "5", "WORLD_SIZE": "8", "KEEP": "1"}
+    envs = launch.rank_envs(2, 29600, base=base)
+    for e in envs:
+        assert not any(k.startswith("TORCHELASTIC_") for k in e)
+        assert "GROUP_WORLD_SIZE" not in e and "ROLE_WORLD_SIZE" not in e and e["KEEP"] == "1"
+        assert e["WORLD_SIZE"] == "2"

@@ -29,7 +29,7 @@ def test_resnet50_full_vs_oracle(r50):
     x = _img(4)
     ref = ReferenceExecutor(g, w, device="cuda")
     want = ref(x.cuda())
-    ex = SliceExecutor(g, w, batch=4)
+    ex = SliceExecutor(g, w, batch=4, precision="bf16")
     got = ex(x.cuda()).float()
     torch.cuda.synchronize()
     # probabilities: compare top-1 and L1 distance of the distributions
@@ -39,7 +39,7 @@ def test_resnet50_full_vs_oracle(r50):
     assert l1 < 0.1, f"softmax L1 distance {l1}"
     # pre-softmax features: compare the GAP vector (bf16 path vs fp32)
     feats_ref = ref.run({g.input: x.cuda()}, outputs=["avg_pool"])["avg_pool"]
-    ex2 = SliceExecutor(g, w, batch=4, outputs=["avg_pool"])
+    ex2 = SliceExecutor(g, w, batch=4, outputs=["avg_pool"], precision="bf16")
     feats = ex2(x.cuda()).float()
     rel = ((feats - feats_ref).norm() / feats_ref.norm()).item()
     assert rel < 3e-2, f"relative feature error {rel}"
@@ -51,13 +51,13 @@ def test_resnet50_full_vs_oracle(r50):
 def test_sliced_equals_unsliced(r50, cuts):
     g, w = r50
     x = _img(2, seed=3).cuda()
-    full = SliceExecutor(g, w, batch=2)
+    full = SliceExecutor(g, w, batch=2, precision="bf16")
     want = full(x).float().clone()
     slices = partition(g, cuts)
     vals = {g.input: x}
     for s in slices:
         sg = subgraph(g, s)
-        ex = SliceExecutor(sg, w, batch=2)
+        ex = SliceExecutor(sg, w, batch=2, precision="bf16")
         outs = ex.run({n: vals[n] for n in s.inputs})
         vals = {k: v.clone() for k, v in outs.items()}
     got = vals[g.output].float()
@@ -67,7 +67,7 @@ def test_sliced_equals_unsliced(r50, cuts):
 
 def test_graph_capture_replay(r50):
     g, w = r50
-    ex = SliceExecutor(g, w, batch=8)
+    ex = SliceExecutor(g, w, batch=8, precision="bf16")
     x = _img(8, seed=5).cuda()
     eager = ex(x).clone()
     ex.capture()
@@ -86,7 +86,7 @@ def test_resnet152_bf16_logits_vs_fp32_oracle(batch):
     g = build_resnet("resnet152")
     w = init_weights(g, seed=1)
     x = _img(batch, seed=11).cuda()
-    ex = SliceExecutor(g, w, batch=batch)
+    ex = SliceExecutor(g, w, batch=batch, precision="bf16")
     ex(x)
     got = ex.logits().double()
     ref = ReferenceExecutor(g, w, device="cuda")

@@ -115,7 +115,7 @@ def test_resnet152_bf16_four_stage_defer_matches_unsliced(kind):
         for x in xs:
             inq.put(x)
         got = np.concatenate([outq.get(timeout=300) for _ in xs])
-        full = SliceExecutor(m.graph, m.weights, batch=8, device="cuda:0")
+        full = SliceExecutor(m.graph, m.weights, batch=8, device="cuda:0", precision="bf16")
         want = np.concatenate([full(torch.from_numpy(x).cuda()).float().cpu().numpy() for x in xs])
         l1 = np.abs(got - want).sum(-1).max()
         top1 = (got.argmax(-1) == want.argmax(-1)).mean()

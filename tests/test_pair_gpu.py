@@ -73,7 +73,7 @@ def test_resnet50_with_pairs_matches_unfused(monkeypatch):
     outs = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("ADAPT_FUSED_PAIR", flag)
-        ex = exe.SliceExecutor(g, w, batch=4, device="cuda:0")
+        ex = exe.SliceExecutor(g, w, batch=4, device="cuda:0", precision="bf16")
         assert sum(s.kind == "pair" for s in ex.steps) == (3 if flag == "1" else 0)
         ex(x)
         outs[flag] = ex.logits().double().clone()

@@ -50,7 +50,7 @@ def _worker(rank, world, codec, port, outdir):
             np.save(os.path.join(outdir, "ratio.npy"), np.array([job.link.ratio]))
         if rank == world - 1:
             got = job.ex.output_buf(job.slice.outputs[0], 0).float().cpu().numpy()
-            ex = importlib.import_module(f"{PKG}.runtime.executor").SliceExecutor(g, w, B, device=dev)
+            ex = importlib.import_module(f"{PKG}.runtime.executor").SliceExecutor(g, w, B, device=dev, precision="bf16")
             want = ex(x).float().cpu().numpy()
             np.save(os.path.join(outdir, "got.npy"), got)
             np.save(os.path.join(outdir, "want.npy"), want)

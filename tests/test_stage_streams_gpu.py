@@ -24,7 +24,7 @@ def r50():
 
 def test_private_sets_replay_concurrently(r50):
     g, w = r50
-    ex = SliceExecutor(g, w, batch=8, device="cuda:0", num_sets=2, private_sets=True)
+    ex = SliceExecutor(g, w, batch=8, device="cuda:0", num_sets=2, private_sets=True, precision="bf16")
     ex.capture()
     rng = np.random.default_rng(0)
     xs = [torch.from_numpy(rng.standard_normal((8, 224, 224, 3)).astype(np.float32)).cuda() for _ in range(2)]

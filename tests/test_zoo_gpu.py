@@ -97,7 +97,7 @@ def _model_check(g, w, batch, feat, size, rel_tol=3e-2):
     gen = torch.Generator().manual_seed(0)
     x = torch.randn(batch, *size, generator=gen).cuda()
     ref = ref_mod.ReferenceExecutor(g, w, device="cuda").run({g.input: x}, outputs=[feat, g.output])
-    ex = ex_mod.SliceExecutor(g, w, batch=batch, outputs=[feat, g.output])
+    ex = ex_mod.SliceExecutor(g, w, batch=batch, outputs=[feat, g.output], precision="bf16")
     ex.capture()
     got = ex.run({g.input: x})
     torch.cuda.synchronize()

@@ -48,7 +48,7 @@ def main():
         env = dict(kv.split("=", 1) for kv in (a.env_a if variant == "tuned" else a.env_b).split(";") if kv)
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        ex = SliceExecutor(g, w, a.batch)
+        ex = SliceExecutor(g, w, a.batch, precision="bf16")
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)

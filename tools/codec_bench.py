@@ -44,13 +44,13 @@ def main():
     a = ap.parse_args()
     g = build_resnet("resnet50")
     w = init_weights(g, 0)
-    ex = SliceExecutor(g, w, a.batch, outputs=CUTS + [g.output])
+    ex = SliceExecutor(g, w, a.batch, outputs=CUTS + [g.output], precision="bf16")
     x = torch.randn(a.batch, 224, 224, 3, device="cuda")
     outs = ex.run({g.input: x})
     torch.cuda.synchronize()
     rt = runtime()
     rows = []
-    full = SliceExecutor(g, w, a.batch)
+    full = SliceExecutor(g, w, a.batch, precision="bf16")
     full.capture()
     t_fwd = gpu_time(lambda: full.forward(0), reps=20)
     for name in CUTS:

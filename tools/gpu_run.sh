@@ -8,7 +8,9 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     default bench.py (fp32 headline + bf16 companion), then a longer run
 #   bench152  ResNet-152 (bf16 and fp32)
-#   rehearse  bench.py --gpus 2 --backend gloo (the multi-GPU record, ranks sharing one GPU)
+#   rehearse  bench.py --gpus 2 --backend gloo (the multi-GPU record, ranks sharing one GPU, with its
+#             pp / fault sub-runs); rehearse4 the same at --gpus 4 (adds the ResNet-152 4-stage sub-run)
+#   queues    compute stream vs spinning link / side streams (tests/test_stream_queues_gpu.py)
 #   prof      rocprofv3 kernel trace + stats of the fp32 and bf16 benches
 #   fp32t     the fp32 kernel / model tests only
 #   models    model numerics + multi-GPU link twins + DEFER GPU tests
@@ -39,7 +41,9 @@ for p in "${P[@]}"; do
     bench)    steps+=("240|$out/bench_default|python -u bench.py")
               steps+=("240|$out/bench_long|python -u bench.py --steps 200 --warmup 20") ;;
     bench152) steps+=("240|$out/bench_r152|python -u bench.py --model resnet152 --steps 50 --warmup 10") ;;
-    rehearse) steps+=("300|$out/bench_gloo2|python -u bench.py --gpus 2 --backend gloo --steps 10 --warmup 3") ;;
+    rehearse) steps+=("500|$out/bench_gloo2|python -u bench.py --gpus 2 --backend gloo --steps 10 --warmup 3") ;;
+    rehearse4) steps+=("600|$out/bench_gloo4|python -u bench.py --gpus 4 --backend gloo --steps 10 --warmup 3") ;;
+    queues)   steps+=("180|$out/pytest_queues|python -u -m pytest tests/test_stream_queues_gpu.py -m gpu -v -s --timeout 120 --timeout-method thread") ;;
     prof)     steps+=("240|$out/prof_fp32|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_fp32 -o run -- python3 bench.py --no-bf16 --steps 30 --warmup 5")
               steps+=("240|$out/prof_bf16|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_bf16 -o run -- python3 bench.py --dtype bf16 --steps 50 --warmup 10") ;;
     fp32t)    steps+=("400|$out/pytest_fp32|python -u -m pytest tests/test_fp32_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread") ;;

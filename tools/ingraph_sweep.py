@@ -34,7 +34,7 @@ def main():
     a = ap.parse_args()
     g = build_model(a.model)
     w = init_weights(g, 0)
-    ex = SliceExecutor(g, w, a.batch)
+    ex = SliceExecutor(g, w, a.batch, precision="bf16")
     x = torch.randn((a.batch,) + tuple(g.layers[g.input].out_shape), device="cuda")
     ex.input_buf(g.input).copy_(x)
     rec = {}

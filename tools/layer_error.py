@@ -32,7 +32,7 @@ def main():
     names = [n for n in g.order if g.layers[n].op in ops]
     x = torch.randn(a.batch, a.size, a.size, 3, generator=torch.Generator().manual_seed(0)).cuda()
     ref = ReferenceExecutor(g, w, device="cuda").run({g.input: x}, outputs=names)
-    ex = SliceExecutor(g, w, batch=a.batch, outputs=names)
+    ex = SliceExecutor(g, w, batch=a.batch, outputs=names, precision="bf16")
     got = ex.run({g.input: x})
     torch.cuda.synchronize()
     for n in names:

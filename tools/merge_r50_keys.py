@@ -16,7 +16,7 @@ before = json.load(open(sys.argv[1]))
 g = build_model("resnet50")
 keys = set()
 for bs in (32, 16, 1):
-    ex = E.SliceExecutor(g, init_weights(g, 0), bs)
+    ex = E.SliceExecutor(g, init_weights(g, 0), bs, precision="bf16")
     for i in ex.cfg:
         B, H, W, C, OH, OW, pc = ex._conv_geom(i)
         keys.add(E.conv_key(B, H, W, C, pc))

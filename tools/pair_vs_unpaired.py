@@ -18,7 +18,7 @@ for bs in (4, 32):
     res = {}
     for flag in ("0", "1"):
         os.environ["ADAPT_FUSED_PAIR"] = flag
-        ex = SliceExecutor(g, w, bs, device="cuda:0")
+        ex = SliceExecutor(g, w, bs, device="cuda:0", precision="bf16")
         p = ex(x).float().clone()
         res[flag] = (p, ex.logits().double().clone(), [ex.cfg.get(i) for i in sorted(ex.cfg)][:12])
     torch.cuda.synchronize()
