@@ -989,6 +989,10 @@ def main(argv=None):
     # epoch communicators are aborted by this runtime (re-plan, stall watch): the
     # NCCL watchdog must not kill the worker over receives an idle pipeline keeps posted
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+    # before the first HIP call: compute, capture, link, RCCL, codec and copy streams
+    # must not share the default 4 hardware queues (utils/hwqueues.py)
+    from .utils.hwqueues import ensure_hw_queues
+    ensure_hw_queues()
     ap = argparse.ArgumentParser(description="ADAPT worker node (one per GPU)")
     ap.add_argument("--dispatcher", default="127.0.0.1", help="dispatcher / membership host")
     ap.add_argument("--membership-port", type=int, default=2379)

@@ -55,10 +55,13 @@ import socket
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 PKG = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
+# before the first HIP call: a pipeline stage's streams must not share the default 4
+# hardware queues (a spinning receive would hold back compute; utils/hwqueues.py)
+__import__(f"{PKG}.utils.hwqueues", fromlist=["ensure_hw_queues"]).ensure_hw_queues()
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 
 def parse(argv=None):

@@ -159,3 +159,18 @@ def test_subrun_of_a_real_job_fails_cleanly_without_gpu(tmp_path):
     b = _bench()
     rec = b.run_subrun("pp", "bench", ["--sub", "pp", "--steps", "1", "--warmup", "0"], 2, 120, "cpu", launch)
     assert rec["ok"] is False and rec["rc"] != 0 and "rank" in rec["error"]
+
+
+def test_fault_subrun_through_the_launcher_on_cpu():
+    """bench.py's config-4 sub-run path end to end on CPU workers: the fault run
+    started as `python -m <pkg>.parallel.fault_run` by the rank launcher (the
+    module-run package name once resolved to `__main__` and no worker started)."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel import launch
+    b = _bench()
+    argv = ["--workers", "2", "--devices", "cpu", "--model", "resnet_tiny", "--image", "32", "--batch", "1",
+            "--duration", "4", "--kill-at", "2", "--ready-timeout", "60"]
+    rec = b.run_subrun("fault", "fault", argv, 1, 150, "cpu twin", launch)
+    assert rec["rc"] if not rec["ok"] else True, rec
+    assert rec["ok"] is True and rec["exactly_once"] is True, rec
+    assert rec["workers"] == 2 and rec["devices"] == ["cpu", "cpu"] and rec["precision"] == "fp32"
+    assert rec["epoch_transport"] == "tcp" and rec["hb_timeout"] == 0.25 and rec["victim"] == "w1"

@@ -43,6 +43,7 @@ for p in "${P[@]}"; do
     bench152) steps+=("240|$out/bench_r152|python -u bench.py --model resnet152 --steps 50 --warmup 10") ;;
     rehearse) steps+=("500|$out/bench_gloo2|python -u bench.py --gpus 2 --backend gloo --steps 10 --warmup 3") ;;
     rehearse4) steps+=("600|$out/bench_gloo4|python -u bench.py --gpus 4 --backend gloo --steps 10 --warmup 3") ;;
+    qprobe)   for q in 4 8 16; do steps+=("90|$out/qprobe_$q|GPU_MAX_HW_QUEUES=$q python -u tools/queue_probe.py"); done ;;
     queues)   steps+=("180|$out/pytest_queues|python -u -m pytest tests/test_stream_queues_gpu.py -m gpu -v -s --timeout 120 --timeout-method thread") ;;
     prof)     steps+=("240|$out/prof_fp32|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_fp32 -o run -- python3 bench.py --no-bf16 --steps 30 --warmup 5")
               steps+=("240|$out/prof_bf16|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_bf16 -o run -- python3 bench.py --dtype bf16 --steps 50 --warmup 10") ;;
