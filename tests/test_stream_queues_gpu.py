@@ -16,8 +16,12 @@ ends) on the busy streams and checks that a ResNet-50 slice's graph replay on
 the compute stream still finishes.  With 4 queues it does not once 3 other
 streams are busy (measured: the first GPU run of this test), so stage
 processes (`node.py`, `bench.py`) ask for 8 (`utils/hwqueues.py`); the test
-requires the stage set and up to 6 busy streams to pass at that setting, and
-records the 4-queue behaviour.
+requires the stage set (links, codec side and copy streams all busy) to pass at
+that setting, and records the sweep over k fresh busy streams and the 4-queue
+behaviour.  The sweep is not monotonic in k at any queue count (measured at 4 /
+8 / 16: `profiles/r4/queue_probe.txt`): which hardware queue a new stream lands
+on depends on every stream the process created before it, so it is the stage
+set, in its real creation order, that is asserted.
 
 The reference's hop is a blocking TCP send from the worker's compute loop
 (`src/node.py:163-179`), so its compute and transfer never overlap at all.
@@ -52,13 +56,14 @@ def test_stage_streams_do_not_block_compute_at_stage_queue_count():
     assert st["links"]["released"] and st["links_side_copy"]["released"], "a spinner hit its time bound"
     assert st["links"]["ok"], f"compute waited for a spinning link stream: {st}"
     assert st["links_side_copy"]["ok"], f"compute waited for a spinning auxiliary stream: {st}"
-    sweep = {int(k): v for k, v in rec["sweep"].items()}
-    assert all(sweep[k]["ok"] for k in range(1, 7)), sweep
+    assert all(v["released"] for v in rec["sweep"].values())
 
 
-def test_default_queue_count_behaviour_is_recorded():
-    """Diagnostic twin at the HIP default (4 queues): printed, not asserted
-    beyond the probe completing (every spinner released by its flag)."""
+def test_default_queue_count_blocks_compute():
+    """The HIP default (4 queues): with the stage set busy, compute waits (the
+    reason stage processes raise the count); every spinner is still released
+    by its flag, never by its time bound."""
     rec = _probe(4)
     print(json.dumps(rec))
     assert all(v["released"] for v in rec["sweep"].values())
+    assert not rec["stage"]["links_side_copy"]["ok"]
