@@ -44,6 +44,13 @@ __device__ __attribute__((aligned(64))) float g_wino_zero[64];
 
 constexpr int WINO_CPOL_SC1 = 16;   // gfx950 cache policy: sc1 (write-through L2, bypass L1)
 
+// floor(a / b) for 0 <= a < 2^20 and 1 <= b < 2^12, with rb = 1.0f / b correctly rounded:
+// (a + 1/2) / b lies at least 1/(2b) away from an integer and the float product errs by at
+// most a * 2^-23 / b, so the truncation is exact.  Replaces the ~25-VALU integer division
+// sequence the index math of a block's prologue and epilogue otherwise runs once per piece
+// and per tile (a C = 64 layer has only 4 K chunks to amortise it over).
+__device__ __forceinline__ int wino_div(int a, float rb) { return (int)(((float)a + 0.5f) * rb); }
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_ws_rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
 }
@@ -56,11 +63,19 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
                                            int ns) {
   const int tpi = p.TH * p.TW;
   float ld[S][4][FN][4];
+  const float rtpi = 1.0f / (float)tpi, rtw = 1.0f / (float)p.TW;
+  int oys[4], oxs[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int tt = tw0 + 4 * q + i;
-    const int rr = tt - (tt / tpi) * tpi;
-    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+    const int rr = tt - wino_div(tt, rtpi) * tpi;
+    const int ry = wino_div(rr, rtw);
+    oys[i] = 2 * ry;
+    oxs[i] = 2 * (rr - ry * p.TW);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oy = oys[i], ox = oxs[i];
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -79,9 +94,7 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (ok[i] < 0) continue;
-    const int tt = tw0 + 4 * q + i;
-    const int rr = tt - (tt / tpi) * tpi;
-    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+    const int oy = oys[i], ox = oxs[i];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = (nf0 + j) * 16 + r;
@@ -124,13 +137,15 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
   const __amdgpu_buffer_rsrc_t wsr = wino_ws_rsrc(p.ws);
   float yk[4][FN][4];                                 // fused: this split's partial outputs
   int ok[4];                                          // their NHWC offsets at channel 0 (-1: outside)
+  const float rtpi = 1.0f / (float)tpi, rtw = 1.0f / (float)p.TW;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int tt = tw0 + 4 * q + i;
     ok[i] = -1;
     if (tt >= p.T) continue;
-    const int im = tt / tpi, rr = tt - im * tpi;
-    const int oy = 2 * (rr / p.TW), ox = 2 * (rr - (rr / p.TW) * p.TW);
+    const int im = wino_div(tt, rtpi), rr = tt - im * tpi;
+    const int ry = wino_div(rr, rtw);
+    const int oy = 2 * ry, ox = 2 * (rr - ry * p.TW);
     ok[i] = ((im * p.H + oy) * p.W + ox) * p.N;
     const bool iny = oy + 1 < p.H, inx = ox + 1 < p.W;
 #pragma unroll
@@ -387,11 +402,13 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   const int TR = p.B * p.TH;                         // tile rows over the batch
 
   // ---- the wave's row segments (wave-uniform)
+  const float rtw = 1.0f / (float)p.TW, rth = 1.0f / (float)p.TH;
   const int tw0 = (tg * NW + wave) * 16;
   const int tlast = min(tw0 + 15, p.T - 1);
-  const int R0 = tw0 / p.TW;
-  const int nseg = tw0 < p.T ? tlast / p.TW - R0 + 1 : 0;
+  const int R0 = wino_div(tw0, rtw);
+  const int nseg = tw0 < p.T ? wino_div(tlast, rtw) - R0 + 1 : 0;
   int seg_lo[4], seg_w[4], seg_b[5];
+  float seg_rw[4];
   seg_b[0] = 0;
 #pragma unroll
   for (int sg = 0; sg < 4; ++sg) {
@@ -399,6 +416,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
     const int hi = sg == nseg - 1 ? tlast - (R0 + sg) * p.TW : p.TW - 1;
     seg_lo[sg] = lo;
     seg_w[sg] = sg < nseg ? 2 * (hi - lo + 1) + 2 : 0;
+    seg_rw[sg] = sg < nseg ? 1.0f / (float)seg_w[sg] : 0.f;
     seg_b[sg + 1] = seg_b[sg] + 4 * seg_w[sg];
   }
 
@@ -413,12 +431,13 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 #pragma unroll
     for (int k = 1; k < 4; ++k) sg += pix >= seg_b[k] ? 1 : 0;
     const int wdt = sg == 0 ? seg_w[0] : sg == 1 ? seg_w[1] : sg == 2 ? seg_w[2] : seg_w[3];
+    const float rw = sg == 0 ? seg_rw[0] : sg == 1 ? seg_rw[1] : sg == 2 ? seg_rw[2] : seg_rw[3];
     const int lo = sg == 0 ? seg_lo[0] : 0;
     const int bb = sg == 0 ? seg_b[0] : sg == 1 ? seg_b[1] : sg == 2 ? seg_b[2] : seg_b[3];
     const int lp = pix - bb;
-    const int prow = wdt ? lp / wdt : 0, pcol = lp - prow * wdt;
+    const int prow = (wdt && lp >= 0) ? wino_div(lp, rw) : 0, pcol = lp - prow * wdt;
     const int R = R0 + sg;
-    const int img = R / p.TH, ty = R - img * p.TH;
+    const int img = wino_div(R, rth), ty = R - img * p.TH;
     const int iy = 2 * ty - 1 + prow, ix = 2 * lo - 1 + pcol;
     const bool in = pix < seg_b[4] && R < TR && (unsigned)iy < (unsigned)p.H &&
                     (unsigned)ix < (unsigned)p.W;
@@ -435,7 +454,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 
   // ---- this lane's patch in the wave image: pixel index of (dy, dx) = prow0 + dy * pw + dx
   const int t = tw0 + r;
-  const int tsg = t < p.T ? t / p.TW - R0 : 0;
+  const int tsg = t < p.T ? wino_div(t, rtw) - R0 : 0;
   const int pw = tsg == 0 ? seg_w[0] : tsg == 1 ? seg_w[1] : tsg == 2 ? seg_w[2] : seg_w[3];
   const int pb0 = tsg == 0 ? seg_b[0] : tsg == 1 ? seg_b[1] : tsg == 2 ? seg_b[2] : seg_b[3];
   const int plo = tsg == 0 ? seg_lo[0] : 0;
