@@ -40,7 +40,7 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void_w;
 
-__device__ __attribute__((aligned(64))) float g_wino_zero[64];
+__device__ __attribute__((aligned(64))) float g_wino_zero[256];   // 1 KiB: a whole dummy DMA piece
 
 constexpr int WINO_CPOL_SC1 = 16;   // gfx950 cache policy: sc1 (write-through L2, bypass L1)
 
@@ -387,7 +387,7 @@ struct WinoV2Shape {
 
 // one (tile group tg, channel group cg, K chunks [kc0, kc1)) unit of work; zs / ns / ctr_idx: its partial's
 // slab, the partials of its output block and their arrival counter (ns == 1: whole K, plain epilogue)
-template <int NW, int FN, bool SW, bool EP>
+template <int NW, int FN, bool SW, bool EP, bool PL = false>
 __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem, int tg, int cg, int kc0, int kc1,
                                              int zs, int ns, int ctr_idx) {
   using S = WinoV2Shape<NW, FN>;
@@ -492,6 +492,112 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         else d[dy][dx] = *(const f32x4*)(prd + dy * pws + dx * 64);
       }
   };
+  if constexpr (PL) {
+    // v3 (cfgs 116-117, FN = 1): one basic block per chunk, software-pipelined.
+    //  * the 16 (pa, pb) MFMA groups each read the NEXT group's weight fragments (FN ds_read_b128) ahead
+    //    of their own MFMAs, so an LDS read latency is never exposed right before the MFMA that needs it
+    //    (v2: `R R R R lgkmcnt(0) M...` eight times per chunk);
+    //  * the next chunk's LDS-DMA pieces (PPW weight pieces, then PMAX input pieces) are spread one per
+    //    group instead of 14 back to back after the barrier, where both waves of a SIMD issued them at
+    //    once and left the matrix core idle;
+    //  * FN = 1: two groups' accumulation chains alternate (a dependent 16x16x4 f32 MFMA waits 40 of its
+    //    32 issue cycles);
+    //  * the next chunk's patch is read at the end of the chunk (as EP), unconditionally: the last chunk
+    //    reads / DMAs a harmless dummy, so nothing in the loop branches.
+    f32x4 d[4][4];
+    auto read_patch_pl = [&]() {
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx) d[dy][dx] = *(const f32x4*)(pimg + wino_sw(ps0 + dy * pw * 4 + dx * 4) * 16);
+    };
+    f32x4 acc[16][FN];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (kc0 < kc1) {
+      issue_w(kc0, 0);
+      issue_x(kc0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      read_patch_pl();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    for (int kc = kc0; kc < kc1; ++kc) {
+      const int slot = (kc - kc0) & 1;
+      __builtin_amdgcn_s_barrier();                  // every wave's weight pieces of chunk kc are in
+      asm volatile("" ::: "memory");
+      const bool more = kc + 1 < kc1;
+      const float* wsrc = more ? ub + (size_t)(kc + 1) * uchunk : g_wino_zero;
+      const int wstep = more ? 256 : 0;              // the dummy piece: one 1 KiB buffer for every piece
+      char* wdst = ring + (slot ^ 1) * SLOT;
+      // B^T d: rows, in place
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) {
+        const f32x4 a0 = d[0][dx], a1 = d[1][dx], a2 = d[2][dx], a3 = d[3][dx];
+        d[0][dx] = a0 - a2;
+        d[1][dx] = a1 + a2;
+        d[2][dx] = a2 - a1;
+        d[3][dx] = a1 - a3;
+      }
+      const char* sl = ring + slot * SLOT;
+      constexpr int NB = FN >= 2 ? 2 : 4;            // FN = 1 pairs groups: g-1's fragments must survive g's read
+      f32x4 u[NB][FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + 0) * 64 + lane) * 16);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int pa = g >> 2, pb = g & 3;
+        if (pb == 0) {                               // (B^T d B)[pa][*], in place over row pa
+          const f32x4 e0 = d[pa][0], e1 = d[pa][1], e2 = d[pa][2], e3 = d[pa][3];
+          d[pa][0] = e0 - e2;
+          d[pa][1] = e1 + e2;
+          d[pa][2] = e2 - e1;
+          d[pa][3] = e1 - e3;
+        }
+        if (g < 15) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            u[(g + 1) % NB][j] = *(const f32x4*)(sl + ((j * 16 + g + 1) * 64 + lane) * 16);
+        }
+        if (g < PPW) {                               // next chunk's weight piece g of this wave
+          const int pc = wave * PPW + g;
+          if (PIECES % NW == 0 || pc < PIECES)
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc + pc * wstep + lane * 4),
+                                             (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
+        } else if (g - PPW < PMAX) {                 // next chunk's input piece
+          const int i = g - PPW;
+          const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : g_wino_zero;
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+        }
+        // fence: the next fragments' reads and the DMA piece issue above this group's MFMAs (left to
+        // itself the scheduler sinks each prefetch next to its use, at ~250 VGPRs, and waits lgkmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x4 vv = d[pa][pb];
+        if constexpr (FN >= 2) {
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u[g % NB][j][ss], acc[g][j], 0, 0, 0);
+        } else if ((g & 1) == 1) {                   // FN = 1: groups g-1 and g alternate their chains
+          const f32x4 vp = d[pa][pb - 1];
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss) {
+            acc[g - 1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(vp[ss], u[(g - 1) % NB][0][ss], acc[g - 1][0], 0, 0,
+                                                                 0);
+            acc[g][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u[g % NB][0][ss], acc[g][0], 0, 0, 0);
+          }
+        }
+      }
+      // the next chunk's patch (its DMA went out during this chunk's groups)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      read_patch_pl();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx);
+    return;
+  }
   if (kc0 < kc1) {
     issue_w(kc0, 0);
     issue_x(kc0);
@@ -562,15 +668,15 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 // units x KC space (unit = channel group major, tile group minor).  A ResNet 3x3 has 196-400 units of
 // 4-16 chunks, i.e. 0.77-1.53 rounds of the 256 CUs: the last partial round idled 23-50 % of the chip.
 // Partial units meet through the fused fixup (deterministic, segment order).
-template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false>
+template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false, bool PL = false>
 __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
   __shared__ __attribute__((aligned(16))) char smem[WinoV2Shape<NW, FN>::LDS];
   const int KC = p.C / 16;
   if constexpr (!SK) {
     const int kper = (KC + p.ksplit - 1) / p.ksplit;
     const int kc0 = blockIdx.z * kper;
-    wino_v2_unit<NW, FN, SW, EP>(p, smem, blockIdx.x, blockIdx.y, kc0, min(KC, kc0 + kper), blockIdx.z, p.ksplit,
-                                 blockIdx.x + gridDim.x * blockIdx.y);
+    wino_v2_unit<NW, FN, SW, EP, PL>(p, smem, blockIdx.x, blockIdx.y, kc0, min(KC, kc0 + kper), blockIdx.z,
+                                     p.ksplit, blockIdx.x + gridDim.x * blockIdx.y);
     return;
   }
   const bool sk = SK;
@@ -605,7 +711,7 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
       }
       __syncthreads();                               // the previous segment's ring / flag / images are dead
     }
-    wino_v2_unit<NW, FN, SW, EP>(p, smem, tg, cg, kb, ke, zs, ns, ctr);
+    wino_v2_unit<NW, FN, SW, EP, PL>(p, smem, tg, cg, kb, ke, zs, ns, ctr);
     it = sk ? it + (ke - kb) : it_end;
   }
 }
@@ -613,7 +719,7 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
 // v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
 bool wino_v2_shape_ok(int TW) { return TW >= 5 || TW == 4; }
 
-template <int NW, int FN, bool SW, bool EP, bool SK>
+template <int NW, int FN, bool SW, bool EP, bool SK, bool PL>
 hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || SK != (p.sk_iters > 0)) return hipErrorInvalidValue;
   dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
@@ -623,7 +729,7 @@ hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
     if (iters != p.sk_iters || smax > 4 || !p.counters || !p.ws) return hipErrorInvalidValue;
     grid = dim3(G, 1, 1);
   }
-  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP, SK>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP, SK, PL>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
@@ -657,22 +763,25 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(98, 4, 2, 2, false, 8) \
   X(99, 4, 2, 2, false, 9)
 // v2 (input patches staged by LDS-DMA): id -> waves, 16-channel output fragments per wave, swizzled image,
-// early patch read, stream-K (110-114: the host passes ksplit <= -100)
-#define ADAPT_WINO2_CFGS(X)          \
-  X(100, 8, 2, false, false, false)  \
-  X(101, 8, 1, false, false, false)  \
-  X(102, 4, 1, false, false, false)  \
-  X(103, 8, 2, true, false, false)   \
-  X(104, 8, 1, true, false, false)   \
-  X(105, 4, 1, true, false, false)   \
-  X(106, 8, 2, true, true, false)    \
-  X(107, 8, 1, true, true, false)    \
-  X(108, 4, 1, true, true, false)    \
-  X(110, 8, 2, true, true, true)     \
-  X(111, 8, 2, true, false, true)    \
-  X(112, 4, 1, true, true, true)     \
-  X(113, 4, 1, true, false, true)    \
-  X(114, 8, 1, true, true, true)
+// early patch read, stream-K (110-114: the host passes ksplit <= -100), pipelined chunk body (116-117: v3;
+// FN = 2 spills once the next fragments are held across a group)
+#define ADAPT_WINO2_CFGS(X)                 \
+  X(100, 8, 2, false, false, false, false)  \
+  X(101, 8, 1, false, false, false, false)  \
+  X(102, 4, 1, false, false, false, false)  \
+  X(103, 8, 2, true, false, false, false)   \
+  X(104, 8, 1, true, false, false, false)   \
+  X(105, 4, 1, true, false, false, false)   \
+  X(106, 8, 2, true, true, false, false)    \
+  X(107, 8, 1, true, true, false, false)    \
+  X(108, 4, 1, true, true, false, false)    \
+  X(110, 8, 2, true, true, true, false)     \
+  X(111, 8, 2, true, false, true, false)    \
+  X(112, 4, 1, true, true, true, false)     \
+  X(113, 4, 1, true, false, true, false)    \
+  X(114, 8, 1, true, true, true, false)     \
+  X(116, 8, 1, true, true, false, true)     \
+  X(117, 4, 1, true, true, false, true)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)
@@ -693,7 +802,7 @@ void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* 
 
 bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_, SK_) case id: *nw = NW_; *fn = FN_; return true;
+#define X(id, NW_, FN_, SW_, EP_, SK_, PL_) case id: *nw = NW_; *fn = FN_; return true;
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: *nw = NWM_; *fn = FN_; return true;
@@ -705,7 +814,7 @@ bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
 
 bool conv_wino_f32_ok(int cfg, int C, int N) {
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_, SK_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
+#define X(id, NW_, FN_, SW_, EP_, SK_, PL_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
@@ -724,7 +833,7 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) 
     return hipErrorInvalidValue;                     // fused split-K: 32-bit slab offsets
   }
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_, SK_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_, SK_>(p, s);
+#define X(id, NW_, FN_, SW_, EP_, SK_, PL_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_, SK_, PL_>(p, s);
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return launch_wino<NWM_, FN_, S_, PF_, A_>(p, s);
