@@ -126,10 +126,71 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
 // launch.  Nobody waits on anybody, so the grid never needs to be co-resident.
 template <int FN, int ABL>
 __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x4 (&acc)[16][FN], int tw0, int r,
-                                              int q, int nf0, int* flag, int zs, int ns, int ctr_idx) {
+                                              int q, int nf0, int* flag, int zs, int ns, int ctr_idx,
+                                              char* stage = nullptr) {
   // zs / ns: this partial's slab index / the partials of its output block (ns == 1: whole K);
   // fused fixup when the host passed arrival counters, else slab ws[zs] for splitk_reduce_f32
   const bool split = ns > 1;
+  if (stage != nullptr && !split) {
+    // Whole-K output through the wave's own LDS image (free after its last patch read): the
+    // accumulator layout puts 16 channels of a pixel in 16 lanes, which the plain path stores as
+    // 4-byte scattered writes (32 store instructions per lane at FN = 2); transposed through LDS, a
+    // lane stores 16 contiguous bytes (4 FN dwordx4 per lane), with bias / residual / ReLU applied on
+    // the float4.  Runs: (tile of the wave 0..15, pixel 0..3) x 16 FN channels.
+    constexpr int RUN = 16 * FN;                        // floats per (tile, pixel) run
+    float* st = (float*)stage;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int tl = 4 * q + i;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float m[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) m[a][b] = acc[a * 4 + b][j][i];
+        float w0[4], w1[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          w0[b] = m[0][b] + m[1][b] + m[2][b];
+          w1[b] = m[1][b] - m[2][b] - m[3][b];
+        }
+        st[(tl * 4 + 0) * RUN + j * 16 + r] = w0[0] + w0[1] + w0[2];
+        st[(tl * 4 + 1) * RUN + j * 16 + r] = w0[1] - w0[2] - w0[3];
+        st[(tl * 4 + 2) * RUN + j * 16 + r] = w1[0] + w1[1] + w1[2];
+        st[(tl * 4 + 3) * RUN + j * 16 + r] = w1[1] - w1[2] - w1[3];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: LDS is in order per wave
+    // opaque copies: keep the store-phase index math from being hoisted above the K loop, where its
+    // registers would be live beside the accumulators (the FN = 2 kernels sit at 250+ VGPRs)
+    int lane = q * 16 + r;
+    asm volatile("" : "+v"(lane));
+    const int tpi = p.TH * p.TW;
+    const float rtpi = 1.0f / (float)tpi, rtw = 1.0f / (float)p.TW;
+#pragma unroll
+    for (int it = 0; it < 4 * FN; ++it) {
+      const int g = it * 64 + lane;                     // float4 index in the wave's 64 runs
+      const int run = g / (4 * FN), part = g - run * (4 * FN);
+      const int tl = run >> 2, px = run & 3;
+      const int tt = tw0 + tl;
+      const f32x4 y = *(const f32x4*)(st + run * RUN + part * 4);
+      if (tt >= p.T) continue;
+      const int im = wino_div(tt, rtpi), rr = tt - im * tpi;
+      const int ry = wino_div(rr, rtw);
+      const int oy = 2 * ry + (px >> 1), ox = 2 * (rr - ry * p.TW) + (px & 1);
+      if (oy >= p.H || ox >= p.W) continue;
+      const int n = nf0 * 16 + part * 4;
+      const size_t o = ((size_t)(im * p.H + oy) * p.W + ox) * p.N + n;
+      f32x4 v = y + *(const f32x4*)(p.bias + n);
+      if (p.res) v += *(const f32x4*)(p.res + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], p.relu);
+      if constexpr (ABL & 4) asm volatile("" ::"v"(v));
+      else *(f32x4*)(p.out + o) = v;
+    }
+    return;
+  }
   const bool fused = split && p.counters != nullptr;
   float* dst = split ? p.ws + (size_t)zs * p.B * p.H * p.W * p.N : p.out;
   const int tpi = p.TH * p.TW;
@@ -595,7 +656,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       read_patch_pl();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx);
+    wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx, pimg);
     return;
   }
   if (kc0 < kc1) {
@@ -660,7 +721,8 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   // the fused split-K arrival flag lives in the ring (dead after the loop): a second __shared__ object
   // makes the compiler's LDS-DMA alias tracking put a vmcnt(0) between every chunk's weight DMA issue
   // and the patch reads, which serialises the whole prefetch
-  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx);
+  if (!EP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may still be landing in the image
+  wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx, pimg);
 }
 
 // Stream-K (p.sk_iters > 0, cfgs 103-108 with ksplit <= -100 on the host): a 1-D grid of about

@@ -23,6 +23,9 @@
 #   cs3       channel-split 3x3 (stage 4/5) numerics, isolated timings vs the tile kernels, whole-model A/B
 #   wino      fp32 Winograd numerics + isolated timings of the v2 configs on the four ResNet-50 3x3 shapes
 #   pmcw      PMC passes over the fp32 Winograd kernel (tools/pmc_f32.sh), stage 2-5 shapes
+#   faultd    config 4 at the shipped DEFER defaults (fp32, transport auto, 0.25 s heartbeat): 4- and
+#             8-worker SIGKILL and a 4-worker hang, all workers on cuda:0 (parallel/fault_run.py)
+#   wino4     fp32 Winograd numerics + isolated timings incl. the v3 cfgs 116/117
 #   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -64,6 +67,8 @@ for p in "${P[@]}"; do
               steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108 --ks 1,2,4,-2,-4") ;;
     wino4)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py tests/test_wino.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108,116,117 --ks 1,2,-2,-4") ;;
+    faultd)   for w in 4 8; do steps+=("300|$out/fault${w}_defaults|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel.fault_run --workers $w --devices cuda:0 --model resnet50 --image 224 --batch 32 --duration 20 --kill-at 8 --json gpurun_out/$out/fault_r50_${w}w_defaults.json"); done
+              steps+=("300|$out/hang4_defaults|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel.fault_run --workers 4 --devices cuda:0 --model resnet50 --image 224 --batch 32 --duration 20 --kill-at 8 --fault hang --json gpurun_out/$out/hang_r50_4w_defaults.json") ;;
     pmcw)     steps+=("500|$out/pmcw|bash tools/pmc_f32.sh gpurun_out/$out/pmcw 32,56,56,64,64,3,1,1,0:106:1 32,56,56,64,64,3,1,1,0:103:1 32,28,28,128,128,3,1,1,0:106:1 32,28,28,128,128,3,1,1,0:103:1 32,14,14,256,256,3,1,1,0:108:1 32,14,14,256,256,3,1,1,0:105:1") ;;
     pmc1x1)   steps+=("500|$out/pmc1x1|bash tools/pmc_f32.sh gpurun_out/$out/pmc1x1 32,14,14,1024,256,1,1,0,0:18:-2 32,14,14,256,1024,1,1,0,1:38:1 32,56,56,64,256,1,1,0,1:3:1 32,28,28,512,1024,1,2,0,0:20:-1") ;;
     *) echo "unknown preset $p"; exit 2 ;;
