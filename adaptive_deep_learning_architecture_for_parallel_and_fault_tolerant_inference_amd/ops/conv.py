@@ -434,9 +434,11 @@ WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85:
                  103: (8, 2), 104: (8, 1), 105: (4, 1),       # v2 with the bank-swizzled wave image
                  106: (8, 2), 107: (8, 1), 108: (4, 1),       # ... and the next patch read before the barrier
                  110: (8, 2), 111: (8, 2), 112: (4, 1), 113: (4, 1), 114: (8, 1),    # stream-K twins
-                 116: (8, 1), 117: (4, 1)}                    # v3: pipelined chunk body (fragment prefetch,
+                 116: (8, 1), 117: (4, 1),                    # v3: pipelined chunk body (fragment prefetch,
                                                               # DMA spread over the MFMA groups)
-WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114, 116, 117))
+                 130: (4, 1), 131: (8, 2), 132: (4, 1)}       # 105 / 103 / 117 with the XCD-aware block order
+WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114, 116, 117,
+                          130, 131, 132))
 # stream-K Winograd configs: ksplit <= -100 means (-ksplit - 100) x 256 blocks over the (unit, chunk) space
 WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114))
 WINO_SK_BASE = -100

@@ -730,15 +730,40 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 // units x KC space (unit = channel group major, tile group minor).  A ResNet 3x3 has 196-400 units of
 // 4-16 chunks, i.e. 0.77-1.53 rounds of the 256 CUs: the last partial round idled 23-50 % of the chip.
 // Partial units meet through the fused fixup (deterministic, segment order).
-template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false, bool PL = false>
+// XM (cfgs 130-132): XCD-aware block order.  Blocks are dispatched round-robin over the 8 XCDs, each
+// with its own 4 MiB L2, so with the plain grid every XCD fetches every tile group's input and every
+// channel group's weights from the Infinity Cache.  Here the physical block id is remapped so XCD k
+// runs one contiguous logical range, and that range is a 2-D patch: one half of the channel groups x
+// a quarter of the tile groups -- per chunk step an input line is fetched by 2 L2s and a weight line
+// by 4, instead of by all 8.
+__device__ __forceinline__ void wino_xcd_unit(int& tg, int& cg, int& z) {
+  const int gx = gridDim.x, gy = gridDim.y, plane = gx * gy;
+  const int total = plane * gridDim.z;
+  const int phys = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int lg = xcd_remap(phys, total);
+  z = lg / plane;
+  const int rem = lg - z * plane;
+  const int h0 = (gy + 1) / 2, h1 = gy - h0;
+  if (rem < gx * h0) {
+    tg = rem / h0;
+    cg = rem - tg * h0;
+  } else {
+    const int r2 = rem - gx * h0;
+    tg = r2 / h1;
+    cg = h0 + (r2 - tg * h1);
+  }
+}
+
+template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false, bool PL = false, bool XM = false>
 __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
   __shared__ __attribute__((aligned(16))) char smem[WinoV2Shape<NW, FN>::LDS];
   const int KC = p.C / 16;
   if constexpr (!SK) {
+    int tg = blockIdx.x, cg = blockIdx.y, z = blockIdx.z;
+    if constexpr (XM) wino_xcd_unit(tg, cg, z);
     const int kper = (KC + p.ksplit - 1) / p.ksplit;
-    const int kc0 = blockIdx.z * kper;
-    wino_v2_unit<NW, FN, SW, EP, PL>(p, smem, blockIdx.x, blockIdx.y, kc0, min(KC, kc0 + kper), blockIdx.z,
-                                     p.ksplit, blockIdx.x + gridDim.x * blockIdx.y);
+    const int kc0 = z * kper;
+    wino_v2_unit<NW, FN, SW, EP, PL>(p, smem, tg, cg, kc0, min(KC, kc0 + kper), z, p.ksplit, tg + gridDim.x * cg);
     return;
   }
   const bool sk = SK;
@@ -781,7 +806,7 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
 // v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
 bool wino_v2_shape_ok(int TW) { return TW >= 5 || TW == 4; }
 
-template <int NW, int FN, bool SW, bool EP, bool SK, bool PL>
+template <int NW, int FN, bool SW, bool EP, bool SK, bool PL, bool XM>
 hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || SK != (p.sk_iters > 0)) return hipErrorInvalidValue;
   dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
@@ -791,7 +816,7 @@ hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
     if (iters != p.sk_iters || smax > 4 || !p.counters || !p.ws) return hipErrorInvalidValue;
     grid = dim3(G, 1, 1);
   }
-  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP, SK, PL>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP, SK, PL, XM>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
@@ -826,24 +851,27 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(99, 4, 2, 2, false, 9)
 // v2 (input patches staged by LDS-DMA): id -> waves, 16-channel output fragments per wave, swizzled image,
 // early patch read, stream-K (110-114: the host passes ksplit <= -100), pipelined chunk body (116-117: v3;
-// FN = 2 spills once the next fragments are held across a group)
+// FN = 2 spills once the next fragments are held across a group), XCD-aware block order (130-132)
 #define ADAPT_WINO2_CFGS(X)                 \
-  X(100, 8, 2, false, false, false, false)  \
-  X(101, 8, 1, false, false, false, false)  \
-  X(102, 4, 1, false, false, false, false)  \
-  X(103, 8, 2, true, false, false, false)   \
-  X(104, 8, 1, true, false, false, false)   \
-  X(105, 4, 1, true, false, false, false)   \
-  X(106, 8, 2, true, true, false, false)    \
-  X(107, 8, 1, true, true, false, false)    \
-  X(108, 4, 1, true, true, false, false)    \
-  X(110, 8, 2, true, true, true, false)     \
-  X(111, 8, 2, true, false, true, false)    \
-  X(112, 4, 1, true, true, true, false)     \
-  X(113, 4, 1, true, false, true, false)    \
-  X(114, 8, 1, true, true, true, false)     \
-  X(116, 8, 1, true, true, false, true)     \
-  X(117, 4, 1, true, true, false, true)
+  X(100, 8, 2, false, false, false, false, false)  \
+  X(101, 8, 1, false, false, false, false, false)  \
+  X(102, 4, 1, false, false, false, false, false)  \
+  X(103, 8, 2, true, false, false, false, false)   \
+  X(104, 8, 1, true, false, false, false, false)   \
+  X(105, 4, 1, true, false, false, false, false)   \
+  X(106, 8, 2, true, true, false, false, false)    \
+  X(107, 8, 1, true, true, false, false, false)    \
+  X(108, 4, 1, true, true, false, false, false)    \
+  X(110, 8, 2, true, true, true, false, false)     \
+  X(111, 8, 2, true, false, true, false, false)    \
+  X(112, 4, 1, true, true, true, false, false)     \
+  X(113, 4, 1, true, false, true, false, false)    \
+  X(114, 8, 1, true, true, true, false, false)     \
+  X(116, 8, 1, true, true, false, true, false)     \
+  X(117, 4, 1, true, true, false, true, false)  \
+  X(130, 4, 1, true, false, false, false, true)  \
+  X(131, 8, 2, true, false, false, false, true)  \
+  X(132, 4, 1, true, true, false, true, true)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)
@@ -864,7 +892,7 @@ void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* 
 
 bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_, SK_, PL_) case id: *nw = NW_; *fn = FN_; return true;
+#define X(id, NW_, FN_, SW_, EP_, SK_, PL_, XM_) case id: *nw = NW_; *fn = FN_; return true;
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: *nw = NWM_; *fn = FN_; return true;
@@ -876,7 +904,7 @@ bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
 
 bool conv_wino_f32_ok(int cfg, int C, int N) {
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_, SK_, PL_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
+#define X(id, NW_, FN_, SW_, EP_, SK_, PL_, XM_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
@@ -895,7 +923,7 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) 
     return hipErrorInvalidValue;                     // fused split-K: 32-bit slab offsets
   }
   switch (cfg) {
-#define X(id, NW_, FN_, SW_, EP_, SK_, PL_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_, SK_, PL_>(p, s);
+#define X(id, NW_, FN_, SW_, EP_, SK_, PL_, XM_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_, SK_, PL_, XM_>(p, s);
     ADAPT_WINO2_CFGS(X)
 #undef X
 #define X(id, NWM_, FN_, S_, PF_, A_) case id: return launch_wino<NWM_, FN_, S_, PF_, A_>(p, s);
