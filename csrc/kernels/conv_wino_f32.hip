@@ -131,7 +131,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
   // zs / ns: this partial's slab index / the partials of its output block (ns == 1: whole K);
   // fused fixup when the host passed arrival counters, else slab ws[zs] for splitk_reduce_f32
   const bool split = ns > 1;
-  if (stage != nullptr && !split) {
+  if (stage != nullptr && (!split || p.counters != nullptr)) {
     // Whole-K output through the wave's own LDS image (free after its last patch read): the
     // accumulator layout puts 16 channels of a pixel in 16 lanes, which the plain path stores as
     // 4-byte scattered writes (32 store instructions per lane at FN = 2); transposed through LDS, a
@@ -168,26 +168,73 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
     asm volatile("" : "+v"(lane));
     const int tpi = p.TH * p.TW;
     const float rtpi = 1.0f / (float)tpi, rtw = 1.0f / (float)p.TW;
+    int oo[4 * FN];                                     // NHWC offset of each float4 this lane owns (-1: outside)
 #pragma unroll
     for (int it = 0; it < 4 * FN; ++it) {
       const int g = it * 64 + lane;                     // float4 index in the wave's 64 runs
       const int run = g / (4 * FN), part = g - run * (4 * FN);
       const int tl = run >> 2, px = run & 3;
       const int tt = tw0 + tl;
-      const f32x4 y = *(const f32x4*)(st + run * RUN + part * 4);
-      if (tt >= p.T) continue;
       const int im = wino_div(tt, rtpi), rr = tt - im * tpi;
       const int ry = wino_div(rr, rtw);
       const int oy = 2 * ry + (px >> 1), ox = 2 * (rr - ry * p.TW) + (px & 1);
-      if (oy >= p.H || ox >= p.W) continue;
-      const int n = nf0 * 16 + part * 4;
-      const size_t o = ((size_t)(im * p.H + oy) * p.W + ox) * p.N + n;
-      f32x4 v = y + *(const f32x4*)(p.bias + n);
+      oo[it] = (tt < p.T && oy < p.H && ox < p.W) ? ((im * p.H + oy) * p.W + ox) * p.N + nf0 * 16 + part * 4 : -1;
+    }
+    auto own = [&](int it) -> f32x4 {
+      const int g = it * 64 + lane;
+      return *(const f32x4*)(st + (g / (4 * FN)) * RUN + (g % (4 * FN)) * 4);
+    };
+    auto finish = [&](int it, f32x4 v) {
+      const int o = oo[it];
+      v += *(const f32x4*)(p.bias + nf0 * 16 + ((it * 64 + lane) % (4 * FN)) * 4);
       if (p.res) v += *(const f32x4*)(p.res + o);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], p.relu);
       if constexpr (ABL & 4) asm volatile("" ::"v"(v));
       else *(f32x4*)(p.out + o) = v;
+    };
+    if (!split) {
+#pragma unroll
+      for (int it = 0; it < 4 * FN; ++it)
+        if (oo[it] >= 0) finish(it, own(it));
+      return;
+    }
+    // fused split-K: every split publishes its partial outputs as 16-byte sc1 stores to its slab; the
+    // last split of the output block (arrival counter) adds the slabs in split order -- the same sums,
+    // in the same order, as the per-element path and splitk_reduce_f32 -- then bias / residual / ReLU
+    const int MN = p.B * p.H * p.W * p.N;
+    const __amdgpu_buffer_rsrc_t wsr = wino_ws_rsrc(p.ws);
+#pragma unroll
+    for (int it = 0; it < 4 * FN; ++it)
+      if (oo[it] >= 0)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, own(it)), wsr, (zs * MN + oo[it]) * 4, 0,
+                                               WINO_CPOL_SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int* ctr = p.counters + ctr_idx;
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == ns - 1;
+      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+#pragma unroll
+    for (int it = 0; it < 4 * FN; ++it) {
+      if (oo[it] < 0) continue;
+      f32x4 sl[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        sl[z] = (z < ns && z != zs) ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                     wsr, (z * MN + oo[it]) * 4, 0, WINO_CPOL_SC1))
+                                    : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const f32x4 mine = own(it);
+      f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        if (z < ns) v += z == zs ? mine : sl[z];
+      finish(it, v);
     }
     return;
   }
