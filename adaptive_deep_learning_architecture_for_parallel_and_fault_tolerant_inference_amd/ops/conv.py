@@ -476,10 +476,12 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 
 # fp32 persistent pointwise configs (csrc/kernels/pw_f32.hip): id -> pixels per tile; 1x1 / s1 / p0 convs
 # with K in {64, 128, 256, 512} and N a multiple of the slice (FPW x 128 channels), ksplit 1
-PW_F32_CFGS = {120: 16, 121: 32}
+# 122 / 123: the streaming variant (no LDS, no block barrier; bm codes 1 / 2: two waves per SIMD / the
+# widest channel slice per wave)
+PW_F32_CFGS = {120: 16, 121: 32, 122: 1, 123: 2}
 PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1, 1024: 1}     # 16-channel fragments per wave
 PW_F32_KG = {1024: 2}                                       # K groups of waves (partials meet in LDS)
-PW_F32_BMS = {64: (16, 32), 128: (16, 32), 256: (16, 32), 512: (16, 32), 1024: (16,)}
+PW_F32_BMS = {64: (1, 2, 16, 32), 128: (1, 2, 16, 32), 256: (1, 2, 16, 32), 512: (1, 2, 16, 32), 1024: (1, 2, 16)}
 
 
 def pw_f32_slice(K: int) -> int:

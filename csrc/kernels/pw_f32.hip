@@ -186,6 +186,128 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming pointwise conv (bm codes 1 / 2 on the host, cfgs 122 / 123): the same math with no LDS
+// and no block barrier.  Every wave is independent: it owns FPW 16-channel fragments x all of K in
+// VGPRs (as above) and walks its own pixel tiles (slot, slot + nslots, ...), reading each tile's
+// activation fragments straight from global memory into a ring of D float4 registers that is kept
+// D K-steps ahead across tile boundaries, so the loads of tile t+1 stream in under the MFMAs of tile
+// t.  pw_f32_kernel shares one LDS-staged tile between its 8 waves and pays a block barrier, the
+// staging stores and an exposed epilogue per 16-pixel tile; the GEMM sweep put it at 61-80 % of
+// the fp32 MFMA rate inside its loop plus ~6 us per launch (profiles/r4/gemm1x1_vs_k.log).  The
+// waves that read one tile are the ncg channel groups of one slot; the XCD-aware block order keeps
+// them on one XCD, so a tile crosses the fabric once per XCD.  FPW = 1 alternates two accumulators
+// by K step (a dependent 16x16x4 f32 MFMA waits 40 of its 32 issue cycles).
+template <int K, int FPW, int D, int OCC>
+__global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, int ncg, int nslots) {
+  constexpr int KH = K / 16;
+  constexpr int NA = FPW >= 2 ? 1 : 2;                // accumulator sets per fragment
+  static_assert(KH % D == 0, "ring depth must divide the K steps");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+  if (gw >= ncg * nslots) return;                     // wave-uniform
+  const int cg = gw % ncg, slot = gw / ncg;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ntiles = (p.M + 15) / 16;
+  if (slot >= ntiles) return;
+
+  f32x4 wr[FPW][KH];
+  f32x4 bias[FPW];
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    const int gf = cg * FPW + j;
+#pragma unroll
+    for (int h = 0; h < KH; ++h) wr[j][h] = *(const f32x4*)(p.w + ((size_t)(gf * KH + h) * 64 + lane) * 4);
+    bias[j] = *(const f32x4*)(p.bias + gf * 16 + fq * 4);
+  }
+  const bool second = p.n_split > 0 && cg * FPW * 16 >= p.n_split;
+  float* const dst = second ? p.out2 : p.out;
+  const int ldo = p.n_split > 0 ? (second ? p.N - p.n_split : p.n_split) : p.N;
+  const int cof = second ? p.n_split : 0;
+  const int relu = second ? p.relu2 : p.relu;
+  const bool has_res = p.res != nullptr;
+  const int ohw = p.OH * p.OW;
+  auto xptr = [&](int t, int h) __attribute__((always_inline)) {
+    int m = min(t * 16 + fr, p.M - 1);
+    if (p.stride != 1) {
+      const int img = m / ohw, r = m - img * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+      m = (img * p.H + oh * p.stride) * p.W + ow * p.stride;
+    }
+    return p.x + (size_t)m * K + h * 16 + fq * 4;
+  };
+
+  int t = slot;
+  f32x4 ring[D];
+  const float* xb = xptr(t, 0);
+#pragma unroll
+  for (int i = 0; i < D; ++i) ring[i] = *(const f32x4*)(xb + i * 16);
+  while (true) {
+    const int tn = t + nslots;
+    const bool more = tn < ntiles;
+    const float* xn = xptr(more ? tn : t, 0);         // the last tile re-reads its own (valid) rows
+    const int m = t * 16 + fr;
+    f32x4 res[FPW];
+    if (has_res) {
+#pragma unroll
+      for (int j = 0; j < FPW; ++j)
+        res[j] = *(const f32x4*)(p.res + (size_t)min(m, p.M - 1) * p.N + (cg * FPW + j) * 16 + fq * 4);
+    }
+    f32x4 acc[NA][FPW];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int j = 0; j < FPW; ++j) acc[a][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < KH; ++h) {
+      const f32x4 xf = ring[h % D];
+      ring[h % D] = h + D < KH ? *(const f32x4*)(xb + (h + D) * 16) : *(const f32x4*)(xn + (h + D - KH) * 16);
+      // keep the refill D steps ahead of its use (the scheduler otherwise sinks it next to the use)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+        for (int j = 0; j < FPW; ++j)
+          acc[h % NA][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][h][ss], xf[ss], acc[h % NA][j], 0, 0, 0);
+    }
+    if (m < p.M) {
+#pragma unroll
+      for (int j = 0; j < FPW; ++j) {
+        f32x4 v = acc[0][j] + bias[j];
+        if constexpr (NA > 1) v += acc[1][j];
+        if (has_res) v += res[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
+        *(f32x4*)(dst + (size_t)m * ldo + (cg * FPW + j) * 16 + fq * 4 - cof) = v;
+      }
+    }
+    if (!more) break;
+    t = tn;
+    xb = xn;
+  }
+}
+
+// (K, FPW, D, OCC): weights FPW x K / 4 VGPRs; OCC 2 where they leave room for a second wave per SIMD
+#define ADAPT_PW_STREAM_CFGS(X) \
+  X(64, 4, 4, 2)                \
+  X(128, 4, 8, 2)               \
+  X(256, 2, 8, 2)               \
+  X(256, 4, 8, 1)               \
+  X(512, 1, 8, 2)               \
+  X(512, 2, 8, 1)               \
+  X(1024, 1, 8, 1)
+
+static int pw_stream_pick(int K, int N, int n_split, int wide) {
+  // wide (bm code 2): the largest built FPW; else the one that keeps two waves per SIMD
+  int best = 0;
+#define X(K_, F_, D_, O_)                                                                    \
+  if (K == K_ && N % (F_ * 16) == 0 && n_split % (F_ * 16) == 0 && (wide ? 1 : O_ == 2 || K_ == 1024)) \
+    best = best > F_ ? best : F_;
+  ADAPT_PW_STREAM_CFGS(X)
+#undef X
+  return best;
+}
+
 // (K, FPW, BM, KG) instances: FPW x K / KG <= 512 resident weight floats per lane (<= 128 VGPRs)
 #define ADAPT_PW_F32_CFGS(X) \
   X(64, 2, 16, 1)            \
@@ -215,11 +337,38 @@ static int pw_f32_pick(int K, int N, int n_split, int bm) {
   }
   return 0;
 }
-int pw_f32_fpw(int K, int N, int n_split, int bm) { return pw_f32_pick(K, N, n_split, bm); }
+int pw_f32_fpw(int K, int N, int n_split, int bm) {
+  return bm <= 2 ? pw_stream_pick(K, N, n_split, bm == 2) : pw_f32_pick(K, N, n_split, bm);
+}
 
-bool pw_f32_supported(int K, int N, int bm) { return pw_f32_pick(K, N, 0, bm) > 0; }
+bool pw_f32_supported(int K, int N, int bm) { return pw_f32_fpw(K, N, 0, bm) > 0; }
+
+static hipError_t pw_stream_f32_forward(const PwF32Params& p, int wide, hipStream_t s) {
+  const int fpw = pw_stream_pick(p.K, p.N, p.n_split, wide);
+  if (!fpw) return hipErrorInvalidValue;
+  const int ncg = p.N / (16 * fpw);
+  const int ntiles = (p.M + 15) / 16;
+#define X(K_, F_, D_, O_)                                                                                  \
+  if (p.K == K_ && fpw == F_) {                                                                            \
+    int nslots = (1024 * O_) / ncg;                   /* ~O_ waves per SIMD over the chip */               \
+    if (nslots < 1) nslots = 1;                                                                            \
+    if (nslots > ntiles) nslots = ntiles;                                                                  \
+    const int blocks = (ncg * nslots + 3) / 4;                                                             \
+    hipLaunchKernelGGL((pw_stream_f32_kernel<K_, F_, D_, O_>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots); \
+    return hipGetLastError();                                                                              \
+  }
+  ADAPT_PW_STREAM_CFGS(X)
+#undef X
+  return hipErrorInvalidValue;
+}
 
 hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s) {
+  if (bm == 1 || bm == 2) {
+    if (p.M < 1 || p.stride < 1 || (p.n_split && (!p.out2 || p.res)) || p.M != p.B * p.OH * p.OW ||
+        (p.stride == 1 && (p.H != p.OH || p.W != p.OW)))
+      return hipErrorInvalidValue;
+    return pw_stream_f32_forward(p, bm == 2, s);
+  }
   const int fpw = pw_f32_pick(p.K, p.N, p.n_split, bm);
   if (!fpw || p.M < 1 || p.stride < 1 || (p.n_split && (!p.out2 || p.res)) ||
       p.M != p.B * p.OH * p.OW || (p.stride == 1 && (p.H != p.OH || p.W != p.OW)))

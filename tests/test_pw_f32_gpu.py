@@ -46,7 +46,7 @@ def test_pw_f32_matches_fp64(shape, cfg):
     assert err < 2e-5, f"cfg {cfg}: rel err {err}"
 
 
-@pytest.mark.parametrize("cfg", [120])
+@pytest.mark.parametrize("cfg", [120, 122, 123])
 @pytest.mark.parametrize("B,H,K,N0,N1", [(2, 56, 256, 512, 128), (2, 28, 512, 1024, 256), (1, 9, 256, 512, 128)])
 def test_pw_f32_strided_dual_output(cfg, B, H, K, N0, N1):
     """Merged sibling stride-2 1x1 convs (the ResNet projection shortcut + block-1 `_1` conv): one pointwise
