@@ -436,9 +436,12 @@ WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85:
                  110: (8, 2), 111: (8, 2), 112: (4, 1), 113: (4, 1), 114: (8, 1),    # stream-K twins
                  116: (8, 1), 117: (4, 1),                    # v3: pipelined chunk body (fragment prefetch,
                                                               # DMA spread over the MFMA groups)
-                 130: (4, 1), 131: (8, 2), 132: (4, 1)}       # 105 / 103 / 117 with the XCD-aware block order
+                 130: (4, 1), 131: (8, 2), 132: (4, 1),       # 105 / 103 / 117 with the XCD-aware block order
+                 140: (4, 1), 141: (8, 1)}                    # persistent: two blocks per CU walk the units as
+                                                              # one chunk stream (whole K only)
 WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114, 116, 117,
-                          130, 131, 132))
+                          130, 131, 132, 140, 141))
+WINO_PU_CFGS = frozenset((140, 141))
 # stream-K Winograd configs: ksplit <= -100 means (-ksplit - 100) x 256 blocks over the (unit, chunk) space
 WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114))
 WINO_SK_BASE = -100
@@ -631,6 +634,8 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
                              f"{sorted(WINO_SK_CFGS)} take ksplit <= {WINO_SK_BASE}")
         if not sk and (abs(ksplit) > (C // 16) or ksplit < -4):
             raise ValueError(f"Winograd split-K {ksplit} exceeds the {C // 16} channel chunks (fused: <= 4 splits)")
+        if cfg in WINO_PU_CFGS and ksplit != 1:
+            raise ValueError(f"persistent Winograd config {cfg} runs whole K only (ksplit 1)")
         if sk and wino_sk_plan(cfg, B, H, W, N, C, ksplit)[2] > 4:
             raise ValueError("Winograd stream-K would cut a unit into more than 4 partials")
         ws_ptr = ctr_ptr = 0

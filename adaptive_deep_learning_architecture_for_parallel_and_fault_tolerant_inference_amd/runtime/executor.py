@@ -568,6 +568,8 @@ class SliceExecutor:
                     kts, sks = C // 16, (-2, -4)          # fused split-K (fixup in the kernel, <= 4 splits)
                     if cfg in conv_ops.WINO_SK_CFGS:       # stream-K twins: 1 or 2 x 256 blocks only
                         kts, sks = C // 16, (conv_ops.WINO_SK_BASE - 1, conv_ops.WINO_SK_BASE - 2)
+                    if cfg in conv_ops.WINO_PU_CFGS:       # persistent: whole K in one launch
+                        kts, sks = 1, ()
                 else:
                     bm, bn = conv_ops.F32_TILES[cfg]
                     tiles = math.ceil(M / bm) * math.ceil(N / bn)

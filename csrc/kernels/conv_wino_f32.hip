@@ -853,6 +853,206 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
 // v2 needs every wave's 16 tiles in <= 4 row segments (<= 160 input pixels)
 bool wino_v2_shape_ok(int TW) { return TW >= 5 || TW == 4; }
 
+// ---------------------------------------------------------------------------
+// Persistent v2 (cfgs 140 / 141): a grid of two blocks per CU walks the (tile group, channel group) units
+// u = blockIdx.x, + gridDim.x, ... as ONE flattened chunk stream.  The non-persistent grid pays, per round
+// of blocks, the first chunk's load burst (every block's weights and wave images at once, nothing to
+// overlap) and an exposed epilogue -- about 10 us a round, a third of the stage-2 layer
+// (profiles/r4/wino_vs_cin.log: 19.5 us + 9.8 us per chunk at 56x56x64).  Here the DMA of the next unit's
+// first chunk (its weights, its wave images from its own row-segment geometry) goes out under the
+// current unit's last chunk, and the current unit's output transform and 16-byte stores (staged in the
+// wave image, which the next unit's first patch has just left) run while the CU's other block keeps
+// the matrix cores busy.  Whole units per block: no partial sums, no fixup.
+struct WinoGeom {
+  int src_off[10];
+  unsigned src_ok;
+  int ps0, pw, tw0;
+};
+
+template <int NW>
+__device__ __forceinline__ void wino_geom(const WinoF32Params& p, int tg, int wave, int lane, WinoGeom& G) {
+  const int r = lane & 15, q = lane >> 4;
+  const int TR = p.B * p.TH;
+  const float rtw = 1.0f / (float)p.TW, rth = 1.0f / (float)p.TH;
+  const int tw0 = (tg * NW + wave) * 16;
+  const int tlast = min(tw0 + 15, p.T - 1);
+  const int R0 = wino_div(tw0, rtw);
+  const int nseg = tw0 < p.T ? wino_div(tlast, rtw) - R0 + 1 : 0;
+  int seg_lo[4], seg_w[4], seg_b[5];
+  float seg_rw[4];
+  seg_b[0] = 0;
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {
+    const int lo = sg == 0 ? tw0 - R0 * p.TW : 0;
+    const int hi = sg == nseg - 1 ? tlast - (R0 + sg) * p.TW : p.TW - 1;
+    seg_lo[sg] = lo;
+    seg_w[sg] = sg < nseg ? 2 * (hi - lo + 1) + 2 : 0;
+    seg_rw[sg] = sg < nseg ? 1.0f / (float)seg_w[sg] : 0.f;
+    seg_b[sg + 1] = seg_b[sg] + 4 * seg_w[sg];
+  }
+  G.src_ok = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int sl = wino_sw(i * 64 + lane);
+    const int pix = sl >> 2, qq = sl & 3;
+    int sg = 0;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) sg += pix >= seg_b[k] ? 1 : 0;
+    const int wdt = sg == 0 ? seg_w[0] : sg == 1 ? seg_w[1] : sg == 2 ? seg_w[2] : seg_w[3];
+    const float rw = sg == 0 ? seg_rw[0] : sg == 1 ? seg_rw[1] : sg == 2 ? seg_rw[2] : seg_rw[3];
+    const int lo = sg == 0 ? seg_lo[0] : 0;
+    const int bb = sg == 0 ? seg_b[0] : sg == 1 ? seg_b[1] : sg == 2 ? seg_b[2] : seg_b[3];
+    const int lp = pix - bb;
+    const int prow = (wdt && lp >= 0) ? wino_div(lp, rw) : 0, pcol = lp - prow * wdt;
+    const int R = R0 + sg;
+    const int img = wino_div(R, rth), ty = R - img * p.TH;
+    const int iy = 2 * ty - 1 + prow, ix = 2 * lo - 1 + pcol;
+    const bool in = pix < seg_b[4] && R < TR && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+    G.src_off[i] = in ? ((img * p.H + iy) * p.W + ix) * p.C + 4 * qq : 0;
+    G.src_ok |= in ? 1u << i : 0u;
+  }
+  const int t = tw0 + r;
+  const int tsg = t < p.T ? wino_div(t, rtw) - R0 : 0;
+  G.pw = tsg == 0 ? seg_w[0] : tsg == 1 ? seg_w[1] : tsg == 2 ? seg_w[2] : seg_w[3];
+  const int pb0 = tsg == 0 ? seg_b[0] : tsg == 1 ? seg_b[1] : tsg == 2 ? seg_b[2] : seg_b[3];
+  const int plo = tsg == 0 ? seg_lo[0] : 0;
+  const int prow0 = t < p.T ? pb0 + 2 * (t - (R0 + tsg) * p.TW - plo) : 0;
+  G.ps0 = prow0 * 4 + q;
+  G.tw0 = tw0;
+}
+
+template <int NW, int FN>
+__global__ __launch_bounds__(NW * 64, 2) void conv_wino_f32_pu_kernel(WinoF32Params p) {
+  using S = WinoV2Shape<NW, FN>;
+  constexpr int PMAX = S::PMAX, PIECES = S::PIECES, PPW = S::PPW, SLOT = S::SLOT;
+  static_assert(PMAX == 10, "wave image pieces");
+  __shared__ __attribute__((aligned(16))) char smem[S::LDS];
+  char* ring = smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  char* pimg = smem + 2 * SLOT + wave * PMAX * 1024;
+  const int KC = p.C / 16;
+  const int NF = p.N / 16;
+  const int gx = (p.T + 16 * NW - 1) / (16 * NW), gy = p.N / (16 * FN);
+  const int units = gx * gy;
+  int u = blockIdx.x;
+  if (u >= units) return;
+  const size_t uchunk = (size_t)NF * 16 * 256;
+  // unit -> (tile group, channel group), tile group fastest: blocks running at once share weights
+  int tg = u % gx, cg = u / gx;
+  WinoGeom cur;
+  wino_geom<NW>(p, tg, wave, lane, cur);
+  auto issue_w = [&](int cgi, int kc, int slot) {
+    const float* src = p.u + (size_t)cgi * FN * 16 * 256 + (size_t)kc * uchunk;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;
+      if (PIECES % NW == 0 || pc < PIECES)
+        __builtin_amdgcn_global_load_lds((const void*)(src + pc * 256 + lane * 4),
+                                         (lds_void_w*)(ring + slot * SLOT + pc * 1024), 16, 0, 0);
+    }
+  };
+  auto issue_x = [&](const WinoGeom& G, int kc) {
+#pragma unroll
+    for (int i = 0; i < PMAX; ++i) {
+      const float* src = ((G.src_ok >> i) & 1u) ? p.x + G.src_off[i] + kc * 16 : g_wino_zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+    }
+  };
+  f32x4 d[4][4];
+  auto read_patch = [&](const WinoGeom& G) {
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) d[dy][dx] = *(const f32x4*)(pimg + wino_sw(G.ps0 + dy * G.pw * 4 + dx * 4) * 16);
+  };
+  issue_w(cg, 0, 0);
+  issue_x(cur, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  read_patch(cur);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int slot = 0;
+  while (true) {
+    // the next unit's geometry, computed here while no accumulator is live yet (inside the chunk loop
+    // its temporaries would sit beside acc and d and spill)
+    const int un = u + gridDim.x;
+    const bool has_next = un < units;
+    const int ntg = has_next ? un % gx : tg, ncg = has_next ? un / gx : cg;
+    WinoGeom nxt;
+    wino_geom<NW>(p, ntg, wave, lane, nxt);
+    f32x4 acc[16][FN];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < KC; ++kc) {
+      __builtin_amdgcn_s_barrier();                  // every wave's pieces of this step landed
+      asm volatile("" ::: "memory");
+      const bool last = kc + 1 == KC;
+      const bool step = !last || has_next;
+      if (step) {
+        issue_w(last ? ncg : cg, last ? 0 : kc + 1, slot ^ 1);
+        issue_x(last ? nxt : cur, last ? 0 : kc + 1);  // this step's patch is already in registers
+      }
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) {
+        const f32x4 a0 = d[0][dx], a1 = d[1][dx], a2 = d[2][dx], a3 = d[3][dx];
+        d[0][dx] = a0 - a2;
+        d[1][dx] = a1 + a2;
+        d[2][dx] = a2 - a1;
+        d[3][dx] = a1 - a3;
+      }
+      const char* sl = ring + slot * SLOT;
+#pragma unroll
+      for (int pa = 0; pa < 4; ++pa) {
+        f32x4 v[4];
+        v[0] = d[pa][0] - d[pa][2];
+        v[1] = d[pa][1] + d[pa][2];
+        v[2] = d[pa][2] - d[pa][1];
+        v[3] = d[pa][1] - d[pa][3];
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          f32x4 uu[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) uu[j] = *(const f32x4*)(sl + ((j * 16 + pa * 4 + pb) * 64 + lane) * 16);
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[pa * 4 + pb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[pb][ss], uu[j][ss], acc[pa * 4 + pb][j],
+                                                                           0, 0, 0);
+        }
+      }
+      if (step) {                                    // the next step's patch (its DMA went out above)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        read_patch(last ? nxt : cur);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      slot ^= 1;
+    }
+    // unit done: output transform + stores through the wave image (the next unit's first patch has
+    // already left it for the registers; its next DMA goes out only after the coming barrier)
+    wino_epilogue<FN, 0>(p, acc, cur.tw0, r, q, cg * FN, (int*)smem, 0, 1, 0, pimg);
+    if (!has_next) break;
+    u = un;
+    tg = ntg;
+    cg = ncg;
+    cur = nxt;
+  }
+}
+
+template <int NW, int FN>
+hipError_t launch_wino_pu(const WinoF32Params& p, hipStream_t s) {
+  if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || p.ksplit != 1 || p.sk_iters > 0 || p.counters)
+    return hipErrorInvalidValue;
+  const int units = ((p.T + 16 * NW - 1) / (16 * NW)) * (p.N / (16 * FN));
+  const int grid = units < 512 ? units : 512;        // two blocks per CU
+  hipLaunchKernelGGL((conv_wino_f32_pu_kernel<NW, FN>), dim3(grid), dim3(NW * 64), 0, s, p);
+  return hipGetLastError();
+}
+
+
 template <int NW, int FN, bool SW, bool EP, bool SK, bool PL, bool XM>
 hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || SK != (p.sk_iters > 0)) return hipErrorInvalidValue;
@@ -939,6 +1139,8 @@ void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* 
 
 bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
   switch (cfg) {
+    case 140: *nw = 4; *fn = 1; return true;         // persistent (conv_wino_f32_pu_kernel)
+    case 141: *nw = 8; *fn = 1; return true;
 #define X(id, NW_, FN_, SW_, EP_, SK_, PL_, XM_) case id: *nw = NW_; *fn = FN_; return true;
     ADAPT_WINO2_CFGS(X)
 #undef X
@@ -951,6 +1153,8 @@ bool conv_wino_f32_cfg(int cfg, int* nw, int* fn) {
 
 bool conv_wino_f32_ok(int cfg, int C, int N) {
   switch (cfg) {
+    case 140:
+    case 141: return C % 16 == 0 && N % 16 == 0;
 #define X(id, NW_, FN_, SW_, EP_, SK_, PL_, XM_) case id: return C % 16 == 0 && N % (16 * FN_) == 0;
     ADAPT_WINO2_CFGS(X)
 #undef X
@@ -970,6 +1174,8 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) 
     return hipErrorInvalidValue;                     // fused split-K: 32-bit slab offsets
   }
   switch (cfg) {
+    case 140: return launch_wino_pu<4, 1>(p, s);
+    case 141: return launch_wino_pu<8, 1>(p, s);
 #define X(id, NW_, FN_, SW_, EP_, SK_, PL_, XM_) case id: return launch_wino_v2<NW_, FN_, SW_, EP_, SK_, PL_, XM_>(p, s);
     ADAPT_WINO2_CFGS(X)
 #undef X

@@ -37,6 +37,8 @@ def bench(shape, only=None, ks_list=(1, 2, 4, -1, -2), reps=10, top=20):
         for ks in ks_list:
             if wino and (ks <= C.WINO_SK_BASE) != (cfg in C.WINO_SK_CFGS):
                 continue                              # stream-K twins take ksplit <= -100 only
+            if cfg in C.WINO_PU_CFGS and ks != 1:
+                continue                              # persistent Winograd: whole K
             if -100 < ks and abs(ks) > 1 and (wino or ks > 0) and (Cin // 16 if wino else pc.Kpad // C.F32_BK) // abs(ks) < 2:
                 continue
             if ks < 0 and cfg not in C.F32G_CFGS and not (wino and ks <= -2):
