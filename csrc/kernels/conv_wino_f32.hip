@@ -922,7 +922,7 @@ __device__ __forceinline__ void wino_geom(const WinoF32Params& p, int tg, int wa
 }
 
 template <int NW, int FN>
-__global__ __launch_bounds__(NW * 64, 2) void conv_wino_f32_pu_kernel(WinoF32Params p) {
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_wino_f32_pu_kernel(WinoF32Params p) {
   using S = WinoV2Shape<NW, FN>;
   constexpr int PMAX = S::PMAX, PIECES = S::PIECES, PPW = S::PPW, SLOT = S::SLOT;
   static_assert(PMAX == 10, "wave image pieces");
@@ -1047,7 +1047,8 @@ hipError_t launch_wino_pu(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || p.ksplit != 1 || p.sk_iters > 0 || p.counters)
     return hipErrorInvalidValue;
   const int units = ((p.T + 16 * NW - 1) / (16 * NW)) * (p.N / (16 * FN));
-  const int grid = units < 512 ? units : 512;        // two blocks per CU
+  const int slots = NW == 4 ? 512 : 256;             // 8 waves per CU: two 4-wave blocks or one 8-wave block
+  const int grid = units < slots ? units : slots;
   hipLaunchKernelGGL((conv_wino_f32_pu_kernel<NW, FN>), dim3(grid), dim3(NW * 64), 0, s, p);
   return hipGetLastError();
 }
