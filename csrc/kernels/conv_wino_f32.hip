@@ -495,7 +495,7 @@ struct WinoV2Shape {
 
 // one (tile group tg, channel group cg, K chunks [kc0, kc1)) unit of work; zs / ns / ctr_idx: its partial's
 // slab, the partials of its output block and their arrival counter (ns == 1: whole K, plain epilogue)
-template <int NW, int FN, bool SW, bool EP, bool PL = false>
+template <int NW, int FN, bool SW, bool EP, int PL = 0>
 __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem, int tg, int cg, int kc0, int kc1,
                                              int zs, int ns, int ctr_idx) {
   using S = WinoV2Shape<NW, FN>;
@@ -600,8 +600,9 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         else d[dy][dx] = *(const f32x4*)(prd + dy * pws + dx * 64);
       }
   };
-  if constexpr (PL) {
-    // v3 (cfgs 116-117, FN = 1): one basic block per chunk, software-pipelined.
+  if constexpr (PL != 0) {
+    // v3 (cfgs 116-117, FN = 1; PL = 2, cfgs 118-119: FN = 2 with only the DMA spread): one basic block per
+    // chunk, software-pipelined.
     //  * the 16 (pa, pb) MFMA groups each read the NEXT group's weight fragments (FN ds_read_b128) ahead
     //    of their own MFMAs, so an LDS read latency is never exposed right before the MFMA that needs it
     //    (v2: `R R R R lgkmcnt(0) M...` eight times per chunk);
@@ -649,10 +650,13 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         d[3][dx] = a1 - a3;
       }
       const char* sl = ring + slot * SLOT;
-      constexpr int NB = FN >= 2 ? 2 : 4;            // FN = 1 pairs groups: g-1's fragments must survive g's read
+      constexpr bool PFR = PL == 1;                  // fragments of group g+1 read ahead of g's MFMAs
+      constexpr int NB = !PFR ? 1 : FN >= 2 ? 2 : 4; // FN = 1 pairs groups: g-1's fragments must survive g's read
       f32x4 u[NB][FN];
+      if constexpr (PFR) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + 0) * 64 + lane) * 16);
+        for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + 0) * 64 + lane) * 16);
+      }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int pa = g >> 2, pb = g & 3;
@@ -663,10 +667,15 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
           d[pa][2] = e2 - e1;
           d[pa][3] = e1 - e3;
         }
-        if (g < 15) {
+        if constexpr (PFR) {
+          if (g < 15) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            u[(g + 1) % NB][j] = *(const f32x4*)(sl + ((j * 16 + g + 1) * 64 + lane) * 16);
+            for (int j = 0; j < FN; ++j)
+              u[(g + 1) % NB][j] = *(const f32x4*)(sl + ((j * 16 + g + 1) * 64 + lane) * 16);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + g) * 64 + lane) * 16);
         }
         if (g < PPW) {                               // next chunk's weight piece g of this wave
           const int pc = wave * PPW + g;
@@ -680,9 +689,19 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         }
         // fence: the next fragments' reads and the DMA piece issue above this group's MFMAs (left to
         // itself the scheduler sinks each prefetch next to its use, at ~250 VGPRs, and waits lgkmcnt(0))
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PFR) __builtin_amdgcn_sched_barrier(0);
         const f32x4 vv = d[pa][pb];
-        if constexpr (FN >= 2) {
+        if constexpr (!PFR) {
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u[0][j][ss], acc[g][j], 0, 0, 0);
+          // this group: its fragment reads, its DMA piece, then its MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+          if (g < PPW + PMAX) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4 * FN, 0);
+        } else if constexpr (FN >= 2) {
 #pragma unroll
           for (int ss = 0; ss < 4; ++ss)
 #pragma unroll
@@ -801,7 +820,7 @@ __device__ __forceinline__ void wino_xcd_unit(int& tg, int& cg, int& z) {
   }
 }
 
-template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false, bool PL = false, bool XM = false>
+template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false, int PL = 0, bool XM = false>
 __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
   __shared__ __attribute__((aligned(16))) char smem[WinoV2Shape<NW, FN>::LDS];
   const int KC = p.C / 16;
@@ -1054,7 +1073,7 @@ hipError_t launch_wino_pu(const WinoF32Params& p, hipStream_t s) {
 }
 
 
-template <int NW, int FN, bool SW, bool EP, bool SK, bool PL, bool XM>
+template <int NW, int FN, bool SW, bool EP, bool SK, int PL, bool XM>
 hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
   if (p.N % (16 * FN) || !wino_v2_shape_ok(p.TW) || SK != (p.sk_iters > 0)) return hipErrorInvalidValue;
   dim3 grid((p.T + 16 * NW - 1) / (16 * NW), p.N / (16 * FN), p.ksplit), block(NW * 64);
@@ -1101,25 +1120,27 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
 // early patch read, stream-K (110-114: the host passes ksplit <= -100), pipelined chunk body (116-117: v3;
 // FN = 2 spills once the next fragments are held across a group), XCD-aware block order (130-132)
 #define ADAPT_WINO2_CFGS(X)                 \
-  X(100, 8, 2, false, false, false, false, false)  \
-  X(101, 8, 1, false, false, false, false, false)  \
-  X(102, 4, 1, false, false, false, false, false)  \
-  X(103, 8, 2, true, false, false, false, false)   \
-  X(104, 8, 1, true, false, false, false, false)   \
-  X(105, 4, 1, true, false, false, false, false)   \
-  X(106, 8, 2, true, true, false, false, false)    \
-  X(107, 8, 1, true, true, false, false, false)    \
-  X(108, 4, 1, true, true, false, false, false)    \
-  X(110, 8, 2, true, true, true, false, false)     \
-  X(111, 8, 2, true, false, true, false, false)    \
-  X(112, 4, 1, true, true, true, false, false)     \
-  X(113, 4, 1, true, false, true, false, false)    \
-  X(114, 8, 1, true, true, true, false, false)     \
-  X(116, 8, 1, true, true, false, true, false)     \
-  X(117, 4, 1, true, true, false, true, false)  \
-  X(130, 4, 1, true, false, false, false, true)  \
-  X(131, 8, 2, true, false, false, false, true)  \
-  X(132, 4, 1, true, true, false, true, true)
+  X(100, 8, 2, false, false, false, 0, false)  \
+  X(101, 8, 1, false, false, false, 0, false)  \
+  X(102, 4, 1, false, false, false, 0, false)  \
+  X(103, 8, 2, true, false, false, 0, false)   \
+  X(104, 8, 1, true, false, false, 0, false)   \
+  X(105, 4, 1, true, false, false, 0, false)   \
+  X(106, 8, 2, true, true, false, 0, false)    \
+  X(107, 8, 1, true, true, false, 0, false)    \
+  X(108, 4, 1, true, true, false, 0, false)    \
+  X(110, 8, 2, true, true, true, 0, false)     \
+  X(111, 8, 2, true, false, true, 0, false)    \
+  X(112, 4, 1, true, true, true, 0, false)     \
+  X(113, 4, 1, true, false, true, 0, false)    \
+  X(114, 8, 1, true, true, true, 0, false)     \
+  X(116, 8, 1, true, true, false, 1, false)     \
+  X(117, 4, 1, true, true, false, 1, false)  \
+  X(130, 4, 1, true, false, false, 0, true)  \
+  X(131, 8, 2, true, false, false, 0, true)  \
+  X(132, 4, 1, true, true, false, 1, true)  \
+  X(118, 8, 2, true, true, false, 2, false)  \
+  X(119, 8, 2, true, true, false, 2, true)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

@@ -67,6 +67,9 @@ for p in "${P[@]}"; do
               steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108 --ks 1,2,4,-2,-4") ;;
     wino4)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py tests/test_wino.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108,116,117,130,131,132,140,141 --ks 1,2,-2,-4") ;;
+    wino23)   steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/wino23_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --only 103,106,131,118,119 --ks 1")
+              steps+=("300|$out/wino23_bench_b|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --only 103,106,131,118,119 --ks 1") ;;
     pw4)      steps+=("200|$out/pytest_pw|python -u -m pytest tests/test_pw_f32_gpu.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/pw_bench|python -u tools/conv_bench_f32.py --only 18,38,120,121,122,123 --ks 1,-2 --shape 32,28,28,128,512,1,1,0,1 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,56,56,64,256,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0") ;;
     faultd)   for w in 4 8; do steps+=("300|$out/fault${w}_defaults|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel.fault_run --workers $w --devices cuda:0 --model resnet50 --image 224 --batch 32 --duration 20 --kill-at 8 --json gpurun_out/$out/fault_r50_${w}w_defaults.json"); done
