@@ -38,7 +38,8 @@ def _worker(rank, world, codec, port, outdir):
         runner = importlib.import_module(f"{PKG}.parallel.runner")
         g = resnet.build_resnet("resnet50")
         w = resnet.init_weights(g, seed=0)
-        job = runner.PipelineJob(g, w, world, rank, dev, B, world, ["conv4_block1_out"], host_staged=True, codec=codec)
+        job = runner.PipelineJob(g, w, world, rank, dev, B, world, ["conv4_block1_out"], host_staged=True, codec=codec,
+                                 precision="bf16")
         x = torch.randn((B, 224, 224, 3), generator=torch.Generator(device=dev).manual_seed(5), device=dev)
         job.set_synthetic_input(x)
         job.set_total_steps(STEPS)
