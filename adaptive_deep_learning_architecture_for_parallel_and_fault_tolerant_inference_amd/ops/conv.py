@@ -334,17 +334,39 @@ def stem_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool: bool 
     return out
 
 
-STEM_F32_K = 176      # 7 filter rows x (8 kw x 3 channels) = 168, padded to 11 halves of 16 (stem_f32.hip SF_K)
+STEM_F32_K = 160      # 9 halves of 16 + one MFMA's 4 slots (stem_f32.hip SF_K): 37 MFMAs for K = 147
+
+
+def stem_f32_k_order() -> np.ndarray:
+    """[160] flat (kh*21 + kw*3 + c) tap of each packed K position, -1 = zero.
+
+    Slot p = 4h + fq (16h + 4fq + e in the packed row) for p < 35 holds filter
+    row p // 5, taps 4 (p % 5) + e: five float4 LDS reads per filter row.  Slot
+    35 holds tap 20 (kw = 6, c = 2) of rows 0..3 (a gather), and element 0 of
+    the last four slots (positions 144, 148, 152) tap 20 of rows 4..6: the
+    kernel's 37th MFMA.
+    """
+    order = np.full(STEM_F32_K, -1, np.int64)
+    for p in range(35):
+        for e in range(4):
+            order[4 * p + e] = (p // 5) * 21 + 4 * (p % 5) + e
+    for e in range(4):
+        order[140 + e] = e * 21 + 20
+    for fq in range(3):
+        order[144 + 4 * fq] = (4 + fq) * 21 + 20
+    return order
 
 
 def pack_stem_f32(kernel_hwio: np.ndarray, bias: np.ndarray, pads, device) -> PackedStem:
-    """conv1 (7x7/s2, 3 -> 64, BN folded) for the fp32 stem: [64][s*24 + kw*3 + c] fp32."""
+    """conv1 (7x7/s2, 3 -> 64, BN folded) for the fp32 stem: [64][160] fp32 in
+    `stem_f32_k_order` (every tap once, zeros elsewhere)."""
     kh, kw, cin, cout = kernel_hwio.shape
     if (kh, kw, cin, cout) != (7, 7, 3, 64):
         raise ValueError(f"fp32 stem kernel must be 7x7x3x64, got {kernel_hwio.shape}")
+    flat = np.asarray(kernel_hwio, np.float32).transpose(3, 0, 1, 2).reshape(64, 147)
+    order = stem_f32_k_order()
     wt = np.zeros((64, STEM_F32_K), np.float32)
-    wt[:, :168] = np.pad(np.asarray(kernel_hwio, np.float32).transpose(3, 0, 1, 2),
-                         ((0, 0), (0, 0), (0, 1), (0, 0))).reshape(64, 7 * 8 * 3)
+    wt[:, order >= 0] = flat[:, order[order >= 0]]
     (pt, pb), (pl, pr) = pads
     return PackedStem(w=torch.from_numpy(wt).to(device=device).contiguous(),
                       bias=torch.from_numpy(np.ascontiguousarray(bias, np.float32)).to(device),

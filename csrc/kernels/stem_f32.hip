@@ -12,16 +12,19 @@
 //   new conv rows a pool row needs (three on the first step) into a 3-row LDS
 //   ring and emits the pool row from it, so the conv output never leaves LDS;
 // * input rows live in a 16-row LDS ring with the 3 channels packed
-//   ([col][c]): the 21 (kw, c) taps of one filter row are 21 consecutive floats,
-//   so K = 7 rows x 24 (kw = 7 carries zero weights) = 168, padded to 176:
-//   84 % of the MFMA work is real (a 4-channel layout would be 66 %);
+//   ([col][c]): the 21 (kw, c) taps of one filter row are 21 consecutive floats.
+//   K is ordered so that every MFMA is real work: taps 0..19 of a filter row are
+//   five float4 reads (35 K slots of 4 for the 7 rows), tap 20 of rows 0..3 is
+//   a 4-row gather in the 36th slot and tap 20 of rows 4..6 is one more MFMA
+//   (element 0 of the 37th slot): 37 MFMAs per 16 px x 16 ch tile for K = 147
+//   (a 24-tap row layout needs 44, a 4-channel layout 56);
 // * a step's 2 x 7 pixel tiles x 4 channel tiles are 56 (16 px x 16 ch) units,
 //   7 per wave on 8 waves; a wave always works on the same 16 channels, so its
-//   A operand (the weights: 11 float4 per lane) stays in VGPRs for the launch;
+//   A operand (the weights: 9 float4 + 1 float per lane) stays in VGPRs;
 // * the next step's 4 input rows are loaded into registers before this step's
 //   MFMAs and land in LDS after them;
 // * each unit keeps two accumulators (even / odd K halves): two independent
-//   MFMA chains instead of one 44-long dependent chain.
+//   MFMA chains instead of one 37-long dependent chain.
 #include "kernels.h"
 
 namespace adapt {
@@ -35,8 +38,8 @@ constexpr int SF_COLS = 2 * SF_OWMAX + 8;    // patch columns (input col + pad_l
 constexpr int SF_OFF = 4;                    // row origin: even, so 6*ow + j + OFF stays 8-byte aligned
 constexpr int SF_ROWLEN = 704;               // >= SF_OFF + SF_COLS * 3, 16-byte multiple
 constexpr int SF_RING = 16;                  // input-row ring
-constexpr int SF_K = 176;                    // 7 x 24 taps, padded to 11 halves of 16
-constexpr int SF_KH = SF_K / 16;
+constexpr int SF_K = 160;                    // packed weight row: 9 full halves of 16 + element 0 of 4 slots
+constexpr int SF_KH = 9;                     // full K halves (4 MFMAs each); one single MFMA follows
 static_assert(SF_OFF + SF_COLS * 3 <= SF_ROWLEN, "row length");
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -109,14 +112,20 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   f32x4 wa[SF_KH];
 #pragma unroll
   for (int h = 0; h < SF_KH; ++h) wa[h] = *(const f32x4*)(w + (size_t)(ct * 16 + fr) * SF_K + h * 16 + fq * 4);
+  const float wa9 = w[(size_t)(ct * 16 + fr) * SF_K + SF_KH * 16 + fq * 4];
   const f32x4 b4 = *(const f32x4*)(bias + ct * 16 + fq * 4);
-  // per-lane k layout: half h covers kk = 16h + 4fq .. +3 -> filter row kk / 24, tap j = kk % 24
-  int koff[SF_KH];
+  // per-lane k layout: slot p = 4h + fq (h < 8) is filter row p / 5, taps 4 (p % 5) .. +3;
+  // half 8: slots 32..34 likewise (row 6), slot 35 (fq = 3) is tap 20 of rows 0..3;
+  // the last MFMA: lane fq supplies tap 20 of row 4 + fq (fq = 3: zero weight, row 4 read)
+  int koff[SF_KH - 1];
 #pragma unroll
-  for (int h = 0; h < SF_KH; ++h) {
-    const int kk = 16 * h + 4 * fq;
-    koff[h] = (kk / 24) * 0x10000 + (kk % 24);                  // (filter row, tap) packed
+  for (int h = 0; h < SF_KH - 1; ++h) {
+    const int p = 4 * h + fq;
+    koff[h] = (p / 5) * 0x10000 + 4 * (p % 5);                  // (filter row, first tap) packed
   }
+  const bool g8 = fq == 3;
+  const int j8 = g8 ? 20 : 4 * (fq + 2);                        // half 8: tap of element 0
+  const int r9 = fq < 3 ? 4 + fq : 4;                           // last MFMA: filter row
   __syncthreads();
 
   for (int t = t0; t < t1; ++t) {
@@ -151,19 +160,29 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
       // the even / odd K halves alternate MFMA by MFMA: two independent chains back to back
       // instead of runs of four dependent MFMAs (40-cycle dependent latency vs 32-cycle issue)
 #pragma unroll
-      for (int h = 0; h < SF_KH; h += 2) {
+      for (int h = 0; h < SF_KH - 1; h += 2) {
         const f32x4 pb0 = bop(h);
-        if (h + 1 < SF_KH) {
-          const f32x4 pb1 = bop(h + 1);
+        const f32x4 pb1 = bop(h + 1);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb0[e], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], pb1[e], acc1, 0, 0, 0);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb0[e], acc0, 0, 0, 0);
+        for (int e = 0; e < 4; ++e) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb0[e], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], pb1[e], acc1, 0, 0, 0);
         }
+      }
+      {
+        // half 8: lanes fq < 3 read taps j8 .. j8+3 of row 6, lane group 3 gathers tap 20 of rows 0..3
+        f32x4 pb8;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int s = g8 ? e : 6;
+          pb8[e] = pcol[((rb + s) & (SF_RING - 1)) * SF_ROWLEN + j8 + (g8 ? 0 : e)];
+        }
+        const float pb9 = pcol[((rb + r9) & (SF_RING - 1)) * SF_ROWLEN + 20];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][0], pb8[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][1], pb8[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][2], pb8[2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][3], pb8[3], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa9, pb9, acc0, 0, 0, 0);
       }
       // C^T fragment: channel = 16ct + 4fq + e, pixel = c0 + fr
       if (c0 + fr < OW) {
@@ -197,7 +216,7 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   }
 }
 
-// weights [64][176] fp32: k = s * 24 + kw * 3 + c (kw = 7 and k >= 168 zero); image NHWC, C = 3
+// weights [64][160] fp32 in the slot order above (ops/conv.py pack_stem_f32); image NHWC, C = 3
 bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
   return C == 3 && W % 4 == 0 && OW >= 1 && OW <= SF_OWMAX && 2 * OW + 8 <= SF_COLS && pool_pad == 1;
 }

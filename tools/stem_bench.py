@@ -1,77 +1,46 @@
-#!/usr/bin/env python3
-"""Fused stem kernel (csrc/kernels/stem.hip) vs the unfused pack -> conv -> maxpool
-chain on the ResNet-50 bs=32 stem, hipGraph-timed (device time only).
-
-    python tools/stem_bench.py [--batch 32] [--only fused|unfused]
-"""
+"""Isolated timing of the fp32 fused stem (csrc/kernels/stem_f32.hip) at the
+ResNet-50 shape: conv1 7x7/s2 3->64 + BN/ReLU + 3x3/s2 max-pool, bs=32.
+Floor columns: MFMA work at the kernel's K (37 MFMAs per 16x16 tile for K=147)
+and at the true K, both at the measured fp32 matrix ceiling."""
 import argparse
-import math
-import os
-import sys
+import json
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
-import torch  # noqa: E402
+import numpy as np
+import torch
 
-from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C  # noqa: E402
-from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import eltwise as E  # noqa: E402
+from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C
 
-
-def graph_time(fn, reps=20, rounds=5):
-    fn()
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for _ in range(reps):
-            fn()
-    g.replay()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(rounds):
-        g.replay()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) * 1000 / (reps * rounds)
+PEAK_TF = 150.0
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--only", default="")
+    ap.add_argument("--iters", type=int, default=200)
     a = ap.parse_args()
-    B, dev = a.batch, "cuda"
-    x = torch.randn(B, 224, 224, 3, device=dev)
-    k = (torch.randn(7, 7, 3, 64) / math.sqrt(147)).numpy()
-    b = (torch.randn(64) * 0.1).numpy()
-    ps = C.pack_stem(k, b, ((3, 3), (3, 3)), dev)
-    pooled = torch.empty(B, 56, 56, 64, device=dev, dtype=torch.bfloat16)
-    res = {}
-    if a.only in ("", "fused"):
-        res["fused stem auto"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
-        os.environ["ADAPT_STEM_V1"] = "0"
-        res["fused stem v2 (conv+pool, row groups)"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
-        ref = pooled.clone()
-        os.environ["ADAPT_STEM_V1"] = "1"
-        res["fused stem v1 (conv+pool)"] = graph_time(lambda: C.stem_forward(x, ps, pooled, pool=True))
-        del os.environ["ADAPT_STEM_V1"]
-        print("v1 == v2:", bool(torch.equal(ref, pooled)))
-        full = torch.empty(B, 112, 112, 64, device=dev, dtype=torch.bfloat16)
-        res["fused stem (conv only)"] = graph_time(lambda: C.stem_forward(x, ps, full, pool=False))
-    if a.only in ("", "unfused"):
-        k8 = torch.zeros(7, 7, 8, 64)
-        k8[:, :, :3] = torch.from_numpy(k)
-        pc = C.pack_conv(k8.numpy(), b, 2, ((3, 3), (3, 3)), dev)
-        xp = torch.empty(B, 224, 224, 8, device=dev, dtype=torch.bfloat16)
-        y = torch.empty(B, 112, 112, 64, device=dev, dtype=torch.bfloat16)
-        cfg, ks = C.choose_cfg(B * 112 * 112, 64, pc.Kpad)
-
-        def chain():
-            E.input_pack(x, xp)
-            C.conv_forward(xp, pc, y, relu=True, cfg=1, ksplit=1)
-            E.maxpool(y, pooled, 3, 2, 1, 1, True)
-        res["unfused pack+conv+maxpool"] = graph_time(chain)
-    for n, t in res.items():
-        print(f"{n:30s} {t:8.2f} us")
+    B, H = a.batch, 224
+    rng = np.random.default_rng(0)
+    kern = (rng.standard_normal((7, 7, 3, 64)) / np.sqrt(147)).astype(np.float32)
+    ps = C.pack_stem_f32(kern, np.zeros(64, np.float32), ((3, 3), (3, 3)), "cuda")
+    x = torch.randn(B, H, H, 3, device="cuda")
+    out = torch.empty(B, 56, 56, 64, device="cuda")
+    for _ in range(10):
+        C.stem_f32_forward(x, ps, out)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(a.iters):
+        C.stem_f32_forward(x, ps, out)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) * 1e3 / a.iters
+    px = B * 112 * 112
+    true_flop = 2.0 * px * 64 * 147
+    kernel_flop = 2.0 * px * 64 * 148 * 15 / 14          # 37 MFMAs x K=4, one extra conv row per 7 pool rows
+    rec = {"kernel": "stem_f32", "batch": B, "us": round(us, 2),
+           "floor_true_us": round(true_flop / PEAK_TF / 1e6, 1),
+           "floor_kernel_us": round(kernel_flop / PEAK_TF / 1e6, 1)}
+    print(json.dumps(rec))
 
 
 if __name__ == "__main__":
