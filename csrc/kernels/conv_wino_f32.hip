@@ -651,6 +651,10 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       }
       const char* sl = ring + slot * SLOT;
       constexpr bool PFR = PL == 1;                  // fragments of group g+1 read ahead of g's MFMAs
+      // DMA pieces per group: PL >= 3 front-loads the next chunk's pieces (PL - 1 per group), so the
+      // last one has most of the chunk to land instead of the last two groups (cfgs 150-153)
+      constexpr int DPG = PL >= 3 ? PL - 1 : 1;
+      constexpr int NPG = (PPW + PMAX + DPG - 1) / DPG;   // groups that issue DMA
       constexpr int NB = !PFR ? 1 : FN >= 2 ? 2 : 4; // FN = 1 pairs groups: g-1's fragments must survive g's read
       f32x4 u[NB][FN];
       if constexpr (PFR) {
@@ -677,15 +681,18 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 #pragma unroll
           for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + g) * 64 + lane) * 16);
         }
-        if (g < PPW) {                               // next chunk's weight piece g of this wave
-          const int pc = wave * PPW + g;
-          if (PIECES % NW == 0 || pc < PIECES)
-            __builtin_amdgcn_global_load_lds((const void*)(wsrc + pc * wstep + lane * 4),
-                                             (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
-        } else if (g - PPW < PMAX) {                 // next chunk's input piece
-          const int i = g - PPW;
-          const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : g_wino_zero;
-          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+#pragma unroll
+        for (int pi = g * DPG; pi < (g + 1) * DPG; ++pi) {
+          if (pi < PPW) {                            // next chunk's weight piece pi of this wave
+            const int pc = wave * PPW + pi;
+            if (PIECES % NW == 0 || pc < PIECES)
+              __builtin_amdgcn_global_load_lds((const void*)(wsrc + pc * wstep + lane * 4),
+                                               (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
+          } else if (pi - PPW < PMAX) {              // next chunk's input piece
+            const int i = pi - PPW;
+            const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : g_wino_zero;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+          }
         }
         // fence: the next fragments' reads and the DMA piece issue above this group's MFMAs (left to
         // itself the scheduler sinks each prefetch next to its use, at ~250 VGPRs, and waits lgkmcnt(0))
@@ -699,7 +706,8 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
               acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u[0][j][ss], acc[g][j], 0, 0, 0);
           // this group: its fragment reads, its DMA piece, then its MFMAs
           __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
-          if (g < PPW + PMAX) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+          if (g < NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, DPG, 0);
+          else if (g == NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, PPW + PMAX - (NPG - 1) * DPG, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 4 * FN, 0);
         } else if constexpr (FN >= 2) {
 #pragma unroll
@@ -1140,7 +1148,11 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(131, 8, 2, true, false, false, 0, true)  \
   X(132, 4, 1, true, true, false, 1, true)  \
   X(118, 8, 2, true, true, false, 2, false)  \
-  X(119, 8, 2, true, true, false, 2, true)
+  X(119, 8, 2, true, true, false, 2, true)  \
+  X(150, 8, 2, true, true, false, 3, false)  \
+  X(151, 8, 2, true, true, false, 3, true)   \
+  X(152, 8, 2, true, true, false, 4, false)  \
+  X(153, 8, 2, true, true, false, 4, true)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

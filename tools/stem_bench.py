@@ -4,10 +4,13 @@ Floor columns: MFMA work at the kernel's K (37 MFMAs per 16x16 tile for K=147)
 and at the true K, both at the measured fp32 matrix ceiling."""
 import argparse
 import json
+import os
+import sys
 
 import numpy as np
 import torch
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C
 
 PEAK_TF = 150.0
