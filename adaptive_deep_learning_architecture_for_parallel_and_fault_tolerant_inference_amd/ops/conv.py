@@ -373,8 +373,11 @@ def pack_stem_f32(kernel_hwio: np.ndarray, bias: np.ndarray, pads, device) -> Pa
                       cin=3, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
 
 
+STEM_F32_VARIANT = 1  # stem_f32.hip: 0 = one unit at a time, 1 = software-pipelined units
+
+
 def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pad: int = 1,
-                     stream=None) -> torch.Tensor:
+                     stream=None, variant: int = None) -> torch.Tensor:
     """x: [B,H,W,3] fp32 NHWC -> maxpool3x3/s2(relu(conv7x7/s2(x))), fp32 NHWC 64 ch (csrc/kernels/stem_f32.hip)."""
     if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 4 or x.shape[-1] != 3:
         raise ValueError("fp32 stem input must be contiguous fp32 NHWC with 3 channels")
@@ -387,7 +390,8 @@ def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pa
     if out.numel() != need or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError(f"fp32 stem output buffer must be contiguous fp32 with {need} elements")
     kernels().stem_f32_forward(ptr(x), ptr(ps.w), ptr(ps.bias), ptr(out), B, H, W, 3, OH, OW, ps.pad_t, ps.pad_l,
-                               PH, PW, pool_pad, stream_handle(stream))
+                               PH, PW, pool_pad, stream_handle(stream),
+                               STEM_F32_VARIANT if variant is None else int(variant))
     return out
 
 

@@ -235,10 +235,10 @@ PYBIND11_MODULE(_C, m) {
     return std::make_pair(g, it);
   });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,
-                               int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s) {
+                               int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s, int variant) {
     py::gil_scoped_release nogil;
     check(adapt::stem_f32_forward(P<const float>(x), P<const float>(w), P<const float>(bias), P<float>(out), B, H, W,
-                                  C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, S(s)),
+                                  C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, S(s), variant),
           "stem_f32_forward");
   });
   m.def("maxpool_f32", [](u64 x, u64 y, int B, int H, int W, int C, int OH, int OW, int K, int Sd, int pad_t,

@@ -50,8 +50,16 @@ __device__ __forceinline__ int cring_off(int slot, int px, int chunk) {
   return ((slot * SF_OWMAX + px) * 16 + (chunk ^ (px & 15))) * 4;
 }
 
+// one unit's B operand: 8 K halves, the gathered half 8, element 0 of the last MFMA
+struct StemB {
+  f32x4 h[SF_KH - 1];
+  f32x4 g8;
+  float g9;
+};
+
 }  // namespace
 
+template <bool PIPE>
 __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ bias,
@@ -112,8 +120,8 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   f32x4 wa[SF_KH];
 #pragma unroll
   for (int h = 0; h < SF_KH; ++h) wa[h] = *(const f32x4*)(w + (size_t)(ct * 16 + fr) * SF_K + h * 16 + fq * 4);
-  const float wa9 = w[(size_t)(ct * 16 + fr) * SF_K + SF_KH * 16 + fq * 4];
-  const f32x4 b4 = *(const f32x4*)(bias + ct * 16 + fq * 4);
+  float wa9 = w[(size_t)(ct * 16 + fr) * SF_K + SF_KH * 16 + fq * 4];
+  f32x4 b4 = *(const f32x4*)(bias + ct * 16 + fq * 4);
   // per-lane k layout: slot p = 4h + fq (h < 8) is filter row p / 5, taps 4 (p % 5) .. +3;
   // half 8: slots 32..34 likewise (row 6), slot 35 (fq = 3) is tap 20 of rows 0..3;
   // the last MFMA: lane fq supplies tap 20 of row 4 + fq (fq = 3: zero weight, row 4 read)
@@ -126,6 +134,14 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   const bool g8 = fq == 3;
   const int j8 = g8 ? 20 : 4 * (fq + 2);                        // half 8: tap of element 0
   const int r9 = fq < 3 ? 4 + fq : 4;                           // last MFMA: filter row
+  // the weights must have landed before the step loop: otherwise the wait-count pass, which cannot
+  // tell the first unit from the others, puts vmcnt waits for them between the MFMAs of every unit,
+  // and those also wait for the next step's input rows (issued just before the units).  The empty
+  // asm consumes and redefines each register, so the loads complete here and cannot sink below.
+#pragma unroll
+  for (int h = 0; h < SF_KH; ++h) asm volatile("" : "+v"(wa[h]));
+  asm volatile("" : "+v"(wa9));
+  asm volatile("" : "+v"(b4));
   __syncthreads();
 
   for (int t = t0; t < t1; ++t) {
@@ -140,74 +156,110 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
     f32x4 pv[MAXC];
     if (more) get_rows(pv, nxt_lo, 4);
     const int units = nr * tpr;                                 // pixel tiles this step (x 4 channel tiles)
-    for (int u = wave >> 2; u < units; u += SF_WAVES / 4) {
+    // unit u: conv row ra + u / tpr, pixels c0 .. c0+15 (ragged last tile: clamp the read, skip the store)
+    auto load_unit = [&](int u, StemB& b) {
       const int q = u / tpr;
       const int r = ra + q;
-      if (r < 0 || r >= OH) continue;                           // wave-uniform
       const int c0 = (u - q * tpr) * 16;
-      const int ow = min(c0 + fr, OW - 1);                      // ragged last tile: clamp the read, skip the store
-      const int ihb = 2 * r - pad_t;                            // input row of filter row 0
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      // ring row of filter row s: (ihb + s) mod 16 with ihb + s + 64 > 0, so a mask, not a signed %
-      const unsigned rb = (unsigned)(ihb + 4 * SF_RING);
+      const int ow = min(c0 + fr, OW - 1);
+      // ring row of filter row s: (2r - pad_t + s) mod 16, with the sum + 64 > 0, so a mask, not a signed %
+      const unsigned rb = (unsigned)(2 * r - pad_t + 4 * SF_RING);
       const float* pcol = patch + SF_OFF + 6 * ow;
-      auto bop = [&](int h) {
-        const int s = koff[h] >> 16, j = koff[h] & 0xffff;
-        const float* src = pcol + ((rb + s) & (SF_RING - 1)) * SF_ROWLEN + j;
+#pragma unroll
+      for (int h = 0; h < SF_KH - 1; ++h) {
+        const int sr = koff[h] >> 16, j = koff[h] & 0xffff;
+        const float* src = pcol + ((rb + sr) & (SF_RING - 1)) * SF_ROWLEN + j;
         const f32x2 lo = *(const f32x2*)src, hi = *(const f32x2*)(src + 2);
-        return (f32x4){lo[0], lo[1], hi[0], hi[1]};
-      };
-      // the even / odd K halves alternate MFMA by MFMA: two independent chains back to back
-      // instead of runs of four dependent MFMAs (40-cycle dependent latency vs 32-cycle issue)
+        b.h[h] = (f32x4){lo[0], lo[1], hi[0], hi[1]};
+      }
+      // half 8: lanes fq < 3 read taps j8 .. j8+3 of row 6, lane group 3 gathers tap 20 of rows 0..3
 #pragma unroll
-      for (int h = 0; h < SF_KH - 1; h += 2) {
-        const f32x4 pb0 = bop(h);
-        const f32x4 pb1 = bop(h + 1);
+      for (int e = 0; e < 4; ++e) {
+        const int sr = g8 ? e : 6;
+        b.g8[e] = pcol[((rb + sr) & (SF_RING - 1)) * SF_ROWLEN + j8 + (g8 ? 0 : e)];
+      }
+      b.g9 = pcol[((rb + r9) & (SF_RING - 1)) * SF_ROWLEN + 20];
+    };
+    // 37 MFMAs; the even / odd K halves alternate MFMA by MFMA: two independent chains back to back
+    // instead of runs of four dependent MFMAs (40-cycle dependent latency vs 32-cycle issue)
+    auto run_unit = [&](int u, const StemB& b) {
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < SF_KH - 1; h += 2)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], pb0[e], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], pb1[e], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], b.h[h][e], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], b.h[h + 1][e], acc1, 0, 0, 0);
         }
-      }
-      {
-        // half 8: lanes fq < 3 read taps j8 .. j8+3 of row 6, lane group 3 gathers tap 20 of rows 0..3
-        f32x4 pb8;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int s = g8 ? e : 6;
-          pb8[e] = pcol[((rb + s) & (SF_RING - 1)) * SF_ROWLEN + j8 + (g8 ? 0 : e)];
-        }
-        const float pb9 = pcol[((rb + r9) & (SF_RING - 1)) * SF_ROWLEN + 20];
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][0], pb8[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][1], pb8[1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][2], pb8[2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][3], pb8[3], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa9, pb9, acc0, 0, 0, 0);
-      }
-      // C^T fragment: channel = 16ct + 4fq + e, pixel = c0 + fr
-      if (c0 + fr < OW) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][0], b.g8[0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][1], b.g8[1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][2], b.g8[2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][3], b.g8[3], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa9, b.g9, acc0, 0, 0, 0);
+      // C^T fragment: channel = 16ct + 4fq + e, pixel = c0 + fr; rows outside the image are
+      // computed (their ring reads are in bounds) and dropped here
+      const int q = u / tpr;
+      const int r = ra + q;
+      const int c0 = (u - q * tpr) * 16;
+      if (r >= 0 && r < OH && c0 + fr < OW) {
         f32x4 y = acc0 + acc1 + b4;
         y[0] = fmaxf(y[0], 0.f); y[1] = fmaxf(y[1], 0.f); y[2] = fmaxf(y[2], 0.f); y[3] = fmaxf(y[3], 0.f);
         *(f32x4*)(cring + cring_off((r + 3) % 3, c0 + fr, ct * 4 + fq)) = y;
+      }
+    };
+    const int u0 = wave >> 2;                                   // this wave's units: u0, u0 + 2, ...
+    if constexpr (!PIPE) {
+      for (int u = u0; u < units; u += 2) {
+        StemB b;
+        load_unit(u, b);
+        run_unit(u, b);
+      }
+    } else {
+      // software-pipelined: the next unit's B operand (21 LDS reads) is in flight under this unit's
+      // 37 MFMAs.  Unpipelined, the two waves of a SIMD leave every step's barrier in lockstep and
+      // wait on their LDS reads at the same time, so the matrix core idled between units (MFMA busy
+      // 0.50, profiles/r4/roofline_r50_fp32_bs32.txt).  Out-of-range prefetches re-read the last unit.
+      const int last = units - 1 - ((units - 1 - u0) & 1);
+      StemB ba, bb;
+      load_unit(u0, ba);
+      for (int u = u0; u < units; u += 4) {
+        load_unit(min(u + 2, last), bb);
+        __builtin_amdgcn_sched_barrier(0);
+        run_unit(u, ba);
+        load_unit(min(u + 4, last), ba);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 2 < units) run_unit(u + 2, bb);
       }
     }
     if (more) put_rows(pv, nxt_lo, 4);
     __syncthreads();
     // pool row t from conv rows 2t-pp .. 2t-pp+2; post-ReLU values are >= 0, so the
     // zero padding is the 0 the max starts from
+    // (all 9 reads unconditional, out-of-image taps clamped and masked to 0, so they issue back to back)
     for (int idx = tid; idx < PW * 16; idx += SF_NT) {
       const int ch = idx & 15, pw = idx >> 4;
+      f32x4 v[3][3];
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const int oh = 2 * t - pool_pad + dr;
+        const int ohc = min(max(oh, 0), OH - 1);
+#pragma unroll
+        for (int dc = 0; dc < 3; ++dc) {
+          const int oc = 2 * pw - pool_pad + dc;
+          const int occ = min(max(oc, 0), OW - 1);
+          v[dr][dc] = *(const f32x4*)(cring + cring_off((ohc + 3) % 3, occ, ch));
+        }
+      }
       f32x4 m = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int dr = 0; dr < 3; ++dr) {
         const int oh = 2 * t - pool_pad + dr;
-        if ((unsigned)oh >= (unsigned)OH) continue;
 #pragma unroll
         for (int dc = 0; dc < 3; ++dc) {
           const int oc = 2 * pw - pool_pad + dc;
-          if ((unsigned)oc >= (unsigned)OW) continue;
-          const f32x4 v = *(const f32x4*)(cring + cring_off((oh + 3) % 3, oc, ch));
-          m[0] = fmaxf(m[0], v[0]); m[1] = fmaxf(m[1], v[1]); m[2] = fmaxf(m[2], v[2]); m[3] = fmaxf(m[3], v[3]);
+          if ((unsigned)oh >= (unsigned)OH || (unsigned)oc >= (unsigned)OW) continue;
+          m[0] = fmaxf(m[0], v[dr][dc][0]); m[1] = fmaxf(m[1], v[dr][dc][1]);
+          m[2] = fmaxf(m[2], v[dr][dc][2]); m[3] = fmaxf(m[3], v[dr][dc][3]);
         }
       }
       *(f32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch * 4) = m;
@@ -222,13 +274,18 @@ bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
 }
 
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
-                            int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s) {
-  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || B < 1 || PH < 1 || PW < 1 ||
+                            int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s,
+                            int variant) {
+  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 1 || B < 1 || PH < 1 || PW < 1 ||
       PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
     return hipErrorInvalidValue;
   const int groups = (PH + SF_SP - 1) / SF_SP;
-  hipLaunchKernelGGL(stem_pool_f32_kernel, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW, pad_t,
-                     pad_l, PH, PW, pool_pad, groups);
+  if (variant == 0)
+    hipLaunchKernelGGL(stem_pool_f32_kernel<false>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+                       pad_t, pad_l, PH, PW, pool_pad, groups);
+  else
+    hipLaunchKernelGGL(stem_pool_f32_kernel<true>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+                       pad_t, pad_l, PH, PW, pool_pad, groups);
   return hipGetLastError();
 }
 

@@ -258,8 +258,9 @@ def test_other_families_fp32_logits_match_oracle(name):
     assert torch.isfinite(probs).all()
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("B,H", [(2, 224), (1, 64), (3, 112)])
-def test_stem_f32_fused_matches_fp64(B, H):
+def test_stem_f32_fused_matches_fp64(B, H, variant):
     """csrc/kernels/stem_f32.hip: 7x7/s2 conv (+bias, ReLU) + 3x3/s2 max-pool in one launch vs a float64 oracle."""
     rng = np.random.default_rng(H + B)
     x = rng.standard_normal((B, H, H, 3)).astype(np.float32)
@@ -271,7 +272,7 @@ def test_stem_f32_fused_matches_fp64(B, H):
     want = F.max_pool2d(F.pad(t, (1, 1, 1, 1)), 3, 2).permute(0, 2, 3, 1).numpy()
     ps = C.pack_stem_f32(kern, bias, pads, "cuda")
     out = torch.full(want.shape, float("nan"), dtype=torch.float32, device="cuda")
-    C.stem_f32_forward(torch.from_numpy(x).cuda(), ps, out)
+    C.stem_f32_forward(torch.from_numpy(x).cuda(), ps, out, variant=variant)
     got = out.cpu().numpy()
     err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
     assert np.isfinite(got).all() and err < 2e-5, f"rel err {err}"

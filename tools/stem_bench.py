@@ -27,20 +27,25 @@ def main():
     ps = C.pack_stem_f32(kern, np.zeros(64, np.float32), ((3, 3), (3, 3)), "cuda")
     x = torch.randn(B, H, H, 3, device="cuda")
     out = torch.empty(B, 56, 56, 64, device="cuda")
-    for _ in range(10):
-        C.stem_f32_forward(x, ps, out)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(a.iters):
-        C.stem_f32_forward(x, ps, out)
-    e.record()
-    torch.cuda.synchronize()
-    us = s.elapsed_time(e) * 1e3 / a.iters
+    res = {}
+    for variant in (0, 1):
+        for _ in range(10):
+            C.stem_f32_forward(x, ps, out, variant=variant)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            C.stem_f32_forward(x, ps, out, variant=variant)
+        e.record()
+        torch.cuda.synchronize()
+        res[variant] = (s.elapsed_time(e) * 1e3 / a.iters, out.clone())
+    us = res[C.STEM_F32_VARIANT][0]
+    same = bool(torch.equal(res[0][1], res[1][1]))
     px = B * 112 * 112
     true_flop = 2.0 * px * 64 * 147
     kernel_flop = 2.0 * px * 64 * 148 * 15 / 14          # 37 MFMAs x K=4, one extra conv row per 7 pool rows
     rec = {"kernel": "stem_f32", "batch": B, "us": round(us, 2),
+           "us_by_variant": {v: round(t, 2) for v, (t, _) in res.items()}, "variants_bitwise_equal": same,
            "floor_true_us": round(true_flop / PEAK_TF / 1e6, 1),
            "floor_kernel_us": round(kernel_flop / PEAK_TF / 1e6, 1)}
     print(json.dumps(rec))
