@@ -135,10 +135,10 @@ __device__ __forceinline__ F32Dst f32_dst(const ConvF32Params& p, int n) {
 }
 bool conv_f32g_cfg_tile(int cfg, int* bm, int* bn);
 // fp32 stem (stem_f32.hip): 7x7/s2 conv (+BN, ReLU) + 3x3/s2 max-pool, weights [64][160] fp32;
-// variant 0 = one unit at a time, 1 = software-pipelined units
+// variant 0 = one unit at a time, 1 = software-pipelined units, 2 = whole 112-wide rows (else 1)
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                             int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s,
-                            int variant = 1);
+                            int variant = 2);
 // v2 fp32 kernel family (conv_f32g.hip, cfg ids >= 10): LDS-DMA ring
 bool conv_f32g_ok(int cfg, int Cin, int N);
 hipError_t conv_f32g_launch(const ConvF32Params& p, int cfg, bool pure, hipStream_t s);

@@ -59,7 +59,12 @@ struct StemB {
 
 }  // namespace
 
-template <bool PIPE>
+constexpr int SF_TPR = SF_OWMAX / 16;        // variant 2: pixel tiles of a 112-wide conv row
+
+// V = 0: one unit (16 px x 16 ch) at a time; 1: units software-pipelined; 2: each wave of a pair
+// takes a whole conv row per step, its 7 tiles unrolled with every LDS address a per-row base plus
+// an immediate (OW = 112 only)
+template <int V>
 __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ bias,
@@ -208,7 +213,62 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
       }
     };
     const int u0 = wave >> 2;                                   // this wave's units: u0, u0 + 2, ...
-    if constexpr (!PIPE) {
+    if constexpr (V == 2) {
+      // The unit loops spend ~150 VALU per unit (8 ring-row addresses, the gather, the unit's
+      // geometry, the ring store address: 7.9k VALU per wave for 1.9k MFMAs, profiles/r4/pmc_stem_r4j.txt),
+      // and the two waves of a SIMD reach that VALU phase together.  A whole row has one ring base
+      // per K half; its tiles are 96 floats apart in the patch and 1024 apart in the conv ring.
+      if (first) {                                              // the extra first row, split 4 / 3
+        for (int u = u0; u < tpr; u += 2) {
+          StemB b;
+          load_unit(u, b);
+          run_unit(u, b);
+        }
+      }
+      const int r = ra + (first ? 1 : 0) + u0;
+      if (r >= 0 && r < OH) {                                   // wave-uniform
+        const int rb = 2 * r - pad_t + 4 * SF_RING;
+        const int pbase = SF_OFF + 6 * fr;
+        int ah[SF_KH - 1], ag[4];
+#pragma unroll
+        for (int h = 0; h < SF_KH - 1; ++h)
+          ah[h] = pbase + ((rb + (koff[h] >> 16)) & (SF_RING - 1)) * SF_ROWLEN + (koff[h] & 0xffff);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ag[e] = pbase + ((rb + (g8 ? e : 6)) & (SF_RING - 1)) * SF_ROWLEN + j8 + (g8 ? 0 : e);
+        const int a9 = pbase + ((rb + r9) & (SF_RING - 1)) * SF_ROWLEN + 20;
+        float* cdst = cring + cring_off((r + 3) % 3, fr, ct * 4 + fq);
+#pragma unroll
+        for (int c = 0; c < SF_TPR; ++c) {
+          const int po = c * 96;                                // 16 pixels x 6 floats
+          f32x4 acc0 = b4, acc1 = {0.f, 0.f, 0.f, 0.f};
+          f32x4 bh[SF_KH - 1];
+#pragma unroll
+          for (int h = 0; h < SF_KH - 1; ++h) {
+            const f32x2 lo = *(const f32x2*)(patch + ah[h] + po), hi = *(const f32x2*)(patch + ah[h] + po + 2);
+            bh[h] = (f32x4){lo[0], lo[1], hi[0], hi[1]};
+          }
+          f32x4 b8;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) b8[e] = patch[ag[e] + po];
+          const float b9 = patch[a9 + po];
+#pragma unroll
+          for (int h = 0; h < SF_KH - 1; h += 2)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], bh[h][e], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], bh[h + 1][e], acc1, 0, 0, 0);
+            }
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][0], b8[0], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][1], b8[1], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][2], b8[2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][3], b8[3], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa9, b9, acc0, 0, 0, 0);
+          f32x4 y = acc0 + acc1;
+          y[0] = fmaxf(y[0], 0.f); y[1] = fmaxf(y[1], 0.f); y[2] = fmaxf(y[2], 0.f); y[3] = fmaxf(y[3], 0.f);
+          *(f32x4*)(cdst + c * 1024) = y;
+        }
+      }
+    } else if constexpr (V == 0) {
       for (int u = u0; u < units; u += 2) {
         StemB b;
         load_unit(u, b);
@@ -276,15 +336,19 @@ bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                             int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s,
                             int variant) {
-  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 1 || B < 1 || PH < 1 || PW < 1 ||
+  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 2 || B < 1 || PH < 1 || PW < 1 ||
       PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
     return hipErrorInvalidValue;
   const int groups = (PH + SF_SP - 1) / SF_SP;
+  if (variant == 2 && OW != 16 * SF_TPR) variant = 1;          // the row kernel takes 112-wide rows only
   if (variant == 0)
-    hipLaunchKernelGGL(stem_pool_f32_kernel<false>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+    hipLaunchKernelGGL(stem_pool_f32_kernel<0>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+                       pad_t, pad_l, PH, PW, pool_pad, groups);
+  else if (variant == 1)
+    hipLaunchKernelGGL(stem_pool_f32_kernel<1>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
   else
-    hipLaunchKernelGGL(stem_pool_f32_kernel<true>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+    hipLaunchKernelGGL(stem_pool_f32_kernel<2>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
   return hipGetLastError();
 }
