@@ -218,7 +218,7 @@ def test_rccl_hung_stage_detected_and_replayed_exactly_once():
         stop.set()
         feed.join()
         d.inject_fault(victim, "clear")
-        total = sent[0] - inq.qsize()
+        total = sent[0]                      # queued inputs are consumed too
         while len(res) < total:
             res.append(outq.get(timeout=300))
         time.sleep(0.5)
