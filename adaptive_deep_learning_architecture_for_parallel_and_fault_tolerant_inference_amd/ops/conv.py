@@ -467,10 +467,12 @@ WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85:
                                                               # MFMA groups (119: + XCD order)
                  150: (8, 2), 151: (8, 2), 152: (8, 2), 153: (8, 2),    # 118 / 119 with the next chunk's
                                                               # DMA front-loaded, 2 (150-151) / 3 pieces a group
+                 154: (8, 2), 155: (8, 2), 156: (8, 2),       # 118 + stagger / priority / both for waves 4-7
                  140: (4, 1), 141: (8, 1)}                    # persistent: two blocks per CU walk the units as
                                                               # one chunk stream (whole K only)
 WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114, 116, 117,
-                          118, 119, 130, 131, 132, 140, 141, 150, 151, 152, 153))
+                          118, 119, 130, 131, 132, 140, 141, 150, 151, 152, 153,
+                          154, 155, 156))
 WINO_PU_CFGS = frozenset((140, 141))
 # stream-K Winograd configs: ksplit <= -100 means (-ksplit - 100) x 256 blocks over the (unit, chunk) space
 WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114))

@@ -601,6 +601,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       }
   };
   if constexpr (PL != 0) {
+    constexpr int PLM = PL & 7;                      // chunk body; PL & 8 / 16: stagger / priority (below)
     // v3 (cfgs 116-117, FN = 1; PL = 2, cfgs 118-119: FN = 2 with only the DMA spread): one basic block per
     // chunk, software-pipelined.
     //  * the 16 (pa, pb) MFMA groups each read the NEXT group's weight fragments (FN ds_read_b128) ahead
@@ -625,6 +626,13 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
     for (int i = 0; i < 16; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // PL & 16: the second half of the waves (each SIMD's younger partner) at priority 1 for the whole
+    // loop; PL & 8: it starts every chunk ~128 cycles late, so the two partners' LDS waits stop
+    // coinciding (the two waves of a SIMD run the same program in lock step from each barrier,
+    // MI355X_MICROARCH.md "two waves per SIMD", items 4 and 9)
+    if constexpr ((PL & 16) != 0) {
+      if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    }
     if (kc0 < kc1) {
       issue_w(kc0, 0);
       issue_x(kc0);
@@ -636,6 +644,9 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       const int slot = (kc - kc0) & 1;
       __builtin_amdgcn_s_barrier();                  // every wave's weight pieces of chunk kc are in
       asm volatile("" ::: "memory");
+      if constexpr ((PL & 8) != 0) {
+        if (wave >= NW / 2) __builtin_amdgcn_s_sleep(2);
+      }
       const bool more = kc + 1 < kc1;
       const float* wsrc = more ? ub + (size_t)(kc + 1) * uchunk : g_wino_zero;
       const int wstep = more ? 256 : 0;              // the dummy piece: one 1 KiB buffer for every piece
@@ -650,10 +661,10 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         d[3][dx] = a1 - a3;
       }
       const char* sl = ring + slot * SLOT;
-      constexpr bool PFR = PL == 1;                  // fragments of group g+1 read ahead of g's MFMAs
+      constexpr bool PFR = PLM == 1;                  // fragments of group g+1 read ahead of g's MFMAs
       // DMA pieces per group: PL >= 3 front-loads the next chunk's pieces (PL - 1 per group), so the
       // last one has most of the chunk to land instead of the last two groups (cfgs 150-153)
-      constexpr int DPG = PL >= 3 ? PL - 1 : 1;
+      constexpr int DPG = PLM >= 3 ? PLM - 1 : 1;
       constexpr int NPG = (PPW + PMAX + DPG - 1) / DPG;   // groups that issue DMA
       constexpr int NB = !PFR ? 1 : FN >= 2 ? 2 : 4; // FN = 1 pairs groups: g-1's fragments must survive g's read
       f32x4 u[NB][FN];
@@ -1152,7 +1163,10 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(150, 8, 2, true, true, false, 3, false)  \
   X(151, 8, 2, true, true, false, 3, true)   \
   X(152, 8, 2, true, true, false, 4, false)  \
-  X(153, 8, 2, true, true, false, 4, true)
+  X(153, 8, 2, true, true, false, 4, true)   \
+  X(154, 8, 2, true, true, false, 10, false) \
+  X(155, 8, 2, true, true, false, 18, false) \
+  X(156, 8, 2, true, true, false, 26, false)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

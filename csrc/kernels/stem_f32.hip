@@ -149,7 +149,15 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   asm volatile("" : "+v"(b4));
   __syncthreads();
 
+  // V = 3: waves 4-7 (each SIMD's younger partner) at priority 1; V = 4: they start every step
+  // ~128 cycles late (MI355X_MICROARCH.md "two waves per SIMD", items 4 and 9)
+  if constexpr (V == 3) {
+    if (wave >= SF_WAVES / 2) __builtin_amdgcn_s_setprio(1);
+  }
   for (int t = t0; t < t1; ++t) {
+    if constexpr (V == 4) {
+      if (wave >= SF_WAVES / 2) __builtin_amdgcn_s_sleep(2);
+    }
     const bool first = t == t0;
     const int ra = first ? r_first : 2 * t - pool_pad + 1;     // first conv row this step computes
     const int nr = first ? 3 : 2;
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
       }
     };
     const int u0 = wave >> 2;                                   // this wave's units: u0, u0 + 2, ...
-    if constexpr (V == 2) {
+    if constexpr (V >= 2) {
       // The unit loops spend ~150 VALU per unit (8 ring-row addresses, the gather, the unit's
       // geometry, the ring store address: 7.9k VALU per wave for 1.9k MFMAs, profiles/r4/pmc_stem_r4j.txt),
       // and the two waves of a SIMD reach that VALU phase together.  A whole row has one ring base
@@ -336,19 +344,25 @@ bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                             int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s,
                             int variant) {
-  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 2 || B < 1 || PH < 1 || PW < 1 ||
+  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 4 || B < 1 || PH < 1 || PW < 1 ||
       PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
     return hipErrorInvalidValue;
   const int groups = (PH + SF_SP - 1) / SF_SP;
-  if (variant == 2 && OW != 16 * SF_TPR) variant = 1;          // the row kernel takes 112-wide rows only
+  if (variant >= 2 && OW != 16 * SF_TPR) variant = 1;          // the row kernels take 112-wide rows only
   if (variant == 0)
     hipLaunchKernelGGL(stem_pool_f32_kernel<0>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
   else if (variant == 1)
     hipLaunchKernelGGL(stem_pool_f32_kernel<1>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
-  else
+  else if (variant == 2)
     hipLaunchKernelGGL(stem_pool_f32_kernel<2>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+                       pad_t, pad_l, PH, PW, pool_pad, groups);
+  else if (variant == 3)
+    hipLaunchKernelGGL(stem_pool_f32_kernel<3>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
+                       pad_t, pad_l, PH, PW, pool_pad, groups);
+  else
+    hipLaunchKernelGGL(stem_pool_f32_kernel<4>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
   return hipGetLastError();
 }
