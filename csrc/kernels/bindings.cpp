@@ -234,6 +234,7 @@ PYBIND11_MODULE(_C, m) {
     adapt::conv_f32g_sk_plan(tiles, kt, mult, &g, &it);
     return std::make_pair(g, it);
   });
+  m.def("wino_set_debug", [](u64 buf) { adapt::wino_set_debug(P<unsigned long long>(buf)); });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,
                                int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s, int variant) {
     py::gil_scoped_release nogil;

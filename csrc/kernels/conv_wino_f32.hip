@@ -602,6 +602,17 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   };
   if constexpr (PL != 0) {
     constexpr int PLM = PL & 7;                      // chunk body; PL & 8 / 16: stagger / priority (below)
+    // phase stamps (tools/wino_timeline.py): shader clock at unit start / first chunk landed / loop end /
+    // epilogue end, the 100 MHz wall clock at start and end, HW_ID and XCC_ID; thread 0 only, vector stores
+    unsigned long long* const dbg =
+        p.dbg ? p.dbg + 8 * (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+    const bool stamp = dbg && threadIdx.x == 0;
+    if (stamp) {
+      dbg[0] = __builtin_amdgcn_s_memtime();
+      dbg[4] = __builtin_amdgcn_s_memrealtime();
+      dbg[6] = (unsigned)__builtin_amdgcn_s_getreg(0xF804);       // HW_ID
+      dbg[7] = (unsigned)__builtin_amdgcn_s_getreg(0x7814);       // XCC_ID
+    }
     // v3 (cfgs 116-117, FN = 1; PL = 2, cfgs 118-119: FN = 2 with only the DMA spread): one basic block per
     // chunk, software-pipelined.
     //  * the 16 (pa, pb) MFMA groups each read the NEXT group's weight fragments (FN ds_read_b128) ahead
@@ -640,6 +651,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       read_patch_pl();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if (stamp) dbg[1] = __builtin_amdgcn_s_memtime();
     for (int kc = kc0; kc < kc1; ++kc) {
       const int slot = (kc - kc0) & 1;
       __builtin_amdgcn_s_barrier();                  // every wave's weight pieces of chunk kc are in
@@ -741,7 +753,12 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       read_patch_pl();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if (stamp) dbg[2] = __builtin_amdgcn_s_memtime();
     wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx, pimg);
+    if (stamp) {
+      dbg[3] = __builtin_amdgcn_s_memtime();
+      dbg[5] = __builtin_amdgcn_s_memrealtime();
+    }
     return;
   }
   if (kc0 < kc1) {
@@ -1213,7 +1230,12 @@ bool conv_wino_f32_ok(int cfg, int C, int N) {
   return false;
 }
 
-hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s) {
+static unsigned long long* g_wino_dbg = nullptr;
+void wino_set_debug(unsigned long long* buf) { g_wino_dbg = buf; }
+
+hipError_t conv_wino_f32_launch(const WinoF32Params& p_in, int cfg, hipStream_t s) {
+  WinoF32Params p = p_in;
+  p.dbg = g_wino_dbg;
   if (p.C % 16 || p.ksplit < 1 || p.T != p.B * p.TH * p.TW) return hipErrorInvalidValue;
   if (p.ksplit > 1 && !p.ws) return hipErrorInvalidValue;
   if (p.sk_iters > 0) {                              // stream-K: v2 configs, <= 4 slabs, 32-bit slab offsets

@@ -29,6 +29,7 @@
 #   stem      fp32 stem numerics + isolated timing (tools/stem_bench.py)
 #   wino5     Winograd numerics + isolated timings of 118/119 vs the front-loaded DMA cfgs 150-153
 #   wino6     Winograd numerics + isolated timings of 118 vs the stagger / priority cfgs 154-156
+#   wtl       per-block phase timelines of the Winograd kernel on the four ResNet-50 3x3 shapes
 #   pmcstem   two PMC passes over the fp32 stem (tools/stem_bench.py)
 #   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
@@ -87,6 +88,10 @@ for p in "${P[@]}"; do
               steps+=("300|$out/wino5_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 118,119,150,151,152,153 --ks 1,-2,-4") ;;
     wino6)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
               for rep in a b; do steps+=("300|$out/wino6_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 118,154,155,156 --ks 1,-2,-4"); done ;;
+    wtl)      for spec in "32,56,56,64,64:118:1" "32,56,56,64,64:155:1" "32,28,28,128,128:118:1" "32,14,14,256,256:118:-2" "32,7,7,512,512:118:-4"; do
+                IFS=':' read -r shp cfg ks <<< "$spec"
+                steps+=("120|$out/wtl_${cfg}_${shp//,/x}|python -u tools/wino_timeline.py --shape $shp --cfg $cfg --ks $ks --json gpurun_out/$out/wtl_${cfg}_${shp//,/x}.json")
+              done ;;
     pmcstem)  steps+=("120|$out/pmcstem1|cd /tmp && rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/$out/pmcstem/g1 -o run -- python3 \$GRAFT_REPO_ROOT/tools/stem_bench.py --iters 20")
               steps+=("120|$out/pmcstem2|cd /tmp && rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/$out/pmcstem/g2 -o run -- python3 \$GRAFT_REPO_ROOT/tools/stem_bench.py --iters 20") ;;
     *) echo "unknown preset $p"; exit 2 ;;
