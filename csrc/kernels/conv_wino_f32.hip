@@ -184,19 +184,30 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
       const int g = it * 64 + lane;
       return *(const f32x4*)(st + (g / (4 * FN)) * RUN + (g % (4 * FN)) * 4);
     };
-    auto finish = [&](int it, f32x4 v) {
+    // a lane's channel quad is the same for every float4 it owns (64 runs per pass, 4 FN quads per run),
+    // so the bias is one load; the LDS reads and residual loads of all passes issue before the first
+    // store -- inside the per-pass `oo >= 0` branches each would wait out its own latency in turn
+    const f32x4 bsv = *(const f32x4*)(p.bias + nf0 * 16 + (lane % (4 * FN)) * 4);
+    auto finish = [&](int it, f32x4 v, f32x4 rv) {
       const int o = oo[it];
-      v += *(const f32x4*)(p.bias + nf0 * 16 + ((it * 64 + lane) % (4 * FN)) * 4);
-      if (p.res) v += *(const f32x4*)(p.res + o);
+      v += bsv;
+      if (p.res) v += rv;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], p.relu);
       if constexpr (ABL & 4) asm volatile("" ::"v"(v));
       else *(f32x4*)(p.out + o) = v;
     };
+    f32x4 rvs[4 * FN];
+#pragma unroll
+    for (int it = 0; it < 4 * FN; ++it)
+      rvs[it] = p.res ? *(const f32x4*)(p.res + max(oo[it], 0)) : (f32x4){0.f, 0.f, 0.f, 0.f};
     if (!split) {
+      f32x4 ov[4 * FN];
+#pragma unroll
+      for (int it = 0; it < 4 * FN; ++it) ov[it] = own(it);
 #pragma unroll
       for (int it = 0; it < 4 * FN; ++it)
-        if (oo[it] >= 0) finish(it, own(it));
+        if (oo[it] >= 0) finish(it, ov[it], rvs[it]);
       return;
     }
     // fused split-K: every split publishes its partial outputs as 16-byte sc1 stores to its slab; the
@@ -220,21 +231,28 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
     }
     __syncthreads();
     if (!*flag) return;
+    // two passes' slab loads in flight at a time (all eight would hold 128 VGPRs of slabs)
 #pragma unroll
-    for (int it = 0; it < 4 * FN; ++it) {
-      if (oo[it] < 0) continue;
-      f32x4 sl[4];
+    for (int it0 = 0; it0 < 4 * FN; it0 += 2) {
+      f32x4 sl[2][4];
 #pragma unroll
-      for (int z = 0; z < 4; ++z)
-        sl[z] = (z < ns && z != zs) ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                     wsr, (z * MN + oo[it]) * 4, 0, WINO_CPOL_SC1))
-                                    : (f32x4){0.f, 0.f, 0.f, 0.f};
-      const f32x4 mine = own(it);
-      f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int z = 0; z < 4; ++z)
-        if (z < ns) v += z == zs ? mine : sl[z];
-      finish(it, v);
+        for (int z = 0; z < 4; ++z)
+          sl[k][z] = (z < ns && z != zs)
+                         ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         wsr, (z * MN + max(oo[it0 + k], 0)) * 4, 0, WINO_CPOL_SC1))
+                         : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int it = it0 + k;
+        const f32x4 mine = own(it);
+        f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int z = 0; z < 4; ++z)
+          if (z < ns) v += z == zs ? mine : sl[k][z];
+        if (oo[it] >= 0) finish(it, v, rvs[it]);
+      }
     }
     return;
   }
