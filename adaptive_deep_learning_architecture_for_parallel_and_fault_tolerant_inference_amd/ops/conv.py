@@ -435,6 +435,16 @@ def wino_sk_plan(cfg: int, B: int, H: int, W: int, N: int, C: int, ksplit: int):
     return tuple(kernels().conv_wino_sk_plan(wino_blocks(cfg, B, H, W, N), C // 16, WINO_SK_BASE - ksplit))
 
 
+WINO_SK_V3 = frozenset((157, 158))   # stream-K over the v3 chunk body: a block meets <= 2 units
+
+
+def wino_sk_feasible(cfg: int, B: int, H: int, W: int, N: int, C: int, ksplit: int) -> bool:
+    """A stream-K Winograd launch the kernel accepts: <= 4 partials per unit, and for the v3 body at
+    most as many chunks per block as a unit has (conv_wino_f32.hip launch_wino_v2)."""
+    _, iters, smax = wino_sk_plan(cfg, B, H, W, N, C, ksplit)
+    return smax <= 4 and (cfg not in WINO_SK_V3 or iters <= C // 16)
+
+
 def wino_blocks(cfg: int, B: int, H: int, W: int, N: int) -> int:
     """Blocks per split of a Winograd launch (tile groups x channel groups): the fused split-K
     arrival counters it needs."""
@@ -468,14 +478,15 @@ WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85:
                  150: (8, 2), 151: (8, 2), 152: (8, 2), 153: (8, 2),    # 118 / 119 with the next chunk's
                                                               # DMA front-loaded, 2 (150-151) / 3 pieces a group
                  154: (8, 2), 155: (8, 2), 156: (8, 2),       # 118 + stagger / priority / both for waves 4-7
+                 157: (8, 2), 158: (8, 2),                    # stream-K twins of 118 / 155
                  140: (4, 1), 141: (8, 1)}                    # persistent: two blocks per CU walk the units as
                                                               # one chunk stream (whole K only)
 WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114, 116, 117,
                           118, 119, 130, 131, 132, 140, 141, 150, 151, 152, 153,
-                          154, 155, 156))
+                          154, 155, 156, 157, 158))
 WINO_PU_CFGS = frozenset((140, 141))
 # stream-K Winograd configs: ksplit <= -100 means (-ksplit - 100) x 256 blocks over the (unit, chunk) space
-WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114))
+WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114, 157, 158))
 WINO_SK_BASE = -100
 
 

@@ -519,7 +519,11 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   using S = WinoV2Shape<NW, FN>;
   constexpr int PMAX = S::PMAX, PIECES = S::PIECES, PPW = S::PPW, SLOT = S::SLOT;
   char* ring = smem;
-  const int tid = threadIdx.x, lane = tid & 63;
+  // opaque thread index: in the stream-K loop (several units per block) everything derived from the
+  // lane would otherwise be hoisted out of the loop and held beside the accumulators (128 VGPRs spilled)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
   char* pimg = smem + 2 * SLOT + wave * PMAX * 1024;
@@ -886,6 +890,34 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wi
     wino_v2_unit<NW, FN, SW, EP, PL>(p, smem, tg, cg, kc0, min(KC, kc0 + kper), z, p.ksplit, tg + gridDim.x * cg);
     return;
   }
+  if constexpr (PL != 0) {
+    // stream-K over the v3 chunk body: the host keeps sk_iters <= KC, so a block's range meets at most
+    // two units; the two calls are straight-line code (a loop around the inlined unit kept values of
+    // one unit live through the next one's MFMAs: 128 VGPRs spilled)
+    const int gx = (p.T + 16 * NW - 1) / (16 * NW);
+    const int iters = p.sk_iters;
+    const int it0 = blockIdx.x * iters;
+    const int it_end = min(gx * (p.N / (16 * FN)) * KC, it0 + iters);
+    auto seg = [&](int it) {
+      const int u = it / KC;
+      const int kb = it - u * KC;
+      const int ke = min(KC, kb + (it_end - it));
+      int zs = 0, ns = 1;
+      if (kb != 0 || ke != KC) {
+        const int g_first = (u * KC) / iters, g_last = ((u + 1) * KC - 1) / iters;
+        zs = blockIdx.x - g_first;
+        ns = g_last - g_first + 1;
+      }
+      wino_v2_unit<NW, FN, SW, EP, PL>(p, smem, u % gx, u / gx, kb, ke, zs, ns, u);
+      return it + (ke - kb);
+    };
+    const int it1 = seg(it0);
+    if (it1 < it_end) {
+      __syncthreads();                               // the first unit's ring / flag / images are dead
+      seg(it1);
+    }
+    return;
+  }
   const bool sk = SK;
   const int gx = (p.T + 16 * NW - 1) / (16 * NW);
   const int iters = p.sk_iters;
@@ -1135,6 +1167,7 @@ hipError_t launch_wino_v2(const WinoF32Params& p, hipStream_t s) {
     int G, iters, smax;
     conv_wino_sk_plan(grid.x * grid.y, p.C / 16, p.sk_mult, &G, &iters, &smax);
     if (iters != p.sk_iters || smax > 4 || !p.counters || !p.ws) return hipErrorInvalidValue;
+    if (PL != 0 && iters > p.C / 16) return hipErrorInvalidValue;   // v3 stream-K: <= 2 units per block
     grid = dim3(G, 1, 1);
   }
   hipLaunchKernelGGL((conv_wino_f32_v2_kernel<NW, FN, SW, EP, SK, PL, XM>), grid, block, 0, s, p);
@@ -1201,7 +1234,9 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(153, 8, 2, true, true, false, 4, true)   \
   X(154, 8, 2, true, true, false, 10, false) \
   X(155, 8, 2, true, true, false, 18, false) \
-  X(156, 8, 2, true, true, false, 26, false)
+  X(156, 8, 2, true, true, false, 26, false) \
+  X(157, 8, 2, true, true, true, 2, false)   \
+  X(158, 8, 2, true, true, true, 18, false)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

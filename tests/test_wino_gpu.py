@@ -49,7 +49,7 @@ def test_wino_f32_matches_fp64(shape, ksplit):
             continue
         if cfg in C.WINO_PU_CFGS and ksplit != 1:
             continue
-        if ksplit <= C.WINO_SK_BASE and C.wino_sk_plan(cfg, B, H, W, Cout, Cin, ksplit)[2] > 4:
+        if ksplit <= C.WINO_SK_BASE and not C.wino_sk_feasible(cfg, B, H, W, Cout, Cin, ksplit):
             continue
         ctr = None
         if ksplit < 0:
@@ -66,6 +66,32 @@ def test_wino_f32_matches_fp64(shape, ksplit):
     if ran == 0 and ksplit <= C.WINO_SK_BASE:
         pytest.skip("no stream-K config maps this shape")
     assert ran > 0
+
+
+def test_wino_f32_stream_k_v3_blocks_meet_two_units():
+    """Stream-K over the v3 chunk body (cfgs 157 / 158): with C = 80 (5 chunks) and 2 chunks per block,
+    blocks straddle unit boundaries, so both straight-line segments and the 3-partial fixup run."""
+    B, H, W, Cin, Cout = 20, 28, 28, 80, 64
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((B, H, W, Cin)).astype(np.float32)
+    kern = (rng.standard_normal((3, 3, Cin, Cout)) / np.sqrt(9 * Cin)).astype(np.float32)
+    bias = rng.standard_normal(Cout).astype(np.float32)
+    want = _ref_conv(x, kern, bias, 1, ((1, 1), (1, 1)), None, 1)
+    pc = C.pack_conv_f32(kern, bias, 1, ((1, 1), (1, 1)), "cuda")
+    xd = torch.from_numpy(x).cuda()
+    out = torch.empty((B, H, W, Cout), dtype=torch.float32, device="cuda")
+    for cfg in sorted(C.WINO_SK_V3):
+        grid, iters, smax = C.wino_sk_plan(cfg, B, H, W, Cout, Cin, -101)
+        assert iters == 2 and (Cin // 16) % iters and C.wino_sk_feasible(cfg, B, H, W, Cout, Cin, -101)
+        ctr = torch.zeros(C.wino_blocks(cfg, B, H, W, Cout), dtype=torch.int32, device="cuda")
+        ws = torch.empty(C.workspace_elems_f32(B * H * W, Cout, pc.Kpad, cfg, -101), device="cuda")
+        for rep in range(2):
+            out.fill_(float("nan"))
+            C.conv_forward_f32(xd, pc, out, relu=1, cfg=cfg, ksplit=-101, workspace=ws, counters=ctr)
+            got = out.cpu().numpy()
+            err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
+            assert np.isfinite(got).all() and err < 2e-5, f"cfg {cfg} rep {rep}: rel err {err}"
+        assert int(ctr.abs().sum()) == 0
 
 
 def test_wino_f32_fused_split_matches_slab_split():
