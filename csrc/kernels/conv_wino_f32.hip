@@ -127,7 +127,7 @@ __device__ __forceinline__ void wino_fixup(const WinoF32Params& p, const float (
 template <int FN, int ABL>
 __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x4 (&acc)[16][FN], int tw0, int r,
                                               int q, int nf0, int* flag, int zs, int ns, int ctr_idx,
-                                              char* stage = nullptr) {
+                                              char* stage = nullptr, unsigned long long* dbg = nullptr) {
   // zs / ns: this partial's slab index / the partials of its output block (ns == 1: whole K);
   // fused fixup when the host passed arrival counters, else slab ws[zs] for splitk_reduce_f32
   const bool split = ns > 1;
@@ -162,6 +162,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: LDS is in order per wave
+    if (dbg) dbg[8] = __builtin_amdgcn_s_memtime();      // staged (tools/wino_timeline.py)
     // opaque copies: keep the store-phase index math from being hoisted above the K loop, where its
     // registers would be live beside the accumulators (the FN = 2 kernels sit at 250+ VGPRs)
     int lane = q * 16 + r;
@@ -205,9 +206,17 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
       f32x4 ov[4 * FN];
 #pragma unroll
       for (int it = 0; it < 4 * FN; ++it) ov[it] = own(it);
+      if (dbg) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dbg[9] = __builtin_amdgcn_s_memtime();           // offsets computed, staged values read back
+      }
 #pragma unroll
       for (int it = 0; it < 4 * FN; ++it)
         if (oo[it] >= 0) finish(it, ov[it], rvs[it]);
+      if (dbg) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        dbg[10] = __builtin_amdgcn_s_memtime();          // stores done
+      }
       return;
     }
     // fused split-K: every split publishes its partial outputs as 16-byte sc1 stores to its slab; the
@@ -624,10 +633,11 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   };
   if constexpr (PL != 0) {
     constexpr int PLM = PL & 7;                      // chunk body; PL & 8 / 16: stagger / priority (below)
-    // phase stamps (tools/wino_timeline.py): shader clock at unit start / first chunk landed / loop end /
-    // epilogue end, the 100 MHz wall clock at start and end, HW_ID and XCC_ID; thread 0 only, vector stores
+    // phase stamps (tools/wino_timeline.py), 16 words per block: shader clock at unit start / first chunk
+    // landed / loop end / epilogue end, the 100 MHz wall clock at start and end, HW_ID and XCC_ID, and
+    // inside a whole-K epilogue: staged / read back / stores done; thread 0 only, vector stores
     unsigned long long* const dbg =
-        p.dbg ? p.dbg + 8 * (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
+        p.dbg ? p.dbg + 16 * (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) : nullptr;
     const bool stamp = dbg && threadIdx.x == 0;
     if (stamp) {
       dbg[0] = __builtin_amdgcn_s_memtime();
@@ -776,7 +786,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (stamp) dbg[2] = __builtin_amdgcn_s_memtime();
-    wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx, pimg);
+    wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx, pimg, stamp ? dbg : nullptr);
     if (stamp) {
       dbg[3] = __builtin_amdgcn_s_memtime();
       dbg[5] = __builtin_amdgcn_s_memrealtime();

@@ -158,7 +158,7 @@ struct WinoF32Params {
                       // before the launch, left zero after it (no splitk_reduce_f32 launch)
   int sk_iters;       // > 0: stream-K, (unit, chunk) iterations per block (conv_wino_sk_plan), ksplit 1
   int sk_mult;        // stream-K grid: about sk_mult x 256 blocks
-  unsigned long long* dbg;   // measurement only (tools/wino_timeline.py): 8 words per block, else null
+  unsigned long long* dbg;   // measurement only (tools/wino_timeline.py): 16 words per block, else null
 };
 // tools/wino_timeline.py: v3 Winograd launches (PL != 0) stamp their phases into buf while it is set
 void wino_set_debug(unsigned long long* buf);

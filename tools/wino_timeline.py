@@ -48,7 +48,9 @@ def main():
     nw, fn = C.WINO_F32_CFGS[a.cfg]
     T = B * ((H + 1) // 2) * ((W + 1) // 2)
     nblocks = math.ceil(T / (16 * nw)) * (N // (16 * fn)) * max(1, abs(a.ks))
-    dbg = torch.zeros(nblocks * 8, dtype=torch.int64, device=dev)
+    if a.ks <= C.WINO_SK_BASE:                    # stream-K: a 1-D grid; a block's second unit overwrites its stamps
+        nblocks = C.wino_sk_plan(a.cfg, B, H, W, N, Cin, a.ks)[0]
+    dbg = torch.zeros(nblocks * 16, dtype=torch.int64, device=dev)
 
     def run():
         C.conv_forward_f32(x, pc, out, relu=1, cfg=a.cfg, ksplit=a.ks, workspace=ws, counters=ctr)
@@ -66,7 +68,7 @@ def main():
     finally:
         kernels().wino_set_debug(0)
     launch_us = e0.elapsed_time(e1) * 1e3
-    d = dbg.cpu().numpy().astype(np.int64).reshape(nblocks, 8)
+    d = dbg.cpu().numpy().astype(np.int64).reshape(nblocks, 16)
     if (d[:, 0] == 0).any():
         raise SystemExit(f"{int((d[:, 0] == 0).sum())} of {nblocks} blocks left no stamp (cfg without PL?)")
     wall0, wall1 = d[:, 4], d[:, 5]
@@ -88,6 +90,10 @@ def main():
         "prologue_us": [round(pct(pro, q), 2) for q in (10, 50, 90)],
         "loop_us": [round(pct(loop, q), 2) for q in (10, 50, 90)],
         "epilogue_us": [round(pct(epi, q), 2) for q in (10, 50, 90)],
+        **({"epi_stage_us": round(float(np.median(us(d[:, 8] - d[:, 2]))), 2),
+            "epi_readback_us": round(float(np.median(us(d[:, 9] - d[:, 8]))), 2),
+            "epi_stores_us": round(float(np.median(us(d[:, 10] - d[:, 9]))), 2),
+            "epi_tail_us": round(float(np.median(us(d[:, 3] - d[:, 10]))), 2)} if (d[:, 10] != 0).all() else {}),
         "start_us": [round(pct(start, q), 2) for q in (0, 50, 90, 100)],
         "end_us": [round(pct(end, q), 2) for q in (0, 10, 50, 90, 100)],
         "cu_busy_fraction": round(busy / (256 * span), 3),
