@@ -139,6 +139,16 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
     // the float4.  Runs: (tile of the wave 0..15, pixel 0..3) x 16 FN channels.
     constexpr int RUN = 16 * FN;                        // floats per (tile, pixel) run
     float* st = (float*)stage;
+    // FN = 2: the float4 column of a run is XORed with 4 on odd lane groups (runs 16..31, 48..63), so a
+    // staging write's four lane groups, which land on rows 16 apart (same banks), split over both halves
+    // of the 32 banks: 2-way instead of 4-way conflicts; the read-back applies the same XOR per run
+    // the bias quad of this lane ((16 q + r) % (4 FN) = r % (4 FN)), loaded first so its L2 round trip
+    // runs under the staging; the opaque index keeps the load below the K loop
+    int bidx = nf0 * 16 + (r % (4 * FN)) * 4;
+    asm volatile("" : "+v"(bidx));
+    const f32x4 bsv = *(const f32x4*)(p.bias + bidx);
+    const int swq = FN == 2 ? 4 * (q & 1) : 0;
+    auto swr = [&](int run) { return FN == 2 ? 4 * ((run >> 4) & 1) : 0; };
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int tl = 4 * q + i;
@@ -155,10 +165,11 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
           w0[b] = m[0][b] + m[1][b] + m[2][b];
           w1[b] = m[1][b] - m[2][b] - m[3][b];
         }
-        st[(tl * 4 + 0) * RUN + j * 16 + r] = w0[0] + w0[1] + w0[2];
-        st[(tl * 4 + 1) * RUN + j * 16 + r] = w0[1] - w0[2] - w0[3];
-        st[(tl * 4 + 2) * RUN + j * 16 + r] = w1[0] + w1[1] + w1[2];
-        st[(tl * 4 + 3) * RUN + j * 16 + r] = w1[1] - w1[2] - w1[3];
+        const int cw = ((((j * 16 + r) >> 2) ^ swq) << 2) | (r & 3);
+        st[(tl * 4 + 0) * RUN + cw] = w0[0] + w0[1] + w0[2];
+        st[(tl * 4 + 1) * RUN + cw] = w0[1] - w0[2] - w0[3];
+        st[(tl * 4 + 2) * RUN + cw] = w1[0] + w1[1] + w1[2];
+        st[(tl * 4 + 3) * RUN + cw] = w1[1] - w1[2] - w1[3];
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: LDS is in order per wave
@@ -183,12 +194,12 @@ __device__ __forceinline__ void wino_epilogue(const WinoF32Params& p, const f32x
     }
     auto own = [&](int it) -> f32x4 {
       const int g = it * 64 + lane;
-      return *(const f32x4*)(st + (g / (4 * FN)) * RUN + (g % (4 * FN)) * 4);
+      const int run = g / (4 * FN);
+      return *(const f32x4*)(st + run * RUN + ((g % (4 * FN)) ^ swr(run)) * 4);
     };
     // a lane's channel quad is the same for every float4 it owns (64 runs per pass, 4 FN quads per run),
-    // so the bias is one load; the LDS reads and residual loads of all passes issue before the first
-    // store -- inside the per-pass `oo >= 0` branches each would wait out its own latency in turn
-    const f32x4 bsv = *(const f32x4*)(p.bias + nf0 * 16 + (lane % (4 * FN)) * 4);
+    // so the bias is one load (above); the LDS reads and residual loads of all passes issue before the
+    // first store -- inside the per-pass `oo >= 0` branches each would wait out its own latency in turn
     auto finish = [&](int it, f32x4 v, f32x4 rv) {
       const int o = oo[it];
       v += bsv;
