@@ -544,6 +544,11 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
+  // the dummy DMA source's address, materialised once: referenced inside the chunk loop, the symbol is
+  // re-loaded from the GOT by an s_load there every chunk, and a scalar load in flight (it returns out of
+  // order) turns every LDS wait of the loop into lgkmcnt(0) -- no group could wait on just its older reads
+  const float* wzero = g_wino_zero;
+  asm volatile("" : "+s"(wzero));
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
   char* pimg = smem + 2 * SLOT + wave * PMAX * 1024;
@@ -597,7 +602,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
   auto issue_x = [&](int kc) {
 #pragma unroll
     for (int i = 0; i < PMAX; ++i) {
-      const float* src = ((src_ok >> i) & 1u) ? p.x + src_off[i] + kc * 16 : g_wino_zero;
+      const float* src = ((src_ok >> i) & 1u) ? p.x + src_off[i] + kc * 16 : wzero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
     }
   };
@@ -703,7 +708,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         if (wave >= NW / 2) __builtin_amdgcn_s_sleep(2);
       }
       const bool more = kc + 1 < kc1;
-      const float* wsrc = more ? ub + (size_t)(kc + 1) * uchunk : g_wino_zero;
+      const float* wsrc = more ? ub + (size_t)(kc + 1) * uchunk : wzero;
       const int wstep = more ? 256 : 0;              // the dummy piece: one 1 KiB buffer for every piece
       char* wdst = ring + (slot ^ 1) * SLOT;
       // B^T d: rows, in place
@@ -719,10 +724,17 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       constexpr bool PFR = PLM == 1;                  // fragments of group g+1 read ahead of g's MFMAs
       // DMA pieces per group: PL >= 3 front-loads the next chunk's pieces (PL - 1 per group), so the
       // last one has most of the chunk to land instead of the last two groups (cfgs 150-153)
-      constexpr int DPG = PLM >= 3 ? PLM - 1 : 1;
+      constexpr int DPG = (PLM == 3 || PLM == 4) ? PLM - 1 : 1;
       constexpr int NPG = (PPW + PMAX + DPG - 1) / DPG;   // groups that issue DMA
       constexpr int NB = !PFR ? 1 : FN >= 2 ? 2 : 4; // FN = 1 pairs groups: g-1's fragments must survive g's read
       f32x4 u[NB][FN];
+      // PLM 5 (FN = 2, cfgs 160/161): half prefetch -- the next group's j = 0 fragment is read during this
+      // group, its j = 1 fragment at the group's start behind the four j = 0 MFMAs: 4 more VGPRs instead
+      // of the 8 of a full prefetch (which spills at FN = 2), and no group waits on its first read
+      constexpr bool HP = PLM == 5;
+      static_assert(!HP || FN == 2, "half prefetch is for FN = 2");
+      f32x4 un = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (HP) un = *(const f32x4*)(sl + ((0 * 16 + 0) * 64 + lane) * 16);
       if constexpr (PFR) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + 0) * 64 + lane) * 16);
@@ -737,7 +749,12 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
           d[pa][2] = e2 - e1;
           d[pa][3] = e1 - e3;
         }
-        if constexpr (PFR) {
+        f32x4 u0h = {0.f, 0.f, 0.f, 0.f}, u1h = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (HP) {
+          u0h = un;
+          u1h = *(const f32x4*)(sl + ((1 * 16 + g) * 64 + lane) * 16);
+          if (g < 15) un = *(const f32x4*)(sl + ((0 * 16 + g + 1) * 64 + lane) * 16);
+        } else if constexpr (PFR) {
           if (g < 15) {
 #pragma unroll
             for (int j = 0; j < FN; ++j)
@@ -756,15 +773,23 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
                                                (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
           } else if (pi - PPW < PMAX) {              // next chunk's input piece
             const int i = pi - PPW;
-            const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : g_wino_zero;
+            const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : wzero;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
           }
         }
         // fence: the next fragments' reads and the DMA piece issue above this group's MFMAs (left to
         // itself the scheduler sinks each prefetch next to its use, at ~250 VGPRs, and waits lgkmcnt(0))
-        if constexpr (PFR) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PFR || HP) __builtin_amdgcn_sched_barrier(0);
         const f32x4 vv = d[pa][pb];
-        if constexpr (!PFR) {
+        if constexpr (HP) {
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss)
+            acc[g][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u0h[ss], acc[g][0], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);         // the prefetched half first: nothing waits on u1h yet
+#pragma unroll
+          for (int ss = 0; ss < 4; ++ss)
+            acc[g][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u1h[ss], acc[g][1], 0, 0, 0);
+        } else if constexpr (!PFR) {
 #pragma unroll
           for (int ss = 0; ss < 4; ++ss)
 #pragma unroll
@@ -1257,7 +1282,9 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(155, 8, 2, true, true, false, 18, false) \
   X(156, 8, 2, true, true, false, 26, false) \
   X(157, 8, 2, true, true, true, 2, false)   \
-  X(158, 8, 2, true, true, true, 18, false)
+  X(158, 8, 2, true, true, true, 18, false)  \
+  X(160, 8, 2, true, true, false, 5, false)  \
+  X(161, 8, 2, true, true, false, 21, false)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)
