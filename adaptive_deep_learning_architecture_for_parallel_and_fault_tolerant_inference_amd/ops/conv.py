@@ -525,10 +525,12 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 # with K in {64, 128, 256, 512} and N a multiple of the slice (FPW x 128 channels), ksplit 1
 # 122 / 123: the streaming variant (no LDS, no block barrier; bm codes 1 / 2: two waves per SIMD / the
 # widest channel slice per wave)
-PW_F32_CFGS = {120: 16, 121: 32, 122: 1, 123: 2}
+# 124: 123 with a 16-K-step activation ring (bm code 3; K in 256 / 512 / 1024)
+PW_F32_CFGS = {120: 16, 121: 32, 122: 1, 123: 2, 124: 3}
 PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1, 1024: 1}     # 16-channel fragments per wave
 PW_F32_KG = {1024: 2}                                       # K groups of waves (partials meet in LDS)
-PW_F32_BMS = {64: (1, 2, 16, 32), 128: (1, 2, 16, 32), 256: (1, 2, 16, 32), 512: (1, 2, 16, 32), 1024: (1, 2, 16)}
+PW_F32_BMS = {64: (1, 2, 16, 32), 128: (1, 2, 16, 32), 256: (1, 2, 3, 16, 32), 512: (1, 2, 3, 16, 32),
+              1024: (1, 2, 3, 16)}
 
 
 def pw_f32_slice(K: int) -> int:

@@ -297,6 +297,13 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
   X(512, 2, 8, 1)               \
   X(1024, 1, 8, 1)
 
+// deep-ring twins of the one-wave-per-SIMD instances (bm code 3, cfg 124): with a single wave per SIMD
+// nothing covers a late activation load but the ring, and these have the VGPRs for 16 K-steps of lead
+#define ADAPT_PW_STREAM_DEEP_CFGS(X) \
+  X(256, 4, 16, 1)                  \
+  X(512, 2, 16, 1)                  \
+  X(1024, 1, 16, 1)
+
 static int pw_stream_pick(int K, int N, int n_split, int wide) {
   // wide (bm code 2): the largest built FPW; else the one that keeps two waves per SIMD
   int best = 0;
@@ -337,17 +344,40 @@ static int pw_f32_pick(int K, int N, int n_split, int bm) {
   }
   return 0;
 }
+static int pw_stream_deep_pick(int K, int N, int n_split) {
+  int best = 0;
+#define X(K_, F_, D_, O_) \
+  if (K == K_ && N % (F_ * 16) == 0 && n_split % (F_ * 16) == 0) best = best > F_ ? best : F_;
+  ADAPT_PW_STREAM_DEEP_CFGS(X)
+#undef X
+  return best;
+}
 int pw_f32_fpw(int K, int N, int n_split, int bm) {
+  if (bm == 3) return pw_stream_deep_pick(K, N, n_split);
   return bm <= 2 ? pw_stream_pick(K, N, n_split, bm == 2) : pw_f32_pick(K, N, n_split, bm);
 }
 
 bool pw_f32_supported(int K, int N, int bm) { return pw_f32_fpw(K, N, 0, bm) > 0; }
 
-static hipError_t pw_stream_f32_forward(const PwF32Params& p, int wide, hipStream_t s) {
-  const int fpw = pw_stream_pick(p.K, p.N, p.n_split, wide);
+static hipError_t pw_stream_f32_forward(const PwF32Params& p, int mode, hipStream_t s) {
+  const int fpw = mode == 3 ? pw_stream_deep_pick(p.K, p.N, p.n_split) : pw_stream_pick(p.K, p.N, p.n_split, mode == 2);
   if (!fpw) return hipErrorInvalidValue;
   const int ncg = p.N / (16 * fpw);
   const int ntiles = (p.M + 15) / 16;
+  if (mode == 3) {
+#define X(K_, F_, D_, O_)                                                                                  \
+  if (p.K == K_ && fpw == F_) {                                                                            \
+    int nslots = (1024 * O_) / ncg;                                                                        \
+    if (nslots < 1) nslots = 1;                                                                            \
+    if (nslots > ntiles) nslots = ntiles;                                                                  \
+    const int blocks = (ncg * nslots + 3) / 4;                                                             \
+    hipLaunchKernelGGL((pw_stream_f32_kernel<K_, F_, D_, O_>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots); \
+    return hipGetLastError();                                                                              \
+  }
+    ADAPT_PW_STREAM_DEEP_CFGS(X)
+#undef X
+    return hipErrorInvalidValue;
+  }
 #define X(K_, F_, D_, O_)                                                                                  \
   if (p.K == K_ && fpw == F_) {                                                                            \
     int nslots = (1024 * O_) / ncg;                   /* ~O_ waves per SIMD over the chip */               \
@@ -363,11 +393,11 @@ static hipError_t pw_stream_f32_forward(const PwF32Params& p, int wide, hipStrea
 }
 
 hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s) {
-  if (bm == 1 || bm == 2) {
+  if (bm >= 1 && bm <= 3) {
     if (p.M < 1 || p.stride < 1 || (p.n_split && (!p.out2 || p.res)) || p.M != p.B * p.OH * p.OW ||
         (p.stride == 1 && (p.H != p.OH || p.W != p.OW)))
       return hipErrorInvalidValue;
-    return pw_stream_f32_forward(p, bm == 2, s);
+    return pw_stream_f32_forward(p, bm, s);
   }
   const int fpw = pw_f32_pick(p.K, p.N, p.n_split, bm);
   if (!fpw || p.M < 1 || p.stride < 1 || (p.n_split && (!p.out2 || p.res)) ||
