@@ -55,6 +55,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_ws_rsrc(const float* base
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
 }
 
+// LDS-DMA of one 1 KiB piece (16 B per lane, lane-linear at lds_dst) issued from inline asm, so the
+// compiler does not see it.  Its wait-count model counts an LDS DMA as an LDS access as well as a vector
+// memory access; with one in flight no LDS wait can be partial and every wait in the chunk loop is
+// lgkmcnt(0) -- a group waits on the reads it issued for later groups too.  Hidden, the DMA needs the
+// explicit vmcnt waits the v3 body already has (before the patch reads, before each chunk barrier).
+// M0 (the LDS base of the DMA) is set here; nothing else in these kernels reads M0.
+__device__ __forceinline__ void wino_dma16(const void* src, void* lds_dst) {
+  const unsigned m = (unsigned)(uintptr_t)lds_dst;
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m) : "memory");
+}
+
 // fused split-K, last split of a block: out = act(sum_z slab_z + bias (+ res)) in split order, with
 // this split's own partials from registers; all (S - 1) x 4 x FN x 4 slab loads issue before the sum
 template <int FN, int S>
@@ -692,9 +703,22 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
     if constexpr ((PL & 16) != 0) {
       if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     }
+    constexpr bool OD = (PL & 32) != 0;             // DMA through wino_dma16 (cfgs 164-167)
     if (kc0 < kc1) {
-      issue_w(kc0, 0);
-      issue_x(kc0);
+      if constexpr (OD) {
+        const float* src = ub + (size_t)kc0 * uchunk;
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+          const int pc = wave * PPW + i;
+          if (PIECES % NW == 0 || pc < PIECES) wino_dma16(src + pc * 256 + lane * 4, ring + pc * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < PMAX; ++i)
+          wino_dma16(((src_ok >> i) & 1u) ? p.x + src_off[i] + kc0 * 16 : wzero, pimg + i * 1024);
+      } else {
+        issue_w(kc0, 0);
+        issue_x(kc0);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       read_patch_pl();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -724,7 +748,11 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       constexpr bool PFR = PLM == 1;                  // fragments of group g+1 read ahead of g's MFMAs
       // DMA pieces per group: PL >= 3 front-loads the next chunk's pieces (PL - 1 per group), so the
       // last one has most of the chunk to land instead of the last two groups (cfgs 150-153)
-      constexpr int DPG = (PLM == 3 || PLM == 4) ? PLM - 1 : 1;
+      // PLM 6 (cfgs 162/163): the DMA front-loaded 2 per group (done by group 6) and the next chunk's
+      // patch rows 0-2 read during groups 12-15, into the registers of this chunk's rows 0-2 (dead after
+      // group 11): the chunk end waits only on row 3's four reads instead of the DMA tail plus 16 reads
+      constexpr bool EPR = PLM == 6;
+      constexpr int DPG = (PLM == 3 || PLM == 4) ? PLM - 1 : EPR ? 2 : 1;
       constexpr int NPG = (PPW + PMAX + DPG - 1) / DPG;   // groups that issue DMA
       constexpr int NB = !PFR ? 1 : FN >= 2 ? 2 : 4; // FN = 1 pairs groups: g-1's fragments must survive g's read
       f32x4 u[NB][FN];
@@ -763,18 +791,33 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         } else {
 #pragma unroll
           for (int j = 0; j < FN; ++j) u[0][j] = *(const f32x4*)(sl + ((j * 16 + g) * 64 + lane) * 16);
+          if constexpr (EPR) {
+            // next patch rows 0-2, three reads a group in groups 12-15, issued right after the group's own
+            // fragment reads so the group waits on its fragments only (LDS returns in order)
+            if (g >= 12) {
+              if (g == 12) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the input DMA (done by group 6)
+#pragma unroll
+              for (int rr = 3 * (g - 12); rr < 3 * (g - 12) + 3; ++rr) {
+                const int dy = rr >> 2, dx = rr & 3;
+                d[dy][dx] = *(const f32x4*)(pimg + wino_sw(ps0 + dy * pw * 4 + dx * 4) * 16);
+              }
+            }
+          }
         }
 #pragma unroll
         for (int pi = g * DPG; pi < (g + 1) * DPG; ++pi) {
           if (pi < PPW) {                            // next chunk's weight piece pi of this wave
             const int pc = wave * PPW + pi;
-            if (PIECES % NW == 0 || pc < PIECES)
-              __builtin_amdgcn_global_load_lds((const void*)(wsrc + pc * wstep + lane * 4),
-                                               (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
+            if (PIECES % NW == 0 || pc < PIECES) {
+              if constexpr (OD) wino_dma16(wsrc + pc * wstep + lane * 4, wdst + pc * 1024);
+              else __builtin_amdgcn_global_load_lds((const void*)(wsrc + pc * wstep + lane * 4),
+                                                    (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
+            }
           } else if (pi - PPW < PMAX) {              // next chunk's input piece
             const int i = pi - PPW;
             const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : wzero;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+            if constexpr (OD) wino_dma16(src, pimg + i * 1024);
+            else __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
           }
         }
         // fence: the next fragments' reads and the DMA piece issue above this group's MFMAs (left to
@@ -795,8 +838,9 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 #pragma unroll
             for (int j = 0; j < FN; ++j)
               acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[ss], u[0][j][ss], acc[g][j], 0, 0, 0);
-          // this group: its fragment reads, its DMA piece, then its MFMAs
-          __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+          // this group: its fragment reads (+ EPR's patch reads), its DMA piece, then its MFMAs
+          if (EPR && g >= 12) __builtin_amdgcn_sched_group_barrier(0x100, FN + 3, 0);
+          else __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
           if (g < NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, DPG, 0);
           else if (g == NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, PPW + PMAX - (NPG - 1) * DPG, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 4 * FN, 0);
@@ -818,7 +862,12 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       }
       // the next chunk's patch (its DMA went out during this chunk's groups)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      read_patch_pl();
+      if constexpr (PLM == 6) {
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx) d[3][dx] = *(const f32x4*)(pimg + wino_sw(ps0 + 3 * pw * 4 + dx * 4) * 16);
+      } else {
+        read_patch_pl();
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (stamp) dbg[2] = __builtin_amdgcn_s_memtime();
@@ -1284,7 +1333,13 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(157, 8, 2, true, true, true, 2, false)   \
   X(158, 8, 2, true, true, true, 18, false)  \
   X(160, 8, 2, true, true, false, 5, false)  \
-  X(161, 8, 2, true, true, false, 21, false)
+  X(161, 8, 2, true, true, false, 21, false) \
+  X(162, 8, 2, true, true, false, 6, false)  \
+  X(163, 8, 2, true, true, false, 22, false) \
+  X(164, 8, 2, true, true, false, 38, false) \
+  X(165, 8, 2, true, true, false, 54, false) \
+  X(166, 8, 1, true, true, false, 33, false) \
+  X(167, 4, 1, true, true, false, 33, false)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

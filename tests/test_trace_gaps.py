@@ -32,7 +32,7 @@ def _write_trace(path, steps=5, kernels=30, dur_ns=10_000, gap_ns=2_000, step_ga
 def test_trace_gaps_steps_and_gap_share(tmp_path):
     p = tmp_path / "run_kernel_trace.csv"
     _write_trace(p)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_gaps.py"), str(p)],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_gaps.py"), str(p), "--step-gap", "50"],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     rec = json.loads(r.stdout.strip().splitlines()[-1])

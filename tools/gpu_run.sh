@@ -33,6 +33,8 @@
 #   skp       stream-K Winograd probe (tools/debug/sk_probe.py) + the Winograd tests + v3 stream-K timings
 #   wino7     Winograd numerics + isolated timings of 118 / 155 vs the half-prefetch cfgs 160 / 161
 #   pw5       pointwise numerics + isolated timings incl. the deep-ring streaming cfg 124
+#   wino8     Winograd numerics + isolated timings: 118 / 155 / 116 / 117 vs early patch read (162/163)
+#             and the DMA hidden from the wait model (164-167)
 #   pmcstem   two PMC passes over the fp32 stem (tools/stem_bench.py)
 #   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
@@ -102,6 +104,8 @@ for p in "${P[@]}"; do
               for rep in a b; do steps+=("300|$out/wino7_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 118,155,160,161 --ks 1,-2,-4"); done ;;
     pw5)      steps+=("200|$out/pytest_pw|python -u -m pytest tests/test_pw_f32_gpu.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/pw5_bench|python -u tools/conv_bench_f32.py --only 18,20,38,120,122,123,124 --ks 1,-1,-2 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,28,28,512,1280,1,2,0,0 --shape 32,14,14,1024,2560,1,2,0,0") ;;
+    wino8)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
+              for rep in a b; do steps+=("300|$out/wino8_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 116,117,118,155,162,163,164,165,166,167 --ks 1,-2,-4"); done ;;
     pmcstem)  steps+=("120|$out/pmcstem1|cd /tmp && rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/$out/pmcstem/g1 -o run -- python3 \$GRAFT_REPO_ROOT/tools/stem_bench.py --iters 20")
               steps+=("120|$out/pmcstem2|cd /tmp && rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/$out/pmcstem/g2 -o run -- python3 \$GRAFT_REPO_ROOT/tools/stem_bench.py --iters 20") ;;
     *) echo "unknown preset $p"; exit 2 ;;
