@@ -558,7 +558,7 @@ class SliceExecutor:
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
             for cfg in list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.PW_F32_CFGS):
-                if not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc):
+                if not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc) or cfg in conv_ops.WINO_MEASURE_CFGS:
                     continue
                 if cfg in conv_ops.PW_F32_CFGS:            # persistent pointwise: whole K, one launch
                     tiles, kts, sks = 0, 1, ()

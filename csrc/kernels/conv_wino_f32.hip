@@ -726,8 +726,14 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
     if (stamp) dbg[1] = __builtin_amdgcn_s_memtime();
     for (int kc = kc0; kc < kc1; ++kc) {
       const int slot = (kc - kc0) & 1;
+      // PL & 64 (measurement-only cfg 170): thread 0 stamps chunk kc0 + 2: before / after its barrier,
+      // at group 8, after group 15's MFMAs issue, after the next patch has been read (words 11-15)
+      constexpr bool TM = (PL & 64) != 0;
+      const bool tmc = TM && stamp && kc == kc0 + 2;
+      if (tmc) dbg[11] = __builtin_amdgcn_s_memtime();
       __builtin_amdgcn_s_barrier();                  // every wave's weight pieces of chunk kc are in
       asm volatile("" ::: "memory");
+      if (tmc) dbg[12] = __builtin_amdgcn_s_memtime();
       if constexpr ((PL & 8) != 0) {
         if (wave >= NW / 2) __builtin_amdgcn_s_sleep(2);
       }
@@ -770,6 +776,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int pa = g >> 2, pb = g & 3;
+        if (TM && g == 8 && tmc) dbg[13] = __builtin_amdgcn_s_memtime();
         if (pb == 0) {                               // (B^T d B)[pa][*], in place over row pa
           const f32x4 e0 = d[pa][0], e1 = d[pa][1], e2 = d[pa][2], e3 = d[pa][3];
           d[pa][0] = e0 - e2;
@@ -860,6 +867,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
           }
         }
       }
+      if (tmc) dbg[14] = __builtin_amdgcn_s_memtime();
       // the next chunk's patch (its DMA went out during this chunk's groups)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (PLM == 6) {
@@ -869,6 +877,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         read_patch_pl();
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tmc) dbg[15] = __builtin_amdgcn_s_memtime();
     }
     if (stamp) dbg[2] = __builtin_amdgcn_s_memtime();
     wino_epilogue<FN, 0>(p, acc, tw0, r, q, nf0, (int*)smem, zs, ns, ctr_idx, pimg, stamp ? dbg : nullptr);
@@ -1339,7 +1348,8 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(164, 8, 2, true, true, false, 38, false) \
   X(165, 8, 2, true, true, false, 54, false) \
   X(166, 8, 1, true, true, false, 33, false) \
-  X(167, 4, 1, true, true, false, 33, false)
+  X(167, 4, 1, true, true, false, 33, false) \
+  X(170, 8, 2, true, true, false, 66, false)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

@@ -93,7 +93,7 @@ for p in "${P[@]}"; do
               steps+=("300|$out/wino5_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 118,119,150,151,152,153 --ks 1,-2,-4") ;;
     wino6)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
               for rep in a b; do steps+=("300|$out/wino6_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 118,154,155,156 --ks 1,-2,-4"); done ;;
-    wtl)      for spec in "32,56,56,64,64:118:1" "32,56,56,64,64:155:1" "32,28,28,128,128:118:1" "32,14,14,256,256:118:-2" "32,7,7,512,512:118:-4"; do
+    wtl)      for spec in "32,56,56,64,64:118:1" "32,56,56,64,64:170:1" "32,28,28,128,128:170:1" "32,14,14,256,256:170:-2" "32,7,7,512,512:170:-4"; do
                 IFS=':' read -r shp cfg ks <<< "$spec"
                 steps+=("120|$out/wtl_${cfg}_${shp//,/x}|python -u tools/wino_timeline.py --shape $shp --cfg $cfg --ks $ks --json gpurun_out/$out/wtl_${cfg}_${shp//,/x}.json")
               done ;;

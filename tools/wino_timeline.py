@@ -94,6 +94,11 @@ def main():
             "epi_readback_us": round(float(np.median(us(d[:, 9] - d[:, 8]))), 2),
             "epi_stores_us": round(float(np.median(us(d[:, 10] - d[:, 9]))), 2),
             "epi_tail_us": round(float(np.median(us(d[:, 3] - d[:, 10]))), 2)} if (d[:, 10] != 0).all() else {}),
+        **({"chunk_barrier_wait_us": round(float(np.median(us(d[:, 12] - d[:, 11]))), 3),
+            "chunk_groups_0_7_us": round(float(np.median(us(d[:, 13] - d[:, 12]))), 3),
+            "chunk_groups_8_15_us": round(float(np.median(us(d[:, 14] - d[:, 13]))), 3),
+            "chunk_patch_read_us": round(float(np.median(us(d[:, 15] - d[:, 14]))), 3)}
+           if (d[:, 15] != 0).all() else {}),
         "start_us": [round(pct(start, q), 2) for q in (0, 50, 90, 100)],
         "end_us": [round(pct(end, q), 2) for q in (0, 10, 50, 90, 100)],
         "cu_busy_fraction": round(busy / (256 * span), 3),
