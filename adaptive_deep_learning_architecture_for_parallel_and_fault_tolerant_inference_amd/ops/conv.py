@@ -484,13 +484,15 @@ WINO_F32_CFGS = {80: (4, 2), 81: (4, 1), 82: (2, 2), 83: (8, 2), 84: (4, 3), 85:
                  164: (8, 2), 165: (8, 2),                    # 162 / 163 with the DMA hidden from the wait model
                  166: (8, 1), 167: (4, 1),                    # 116 / 117 likewise (partial waits for the prefetch)
                  170: (8, 2),                                 # 118 + in-loop phase stamps (tools/wino_timeline.py only)
+                 171: (8, 2), 172: (8, 2),                    # 118 with LDS counters instead of the chunk barrier
+                                                              # (172: + the in-loop stamps, measurement only)
                  140: (4, 1), 141: (8, 1)}                    # persistent: two blocks per CU walk the units as
                                                               # one chunk stream (whole K only)
 WINO_V2_CFGS = frozenset((100, 101, 102, 103, 104, 105, 106, 107, 108, 110, 111, 112, 113, 114, 116, 117,
                           118, 119, 130, 131, 132, 140, 141, 150, 151, 152, 153,
                           154, 155, 156, 157, 158, 160, 161, 162, 163,
-                          164, 165, 166, 167, 170))
-WINO_MEASURE_CFGS = frozenset((170,))     # never tuned (stamps cost a few cycles per chunk)
+                          164, 165, 166, 167, 170, 171, 172))
+WINO_MEASURE_CFGS = frozenset((170, 172))     # never tuned (stamps cost a few cycles per chunk)
 WINO_PU_CFGS = frozenset((140, 141))
 # stream-K Winograd configs: ksplit <= -100 means (-ksplit - 100) x 256 blocks over the (unit, chunk) space
 WINO_SK_CFGS = frozenset((110, 111, 112, 113, 114, 157, 158))

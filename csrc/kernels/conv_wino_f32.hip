@@ -540,6 +540,7 @@ struct WinoV2Shape {
   static constexpr int PPW = (PIECES + NW - 1) / NW;
   static constexpr int SLOT = PIECES * 1024;
   static constexpr int LDS = 2 * SLOT + NW * PMAX * 1024;
+  static constexpr int CTR = LDS;                    // + 64 B: the counter-synchronised body's 4 counters (cfg 171)
 };
 
 // one (tile group tg, channel group cg, K chunks [kc0, kc1)) unit of work; zs / ns / ctr_idx: its partial's
@@ -704,6 +705,34 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     }
     constexpr bool OD = (PL & 32) != 0;             // DMA through wino_dma16 (cfgs 164-167)
+    // PL & 128 (cfg 171): no block barrier per chunk.  The two-slot weight ring is guarded by LDS
+    // counters instead -- wready[s]: waves whose weight pieces for slot s have landed, rdone[s]: waves done
+    // reading slot s -- so a wave waits only for the data it needs and the waves of a block may drift up
+    // to ~6 MFMA groups apart (the block barrier held every wave to the slowest: 0.9 us a chunk,
+    // profiles/r4/r4v).  Inputs go out in groups 0-4, weights in 5-8 (after rdone of their slot), and
+    // wready is raised at group 14 after this wave's vmcnt(0).  Every spin is bounded.
+    constexpr bool CS = (PL & 128) != 0;
+    int* const wready = (int*)(smem + S::CTR);
+    int* const rdone = wready + 2;
+    // the counter accesses are inline asm: as plain LDS accesses the compiler cannot tell them from the
+    // LDS-DMA destinations and puts a vmcnt(0) before each, i.e. waits for the DMA just issued
+    auto spin_ge = [&](int* c, int target) {
+      const unsigned a = (unsigned)(uintptr_t)c;
+      for (int it = 0; it < (1 << 22); ++it) {
+        int v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+        if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
+    auto bump = [&](int* c) {
+      const unsigned a = (unsigned)(uintptr_t)c;
+      if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1) : "memory");
+    };
+    if constexpr (CS) {
+      if (threadIdx.x < 4) wready[threadIdx.x] = 0;
+      __syncthreads();
+    }
     if (kc0 < kc1) {
       if constexpr (OD) {
         const float* src = ub + (size_t)kc0 * uchunk;
@@ -720,6 +749,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
         issue_x(kc0);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (CS) bump(&wready[0]);          // chunk kc0's weight pieces of this wave are in
       read_patch_pl();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -731,7 +761,9 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
       constexpr bool TM = (PL & 64) != 0;
       const bool tmc = TM && stamp && kc == kc0 + 2;
       if (tmc) dbg[11] = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_s_barrier();                  // every wave's weight pieces of chunk kc are in
+      const int n = kc - kc0;                        // chunk index within the unit; its ring slot is n & 1
+      if constexpr (CS) spin_ge(&wready[n & 1], 8 * (n / 2 + 1) * NW / 8);
+      else __builtin_amdgcn_s_barrier();             // every wave's weight pieces of chunk kc are in
       asm volatile("" ::: "memory");
       if (tmc) dbg[12] = __builtin_amdgcn_s_memtime();
       if constexpr ((PL & 8) != 0) {
@@ -811,6 +843,26 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
             }
           }
         }
+        if constexpr (CS) {
+          if (g < 5) {                               // next chunk's input pieces 2g, 2g+1 (own image: no hazard)
+#pragma unroll
+            for (int i = 2 * g; i < 2 * g + 2; ++i) {
+              if (i >= PMAX) continue;
+              const float* src = (more && ((src_ok >> i) & 1u)) ? p.x + src_off[i] + (kc + 1) * 16 : wzero;
+              __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
+            }
+          } else if (g < 5 + PPW && more) {          // next chunk's weight piece g - 5, once the slot is free
+            if (g == 5) spin_ge(&rdone[(n + 1) & 1], 8 * ((n + 1) / 2) * NW / 8);
+            const int pc = wave * PPW + (g - 5);
+            if (PIECES % NW == 0 || pc < PIECES)
+              __builtin_amdgcn_global_load_lds((const void*)(wsrc + pc * wstep + lane * 4),
+                                               (lds_void_w*)(wdst + pc * 1024), 16, 0, 0);
+          }
+          if (g == 14) {                             // every DMA of this wave issued by group 8 has landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bump(&wready[(n + 1) & 1]);
+          }
+        } else {
 #pragma unroll
         for (int pi = g * DPG; pi < (g + 1) * DPG; ++pi) {
           if (pi < PPW) {                            // next chunk's weight piece pi of this wave
@@ -826,6 +878,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
             if constexpr (OD) wino_dma16(src, pimg + i * 1024);
             else __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_w*)(pimg + i * 1024), 16, 0, 0);
           }
+        }
         }
         // fence: the next fragments' reads and the DMA piece issue above this group's MFMAs (left to
         // itself the scheduler sinks each prefetch next to its use, at ~250 VGPRs, and waits lgkmcnt(0))
@@ -848,8 +901,13 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
           // this group: its fragment reads (+ EPR's patch reads), its DMA piece, then its MFMAs
           if (EPR && g >= 12) __builtin_amdgcn_sched_group_barrier(0x100, FN + 3, 0);
           else __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
-          if (g < NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, DPG, 0);
-          else if (g == NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, PPW + PMAX - (NPG - 1) * DPG, 0);
+          if constexpr (CS) {
+            if (g < 5) __builtin_amdgcn_sched_group_barrier(0x010, 2, 0);
+            else if (g < 5 + PPW) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+          } else {
+            if (g < NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, DPG, 0);
+            else if (g == NPG - 1) __builtin_amdgcn_sched_group_barrier(0x010, PPW + PMAX - (NPG - 1) * DPG, 0);
+          }
           __builtin_amdgcn_sched_group_barrier(0x008, 4 * FN, 0);
         } else if constexpr (FN >= 2) {
 #pragma unroll
@@ -867,6 +925,7 @@ __device__ __forceinline__ void wino_v2_unit(const WinoF32Params& p, char* smem,
           }
         }
       }
+      if constexpr (CS) bump(&rdone[n & 1]);       // this wave is done reading slot n & 1
       if (tmc) dbg[14] = __builtin_amdgcn_s_memtime();
       // the next chunk's patch (its DMA went out during this chunk's groups)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -984,7 +1043,7 @@ __device__ __forceinline__ void wino_xcd_unit(int& tg, int& cg, int& z) {
 
 template <int NW, int FN, bool SW = false, bool EP = false, bool SK = false, int PL = 0, bool XM = false>
 __global__ __launch_bounds__(NW * 64, (NW == 4 && FN == 1) ? 2 : 1) void conv_wino_f32_v2_kernel(WinoF32Params p) {
-  __shared__ __attribute__((aligned(16))) char smem[WinoV2Shape<NW, FN>::LDS];
+  __shared__ __attribute__((aligned(16))) char smem[WinoV2Shape<NW, FN>::LDS + ((PL & 128) ? 64 : 0)];
   const int KC = p.C / 16;
   if constexpr (!SK) {
     int tg = blockIdx.x, cg = blockIdx.y, z = blockIdx.z;
@@ -1349,7 +1408,9 @@ hipError_t launch_wino(const WinoF32Params& p, hipStream_t s) {
   X(165, 8, 2, true, true, false, 54, false) \
   X(166, 8, 1, true, true, false, 33, false) \
   X(167, 4, 1, true, true, false, 33, false) \
-  X(170, 8, 2, true, true, false, 66, false)
+  X(170, 8, 2, true, true, false, 66, false) \
+  X(171, 8, 2, true, true, false, 130, false) \
+  X(172, 8, 2, true, true, false, 194, false)
 
 // stream-K plan of a Winograd v2 launch: `units` output blocks of kc chunks over about mult x 256 blocks;
 // smax = the most partials one unit is cut into (the fused fixup takes <= 4)

@@ -35,6 +35,8 @@
 #   pw5       pointwise numerics + isolated timings incl. the deep-ring streaming cfg 124
 #   wino8     Winograd numerics + isolated timings: 118 / 155 / 116 / 117 vs early patch read (162/163)
 #             and the DMA hidden from the wait model (164-167)
+#   wino9     Winograd numerics + timings of 118 / 155 / 167 vs the counter-synchronised cfg 171, and the
+#             in-loop timelines of 170 (barrier) vs 172 (counters)
 #   pmcstem   two PMC passes over the fp32 stem (tools/stem_bench.py)
 #   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
@@ -106,6 +108,12 @@ for p in "${P[@]}"; do
               steps+=("300|$out/pw5_bench|python -u tools/conv_bench_f32.py --only 18,20,38,120,122,123,124 --ks 1,-1,-2 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,28,28,512,1280,1,2,0,0 --shape 32,14,14,1024,2560,1,2,0,0") ;;
     wino8)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
               for rep in a b; do steps+=("300|$out/wino8_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 116,117,118,155,162,163,164,165,166,167 --ks 1,-2,-4"); done ;;
+    wino9)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
+              for rep in a b; do steps+=("300|$out/wino9_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 118,155,167,171 --ks 1,-2,-4"); done
+              for spec in "32,56,56,64,64:170:1" "32,56,56,64,64:172:1" "32,28,28,128,128:170:1" "32,28,28,128,128:172:1" "32,14,14,256,256:172:-2"; do
+                IFS=':' read -r shp cfg ks <<< "$spec"
+                steps+=("120|$out/wtl_${cfg}_${shp//,/x}|python -u tools/wino_timeline.py --shape $shp --cfg $cfg --ks $ks")
+              done ;;
     pmcstem)  steps+=("120|$out/pmcstem1|cd /tmp && rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/$out/pmcstem/g1 -o run -- python3 \$GRAFT_REPO_ROOT/tools/stem_bench.py --iters 20")
               steps+=("120|$out/pmcstem2|cd /tmp && rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d \$GRAFT_REPO_ROOT/gpurun_out/$out/pmcstem/g2 -o run -- python3 \$GRAFT_REPO_ROOT/tools/stem_bench.py --iters 20") ;;
     *) echo "unknown preset $p"; exit 2 ;;
