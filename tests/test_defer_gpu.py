@@ -225,10 +225,10 @@ def test_defer_gpu_codec_with_device_link_upstream(codec):
         got = np.concatenate([outq.get(timeout=120) for _ in xs])
         want = m.predict(np.concatenate(xs), device="cpu")
         assert np.abs(got - want).sum(-1).max() < 0.1
+        assert not d.recoveries, d.events            # (a re-formed 1-stage replica would have no link at all)
         last = next(n for n in nodes if n.node_id == d.pipeline.workers[-1])
         first = next(n for n in nodes if n.node_id == d.pipeline.workers[0])
-        assert first.runtime.link == "dev" and last.runtime.gpu_codec
-        assert not d.recoveries, d.events
+        assert first.runtime.link == "dev" and last.runtime.gpu_codec, (first.runtime.link, d.events)
     finally:
         d.shutdown(stop_workers=True)
         for n in nodes:
