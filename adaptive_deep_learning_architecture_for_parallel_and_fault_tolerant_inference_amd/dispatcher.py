@@ -486,6 +486,9 @@ class DEFER:
         ep, old = self._rep_period.get(replica, (epoch, None))
         self._rep_period[replica] = (epoch, dt if old is None or ep != epoch else 0.8 * old + 0.2 * dt)
 
+    HANG_WARMUP = 4          # micro-batches of an epoch a stage completes before the normal threshold applies
+    HANG_WARMUP_S = 2.0      # its threshold until then (seconds)
+
     def hang_threshold(self, replica: int, epoch: int, stage_s: float = 0.0) -> Optional[float]:
         """Seconds without progress that make a stage of `replica` hung:
         max(hang_factor x the stage's own reported time per micro-batch (else
@@ -566,6 +569,11 @@ class DEFER:
                     continue
                 stalled = now - max(now - age, arrived, t0)
                 thr = self.hang_threshold(p.replica, p.epoch, stage_s)
+                if n < self.HANG_WARMUP:
+                    # a stage's first micro-batches of an epoch include one-off work (the hipGraph capture of
+                    # each of its two micro-batch sets, first codec launches) that its measured period does
+                    # not cover: a longer threshold until it has completed a few
+                    thr = max(thr, self.HANG_WARMUP_S)
                 if stalled > thr and oldest_task > thr:
                     self.hangs.append({"t": now, "worker": wid, "stage": idx, "replica": p.replica,
                                        "epoch": p.epoch, "stalled_ms": round(stalled * 1e3, 1),

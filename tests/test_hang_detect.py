@@ -176,3 +176,39 @@ def test_slow_upstream_after_idle_is_not_a_hang(tiny):
             except ProcessLookupError:
                 pass
             p.wait(timeout=10)
+
+
+def test_slow_first_microbatches_are_warmup_not_a_hang(tiny):
+    """A stage whose first micro-batches of an epoch are slow (one-off work such as a GPU stage capturing
+    the hipGraph of its second micro-batch set) is not called hung while it has completed fewer than
+    DEFER.HANG_WARMUP micro-batches, even though the replica's period measured from the first result
+    would put its threshold at the 0.2 s floor."""
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=1, max_inflight=4, weight_codec="lz4",
+              min_workers=2, replicas=1, task_timeout=30, transport="tcp", hang_min_s=0.2, hang_factor=10)
+    d.HANG_WARMUP = 8 if DEFER.HANG_WARMUP else 0        # the 4 requests that measure the period stay in warm-up
+    d.membership_server.start()
+    procs = [_spawn_worker(d.membership_port, f"w{i}") for i in range(2)]
+    try:
+        inq, outq = queue.Queue(8), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, ["conv3_block1_out"], inq, outq), daemon=True).start()
+        x = np.random.default_rng(5).standard_normal((1, 32, 32, 3)).astype(np.float32)
+        for _ in range(4):                               # overlapping requests: the period is measured
+            inq.put(x)
+        for _ in range(4):
+            outq.get(timeout=120)
+        assert d.hang_threshold(d.pipeline.replica, d.pipeline.epoch) is not None
+        d.inject_fault(d.pipeline.workers[1], "delay:0.6")   # stage 1's micro-batches 5 and 6: 0.6 s each
+        for _ in range(2):
+            inq.put(x)
+        for _ in range(2):
+            outq.get(timeout=120)
+        assert not d.hangs, d.hangs
+        assert not d.recoveries and len(d.pipeline.workers) == 2, d.events[-5:]
+    finally:
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait(timeout=10)
