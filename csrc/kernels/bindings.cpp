@@ -175,15 +175,22 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("pw_f32_supported", &adapt::pw_f32_supported);
   m.def("pw_f32_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, int M, int K, int N, int relu, int bm, u64 s,
-                             int B, int H, int W, int OH, int OW, int stride, u64 out2, int n_split, int relu2) {
+                             int B, int H, int W, int OH, int OW, int stride, u64 out2, int n_split, int relu2,
+                             u64 ws, u64 counters) {
     adapt::PwF32Params p{P<const float>(x), P<const float>(w), P<const float>(bias), P<const float>(res), P<float>(out),
-                         M, K, N, relu, B, H, W, OH, OW, stride, P<float>(out2), n_split, relu2};
+                         M, K, N, relu, B, H, W, OH, OW, stride, P<float>(out2), n_split, relu2, P<float>(ws),
+                         P<int>(counters)};
     check(adapt::pw_f32_forward(p, bm, S(s)), "pw_f32_forward");
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("out"), py::arg("M"), py::arg("K"),
      py::arg("N"), py::arg("relu"), py::arg("bm"), py::arg("s"), py::arg("B"), py::arg("H"), py::arg("W"),
      py::arg("OH"), py::arg("OW"), py::arg("stride"), py::arg("out2") = 0, py::arg("n_split") = 0,
-     py::arg("relu2") = 0);
+     py::arg("relu2") = 0, py::arg("ws") = 0, py::arg("counters") = 0);
   m.def("pw_f32_fpw", &adapt::pw_f32_fpw);
+  m.def("pw_f32_tail_plan", [](int M, int K, int N, int n_split, int bm) {
+    int ws = 0, ctr = 0;
+    adapt::pw_f32_tail_plan(M, K, N, n_split, bm, &ws, &ctr);
+    return py::make_tuple(ws, ctr);
+  });
   m.def("pw_pair_f32_supported", &adapt::pw_pair_f32_supported);
   m.def("pw_pair_f32_forward", [](u64 x, u64 w3, u64 b3, u64 res, u64 w1, u64 b1, u64 y, u64 z, int M, int cin,
                                   int co, int cm, int bm, int grid, u64 s) {

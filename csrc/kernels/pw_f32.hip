@@ -25,6 +25,8 @@ namespace adapt {
 
 namespace {
 
+constexpr int PW_CPOL_SC1 = 16;     // gfx950 cache policy: sc1 (write-through L2, bypass L1)
+
 template <int NCH>
 __device__ __forceinline__ int pswz32(int r, int c) {   // 16-byte chunk c of row r (NCH chunks per row)
   return r * (NCH * 16) + (((c & ~15) | ((c ^ r) & 15)) << 4);
@@ -198,8 +200,42 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
 // waves that read one tile are the ncg channel groups of one slot; the XCD-aware block order keeps
 // them on one XCD, so a tile crosses the fabric once per XCD.  FPW = 1 alternates two accumulators
 // by K step (a dependent 16x16x4 f32 MFMA waits 40 of its 32 issue cycles).
-template <int K, int FPW, int D, int OCC>
-__global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, int ncg, int nslots) {
+//
+// TP > 0 (bm codes 4 / 5, cfgs 125 / 126): the tile count rarely divides into the slots -- ResNet-50's
+// 28x28 and 14x14 1x1 convs give every slot 6 tiles and an eighth of the slots a 7th, so 7/8 of the
+// chip idles through the last tile round (12 % of those launches).  Here the slots walk `full` tiles
+// each, then the `tail` left-over tiles are split along K into TP parts over tail x TP slots: a wave
+// MFMAs KH/TP K steps of one tail tile, publishes the partial accumulators to `ws` with sc1 stores
+// and bumps the tile's agent-scope arrival counter; the last of the TP waves adds the TP partials in
+// part order (the same sums whichever wave arrives last), then bias / residual / ReLU, and re-zeroes
+// the counter for the next launch.
+template <int KH, int FPW, int KPH, int H0>
+__device__ __forceinline__ void pw_tail_part(const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[FPW]) {
+  f32x4 xs[KPH];
+#pragma unroll
+  for (int i = 0; i < KPH; ++i) xs[i] = *(const f32x4*)(xt + (H0 + i) * 16);
+#pragma unroll
+  for (int i = 0; i < KPH; ++i)
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+      for (int j = 0; j < FPW; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][H0 + i][ss], xs[i][ss], acc[j], 0, 0, 0);
+}
+template <int KH, int FPW, int TP, int PART = 0>
+__device__ __forceinline__ void pw_tail_pick(int kp, const f32x4 (&wr)[FPW][KH], const float* xt,
+                                             f32x4 (&acc)[FPW]) {
+  if constexpr (PART < TP) {
+    if (kp == PART)                                   // wave-uniform
+      pw_tail_part<KH, FPW, KH / TP, PART * (KH / TP)>(wr, xt, acc);
+    else
+      pw_tail_pick<KH, FPW, TP, PART + 1>(kp, wr, xt, acc);
+  }
+}
+
+template <int K, int FPW, int D, int OCC, int TP = 0>
+__global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, int ncg, int nslots, int full,
+                                                                 int tail) {
   constexpr int KH = K / 16;
   constexpr int NA = FPW >= 2 ? 1 : 2;                // accumulator sets per fragment
   static_assert(KH % D == 0, "ring depth must divide the K steps");
@@ -237,6 +273,7 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
     return p.x + (size_t)m * K + h * 16 + fq * 4;
   };
 
+  const int lim = TP > 0 ? full * nslots : ntiles;     // TP > 0: the host guarantees full >= 1
   int t = slot;
   f32x4 ring[D];
   const float* xb = xptr(t, 0);
@@ -244,7 +281,7 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
   for (int i = 0; i < D; ++i) ring[i] = *(const f32x4*)(xb + i * 16);
   while (true) {
     const int tn = t + nslots;
-    const bool more = tn < ntiles;
+    const bool more = tn < lim;
     const float* xn = xptr(more ? tn : t, 0);         // the last tile re-reads its own (valid) rows
     const int m = t * 16 + fr;
     f32x4 res[FPW];
@@ -284,6 +321,47 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
     if (!more) break;
     t = tn;
     xb = xn;
+  }
+  if constexpr (TP > 0 && KH % TP == 0 && KH / TP <= 8) {
+    const int ti = slot / TP, kp = slot - ti * TP;
+    if (ti >= tail) return;                           // wave-uniform
+    const int tt = lim + ti;
+    f32x4 acc[FPW];
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    pw_tail_pick<KH, FPW, TP>(kp, wr, xptr(tt, 0), acc);
+    const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, 0x7fffffff,
+                                                                         0x00020000);
+    const int base = (ti * ncg + cg) * TP * FPW;      // 64-lane x float4 records
+#pragma unroll
+    for (int j = 0; j < FPW; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), wsr,
+                                             ((base + kp * FPW + j) * 64 + lane) * 16, 0, PW_CPOL_SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) {
+      int* ctr = p.counters + ti * ncg + cg;
+      last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == TP - 1;
+      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    const int m = tt * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      f32x4 pt[TP];
+#pragma unroll
+      for (int q = 0; q < TP; ++q)
+        pt[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              wsr, ((base + q * FPW + j) * 64 + lane) * 16, 0, PW_CPOL_SC1));
+      f32x4 v = pt[0];
+#pragma unroll
+      for (int q = 1; q < TP; ++q) v += pt[q];
+      v += bias[j];
+      if (has_res) v += *(const f32x4*)(p.res + (size_t)min(m, p.M - 1) * p.N + (cg * FPW + j) * 16 + fq * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
+      if (m < p.M) *(f32x4*)(dst + (size_t)m * ldo + (cg * FPW + j) * 16 + fq * 4 - cof) = v;
+    }
   }
 }
 
@@ -354,46 +432,96 @@ static int pw_stream_deep_pick(int K, int N, int n_split) {
 }
 int pw_f32_fpw(int K, int N, int n_split, int bm) {
   if (bm == 3) return pw_stream_deep_pick(K, N, n_split);
+  if (bm == 4 || bm == 5) return pw_stream_pick(K, N, n_split, bm == 5);
   return bm <= 2 ? pw_stream_pick(K, N, n_split, bm == 2) : pw_f32_pick(K, N, n_split, bm);
+}
+
+// parts per tail tile of a K-split-tail launch (0: none fits): the most (8, 4, 2) whose tail x TP
+// waves fit in the slots, with whole K steps of <= 8 per part
+static int pw_tail_parts(int K, int ntiles, int nslots) {
+  const int full = ntiles / nslots, tail = ntiles - full * nslots, kh = K / 16;
+  if (full < 1 || tail < 1) return 0;
+  for (int tp = 8; tp >= 2; tp >>= 1)
+    if (tail * tp <= nslots && kh % tp == 0 && kh / tp <= 8) return tp;
+  return 0;
+}
+
+template <int K, int F, int D, int O, bool TAIL>
+static hipError_t pw_stream_launch(const PwF32Params& p, int ncg, int ntiles, hipStream_t s) {
+  int nslots = (1024 * O) / ncg;                      // ~O waves per SIMD over the chip
+  if (nslots < 1) nslots = 1;
+  if (nslots > ntiles) nslots = ntiles;
+  const int blocks = (ncg * nslots + 3) / 4;
+  if constexpr (!TAIL) {
+    hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots, 0, 0);
+    return hipGetLastError();
+  } else {
+    const int full = ntiles / nslots, tail = ntiles - full * nslots;
+    if (!p.ws || !p.counters) return hipErrorInvalidValue;
+    switch (pw_tail_parts(K, ntiles, nslots)) {
+#define PW_TAIL_CASE(TP_)                                                                                    \
+    case TP_:                                                                                                  \
+      if constexpr ((K / 16) % TP_ == 0 && (K / 16) / TP_ <= 8) {                                              \
+        hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O, TP_>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots, \
+                           full, tail);                                                                        \
+        return hipGetLastError();                                                                              \
+      }                                                                                                        \
+      break;
+      PW_TAIL_CASE(8)
+      PW_TAIL_CASE(4)
+      PW_TAIL_CASE(2)
+#undef PW_TAIL_CASE
+      default:
+        break;
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+void pw_f32_tail_plan(int M, int K, int N, int n_split, int bm, int* ws_elems, int* counters) {
+  *ws_elems = *counters = 0;
+  const int fpw = pw_f32_fpw(K, N, n_split, bm);
+  if (!fpw || (bm != 4 && bm != 5)) return;
+  const int ncg = N / (16 * fpw), ntiles = (M + 15) / 16;
+  int o = 0;
+#define X(K_, F_, D_, O_) if (K == K_ && fpw == F_) o = O_;
+  ADAPT_PW_STREAM_CFGS(X)
+#undef X
+  int nslots = (1024 * o) / ncg;
+  if (nslots < 1) nslots = 1;
+  if (nslots > ntiles) nslots = ntiles;
+  const int tp = pw_tail_parts(K, ntiles, nslots);
+  if (!tp) return;
+  const int tail = ntiles % nslots;
+  *ws_elems = tail * ncg * tp * fpw * 256;
+  *counters = tail * ncg;
 }
 
 bool pw_f32_supported(int K, int N, int bm) { return pw_f32_fpw(K, N, 0, bm) > 0; }
 
 static hipError_t pw_stream_f32_forward(const PwF32Params& p, int mode, hipStream_t s) {
-  const int fpw = mode == 3 ? pw_stream_deep_pick(p.K, p.N, p.n_split) : pw_stream_pick(p.K, p.N, p.n_split, mode == 2);
+  const int fpw = pw_f32_fpw(p.K, p.N, p.n_split, mode);
   if (!fpw) return hipErrorInvalidValue;
   const int ncg = p.N / (16 * fpw);
   const int ntiles = (p.M + 15) / 16;
   if (mode == 3) {
-#define X(K_, F_, D_, O_)                                                                                  \
-  if (p.K == K_ && fpw == F_) {                                                                            \
-    int nslots = (1024 * O_) / ncg;                                                                        \
-    if (nslots < 1) nslots = 1;                                                                            \
-    if (nslots > ntiles) nslots = ntiles;                                                                  \
-    const int blocks = (ncg * nslots + 3) / 4;                                                             \
-    hipLaunchKernelGGL((pw_stream_f32_kernel<K_, F_, D_, O_>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots); \
-    return hipGetLastError();                                                                              \
-  }
+#define X(K_, F_, D_, O_) \
+  if (p.K == K_ && fpw == F_) return pw_stream_launch<K_, F_, D_, O_, false>(p, ncg, ntiles, s);
     ADAPT_PW_STREAM_DEEP_CFGS(X)
 #undef X
     return hipErrorInvalidValue;
   }
-#define X(K_, F_, D_, O_)                                                                                  \
-  if (p.K == K_ && fpw == F_) {                                                                            \
-    int nslots = (1024 * O_) / ncg;                   /* ~O_ waves per SIMD over the chip */               \
-    if (nslots < 1) nslots = 1;                                                                            \
-    if (nslots > ntiles) nslots = ntiles;                                                                  \
-    const int blocks = (ncg * nslots + 3) / 4;                                                             \
-    hipLaunchKernelGGL((pw_stream_f32_kernel<K_, F_, D_, O_>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots); \
-    return hipGetLastError();                                                                              \
-  }
+#define X(K_, F_, D_, O_)                                                                          \
+  if (p.K == K_ && fpw == F_)                                                                      \
+    return mode >= 4 ? pw_stream_launch<K_, F_, D_, O_, true>(p, ncg, ntiles, s)                   \
+                     : pw_stream_launch<K_, F_, D_, O_, false>(p, ncg, ntiles, s);
   ADAPT_PW_STREAM_CFGS(X)
 #undef X
   return hipErrorInvalidValue;
 }
 
 hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s) {
-  if (bm >= 1 && bm <= 3) {
+  if (bm >= 1 && bm <= 5) {
     if (p.M < 1 || p.stride < 1 || (p.n_split && (!p.out2 || p.res)) || p.M != p.B * p.OH * p.OW ||
         (p.stride == 1 && (p.H != p.OH || p.W != p.OW)))
       return hipErrorInvalidValue;
