@@ -44,6 +44,16 @@ __device__ __forceinline__ int stage_off(int row, int pix, int chunk) {
   return ((row * ST_OWMAX + pix) * 8 + (chunk ^ ((pix >> 1) & 7))) * 8;   // in bf16 elements
 }
 
+// Input pixels by buffer load: an out-of-range offset (outside the image, or channel >= C) reads 0 with
+// no branch.  A plain `ok ? px[c] : 0` load compiles to a branch around every load with a vmcnt(0)
+// behind it, so each of a thread's ~20-76 loads was its own round trip.
+__device__ __forceinline__ float stem_ld(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stem_rsrc(const float* xi, int H, int W, int C) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)xi, (short)0, H * W * C * 4, 0x00020000);
+}
+
 }  // namespace
 
 template <bool POOL>
@@ -84,14 +94,15 @@ __global__ __launch_bounds__(ST_NT, 2) void stem_kernel(const float* __restrict_
   {
     const int j = tid, iw = j - pad_l;
     const bool colok = j < pwc && (unsigned)iw < (unsigned)W;
+    const __amdgpu_buffer_rsrc_t xr = stem_rsrc(xi, H, W, C);
     float pv[PROWS][4];
 #pragma unroll
     for (int i = 0; i < PROWS; ++i) {
       const int ih = ih0 + i;
       const bool ok = colok && (unsigned)ih < (unsigned)H;
-      const float* px = xi + (ok ? ((size_t)ih * W + iw) * C : 0);
+      const int off = ((ih * W + iw) * C) * 4;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) pv[i][c] = (ok && c < C) ? px[c] : 0.f;
+      for (int c = 0; c < 4; ++c) pv[i][c] = stem_ld(xr, ok && c < C ? off + 4 * c : 0x7fffffff);
     }
     if (j < pwc) {
 #pragma unroll
@@ -210,6 +221,7 @@ union P8 {                                                 // 8 bf16 as 16 B or 
 template <int ITEMS>
 __device__ __forceinline__ void get_rows(float (&pv)[ITEMS][4], const float* __restrict__ xi, int tid, int row0,
                                          int nrows, int row_end, int ih0, int H, int W, int C, int pwc, int pad_l) {
+  const __amdgpu_buffer_rsrc_t xr = stem_rsrc(xi, H, W, C);
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     const int idx = tid + k * S2_NT;
@@ -217,9 +229,9 @@ __device__ __forceinline__ void get_rows(float (&pv)[ITEMS][4], const float* __r
     const int ih = ih0 + i, iw = j - pad_l;
     const bool ok = idx < nrows * ST_PWC && i < row_end && j < pwc && (unsigned)ih < (unsigned)H &&
                     (unsigned)iw < (unsigned)W;
-    const float* px = xi + (ok ? ((size_t)ih * W + iw) * C : 0);
+    const int off = ((ih * W + iw) * C) * 4;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) pv[k][c] = (ok && c < C) ? px[c] : 0.f;
+    for (int c = 0; c < 4; ++c) pv[k][c] = stem_ld(xr, ok && c < C ? off + 4 * c : 0x7fffffff);
   }
 }
 template <int ITEMS>
@@ -236,6 +248,31 @@ __device__ __forceinline__ void put_rows(const float (&pv)[ITEMS][4], bf16* patc
   }
 }
 
+// patch items [k0, k0 + N) of a block's whole patch -> LDS, rows [rlo, rhi) only (k compile-time: no
+// register indexing; the compiler waits only for the loads of the items it stores)
+template <int K0, int N, int ITEMS>
+__device__ __forceinline__ void put_items(const float (&pv)[ITEMS][4], bf16* patch, int tid, int rlo, int rhi) {
+#pragma unroll
+  for (int k = K0; k < K0 + N; ++k) {
+    const int idx = tid + k * S2_NT;
+    if (idx >= rlo * ST_PWC && idx < rhi * ST_PWC) {
+      bf16x4s v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v.v[c] = f2bf(pv[k][c]);
+      *(bf16x4s*)(patch + idx * 4) = v;
+    }
+  }
+}
+
+// ALL (v3): the block's whole (4*S2_SP+7)-row patch is requested in the prologue -- 19 items of 4 floats
+// per thread in flight at once -- and the first step's 11 rows go to LDS as soon as they land; the
+// other rows are stored during the first step's MFMAs.  v2 requested 4 rows a step, one step ahead,
+// and paid a global-load round trip per step (29 us at bs=32, profiles/r4/r4s: ~4 us a step for
+// ~0.75 us of MFMAs).
+constexpr int S2_ITEMS_ALL = (S2_PROWS * ST_PWC + S2_NT - 1) / S2_NT;   // 19
+constexpr int S2_ITEMS_A = (S2_ROWS0 * ST_PWC + S2_NT - 1) / S2_NT;     // items holding rows 0..10
+
+template <bool ALL>
 __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __restrict__ x,
                                                                 const bf16* __restrict__ w,
                                                                 const float* __restrict__ bias,
@@ -258,8 +295,11 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
   const int pwc = 2 * tpr * 16 + 8;
   const float* xi = x + (size_t)img * H * W * C;
 
-  // first step's 11 input rows: loads in flight while the weight panel loads
-  {
+  // first step's 11 input rows (v3: the whole patch): loads in flight while the weight panel loads
+  float pall[ALL ? S2_ITEMS_ALL : 1][4];
+  if constexpr (ALL) {
+    get_rows<S2_ITEMS_ALL>(pall, xi, tid, 0, row_end, row_end, ih0, H, W, C, pwc, pad_l);
+  } else {
     float pv0[S2_ITEMS0][4];
     get_rows<S2_ITEMS0>(pv0, xi, tid, 0, S2_ROWS0, row_end, ih0, H, W, C, pwc, pad_l);
     put_rows<S2_ITEMS0>(pv0, patch, tid, 0, S2_ROWS0);
@@ -275,13 +315,14 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
   for (int n = 0; n < 4; ++n)
 #pragma unroll
     for (int r = 0; r < 4; ++r) b4[n][r] = bias[n * 16 + 4 * fq + r];
+  if constexpr (ALL) put_items<0, S2_ITEMS_A>(pall, patch, tid, 0, S2_ROWS0);
   __syncthreads();
 
-  for (int t = t0; t < t1; ++t) {
-    // the NEXT step's 4 input rows: issued now, landed in LDS after this step's MFMAs
+  auto step = [&](const int t, auto first) __attribute__((always_inline)) {
+    // v2: the NEXT step's 4 input rows, issued now, landed in LDS after this step's MFMAs
     const int nrow0 = 4 * (t - t0) + S2_ROWS0;
     float pv[S2_ITEMS1][4];
-    const bool more = t + 1 < t1;
+    const bool more = !ALL && t + 1 < t1;
     if (more) get_rows<S2_ITEMS1>(pv, xi, tid, nrow0, 4, row_end, ih0, H, W, C, pwc, pad_l);
     // conv rows of this step: 2t-pp+1 .. 2t-pp+2, plus 2t-pp on the block's first step
     const int ra = 2 * t - pool_pad + (t == t0 ? 0 : 1);
@@ -316,6 +357,8 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
       }
     }
     if (more) put_rows<S2_ITEMS1>(pv, patch, tid, nrow0, 4);
+    if constexpr (ALL && decltype(first)::value)     // v3: the rest of the patch, landed under the MFMAs
+      put_items<S2_ITEMS_A - 1, S2_ITEMS_ALL - S2_ITEMS_A + 1>(pall, patch, tid, S2_ROWS0, row_end);
     __syncthreads();
     // pool row t from conv rows 2t-pp .. 2t-pp+2.  Non-negative bf16 values order
     // like their u16 bit patterns: packed integer max, 2 values per instruction;
@@ -343,7 +386,10 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
       *(u32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch8 * 8) = m.u;
     }
     __syncthreads();                                       // ring slots of rows 2t-pp, 2t-pp+1 are free
-  }
+  };
+  // the first step peeled (straight-line), so v3's remaining patch stores wait only for their own loads
+  step(t0, std::integral_constant<bool, true>{});
+  for (int t = t0 + 1; t < t1; ++t) step(t, std::integral_constant<bool, false>{});
 }
 
 hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
@@ -357,11 +403,16 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
     // dozen blocks (8 at B=1): there the one-pool-row-per-block v1 grid fills more
     // CUs and wins.  ADAPT_STEM_V1=1 / =0 forces v1 / v2 (A/B switch).
     const int groups = (PH + S2_SP - 1) / S2_SP;
+    // ADAPT_STEM_V1=1 / =0 / =3: v1 / v2 / v3 (v3: the row-group kernel with the whole patch requested up front)
     const char* v1 = getenv("ADAPT_STEM_V1");
-    const bool use_v1 = v1 && v1[0] ? v1[0] == '1' : PH * B <= ST_V1_MAX_BLOCKS;
-    if (!use_v1) {
-      hipLaunchKernelGGL(stem_pool_v2_kernel, dim3(groups * B), dim3(S2_NT), 0, s, x, w, bias, out, H, W, C, OH, OW,
-                         pad_t, pad_l, PH, PW, pool_pad, groups);
+    const char ver = v1 && v1[0] ? v1[0] : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : '3');
+    if (ver != '1') {
+      if (ver == '3')
+        hipLaunchKernelGGL(stem_pool_v2_kernel<true>, dim3(groups * B), dim3(S2_NT), 0, s, x, w, bias, out, H, W, C,
+                           OH, OW, pad_t, pad_l, PH, PW, pool_pad, groups);
+      else
+        hipLaunchKernelGGL(stem_pool_v2_kernel<false>, dim3(groups * B), dim3(S2_NT), 0, s, x, w, bias, out, H, W, C,
+                           OH, OW, pad_t, pad_l, PH, PW, pool_pad, groups);
       return hipGetLastError();
     }
     dim3 grid(PH * B);
