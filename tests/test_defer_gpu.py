@@ -233,3 +233,90 @@ def test_defer_gpu_codec_with_device_link_upstream(codec):
         d.shutdown(stop_workers=True)
         for n in nodes:
             n.stop()
+
+
+def test_defer_gpu_hang_over_device_links():
+    """The hang twin on the GPU data plane: three GPU worker processes, links=auto (the stage hops are
+    device links opened by IPC handle), DEFER's default hang detection.  The middle stage's compute loop
+    is wedged over its control channel while its process and heartbeats stay alive: the dispatcher must
+    see its progress counter stand still, re-form the chain on the two survivors and replay, and every
+    request must be answered exactly once with the fp32 oracle's logits (the CPU twins are
+    tests/test_hang_detect.py)."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+    m = resnet("resnet50", seed=0)
+    d = DEFER(membership_port=0, result_port=0, worker_wait=120, batch=2, ordered=True, weight_codec="lz4",
+              min_workers=3, max_inflight=4, links="auto")
+    d.membership_server.start()
+    pkg = "adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd"
+    procs = [subprocess.Popen([sys.executable, "-m", f"{pkg}.node", "--membership-port", str(d.membership_port),
+                               "--data-port", "0", "--config-port", "0", "--device", "cuda:0", "--id", f"hg{i}",
+                               "--ttl", "2.0"], start_new_session=True) for i in range(3)]
+    stop = threading.Event()
+    try:
+        inq, outq = queue.Queue(4), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(m, ["conv3_block1_out", "conv4_block3_out"], inq, outq),
+                         daemon=True).start()
+        x = np.random.default_rng(11).standard_normal((2, 224, 224, 3)).astype(np.float32)
+        want = m.predict(x, device="cpu")
+        sent = [0]
+
+        def feeder():
+            while not stop.is_set():
+                try:
+                    inq.put(x, timeout=0.05)
+                    sent[0] += 1
+                except queue.Full:
+                    continue
+
+        feed = threading.Thread(target=feeder, daemon=True)
+        feed.start()
+        res = [outq.get(timeout=180) for _ in range(30)]
+        assert len(d.pipeline.workers) == 3
+        assert any("links=dev" in ev for _, ev in d.events), d.events[-5:]
+        victim = d.pipeline.workers[1]
+        t_hang = time.time()
+        d.inject_fault(victim, "hang")
+        t_end = time.time() + 60
+        while not d.recoveries and time.time() < t_end:
+            try:
+                res.append(outq.get(timeout=0.05))
+            except queue.Empty:
+                pass
+        assert d.hangs, d.events[-8:]
+        h = d.hangs[0]
+        detect_ms = (h["t"] - t_hang) * 1e3
+        print(f"hung stage {h['stage']} ({h['worker']}) detected {detect_ms:.0f} ms after the hang, "
+              f"threshold {h['threshold_ms']} ms; recoveries {d.recoveries[:1]}")
+        assert h["worker"] == victim and h["stage"] == 1
+        assert detect_ms < h["threshold_ms"] + 500.0
+        for _ in range(10):
+            res.append(outq.get(timeout=180))
+        stop.set()
+        feed.join()
+        d.inject_fault(victim, "clear")          # the wedged stage wakes up: its stale outputs must not leak out
+        time.sleep(0.5)
+        total = sent[0]
+        while len(res) < total:
+            res.append(outq.get(timeout=180))
+        time.sleep(0.5)
+        assert outq.empty() and len(res) == total           # exactly once
+        for y in res:
+            assert np.abs(y - want).sum(-1).max() < 0.1
+        assert victim not in d.pipeline.workers and len(d.pipeline.workers) == 2
+    finally:
+        stop.set()
+        d.shutdown(stop_workers=True)
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
