@@ -235,13 +235,15 @@ def test_defer_gpu_codec_with_device_link_upstream(codec):
             n.stop()
 
 
-def test_defer_gpu_hang_over_device_links():
-    """The hang twin on the GPU data plane: three GPU worker processes, links=auto (the stage hops are
-    device links opened by IPC handle), DEFER's default hang detection.  The middle stage's compute loop
-    is wedged over its control channel while its process and heartbeats stay alive: the dispatcher must
-    see its progress counter stand still, re-form the chain on the two survivors and replay, and every
-    request must be answered exactly once with the fp32 oracle's logits (the CPU twins are
-    tests/test_hang_detect.py)."""
+@pytest.mark.parametrize("fault", ["hang", "kill"])
+def test_defer_gpu_fault_over_device_links(fault):
+    """Config 4 on the GPU data plane: three GPU worker processes, links=auto (the stage hops are device
+    links opened by IPC handle), DEFER's default failure and hang detection.  "hang": the middle stage's
+    compute loop is wedged over its control channel while its process and heartbeats stay alive, so only
+    its standing progress counter gives it away; "kill": its process is SIGKILLed.  Either way the
+    dispatcher must re-form the chain on the two survivors and replay, and every request must be answered
+    exactly once with the fp32 oracle's logits (the CPU twins are tests/test_hang_detect.py and
+    tests/test_integration.py)."""
     import os
     import signal
     import subprocess
@@ -279,25 +281,33 @@ def test_defer_gpu_hang_over_device_links():
         assert any("links=dev" in ev for _, ev in d.events), d.events[-5:]
         victim = d.pipeline.workers[1]
         t_hang = time.time()
-        d.inject_fault(victim, "hang")
+        if fault == "hang":
+            d.inject_fault(victim, "hang")
+        else:
+            os.killpg(procs[int(victim[2:])].pid, signal.SIGKILL)
         t_end = time.time() + 60
         while not d.recoveries and time.time() < t_end:
             try:
                 res.append(outq.get(timeout=0.05))
             except queue.Empty:
                 pass
-        assert d.hangs, d.events[-8:]
-        h = d.hangs[0]
-        detect_ms = (h["t"] - t_hang) * 1e3
-        print(f"hung stage {h['stage']} ({h['worker']}) detected {detect_ms:.0f} ms after the hang, "
-              f"threshold {h['threshold_ms']} ms; recoveries {d.recoveries[:1]}")
-        assert h["worker"] == victim and h["stage"] == 1
-        assert detect_ms < h["threshold_ms"] + 500.0
+        assert d.recoveries, d.events[-8:]
+        r = d.recoveries[0]
+        print(f"{fault}: recovery {r}; ready {(r['t_ready'] - t_hang) * 1e3:.0f} ms after the fault")
+        if fault == "hang":
+            assert d.hangs, d.events[-8:]
+            h = d.hangs[0]
+            detect_ms = (h["t"] - t_hang) * 1e3
+            print(f"hung stage {h['stage']} ({h['worker']}) detected {detect_ms:.0f} ms after the hang, "
+                  f"threshold {h['threshold_ms']} ms")
+            assert h["worker"] == victim and h["stage"] == 1
+            assert detect_ms < h["threshold_ms"] + 500.0
         for _ in range(10):
             res.append(outq.get(timeout=180))
         stop.set()
         feed.join()
-        d.inject_fault(victim, "clear")          # the wedged stage wakes up: its stale outputs must not leak out
+        if fault == "hang":
+            d.inject_fault(victim, "clear")      # the wedged stage wakes up: its stale outputs must not leak out
         time.sleep(0.5)
         total = sent[0]
         while len(res) < total:
