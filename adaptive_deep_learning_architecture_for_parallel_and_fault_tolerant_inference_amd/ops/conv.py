@@ -420,10 +420,7 @@ def f32_sk_plan(M: int, N: int, Kpad: int, cfg: int, mult: int = 1):
 
 def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int:
     """fp32 workspace a launch needs: split-K slabs or stream-K partial slots
-    (Winograd ksplit < 0: -ksplit slabs, the fixup fused into the kernel; pointwise K-split tail
-    configs: the tail partials, bounded)."""
-    if cfg in PW_F32_TAIL:
-        return PW_TAIL_WS
+    (Winograd ksplit < 0: -ksplit slabs, the fixup fused into the kernel)."""
     if ksplit > 1:
         return ksplit * M * N
     if ksplit < 0:
@@ -457,9 +454,7 @@ def wino_blocks(cfg: int, B: int, H: int, W: int, N: int) -> int:
 
 def f32_counter_elems(cfg: int, ksplit: int, B: int, H: int, W: int, OH: int, OW: int, N: int, Kpad: int) -> int:
     """int32 arrival counters an fp32 launch needs: stream-K tiles (v2 GEMM configs) or fused
-    Winograd split-K blocks, pointwise K-split tail tiles; 0 for plain launches."""
-    if cfg in PW_F32_TAIL:
-        return PW_TAIL_CTR
+    Winograd split-K blocks; 0 for plain launches."""
     if ksplit >= 0:
         return 0
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
@@ -539,11 +534,10 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 # 122 / 123: the streaming variant (no LDS, no block barrier; bm codes 1 / 2: two waves per SIMD / the
 # widest channel slice per wave)
 # 124: 123 with a 16-K-step activation ring (bm code 3; K in 256 / 512 / 1024)
-# 125 / 126: 122 / 123 with the left-over tile round split along K (bm codes 4 / 5; needs a workspace and
-#            zeroed counters, pw_f32_tail_plan): launches whose tiles leave a partial last round only
+# 125 / 126: 122 / 123 with the left-over tile round split by output fragment over otherwise idle waves
+#            (bm codes 4 / 5; FPW >= 2 and a partial last round only, pw_f32_tail_plan)
 PW_F32_CFGS = {120: 16, 121: 32, 122: 1, 123: 2, 124: 3, 125: 4, 126: 5}
 PW_F32_TAIL = frozenset((125, 126))
-PW_TAIL_WS, PW_TAIL_CTR = 1024 * 2 * 4 * 256, 1024      # bounds over every built instance
 PW_F32_FPW = {64: 2, 128: 4, 256: 2, 512: 1, 1024: 1}     # 16-channel fragments per wave
 PW_F32_KG = {1024: 2}                                       # K groups of waves (partials meet in LDS)
 PW_F32_BMS = {64: (1, 2, 4, 5, 16, 32), 128: (1, 2, 4, 5, 16, 32), 256: (1, 2, 3, 4, 5, 16, 32),
@@ -680,19 +674,11 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         if not f32_cfg_supported(cfg, C, N, pc) or int(ksplit or 1) != 1 or x.dim() != 4:
             raise ValueError(f"pointwise fp32 config {cfg}: 1x1 / s1-2 conv, K in {sorted(PW_F32_FPW)}, "
                              f"N (and the dual-output split) a multiple of the slice, ksplit 1")
-        ws_ptr = ctr_ptr = 0
-        if cfg in PW_F32_TAIL:
-            need, nctr = kernels().pw_f32_tail_plan(M, C, N, int(ns), PW_F32_CFGS[cfg])
-            if not need:
-                raise ValueError(f"pointwise fp32 config {cfg}: the tiles leave no tail round to split")
-            if workspace is None or workspace.numel() < need or workspace.dtype != torch.float32:
-                raise ValueError(f"pointwise fp32 config {cfg} needs an fp32 workspace of {need} elements")
-            if counters is None or counters.numel() < nctr or counters.dtype != torch.int32:
-                raise ValueError(f"pointwise fp32 config {cfg} needs {nctr} zeroed int32 counters")
-            ws_ptr, ctr_ptr = ptr(workspace), ptr(counters)
+        if cfg in PW_F32_TAIL and not kernels().pw_f32_tail_plan(M, C, N, int(ns), PW_F32_CFGS[cfg])[0]:
+            raise ValueError(f"pointwise fp32 config {cfg}: no partial last tile round to split")
         kernels().pw_f32_forward(ptr(x), ptr(pc.pwf), ptr(pc.bias), ptr(residual), ptr(out), M, C, N, int(relu),
                                  PW_F32_CFGS[cfg], stream_handle(stream), B, H, W, OH, OW, pc.stride, ptr(out2),
-                                 int(ns), int(relu2), ws_ptr, ctr_ptr)
+                                 int(ns), int(relu2))
         return out
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         # ksplit > 1: slabs + splitk_reduce_f32; ksplit <= -2: -ksplit slabs, the last split of

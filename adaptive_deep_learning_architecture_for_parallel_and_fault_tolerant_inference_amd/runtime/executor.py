@@ -474,7 +474,7 @@ class SliceExecutor:
         need = ctr = 0
         for i, (cfg, ks) in self.cfg.items():
             if self.fp32:
-                if ks != 1 or cfg in conv_ops.PW_F32_TAIL:
+                if ks != 1:
                     B, H, W, C, OH, OW, pc = self._conv_geom(i)
                     need = max(need, conv_ops.workspace_elems_f32(B * OH * OW, pc.cout, pc.Kpad, cfg, ks))
                     ctr = max(ctr, conv_ops.f32_counter_elems(cfg, ks, B, H, W, OH, OW, pc.cout, pc.Kpad))

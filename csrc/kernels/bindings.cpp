@@ -175,21 +175,19 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("pw_f32_supported", &adapt::pw_f32_supported);
   m.def("pw_f32_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, int M, int K, int N, int relu, int bm, u64 s,
-                             int B, int H, int W, int OH, int OW, int stride, u64 out2, int n_split, int relu2,
-                             u64 ws, u64 counters) {
+                             int B, int H, int W, int OH, int OW, int stride, u64 out2, int n_split, int relu2) {
     adapt::PwF32Params p{P<const float>(x), P<const float>(w), P<const float>(bias), P<const float>(res), P<float>(out),
-                         M, K, N, relu, B, H, W, OH, OW, stride, P<float>(out2), n_split, relu2, P<float>(ws),
-                         P<int>(counters)};
+                         M, K, N, relu, B, H, W, OH, OW, stride, P<float>(out2), n_split, relu2};
     check(adapt::pw_f32_forward(p, bm, S(s)), "pw_f32_forward");
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("out"), py::arg("M"), py::arg("K"),
      py::arg("N"), py::arg("relu"), py::arg("bm"), py::arg("s"), py::arg("B"), py::arg("H"), py::arg("W"),
      py::arg("OH"), py::arg("OW"), py::arg("stride"), py::arg("out2") = 0, py::arg("n_split") = 0,
-     py::arg("relu2") = 0, py::arg("ws") = 0, py::arg("counters") = 0);
+     py::arg("relu2") = 0);
   m.def("pw_f32_fpw", &adapt::pw_f32_fpw);
   m.def("pw_f32_tail_plan", [](int M, int K, int N, int n_split, int bm) {
-    int ws = 0, ctr = 0;
-    adapt::pw_f32_tail_plan(M, K, N, n_split, bm, &ws, &ctr);
-    return py::make_tuple(ws, ctr);
+    int tail = 0, parts = 0;
+    adapt::pw_f32_tail_plan(M, K, N, n_split, bm, &tail, &parts);
+    return py::make_tuple(tail, parts);
   });
   m.def("pw_pair_f32_supported", &adapt::pw_pair_f32_supported);
   m.def("pw_pair_f32_forward", [](u64 x, u64 w3, u64 b3, u64 res, u64 w1, u64 b1, u64 y, u64 z, int M, int cin,
@@ -242,6 +240,7 @@ PYBIND11_MODULE(_C, m) {
     return std::make_pair(g, it);
   });
   m.def("wino_set_debug", [](u64 buf) { adapt::wino_set_debug(P<unsigned long long>(buf)); });
+  m.def("pw_set_debug", [](u64 buf) { adapt::pw_set_debug(P<unsigned long long>(buf)); });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,
                                int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s, int variant) {
     py::gil_scoped_release nogil;

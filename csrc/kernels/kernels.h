@@ -248,11 +248,11 @@ struct PwF32Params {
   int B, H, W, OH, OW, stride;   // input / output maps (stride-s 1x1: M = B x OH x OW)
   float* out2;         // n_split > 0: columns >= n_split go to out2 (row stride N - n_split, relu2)
   int n_split, relu2;
-  float* ws;           // bm 4 / 5 (K-split tail): tail partials (pw_f32_tail_plan) ...
-  int* counters;       // ... and one zeroed arrival counter per (tail tile, channel group)
+  unsigned long long* dbg = nullptr;   // streaming kernels: 16 stamps per wave (tools/pw_timeline.py)
 };
+void pw_set_debug(unsigned long long* buf);
 int pw_f32_fpw(int K, int N, int n_split, int bm);
-void pw_f32_tail_plan(int M, int K, int N, int n_split, int bm, int* ws_elems, int* counters);
+void pw_f32_tail_plan(int M, int K, int N, int n_split, int bm, int* tail_tiles, int* parts);
 bool pw_f32_supported(int K, int N, int bm);
 hipError_t pw_f32_forward(const PwF32Params& p, int bm, hipStream_t s);
 hipError_t pw_pair_f32_forward(const PwPairF32Params& p, int cin, int co, int cm, int bm, int grid, hipStream_t s);

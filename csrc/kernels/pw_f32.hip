@@ -25,8 +25,6 @@ namespace adapt {
 
 namespace {
 
-constexpr int PW_CPOL_SC1 = 16;     // gfx950 cache policy: sc1 (write-through L2, bypass L1)
-
 template <int NCH>
 __device__ __forceinline__ int pswz32(int r, int c) {   // 16-byte chunk c of row r (NCH chunks per row)
   return r * (NCH * 16) + (((c & ~15) | ((c ^ r) & 15)) << 4);
@@ -201,39 +199,43 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
 // them on one XCD, so a tile crosses the fabric once per XCD.  FPW = 1 alternates two accumulators
 // by K step (a dependent 16x16x4 f32 MFMA waits 40 of its 32 issue cycles).
 //
-// TP > 0 (bm codes 4 / 5, cfgs 125 / 126): the tile count rarely divides into the slots -- ResNet-50's
+// TAIL (bm codes 4 / 5, cfgs 125 / 126): the tile count rarely divides into the slots -- ResNet-50's
 // 28x28 and 14x14 1x1 convs give every slot 6 tiles and an eighth of the slots a 7th, so 7/8 of the
-// chip idles through the last tile round (12 % of those launches).  Here the slots walk `full` tiles
-// each, then the `tail` left-over tiles are split along K into TP parts over tail x TP slots: a wave
-// MFMAs KH/TP K steps of one tail tile, publishes the partial accumulators to `ws` with sc1 stores
-// and bumps the tile's agent-scope arrival counter; the last of the TP waves adds the TP partials in
-// part order (the same sums whichever wave arrives last), then bias / residual / ReLU, and re-zeroes
-// the counter for the next launch.
-template <int KH, int FPW, int KPH, int H0>
-__device__ __forceinline__ void pw_tail_part(const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[FPW]) {
-  f32x4 xs[KPH];
+// chip idles through the last tile round (`tools/pw_timeline.py`: waves with 7 tiles end 3.4 us after
+// those with 6, one whole 4.6 us tile).  Here the slots walk `full` tiles each, then the `tail`
+// left-over tiles are split by output fragment: the FPW waves of slots (ti x FPW + j) -- all holding
+// the same filter slice as the tile's owner -- each run fragment j of tail tile ti over all of K and
+// store it.  No partial sums, so no workspace, fence or counter (a K split needs all three and its
+// chain of dependent round trips cost more than the tile it replaced: measured).
+template <int KH, int FPW, int D, int J>
+__device__ __forceinline__ void pw_tail_frag(const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[2]) {
+  f32x4 ring[D];
 #pragma unroll
-  for (int i = 0; i < KPH; ++i) xs[i] = *(const f32x4*)(xt + (H0 + i) * 16);
+  for (int i = 0; i < D; ++i) ring[i] = *(const f32x4*)(xt + i * 16);
 #pragma unroll
-  for (int i = 0; i < KPH; ++i)
+  for (int h = 0; h < KH; ++h) {
+    const f32x4 xf = ring[h % D];
+    if (h + D < KH) ring[h % D] = *(const f32x4*)(xt + (h + D) * 16);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int ss = 0; ss < 4; ++ss)
-#pragma unroll
-      for (int j = 0; j < FPW; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][H0 + i][ss], xs[i][ss], acc[j], 0, 0, 0);
+    for (int ss = 0; ss < 4; ++ss)       // two chains: a dependent 16x16x4 f32 MFMA waits 40 of 32 cycles
+      acc[h & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[J][h][ss], xf[ss], acc[h & 1], 0, 0, 0);
+  }
 }
-template <int KH, int FPW, int TP, int PART = 0>
-__device__ __forceinline__ void pw_tail_pick(int kp, const f32x4 (&wr)[FPW][KH], const float* xt,
-                                             f32x4 (&acc)[FPW]) {
-  if constexpr (PART < TP) {
-    if (kp == PART)                                   // wave-uniform
-      pw_tail_part<KH, FPW, KH / TP, PART * (KH / TP)>(wr, xt, acc);
-    else
-      pw_tail_pick<KH, FPW, TP, PART + 1>(kp, wr, xt, acc);
+template <int KH, int FPW, int D, int J = 0>
+__device__ __forceinline__ void pw_tail_pick(int jj, const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[2],
+                                             const f32x4 (&bias)[FPW], f32x4& b) {
+  if constexpr (J < FPW) {
+    if (jj == J) {                                    // wave-uniform
+      pw_tail_frag<KH, FPW, D, J>(wr, xt, acc);
+      b = bias[J];
+    } else {
+      pw_tail_pick<KH, FPW, D, J + 1>(jj, wr, xt, acc, bias, b);
+    }
   }
 }
 
-template <int K, int FPW, int D, int OCC, int TP = 0>
+template <int K, int FPW, int D, int OCC, bool TAIL = false>
 __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, int ncg, int nslots, int full,
                                                                  int tail) {
   constexpr int KH = K / 16;
@@ -248,6 +250,17 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
   const int ntiles = (p.M + 15) / 16;
   if (slot >= ntiles) return;
 
+  // per-wave stamps (p.dbg, tools/pw_timeline.py): [0] shader clock at start, [1] wall clock at start,
+  // [2] HW_ID, [3] XCC_ID, [4] weights + first ring landed, [5..12] end of tiles 0..7, [13] shader clock
+  // and [14] wall clock after the last stores, [15] tiles walked
+  unsigned long long* const dbg = p.dbg ? p.dbg + 16 * gw : nullptr;
+  const bool stamp = dbg && lane == 0;
+  if (stamp) {
+    dbg[0] = __builtin_amdgcn_s_memtime();
+    dbg[1] = __builtin_amdgcn_s_memrealtime();
+    dbg[2] = (unsigned)__builtin_amdgcn_s_getreg(0xF804);       // HW_ID
+    dbg[3] = (unsigned)__builtin_amdgcn_s_getreg(0x7814);       // XCC_ID
+  }
   f32x4 wr[FPW][KH];
   f32x4 bias[FPW];
 #pragma unroll
@@ -273,12 +286,17 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
     return p.x + (size_t)m * K + h * 16 + fq * 4;
   };
 
-  const int lim = TP > 0 ? full * nslots : ntiles;     // TP > 0: the host guarantees full >= 1
+  const int lim = TAIL ? full * nslots : ntiles;      // TAIL: the host guarantees full >= 1
   int t = slot;
   f32x4 ring[D];
   const float* xb = xptr(t, 0);
 #pragma unroll
   for (int i = 0; i < D; ++i) ring[i] = *(const f32x4*)(xb + i * 16);
+  if (dbg) {                                          // measurement only: wait for the prologue's loads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) dbg[4] = __builtin_amdgcn_s_memtime();
+  }
+  int nt = 0;
   while (true) {
     const int tn = t + nslots;
     const bool more = tn < lim;
@@ -318,49 +336,42 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
         *(f32x4*)(dst + (size_t)m * ldo + (cg * FPW + j) * 16 + fq * 4 - cof) = v;
       }
     }
+    if (stamp) dbg[5 + min(nt, 7)] = __builtin_amdgcn_s_memtime();
+    ++nt;
     if (!more) break;
     t = tn;
     xb = xn;
   }
-  if constexpr (TP > 0 && KH % TP == 0 && KH / TP <= 8) {
-    const int ti = slot / TP, kp = slot - ti * TP;
+  if (dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      dbg[13] = __builtin_amdgcn_s_memtime();
+      dbg[14] = __builtin_amdgcn_s_memrealtime();
+      dbg[15] = nt;
+    }
+  }
+  if constexpr (TAIL && FPW > 1) {
+    const int ti = slot / FPW, jj = slot - ti * FPW;
     if (ti >= tail) return;                           // wave-uniform
     const int tt = lim + ti;
-    f32x4 acc[FPW];
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    pw_tail_pick<KH, FPW, TP>(kp, wr, xptr(tt, 0), acc);
-    const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, 0x7fffffff,
-                                                                         0x00020000);
-    const int base = (ti * ncg + cg) * TP * FPW;      // 64-lane x float4 records
-#pragma unroll
-    for (int j = 0; j < FPW; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), wsr,
-                                             ((base + kp * FPW + j) * 64 + lane) * 16, 0, PW_CPOL_SC1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int last = 0;
-    if (lane == 0) {
-      int* ctr = p.counters + ti * ncg + cg;
-      last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == TP - 1;
-      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+    f32x4 b;
+    pw_tail_pick<KH, FPW, D>(jj, wr, xptr(tt, 0), acc, bias, b);
     const int m = tt * 16 + fr;
+    const int col = (cg * FPW + jj) * 16 + fq * 4;
+    f32x4 v = acc[0] + b;
+    v += acc[1];
+    if (has_res) v += *(const f32x4*)(p.res + (size_t)min(m, p.M - 1) * p.N + col);
 #pragma unroll
-    for (int j = 0; j < FPW; ++j) {
-      f32x4 pt[TP];
-#pragma unroll
-      for (int q = 0; q < TP; ++q)
-        pt[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              wsr, ((base + q * FPW + j) * 64 + lane) * 16, 0, PW_CPOL_SC1));
-      f32x4 v = pt[0];
-#pragma unroll
-      for (int q = 1; q < TP; ++q) v += pt[q];
-      v += bias[j];
-      if (has_res) v += *(const f32x4*)(p.res + (size_t)min(m, p.M - 1) * p.N + (cg * FPW + j) * 16 + fq * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
-      if (m < p.M) *(f32x4*)(dst + (size_t)m * ldo + (cg * FPW + j) * 16 + fq * 4 - cof) = v;
+    for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
+    if (m < p.M) *(f32x4*)(dst + (size_t)m * ldo + col - cof) = v;
+    if (dbg) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        dbg[13] = __builtin_amdgcn_s_memtime();
+        dbg[14] = __builtin_amdgcn_s_memrealtime();
+        dbg[15] = nt + 100;                           // tiles walked + 100: this wave ran a tail fragment
+      }
     }
   }
 }
@@ -436,18 +447,19 @@ int pw_f32_fpw(int K, int N, int n_split, int bm) {
   return bm <= 2 ? pw_stream_pick(K, N, n_split, bm == 2) : pw_f32_pick(K, N, n_split, bm);
 }
 
-// parts per tail tile of a K-split-tail launch (0: none fits): the most (8, 4, 2) whose tail x TP
-// waves fit in the slots, with whole K steps of <= 8 per part
-static int pw_tail_parts(int K, int ntiles, int nslots) {
-  const int full = ntiles / nslots, tail = ntiles - full * nslots, kh = K / 16;
-  if (full < 1 || tail < 1) return 0;
-  for (int tp = 8; tp >= 2; tp >>= 1)
-    if (tail * tp <= nslots && kh % tp == 0 && kh / tp <= 8) return tp;
-  return 0;
+// a channel-split tail launch fits: whole rounds first, and tail x FPW waves to split the rest
+static bool pw_tail_fits(int fpw, int ntiles, int nslots) {
+  const int full = ntiles / nslots, tail = ntiles - full * nslots;
+  return fpw > 1 && full >= 1 && tail >= 1 && tail * fpw <= nslots;
 }
 
+static unsigned long long* g_pw_dbg = nullptr;
+void pw_set_debug(unsigned long long* buf) { g_pw_dbg = buf; }
+
 template <int K, int F, int D, int O, bool TAIL>
-static hipError_t pw_stream_launch(const PwF32Params& p, int ncg, int ntiles, hipStream_t s) {
+static hipError_t pw_stream_launch(const PwF32Params& p_, int ncg, int ntiles, hipStream_t s) {
+  PwF32Params p = p_;
+  p.dbg = g_pw_dbg;
   int nslots = (1024 * O) / ncg;                      // ~O waves per SIMD over the chip
   if (nslots < 1) nslots = 1;
   if (nslots > ntiles) nslots = ntiles;
@@ -457,29 +469,19 @@ static hipError_t pw_stream_launch(const PwF32Params& p, int ncg, int ntiles, hi
     return hipGetLastError();
   } else {
     const int full = ntiles / nslots, tail = ntiles - full * nslots;
-    if (!p.ws || !p.counters) return hipErrorInvalidValue;
-    switch (pw_tail_parts(K, ntiles, nslots)) {
-#define PW_TAIL_CASE(TP_)                                                                                    \
-    case TP_:                                                                                                  \
-      if constexpr ((K / 16) % TP_ == 0 && (K / 16) / TP_ <= 8) {                                              \
-        hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O, TP_>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots, \
-                           full, tail);                                                                        \
-        return hipGetLastError();                                                                              \
-      }                                                                                                        \
-      break;
-      PW_TAIL_CASE(8)
-      PW_TAIL_CASE(4)
-      PW_TAIL_CASE(2)
-#undef PW_TAIL_CASE
-      default:
-        break;
+    if constexpr (F > 1) {
+      if (pw_tail_fits(F, ntiles, nslots)) {
+        hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O, true>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots,
+                           full, tail);
+        return hipGetLastError();
+      }
     }
   }
   return hipErrorInvalidValue;
 }
 
-void pw_f32_tail_plan(int M, int K, int N, int n_split, int bm, int* ws_elems, int* counters) {
-  *ws_elems = *counters = 0;
+void pw_f32_tail_plan(int M, int K, int N, int n_split, int bm, int* tail_tiles, int* parts) {
+  *tail_tiles = *parts = 0;
   const int fpw = pw_f32_fpw(K, N, n_split, bm);
   if (!fpw || (bm != 4 && bm != 5)) return;
   const int ncg = N / (16 * fpw), ntiles = (M + 15) / 16;
@@ -490,11 +492,9 @@ void pw_f32_tail_plan(int M, int K, int N, int n_split, int bm, int* ws_elems, i
   int nslots = (1024 * o) / ncg;
   if (nslots < 1) nslots = 1;
   if (nslots > ntiles) nslots = ntiles;
-  const int tp = pw_tail_parts(K, ntiles, nslots);
-  if (!tp) return;
-  const int tail = ntiles % nslots;
-  *ws_elems = tail * ncg * tp * fpw * 256;
-  *counters = tail * ncg;
+  if (!pw_tail_fits(fpw, ntiles, nslots)) return;
+  *tail_tiles = ntiles % nslots;
+  *parts = fpw;
 }
 
 bool pw_f32_supported(int K, int N, int bm) { return pw_f32_fpw(K, N, 0, bm) > 0; }

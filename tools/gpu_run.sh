@@ -37,6 +37,7 @@
 #             and the DMA hidden from the wait model (164-167)
 #   wino9     Winograd numerics + timings of 118 / 155 / 167 vs the counter-synchronised cfg 171, and the
 #             in-loop timelines of 170 (barrier) vs 172 (counters)
+#   pwtl      pointwise numerics, timings and per-wave timelines (tools/pw_timeline.py)
 #   pw6       pointwise numerics + isolated timings incl. the K-split tail configs 125 / 126
 #   pmcstem   two PMC passes over the fp32 stem (tools/stem_bench.py)
 #   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
@@ -109,6 +110,12 @@ for p in "${P[@]}"; do
               steps+=("300|$out/pw5_bench|python -u tools/conv_bench_f32.py --only 18,20,38,120,122,123,124 --ks 1,-1,-2 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,28,28,512,1280,1,2,0,0 --shape 32,14,14,1024,2560,1,2,0,0") ;;
     pw6)      steps+=("200|$out/pytest_pw|python -u -m pytest tests/test_pw_f32_gpu.py -v -x --timeout 120 --timeout-method thread")
               for rep in a b; do steps+=("300|$out/pw6_bench_$rep|python -u tools/conv_bench_f32.py --only 18,38,122,123,124,125,126 --ks 1,-2 --shape 32,28,28,512,128,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,56,56,64,256,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0"); done ;;
+    pwtl)     steps+=("200|$out/pytest_pw|python -u -m pytest tests/test_pw_f32_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/pw_bench|python -u tools/conv_bench_f32.py --only 122,123,125,126 --ks 1 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1 --shape 32,56,56,64,256,1,1,0,1")
+              for spec in "32,28,28,512,128:123" "32,14,14,256,1024:123" "32,56,56,256,64:123" "32,28,28,512,128:126" "32,14,14,256,1024:126"; do
+                IFS=':' read -r shp cfg <<< "$spec"
+                steps+=("120|$out/pwtl_${cfg}_${shp//,/x}|python -u tools/pw_timeline.py --shape $shp --cfg $cfg --json gpurun_out/$out/pwtl_${cfg}_${shp//,/x}.json")
+              done ;;
     wino8)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
               for rep in a b; do steps+=("300|$out/wino8_bench_$rep|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 116,117,118,155,162,163,164,165,166,167 --ks 1,-2,-4"); done ;;
     wino9)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py -v -x --timeout 120 --timeout-method thread")
