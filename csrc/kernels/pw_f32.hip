@@ -196,8 +196,8 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
 // staging stores and an exposed epilogue per 16-pixel tile; the GEMM sweep put it at 61-80 % of
 // the fp32 MFMA rate inside its loop plus ~6 us per launch (profiles/r4/gemm1x1_vs_k.log).  The
 // waves that read one tile are the ncg channel groups of one slot; the XCD-aware block order keeps
-// them on one XCD, so a tile crosses the fabric once per XCD.  FPW = 1 alternates two accumulators
-// by K step (a dependent 16x16x4 f32 MFMA waits 40 of its 32 issue cycles).
+// them on one XCD, so a tile crosses the fabric once per XCD.  FPW < 4 spreads each fragment over
+// 4 / FPW accumulators by MFMA step, so every chain's consecutive MFMAs sit 4 apart.
 //
 // TAIL (bm codes 4 / 5, cfgs 125 / 126): the tile count rarely divides into the slots -- ResNet-50's
 // 28x28 and 14x14 1x1 convs give every slot 6 tiles and an eighth of the slots a 7th, so 7/8 of the
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(512, 1) void pw_f32_kernel(PwF32Params p) {
 // store it.  No partial sums, so no workspace, fence or counter (a K split needs all three and its
 // chain of dependent round trips cost more than the tile it replaced: measured).
 template <int KH, int FPW, int D, int J>
-__device__ __forceinline__ void pw_tail_frag(const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[2]) {
+__device__ __forceinline__ void pw_tail_frag(const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[4]) {
   f32x4 ring[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) ring[i] = *(const f32x4*)(xt + i * 16);
@@ -218,16 +218,19 @@ __device__ __forceinline__ void pw_tail_frag(const f32x4 (&wr)[FPW][KH], const f
     if (h + D < KH) ring[h % D] = *(const f32x4*)(xt + (h + D) * 16);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int ss = 0; ss < 4; ++ss)       // two chains: a dependent 16x16x4 f32 MFMA waits 40 of 32 cycles
-      acc[h & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[J][h][ss], xf[ss], acc[h & 1], 0, 0, 0);
+    for (int ss = 0; ss < 4; ++ss)       // four chains: a dependent 16x16x4 f32 MFMA waits 40 of 32 cycles
+      acc[ss] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[J][h][ss], xf[ss], acc[ss], 0, 0, 0);
   }
 }
 template <int KH, int FPW, int D, int J = 0>
-__device__ __forceinline__ void pw_tail_pick(int jj, const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[2],
+__device__ __forceinline__ void pw_tail_pick(int jj, const f32x4 (&wr)[FPW][KH], const float* xt, f32x4 (&acc)[4],
                                              const f32x4 (&bias)[FPW], f32x4& b) {
   if constexpr (J < FPW) {
     if (jj == J) {                                    // wave-uniform
-      pw_tail_frag<KH, FPW, D, J>(wr, xt, acc);
+      // the whole fragment's activations requested at once (the main ring is dead by now): one
+      // fragment has only 4 MFMAs a K step, too few to hide a refill D steps ahead
+      constexpr int TD = KH < 32 ? KH : 32;
+      pw_tail_frag<KH, FPW, TD, J>(wr, xt, acc);
       b = bias[J];
     } else {
       pw_tail_pick<KH, FPW, D, J + 1>(jj, wr, xt, acc, bias, b);
@@ -239,7 +242,10 @@ template <int K, int FPW, int D, int OCC, bool TAIL = false>
 __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, int ncg, int nslots, int full,
                                                                  int tail) {
   constexpr int KH = K / 16;
-  constexpr int NA = FPW >= 2 ? 1 : 2;                // accumulator sets per fragment
+  // accumulator chains per fragment, taken by MFMA step ss: consecutive MFMAs into one chain sit >= 4
+  // MFMAs apart (a dependent 16x16x4 f32 MFMA would wait 40 cycles past its 32 issue cycles -- the FPW = 1
+  // twins used to chain all four steps of a K step back to back: 8.8 us a tile instead of 4.6)
+  constexpr int NA = FPW >= 4 ? 1 : 4 / FPW;
   static_assert(KH % D == 0, "ring depth must divide the K steps");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -323,13 +329,14 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
       for (int ss = 0; ss < 4; ++ss)
 #pragma unroll
         for (int j = 0; j < FPW; ++j)
-          acc[h % NA][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][h][ss], xf[ss], acc[h % NA][j], 0, 0, 0);
+          acc[ss % NA][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[j][h][ss], xf[ss], acc[ss % NA][j], 0, 0, 0);
     }
     if (m < p.M) {
 #pragma unroll
       for (int j = 0; j < FPW; ++j) {
         f32x4 v = acc[0][j] + bias[j];
-        if constexpr (NA > 1) v += acc[1][j];
+#pragma unroll
+        for (int a = 1; a < NA; ++a) v += acc[a][j];
         if (has_res) v += res[j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
@@ -354,13 +361,17 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
     const int ti = slot / FPW, jj = slot - ti * FPW;
     if (ti >= tail) return;                           // wave-uniform
     const int tt = lim + ti;
-    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) acc[a] = (f32x4){0.f, 0.f, 0.f, 0.f};
     f32x4 b;
     pw_tail_pick<KH, FPW, D>(jj, wr, xptr(tt, 0), acc, bias, b);
     const int m = tt * 16 + fr;
     const int col = (cg * FPW + jj) * 16 + fq * 4;
     f32x4 v = acc[0] + b;
     v += acc[1];
+    v += acc[2];
+    v += acc[3];
     if (has_res) v += *(const f32x4*)(p.res + (size_t)min(m, p.M - 1) * p.N + col);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);

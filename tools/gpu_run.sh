@@ -111,7 +111,7 @@ for p in "${P[@]}"; do
     pw6)      steps+=("200|$out/pytest_pw|python -u -m pytest tests/test_pw_f32_gpu.py -v -x --timeout 120 --timeout-method thread")
               for rep in a b; do steps+=("300|$out/pw6_bench_$rep|python -u tools/conv_bench_f32.py --only 18,38,122,123,124,125,126 --ks 1,-2 --shape 32,28,28,512,128,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,56,56,64,256,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0"); done ;;
     pwtl)     steps+=("200|$out/pytest_pw|python -u -m pytest tests/test_pw_f32_gpu.py -v -x --timeout 120 --timeout-method thread")
-              steps+=("300|$out/pw_bench|python -u tools/conv_bench_f32.py --only 122,123,125,126 --ks 1 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1 --shape 32,56,56,64,256,1,1,0,1")
+              steps+=("300|$out/pw_bench|python -u tools/conv_bench_f32.py --only 18,38,122,123,124,125,126 --ks 1,-2 --shape 32,28,28,512,128,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1 --shape 32,56,56,64,256,1,1,0,1 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1")
               for spec in "32,28,28,512,128:123" "32,14,14,256,1024:123" "32,56,56,256,64:123" "32,28,28,512,128:126" "32,14,14,256,1024:126"; do
                 IFS=':' read -r shp cfg <<< "$spec"
                 steps+=("120|$out/pwtl_${cfg}_${shp//,/x}|python -u tools/pw_timeline.py --shape $shp --cfg $cfg --json gpurun_out/$out/pwtl_${cfg}_${shp//,/x}.json")
