@@ -64,7 +64,10 @@ def test_heartbeat_carries_progress_counter():
 @pytest.mark.parametrize("transport", ["tcp", "gloo"])
 def test_hung_stage_detected_and_replayed_exactly_once(tiny, transport):
     d = DEFER(membership_port=0, result_port=0, worker_wait=20, batch=1, max_inflight=4, weight_codec="lz4",
-              min_workers=3, replicas=1, task_timeout=30, transport=transport, hang_min_s=0.2, hang_factor=10)
+              min_workers=3, replicas=1, task_timeout=30, transport=transport, hang_min_s=0.5, hang_factor=10)
+    # hang_min_s 0.5 (default 0.2): three CPU worker processes share this host with the test runner, and a
+    # healthy CPU stage can stall > 200 ms under that contention -- the GPU twin
+    # (tests/test_defer_gpu.py::test_defer_gpu_fault_over_device_links) runs at the default 0.2 s
     d.membership_server.start()
     procs = [_spawn_worker(d.membership_port, f"h{i}") for i in range(3)]
     stop = threading.Event()
@@ -87,7 +90,7 @@ def test_hung_stage_detected_and_replayed_exactly_once(tiny, transport):
         feed = threading.Thread(target=feeder, daemon=True)
         feed.start()
         res = [outq.get(timeout=120) for _ in range(40)]
-        assert len(d.pipeline.workers) == 3
+        assert len(d.pipeline.workers) == 3, (d.hangs, d.events[-6:])
         victim = d.pipeline.workers[1]
         assert d.hang_threshold(d.pipeline.replica, d.pipeline.epoch) is not None
         t_hang = time.time()
@@ -104,8 +107,8 @@ def test_hung_stage_detected_and_replayed_exactly_once(tiny, transport):
         print(f"{transport}: hung stage {h['stage']} ({h['worker']}) detected {detect_ms:.0f} ms after the hang, "
               f"threshold {h['threshold_ms']} ms")
         assert h["worker"] == victim and h["stage"] == 1
-        # the threshold is max(10 x stage time, 200 ms); a loaded CI CPU can stretch the stage time
-        assert detect_ms < max(300.0, h["threshold_ms"] + 100.0)
+        # the threshold is max(10 x stage time, 500 ms); a loaded CI CPU can stretch the stage time
+        assert detect_ms < max(600.0, h["threshold_ms"] + 100.0)
         for _ in range(20):
             res.append(outq.get(timeout=120))
         stop.set()
