@@ -117,7 +117,8 @@ def cmd_serve(argv):
             dev = f"cuda:{i}"
         procs.append(subprocess.Popen([sys.executable, "-m", f"{PKG}.node", "--membership-port",
                                        str(d.membership_port), "--data-port", "0", "--config-port", "0",
-                                       "--device", dev, "--id", f"local{i}", "--ttl", str(cfg.lease_ttl)],
+                                       "--device", dev, "--id", f"local{i}", "--ttl", str(cfg.lease_ttl),
+                                       "--parent-pid", str(os.getpid())],
                                       start_new_session=True))
     inq, outq = queue.Queue(cfg.max_inflight * 2), queue.Queue()
     rng = np.random.default_rng(cfg.seed)

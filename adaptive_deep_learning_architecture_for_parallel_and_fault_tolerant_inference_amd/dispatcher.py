@@ -139,7 +139,7 @@ class DEFER:
                  resident: bool = True, prepare: bool = True, max_replays: int = 3,
                  quarantine_s: float = 30.0, hb_timeout: float = 0.25, precision: str = "fp32",
                  ingest: str = "auto", preprocess: str = "none", links: str = "auto",
-                 hang_factor: float = 20.0, hang_min_s: float = 0.2) -> None:
+                 hang_factor: float = 20.0, hang_min_s: Optional[float] = None) -> None:
         """codec: compression of the TCP hops ("none" default: on a local network
         the host LZ4 of bf16/fp32 activations costs more than it saves, ratio
         ~1.02; "lz4", "zfp+lz4", "zvc" on request).  link_codec: compression of
@@ -166,8 +166,12 @@ class DEFER:
         dead worker (0.06 s is the fault benchmarks' setting; the 0.25 s default
         tolerates a heartbeat thread delayed on a loaded host).  hang_factor /
         hang_min_s: a stage whose progress counter stands still for
-        max(hang_factor x micro-batch period, hang_min_s) while its replica
-        holds work is hung.  task_timeout: age (from submission) at which an
+        max(hang_factor x micro-batch period, the replica's floor) while its
+        replica holds work is hung; the floor is hang_min_s when given, else
+        derived per replica (`hang_floor`): 0.2 s when every stage runs on a
+        GPU, 0.75 s when any runs on a CPU (a healthy CPU stage sharing a host
+        stalls past 200 ms under contention), raised to 8 x the measured jitter
+        of the replica's micro-batch period.  task_timeout: age (from submission) at which an
         in-flight request marks its replica failed; None (default) = per
         replica, max(10 s for an all-GPU replica / 30 s when any stage runs
         on a CPU, 4 x max_inflight x the replica's measured micro-batch
@@ -256,8 +260,9 @@ class DEFER:
         self._hb_port = 0
         self._hb_suspects: set = set()
         self.hang_factor = hang_factor
-        self.hang_min_s = hang_min_s
+        self.hang_min_s = hang_min_s                          # None: derived per replica (hang_floor)
         self._rep_period: Dict[int, Tuple[int, float]] = {}   # replica -> (epoch, EWMA busy completion interval)
+        self._rep_jitter: Dict[int, Tuple[int, float]] = {}   # replica -> (epoch, EWMA |interval - period|)
         self._rep_last_done: Dict[int, Tuple[int, float]] = {}
         self.hangs: List[dict] = []
         self._epoch_results: Dict[int, int] = {}    # epoch -> results received from its last stage
@@ -484,21 +489,47 @@ class DEFER:
             return
         dt = now - last[1]
         ep, old = self._rep_period.get(replica, (epoch, None))
-        self._rep_period[replica] = (epoch, dt if old is None or ep != epoch else 0.8 * old + 0.2 * dt)
+        fresh = old is None or ep != epoch
+        self._rep_period[replica] = (epoch, dt if fresh else 0.8 * old + 0.2 * dt)
+        jep, jold = self._rep_jitter.get(replica, (epoch, 0.0))
+        dev = 0.0 if fresh else abs(dt - old)
+        self._rep_jitter[replica] = (epoch, dev if jep != epoch else 0.8 * jold + 0.2 * dev)
 
     HANG_WARMUP = 4          # micro-batches of an epoch a stage completes before the normal threshold applies
     HANG_WARMUP_S = 2.0      # its threshold until then (seconds)
 
+    HANG_GPU_MIN_S = 0.2     # derived hang floor of an all-GPU replica
+    HANG_CPU_MIN_S = 0.75    # ... of a replica with a CPU stage (tests/test_hang_detect.py: CPU stages sharing a
+                             # host with the test runner stalled > 200 ms in 3 of 9 healthy runs)
+    HANG_JITTER_X = 8.0      # the floor also covers this many times the period's measured jitter
+
+    def hang_floor(self, replica: int, epoch: Optional[int] = None) -> float:
+        """The shortest no-progress time that can make a stage of `replica` hung:
+        `hang_min_s` when the user gave one, else by device kind (all-GPU 0.2 s,
+        any CPU stage 0.75 s) and at least HANG_JITTER_X x the EWMA jitter of
+        the replica's micro-batch period in `epoch`."""
+        if self.hang_min_s is not None:
+            return float(self.hang_min_s)
+        with self._rep_lock:
+            p = self.replicas.get(replica)
+        recs = p.records if p is not None else []
+        gpu = bool(recs) and all(str(r.get("device", "")).startswith("cuda") for r in recs)
+        floor = self.HANG_GPU_MIN_S if gpu else self.HANG_CPU_MIN_S
+        jit = self._rep_jitter.get(replica)
+        if jit is not None and (epoch is None or jit[0] == epoch):
+            floor = max(floor, self.HANG_JITTER_X * jit[1])
+        return floor
+
     def hang_threshold(self, replica: int, epoch: int, stage_s: float = 0.0) -> Optional[float]:
         """Seconds without progress that make a stage of `replica` hung:
         max(hang_factor x the stage's own reported time per micro-batch (else
-        the replica's measured period), hang_min_s).  None until the epoch has
+        the replica's measured period), hang_floor).  None until the epoch has
         completed work (its first micro-batches may be captures and warm-ups)."""
         ent = self._rep_period.get(replica)
         if ent is None or ent[0] != epoch:
             return None
         t = stage_s if stage_s > 0 else ent[1]
-        return max(self.hang_factor * t, self.hang_min_s)
+        return max(self.hang_factor * t, self.hang_floor(replica, epoch))
 
     def _note_counters(self, prog: Dict[str, Tuple[int, float, float, int]], now: float) -> None:
         """Remember when each stage's progress counter reached each value it was
@@ -550,7 +581,7 @@ class DEFER:
             with self.inflight_lock:
                 oldest_task = max((now - t["start_time"] for t in self.inflight_tasks.values()
                                    if t["replica"] == p.replica and t["epoch"] == p.epoch), default=0.0)
-            if oldest_task <= self.hang_min_s:
+            if oldest_task <= self.hang_floor(p.replica, p.epoch):
                 continue
             done = self._epoch_results.get(p.epoch, 0)
             t0 = self._epoch_t0.get(p.epoch, now)
@@ -1468,11 +1499,14 @@ class DEFER:
         now = now or time.time()
         return sum(1 for t in self.completion_times if now - window <= t <= now) * self.batch / window
 
-    def recovery_to_steady_ms(self, t_kill: Optional[float] = None, window: float = 0.5,
-                              frac: float = 0.95) -> List[float]:
-        """Per recovery: ms from the failure (`t_kill` if the caller knows when it
-        injected it, else the detection time) until the windowed throughput first
-        returns to >= frac x the post-recovery steady state."""
+    def recovery_windows(self, t_kill: Optional[float] = None, window: float = 0.5, frac: float = 0.95,
+                         step: float = 0.005) -> List[dict]:
+        """Per recovery, the first `window`-second sliding window that lies wholly after the failure
+        (`t_kill` if the caller knows when it injected it, else the detection time) and whose throughput
+        is >= frac x the post-recovery steady state, scanned in `step` seconds:
+        {"start_ms", "end_ms" (= recovery-to-steady), "ready_ms" (the new epoch serving), "steady_img_s"},
+        all from the failure.  The end of that window is the first moment the recovered throughput is
+        observable, so recovery-to-steady is never shorter than the window itself."""
         out = []
         ts = np.array(self.completion_times)
         for r in self.recoveries:
@@ -1483,15 +1517,19 @@ class DEFER:
             if steady_span <= 0:
                 continue
             steady = (len(post) - len(post) // 2 - 1) / steady_span
-            t = t_kill if t_kill is not None else r["t_fail"]
-            t0 = t
-            found = None
-            while t < post[-1]:
+            t0 = t_kill if t_kill is not None else r["t_fail"]
+            t = t0
+            while t + window <= post[-1]:
                 n = np.count_nonzero((ts > t) & (ts <= t + window))
-                if t > r["t_ready"] and n / window >= frac * steady:
-                    found = t
+                if n / window >= frac * steady:
+                    out.append({"start_ms": (t - t0) * 1e3, "end_ms": (t + window - t0) * 1e3,
+                                "ready_ms": (r["t_ready"] - t0) * 1e3, "steady_img_s": steady * self.batch})
                     break
-                t += window / 10
-            if found is not None:
-                out.append((found - t0) * 1e3)
+                t += step
         return out
+
+    def recovery_to_steady_ms(self, t_kill: Optional[float] = None, window: float = 0.5,
+                              frac: float = 0.95) -> List[float]:
+        """Per recovery: ms from the failure until the END of the first 0.5 s window after it whose
+        throughput is back to >= 95 % of the new steady state (`recovery_windows`)."""
+        return [w["end_ms"] for w in self.recovery_windows(t_kill, window, frac)]

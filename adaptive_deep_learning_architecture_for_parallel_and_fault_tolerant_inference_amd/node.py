@@ -985,6 +985,35 @@ class Node:
                     conn.close()
 
 
+def _follow_parent(ppid: int) -> None:
+    """Die with the launcher: PR_SET_PDEATHSIG (SIGTERM when the parent exits), a check that it has
+    not already gone, and a watcher thread for launchers that are not the direct parent."""
+    import ctypes
+    import signal as _signal
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(_signal.SIGTERM), 0, 0, 0)   # PR_SET_PDEATHSIG = 1
+    except (OSError, AttributeError):
+        pass
+
+    def gone() -> bool:
+        try:
+            os.kill(ppid, 0)
+            return False
+        except ProcessLookupError:
+            return True
+        except PermissionError:
+            return False
+
+    if gone():
+        os._exit(0)
+
+    def watch():
+        while not gone():
+            time.sleep(0.5)
+        os._exit(0)
+    threading.Thread(target=watch, daemon=True, name="parent-watch").start()
+
+
 def main(argv=None):
     # epoch communicators are aborted by this runtime (re-plan, stall watch): the
     # NCCL watchdog must not kill the worker over receives an idle pipeline keeps posted
@@ -1002,7 +1031,12 @@ def main(argv=None):
     ap.add_argument("--id", default=None)
     ap.add_argument("--ttl", type=float, default=1.0, help="membership lease TTL (s)")
     ap.add_argument("--chunk-size", type=int, default=512 * 1000)
+    ap.add_argument("--parent-pid", type=int, default=0,
+                    help="exit when this process (the launcher) is gone: a launcher killed at its time limit "
+                         "must not leave GPU workers behind")
     a = ap.parse_args(argv)
+    if a.parent_pid:
+        _follow_parent(a.parent_pid)
     node = Node(a.dispatcher, a.membership_port, a.data_port, a.config_port, a.device, a.id, a.chunk_size,
                 heartbeat_ttl=a.ttl)
     print(f"node {node.node_id} device={node.device} data={node.data_port} config={node.config_port}", flush=True)

@@ -314,6 +314,20 @@ def plan_subruns(args, world: int, backend: str) -> list:
     return subs
 
 
+def subrun_limit(plan: list, i: int, left: float) -> float:
+    """Time limit of sub-run `i` of `plan` with `left` seconds of the shared budget remaining: its own
+    limit, but never eating into the limits of the sub-runs still to come (the fault run, last, keeps
+    its whole limit even when the pipeline sub-runs before it hit theirs)."""
+    reserve = sum(p[4] for p in plan[i + 1:])
+    return max(0.0, min(plan[i][4], left - reserve))
+
+
+def fault_ready_timeout(limit_s: float, duration: float) -> float:
+    """fault_run's wait for its first pipeline, so that the run ends inside its limit: the limit less
+    the measured window, the settle time (~4 s) and the exactly-once drain (<= 60 s)."""
+    return max(20.0, limit_s - duration - 70.0)
+
+
 def run_subrun(name: str, kind: str, argv: list, nprocs: int, limit_s: float, label: str, launch) -> dict:
     """One sub-run as a fresh job (a process per rank, its own time limit);
     returns its record, or {"ok": false, "error": ...}.  Never raises."""
@@ -489,12 +503,15 @@ def main(argv=None):
     torch.cuda.empty_cache()
     subs = {}
     budget_end = time.monotonic() + args.sub_budget
-    for name, kind, sargv, nprocs, limit, label in plan_subruns(args, world, backend):
-        left = budget_end - time.monotonic()
-        if left < 30:
+    plan = plan_subruns(args, world, backend)
+    for i, (name, kind, sargv, nprocs, limit, label) in enumerate(plan):
+        lim = subrun_limit(plan, i, budget_end - time.monotonic())
+        if lim < 30:
             subs[name] = {"ok": False, "error": f"sub-run budget ({args.sub_budget:.0f} s) spent", "label": label}
             continue
-        subs[name] = run_subrun(name, kind, sargv, nprocs, min(limit, left), label, launch)
+        if kind == "fault":
+            sargv = sargv + ["--ready-timeout", f"{fault_ready_timeout(lim, args.fault_duration):.0f}"]
+        subs[name] = run_subrun(name, kind, sargv, nprocs, lim, label, launch)
     print(json.dumps(make_record(args, world, n_gpus, backend, value, elapsed, image, info, bf16, subs=subs)),
           flush=True)
 

@@ -234,6 +234,11 @@ PYBIND11_MODULE(_C, m) {
     adapt::conv_wino_sk_plan(units, kc, mult, &g, &it, &smax);
     return py::make_tuple(g, it, smax);
   });
+  m.def("conv_wino4_pieces", [](int B, int H, int W) {
+    int align = 0;
+    const int pieces = adapt::conv_wino4_pieces(B, H, W, &align);
+    return py::make_tuple(pieces, align);
+  });
   m.def("conv_f32g_sk_plan", [](int tiles, int kt, int mult) {
     int g = 0, it = 0;
     adapt::conv_f32g_sk_plan(tiles, kt, mult, &g, &it);

@@ -159,6 +159,7 @@ struct WinoF32Params {
   int sk_iters;       // > 0: stream-K, (unit, chunk) iterations per block (conv_wino_sk_plan), ksplit 1
   int sk_mult;        // stream-K grid: about sk_mult x 256 blocks
   unsigned long long* dbg;   // measurement only (tools/wino_timeline.py): 16 words per block, else null
+  int flags;          // F(4x4) (conv_wino4_f32.hip): 1 = segment bases aligned to the bank phase of their tiles
 };
 // tools/wino_timeline.py: v3 Winograd launches (PL != 0) stamp their phases into buf while it is set
 void wino_set_debug(unsigned long long* buf);
@@ -166,6 +167,11 @@ void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* 
 bool conv_wino_f32_ok(int cfg, int C, int N);
 bool conv_wino_f32_cfg(int cfg, int* nw, int* fn);
 hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
+// fp32 Winograd F(4x4, 3x3) (conv_wino4_f32.hip, cfg ids >= 200): u = transformed weights in fragment order
+// [N/32][C/8][36 positions][2 fragments][64 lanes][2] (ops/conv.py wino4_pack_np); TH / TW / T count 4x4 tiles
+int conv_wino4_pieces(int B, int H, int W, int* align = nullptr);
+bool conv_wino4_f32_ok(int C, int N);
+hipError_t conv_wino4_f32_launch(const WinoF32Params& p, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,

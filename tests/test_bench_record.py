@@ -91,11 +91,25 @@ def test_subrun_plan_covers_every_baseline_config():
 
 
 def test_subrun_time_limits_fit_the_driver():
-    """Worst case (every sub-run of N=4 hits its limit) stays under the budget."""
+    """Worst case (every sub-run of N hits its limit) stays under the budget, and the fault sub-run
+    (last) keeps its whole limit even when the pipeline sub-runs before it hit theirs."""
     b = _bench()
     a = b.parse([])
     assert a.sub_budget <= 420
     assert all(v <= a.sub_budget for v in b.SUB_LIMIT_S.values())
+    for world in (2, 4, 8):
+        plan = b.plan_subruns(a, world, "nccl")
+        assert plan[-1][0] == "fault"
+        left, total = a.sub_budget, 0.0
+        for i in range(len(plan)):
+            lim = b.subrun_limit(plan, i, left)
+            if plan[i][0] == "fault":
+                assert lim == min(b.SUB_LIMIT_S["fault"], a.sub_budget)
+                # fault_run's own phases fit its limit: ready wait + settle + window + drain
+                assert b.fault_ready_timeout(lim, a.fault_duration) + a.fault_duration + 70.0 <= lim + 1e-9
+            left -= lim                      # every sub-run takes its whole limit
+            total += lim
+        assert total <= a.sub_budget + 1e-9
 
 
 class _FakeLaunch:

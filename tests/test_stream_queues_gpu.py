@@ -39,7 +39,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _probe(queues: int) -> dict:
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(queues))
+    # ADAPT_HW_QUEUES: the package applies it as given at import (utils/hwqueues.py), lower counts included
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(queues), ADAPT_HW_QUEUES=str(queues))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "queue_probe.py")], env=env,
                        capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
