@@ -111,9 +111,16 @@ class RcclComm:
         self.name = key
         self.nranks, self.rank = nranks, rank
         self.timeout_s = timeout_s
-        uid = _exchange_uid(store, f"{key}/uid", rank, timeout_s=timeout_s)
+        from . import loopback_comm
+        self.loopback = loopback_comm.selected()
         self.t0 = time.perf_counter()
-        self._c = native().Comm(uid, nranks, rank, self.device.index or 0, False, key[-63:])
+        if self.loopback:
+            # TEST-ONLY: two ranks on one GPU (parallel/loopback_comm.py), never a default or a fallback
+            self._c = loopback_comm.LoopbackComm(store, key, nranks, rank, self.device.index or 0)
+        else:
+            uid = _exchange_uid(store, f"{key}/uid", rank, timeout_s=timeout_s)
+            self.t0 = time.perf_counter()
+            self._c = native().Comm(uid, nranks, rank, self.device.index or 0, False, key[-63:])
         if watch_us > 0:
             self._c.start_watch(watch_us, abort_on_error)
         self.stream = stream if stream is not None else torch.cuda.Stream(device=self.device)

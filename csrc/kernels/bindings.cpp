@@ -116,6 +116,23 @@ PYBIND11_MODULE(_C, m) {
                               OH, OW, pad_t, pad_l, pool, PH, PW, pool_pad, S(s)),
           "stem_forward");
   });
+  m.def("lb_wait", [](u64 ctr, unsigned long long target, u64 abort_word, u64 status, double timeout_ms, u64 s) {
+    check(adapt::lb_wait(P<const unsigned long long>(ctr), target, P<const int>(abort_word), P<int>(status),
+                         timeout_ms, S(s)),
+          "lb_wait");
+  });
+  m.def("lb_signal", [](u64 ctr, unsigned long long value, u64 s) {
+    check(adapt::lb_signal(P<unsigned long long>(ctr), value, S(s)), "lb_signal");
+  });
+  // page-lock a host range for the GPU (mapped, portable) and return its device address
+  m.def("host_register", [](u64 ptr, size_t n) {
+    check(hipHostRegister(reinterpret_cast<void*>(ptr), n, hipHostRegisterMapped | hipHostRegisterPortable),
+          "host_register");
+    void* d = nullptr;
+    check(hipHostGetDevicePointer(&d, reinterpret_cast<void*>(ptr), 0), "host_register: device pointer");
+    return reinterpret_cast<u64>(d);
+  });
+  m.def("host_unregister", [](u64 ptr) { check(hipHostUnregister(reinterpret_cast<void*>(ptr)), "host_unregister"); });
   m.def("spin_flag", [](u64 flag, u64 out, double timeout_ms, u64 s) {
     check(adapt::spin_flag(P<const int>(flag), P<int>(out), timeout_ms, S(s)), "spin_flag");
   });
@@ -245,6 +262,7 @@ PYBIND11_MODULE(_C, m) {
     return std::make_pair(g, it);
   });
   m.def("wino_set_debug", [](u64 buf) { adapt::wino_set_debug(P<unsigned long long>(buf)); });
+  m.def("wino4_set_debug", [](u64 buf) { adapt::wino4_set_debug(P<unsigned long long>(buf)); });
   m.def("pw_set_debug", [](u64 buf) { adapt::pw_set_debug(P<unsigned long long>(buf)); });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,
                                int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s, int variant) {

@@ -54,6 +54,13 @@ constexpr int W4_WCH = W4_SLOT / 4;             // floats of one chunk's weights
 constexpr int W4_CPOL_SC1 = 16;                 // gfx950 cache policy: sc1
 constexpr int W4_MAXSEG = 8;                    // tile-row segments per wave (TW >= 2)
 
+// measurement only (tools/wino4_timeline.py): per wave 8 words -- shader clock at start / table built /
+// first patch transformed / K loop done / partial outputs staged / stores issued, and the 100 MHz wall
+// clock at start and end; lane 0 writes them with vector stores
+__device__ __forceinline__ void w4_stamp(unsigned long long* d, int i) {
+  if (d != nullptr && (threadIdx.x & 63) == 0) d[i] = __builtin_amdgcn_s_memtime();
+}
+
 // floor(a / b) for 0 <= a < 2^20, 1 <= b < 2^12 with rb = 1.0f / b (exact: conv_wino_f32.hip wino_div)
 __device__ __forceinline__ int w4_div(int a, float rb) { return (int)(((float)a + 0.5f) * rb); }
 
@@ -161,6 +168,10 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
   const int k0 = zs * kper, k1 = k0 + kper;
   const u32x4 xdesc = w4_desc(p.x);
   const u32x4 udesc = w4_desc(p.u + (size_t)cg * KC * WCH);
+  unsigned long long* const dbg =
+      p.dbg ? p.dbg + 8 * (wave + W4_NW * (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z))) : nullptr;
+  w4_stamp(dbg, 0);
+  if (dbg && lane == 0) dbg[6] = __builtin_amdgcn_s_memrealtime();
 
   // ---- the tile group's tile-row segments (wave-uniform)
   const int tw0 = (blockIdx.x * 2 + tgl) * 16;
@@ -220,6 +231,7 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
     tab[ii * 64 + lane] = ok ? (((im * p.H + iy) * p.W + ix) * p.C + 4 * hh) * 4 : (int)W4_OOB;
   }
 
+  w4_stamp(dbg, 1);
   // ---- this lane's tile (A row r): unit of patch pixel (dy, dx) = u0 + dy * pitch + w4_dxu(dx); the
   // wave reads patch rows H .. H + 4
   const int t = tw0 + r;
@@ -280,6 +292,11 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
 #pragma unroll
     for (int pix = 0; pix < 30; ++pix) read_patch(d, 0, pix);
     transform(d, vA);
+    if (dbg) {
+#pragma unroll
+      for (int i = 0; i < 18; ++i) asm volatile("" : "+v"(vA[i]));
+      w4_stamp(dbg, 2);
+    }
   }
 
   // ---- one chunk: MFMAs on vc (chunk kc, transformed) with ring slot kc & 1; meanwhile the weights of
@@ -335,6 +352,7 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
     body(vB, vA, kc + 1, 1);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the last chunk's spare DMA has landed
+  w4_stamp(dbg, 3);
   __syncthreads();                                   // every wave is done with the ring and the images
 
   // ---- partial output transform: Y_H = A^T[:, 3H..3H+2] M[3H..3H+2][:] A, staged per wave as
@@ -370,6 +388,7 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
         for (int b = 0; b < 4; ++b) st[((4 * q + i) * 16 + a * 4 + b) * 32 + 16 * j + r] = o[b];
       }
     }
+  w4_stamp(dbg, 4);
   __syncthreads();                                   // the pair's partials are both staged
   // read-back: wave H of the pair takes passes it = 16 H .. 16 H + 15 of its tile group; pass it covers
   // tile it / 2, pixels 8 (it & 1) .. + 7, 8 lanes (16 B each) per pixel; Y = Y_0 + Y_1 in that order
@@ -381,7 +400,7 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
   const bool split = ns > 1;
   const bool fused = split && p.counters != nullptr;
   const int MN = p.B * p.H * p.W * p.N;
-  const f32x4 bsv = split ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(p.bias + bidx);
+  const f32x4 bsv = *(const f32x4*)(p.bias + bidx);   // finish(): whole K, or the fused split's last block
   const int tpi = p.TH * p.TW;
   int oo[16];                                        // NHWC offset of each float4 this lane owns (-1: outside)
 #pragma unroll
@@ -411,6 +430,11 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
 #pragma unroll
     for (int k = 0; k < 16; ++k)
       if (oo[k] >= 0) finish(k, own(k));
+    if (dbg) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      w4_stamp(dbg, 5);
+      if (lane == 0) dbg[7] = __builtin_amdgcn_s_memrealtime();
+    }
     return;
   }
   const __amdgpu_buffer_rsrc_t wsr = w4_rsrc(p.ws);
@@ -513,8 +537,12 @@ int conv_wino4_pieces(int B, int H, int W, int* align) {
 bool conv_wino4_f32_ok(int C, int N) { return C % 16 == 0 && N % 32 == 0; }
 
 // F(4x4, 3x3): p.TH / TW / T count 4x4 tiles; ksplit: |splits| (the fused fixup when p.counters is set)
+static unsigned long long* g_wino4_dbg = nullptr;
+void wino4_set_debug(unsigned long long* buf) { g_wino4_dbg = buf; }
+
 hipError_t conv_wino4_f32_launch(const WinoF32Params& p_in, hipStream_t s) {
   WinoF32Params p = p_in;
+  p.dbg = g_wino4_dbg;
   const int KC = p.C / 8;
   const int ns = p.ksplit;
   if (p.C % 16 || p.N % 32 || ns < 1 || KC % ns || (KC / ns) % 2 || p.sk_iters > 0) return hipErrorInvalidValue;

@@ -65,6 +65,11 @@ int conv_num_cfgs();
 void conv_cfg_tile(int cfg, int* bm, int* bn);
 // diagnostic: occupy stream `s` until *flag != 0 (host-written) or timeout_ms; *out = 1 (flag) / 2 (timeout)
 hipError_t spin_flag(const int* flag, int* out, double timeout_ms, hipStream_t s);
+// test-only loopback link (loopback.hip): wait until *ctr >= target (or *abort_word != 0, or timeout_ms) /
+// publish *ctr = value behind the stream's earlier work; ctr / abort_word / status in mapped host memory
+hipError_t lb_wait(const unsigned long long* ctr, unsigned long long target, const int* abort_word, int* status,
+                   double timeout_ms, hipStream_t s);
+hipError_t lb_signal(unsigned long long* ctr, unsigned long long value, hipStream_t s);
 hipError_t input_pack(const float* x, bf16* y, size_t pixels, int C, int Cp, hipStream_t s);
 hipError_t bn_act(const bf16* x, bf16* y, const float* scale, const float* shift, size_t elems, int C, int relu,
                   hipStream_t s);
@@ -171,6 +176,8 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
 // [N/32][C/8][36 positions][2 fragments][64 lanes][2] (ops/conv.py wino4_pack_np); TH / TW / T count 4x4 tiles
 int conv_wino4_pieces(int B, int H, int W, int* align = nullptr);
 bool conv_wino4_f32_ok(int C, int N);
+// tools/wino4_timeline.py: F(4x4) launches stamp 8 words per wave into buf while it is set
+void wino4_set_debug(unsigned long long* buf);
 hipError_t conv_wino4_f32_launch(const WinoF32Params& p, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,

@@ -160,3 +160,17 @@ def test_pairs_from_itertools_cover_every_two_stage_order(fake_comm):
         store = torch.distributed.HashStore()
         out = _start_pipeline(store, list(order), stages=2, prefix=f"pp2/{order}")
         assert isinstance(out[0], rccl.PairLinks) and isinstance(out[1], rccl.PairLinks)
+
+
+def test_loopback_communicator_is_opt_in_only(monkeypatch):
+    """The one-GPU stand-in for RCCL links (parallel/loopback_comm.py) is chosen only by the explicit
+    test flag: unset, any other value, or a missing RCCL never select it."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel import \
+        loopback_comm
+    monkeypatch.delenv(loopback_comm.ENV_FLAG, raising=False)
+    assert not loopback_comm.selected()
+    for v in ("0", "true", "yes", ""):
+        monkeypatch.setenv(loopback_comm.ENV_FLAG, v)
+        assert not loopback_comm.selected()
+    monkeypatch.setenv(loopback_comm.ENV_FLAG, "1")
+    assert loopback_comm.selected()

@@ -2,9 +2,11 @@
 """Activation-compression measurements on real ResNet-50 bs=32 frontier
 tensors: GPU LZ4 (side stream) vs host LZ4 vs host zfp+lz4 (the reference's
 codec), compression ratio and throughput, and how much a side-stream encode
-slows the overlapped next forward.
+slows the overlapped next forward.  --precision fp32 (default: the shipped
+DEFER precision) measures fp32 frontiers; the host LZ4 of byte-shuffled fp32
+(4 byte planes per 16 KiB block) is reported beside the plain host LZ4.
 
-    python tools/codec_bench.py [--batch 32] [--json out.json]
+    python tools/codec_bench.py [--batch 32] [--precision fp32|bf16] [--json out.json]
 """
 import argparse
 import json
@@ -24,7 +26,10 @@ from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inferen
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.native import runtime  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.runtime.executor import SliceExecutor  # noqa: E402
 
-CUTS = ["pool1_pool", "conv2_block3_out", "conv3_block4_out", "conv4_block6_out", "conv5_block3_out"]
+# the single-tensor cut frontiers, plus the two tensors of BASELINE config 2's multi-tensor cut
+# (part_at=['conv3_block1_1_conv']: conv3_block1_1_conv and conv2_block3_out cross it)
+CUTS = ["pool1_pool", "conv2_block3_out", "conv3_block4_out", "conv4_block6_out", "conv5_block3_out",
+        "conv3_block1_1_conv"]
 
 
 def gpu_time(fn, reps=10):
@@ -40,30 +45,38 @@ def gpu_time(fn, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--json", default="")
     a = ap.parse_args()
+    prec = a.precision
+    esz = 4 if prec == "fp32" else 2
     g = build_resnet("resnet50")
     w = init_weights(g, 0)
-    ex = SliceExecutor(g, w, a.batch, outputs=CUTS + [g.output], precision="bf16")
+    ex = SliceExecutor(g, w, a.batch, outputs=CUTS + [g.output], precision=prec)
     x = torch.randn(a.batch, 224, 224, 3, device="cuda")
     outs = ex.run({g.input: x})
     torch.cuda.synchronize()
     rt = runtime()
     rows = []
-    full = SliceExecutor(g, w, a.batch, precision="bf16")
+    full = SliceExecutor(g, w, a.batch, precision=prec)
     full.capture()
     t_fwd = gpu_time(lambda: full.forward(0), reps=20)
     for name in CUTS:
         t = outs[name].contiguous()
-        nbytes = t.numel() * 2
+        nbytes = t.numel() * esz
         codec = GpuLZ4(nbytes)
         codec.compress(t)
         frame = codec.frame_bytes()
         t_gpu = gpu_time(lambda: (codec.compress(t), codec.done.synchronize()), reps=10)
-        host = t.view(torch.int16).cpu().numpy().view(np.uint16)
+        host = t.view(torch.uint8).cpu().numpy().reshape(-1) if prec == "fp32" else \
+            t.view(torch.int16).cpu().numpy().view(np.uint16)
         t0 = time.perf_counter()
         hf = rt.lz4_compress(host)
         t_host = time.perf_counter() - t0
+        shuf_ratio = None
+        if prec == "fp32" and host.size % (4 * 4096) == 0:
+            planes = host.reshape(-1, 4096, 4).transpose(0, 2, 1).copy().reshape(-1)   # 16 KiB blocks
+            shuf_ratio = nbytes / len(rt.lz4_compress(planes))
         f32 = t.float().cpu().numpy()
         t0 = time.perf_counter()
         zf = C.encode(f32, "zfp+lz4")
@@ -82,7 +95,7 @@ def main():
         t0 = time.perf_counter()
         rt.zfp_compress(f32, 8)
         t_hzfp = time.perf_counter() - t0
-        zc = GpuZVC(t.numel(), 2)
+        zc = GpuZVC(t.numel(), esz)
         zc.compress(t)
         zs = zc.stream_bytes()
         t_zvc = gpu_time(lambda: (zc.compress(t), zc.done.synchronize()), reps=20)
@@ -98,7 +111,9 @@ def main():
                      "gpu_zvc_dec_GBps_incl_h2d": nbytes / t_zvc_dec / 1e9,
                      "gpu_lz4_ratio": nbytes / len(frame), "gpu_lz4_GBps": nbytes / t_gpu / 1e9,
                      "host_lz4_ratio": nbytes / len(hf), "host_lz4_GBps": nbytes / t_host / 1e9,
-                     "zfp_lz4_ratio_vs_bf16": nbytes / len(zf), "zfp_lz4_GBps": f32.nbytes / t_zfp / 1e9,
+                     "host_lz4_byteshuffled_ratio": shuf_ratio, "precision": prec,
+                     "zeros": float((t == 0).float().mean()),
+                     "zfp_lz4_ratio_vs_frontier": nbytes / len(zf), "zfp_lz4_GBps": f32.nbytes / t_zfp / 1e9,
                      "gpu_zfp_ratio_fp32": f32.nbytes / len(zc_bytes), "gpu_zfp_GBps": f32.nbytes / t_gzfp / 1e9,
                      "gpu_zfp_dec_GBps_incl_h2d": f32.nbytes / t_gzfp_dec / 1e9,
                      "gpu_zfp_bitexact_with_host": bool(exact), "host_zfp_GBps": f32.nbytes / t_hzfp / 1e9,
@@ -107,7 +122,8 @@ def main():
         print(f"{r['tensor']:18s} {r['mbytes']:7.1f} MB | GPU zvc x{r['gpu_zvc_ratio']:.2f} {r['gpu_zvc_GBps']:7.1f} GB/s"
               f" | GPU lz4 x{r['gpu_lz4_ratio']:.2f} {r['gpu_lz4_GBps']:7.1f} GB/s"
               f" | host lz4 x{r['host_lz4_ratio']:.2f} {r['host_lz4_GBps']:5.2f} GB/s"
-              f" | zfp+lz4 x{r['zfp_lz4_ratio_vs_bf16']:.2f} {r['zfp_lz4_GBps']:5.2f} GB/s"
+              f" | shuffled host lz4 x{(r['host_lz4_byteshuffled_ratio'] or 0):.2f}"
+              f" | zfp+lz4 x{r['zfp_lz4_ratio_vs_frontier']:.2f} {r['zfp_lz4_GBps']:5.2f} GB/s"
               f" | GPU zfp(fp32) x{r['gpu_zfp_ratio_fp32']:.2f} {r['gpu_zfp_GBps']:6.1f} GB/s"
               f" (host {r['host_zfp_GBps']:.2f}, exact={r['gpu_zfp_bitexact_with_host']})"
               f" | fwd {r['fwd_ms']:.3f} ms, fwd||encode {r['fwd_plus_side_encode_ms']:.3f} ms")

@@ -41,6 +41,11 @@
 #   pw6       pointwise numerics + isolated timings incl. the K-split tail configs 125 / 126
 #   pmcstem   two PMC passes over the fp32 stem (tools/stem_bench.py)
 #   pmc1x1    PMC passes over the tuned fp32 1x1 convs of ResNet-50 (stage 2/4 GEMMs, stage-3 shortcut)
+#   w4        Winograd F(4x4, 3x3) numerics (fp64 oracle) + isolated timings vs the tuned F(2x2) configs
+#   rehearse8 bench.py --gpus 8 --backend gloo (8 ranks sharing one GPU: config-3 lz4 pipeline + 8-worker fault)
+#   w4t       per-wave phase timelines of the F(4x4) kernel (tools/wino4_timeline.py)
+#   loop      the RCCL branch of the stage data plane over the test-only loopback communicator (steady,
+#             SIGKILL, hang; tests/test_rccl_loopback_gpu.py)
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -60,6 +65,11 @@ for p in "${P[@]}"; do
     bench152) steps+=("240|$out/bench_r152|python -u bench.py --model resnet152 --steps 50 --warmup 10") ;;
     rehearse) steps+=("500|$out/bench_gloo2|python -u bench.py --gpus 2 --backend gloo --steps 10 --warmup 3") ;;
     rehearse4) steps+=("600|$out/bench_gloo4|python -u bench.py --gpus 4 --backend gloo --steps 10 --warmup 3") ;;
+    rehearse8) steps+=("600|$out/bench_gloo8|python -u bench.py --gpus 8 --backend gloo --steps 10 --warmup 3") ;;
+    w4)       steps+=("300|$out/pytest_wino4|python -u -m pytest tests/test_wino4_gpu.py -v -s -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/wino4_bench|python -u tools/wino4_bench.py") ;;
+    w4t)      steps+=("200|$out/wino4_timeline|python -u tools/wino4_timeline.py --json gpurun_out/$out/wino4_timeline.json") ;;
+    loop)     steps+=("600|$out/pytest_loop|python -u -m pytest tests/test_rccl_loopback_gpu.py -v -s -x --timeout 300 --timeout-method thread") ;;
     qprobe)   for q in 4 8 16; do steps+=("90|$out/qprobe_$q|GPU_MAX_HW_QUEUES=$q python -u tools/queue_probe.py"); done ;;
     queues)   steps+=("180|$out/pytest_queues|python -u -m pytest tests/test_stream_queues_gpu.py -m gpu -v -s --timeout 120 --timeout-method thread") ;;
     prof)     steps+=("240|$out/prof_fp32|rocprofv3 --kernel-trace --stats -d gpurun_out/$out/prof_fp32 -o run -- python3 bench.py --no-bf16 --steps 30 --warmup 5")
