@@ -56,6 +56,12 @@ def runtime_lib_path() -> Path:
     return PKG_DIR / f"_runtime{EXT}"
 
 
+# per-file extra compiler flags (none at present: -fno-slp-vectorize plus scalar storage on the F(4x4)
+# transform measured 10-20 % slower per K chunk than the compiler's packed v_pk_add / v_pk_fma form,
+# gpurun_out/r5k/wino4_exp.json)
+FILE_FLAGS: dict = {}
+
+
 def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
     src_dir = CSRC / "kernels"
     headers = list(src_dir.glob("*.h"))
@@ -69,7 +75,7 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> Path:
     def compile_one(src: Path) -> Path:
         obj = out_dir / (src.name + ".o")
         if _newer(obj, [src] + headers):
-            cmd = common + ["-c", str(src), "-o", str(obj)]
+            cmd = common + FILE_FLAGS.get(src.name, []) + ["-c", str(src), "-o", str(obj)]
             if src.suffix == ".cpp":
                 cmd = common + ["-x", "hip", "-c", str(src), "-o", str(obj)]
             if verbose:

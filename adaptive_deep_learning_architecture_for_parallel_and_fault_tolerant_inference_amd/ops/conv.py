@@ -538,7 +538,12 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 # is 32 tiles (two tile groups of 16 4x4 tiles) x 32 output channels; K walks 8-channel chunks; split-K
 # ksplit > 1 (slabs + splitk_reduce_f32) or <= -2 (fixup fused in the kernel), |ksplit| dividing the
 # chunks into an even number per split
-WINO4_F32_CFGS = {200: "F(4x4,3x3) wave pairs split by transform row, 1 wave per SIMD"}
+WINO4_F32_CFGS = {200: "F(4x4,3x3) wave pairs split by transform row, 1 wave per SIMD",
+                  210: "F(4x4,3x3) producer / consumer: waves 0-3 MFMA only (weights from L2), waves 4-7 "
+                       "image DMA + input transform (conv_wino4pc_f32.hip)"}
+# measured slower than 200 on every ResNet-50 shape (profiles/r5/wino4_attribution.md: the producers' fp32
+# VALU takes MFMA issue time from the consumers on the same SIMD); kept runnable and tested, never tuned
+WINO4_UNTUNED = frozenset((210,))
 # B^T (input), G (weights) and A^T (output) of F(4x4, 3x3), interpolation points 0, +-1, +-2 (Lavin & Gray 2016)
 WINO4_BT = np.array([[4, 0, -5, 0, 1, 0], [0, -4, -4, 1, 1, 0], [0, 4, -4, -1, 1, 0],
                      [0, -2, -1, 2, 1, 0], [0, 2, -1, -2, 1, 0], [0, 4, 0, -5, 0, 1]], np.float64)
@@ -567,8 +572,11 @@ def wino4_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
                                 .astype(np.float32))
 
 
-def wino4_map_ok(B: int, H: int, W: int) -> bool:
-    """The F(4x4) kernel stages a tile group's 16 4x4 tiles as <= 8 tile-row segments in <= 19 KiB."""
+def wino4_map_ok(B: int, H: int, W: int, cfg: int = 200) -> bool:
+    """cfg 200 stages a tile group's 16 4x4 tiles as <= 8 tile-row segments in <= 19 KiB; cfg 210 a block's
+    32 tiles in <= 43 KiB (tile rows of <= 70 tiles)."""
+    if cfg == 210:
+        return kernels().conv_wino4pc_pieces(B, H, W) > 0
     return kernels().conv_wino4_pieces(B, H, W)[0] > 0
 
 
@@ -743,7 +751,7 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         # Winograd F(4x4, 3x3): ksplit > 1 slabs + splitk_reduce_f32, ksplit <= -2 fused fixup (counters)
         ksplit = int(ksplit) or 1
         if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 \
-                or not wino4_map_ok(B, H, W):
+                or not wino4_map_ok(B, H, W, cfg):
             raise ValueError(f"Winograd F(4x4) config {cfg}: 3x3/s1/p1 conv with transformed weights, C % 16 == 0, "
                              f"N % 32 == 0, map tiles at least 2 wide")
         if abs(ksplit) not in wino4_splits(C) or ksplit == -1:

@@ -8,7 +8,9 @@ dispatcher; stage i -> i+1 is a point-to-point send of device-resident
 tensors on the epoch's communicator (parallel/epoch_group.py):
 
     meta   int64[4] = (req_id, count, epoch, 1)      # rides with the data
-    frontier tensors in slice-output order (bf16 on GPU, fp32 on CPU)
+    frontier tensors in slice-output order, in the job's precision (the
+    executor's buffers: fp32 by default, as the reference; bf16 when the
+    job asks for it; always fp32 on CPU stages)
 
 Double-buffered per stage (`nsets` buffer sets): the receive of micro-batch
 t+1 and the send of t-1 run on the communicator's HIP stream while t

@@ -559,10 +559,11 @@ class SliceExecutor:
             best = None
             for cfg in (list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.WINO4_F32_CFGS)
                         + list(conv_ops.PW_F32_CFGS)):
-                if not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc) or cfg in conv_ops.WINO_MEASURE_CFGS:
+                if (not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc) or cfg in conv_ops.WINO_MEASURE_CFGS
+                        or cfg in conv_ops.WINO4_UNTUNED):
                     continue
                 if cfg in conv_ops.WINO4_F32_CFGS:           # Winograd F(4x4,3x3): splits with even chunk counts
-                    if not conv_ops.wino4_map_ok(B, H, W):
+                    if not conv_ops.wino4_map_ok(B, H, W, cfg):
                         continue
                     sp = [k for k in conv_ops.wino4_splits(C) if k > 1]
                     tiles, kts, sks = conv_ops.wino4_blocks(B, H, W, N), C // 8, tuple(sp) + tuple(-k for k in sp)

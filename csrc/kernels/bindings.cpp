@@ -262,7 +262,9 @@ PYBIND11_MODULE(_C, m) {
     return std::make_pair(g, it);
   });
   m.def("wino_set_debug", [](u64 buf) { adapt::wino_set_debug(P<unsigned long long>(buf)); });
-  m.def("wino4_set_debug", [](u64 buf) { adapt::wino4_set_debug(P<unsigned long long>(buf)); });
+  m.def("conv_wino4pc_pieces", &adapt::conv_wino4pc_pieces);
+  m.def("wino4_set_debug", [](u64 buf, int exp) { adapt::wino4_set_debug(P<unsigned long long>(buf), exp); },
+        py::arg("buf"), py::arg("exp") = 0);
   m.def("pw_set_debug", [](u64 buf) { adapt::pw_set_debug(P<unsigned long long>(buf)); });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,
                                int pad_t, int pad_l, int PH, int PW, int pool_pad, u64 s, int variant) {

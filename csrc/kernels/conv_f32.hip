@@ -298,7 +298,7 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
         const int th = (H + 3) / 4, tw = (W + 3) / 4;
         WinoF32Params wp{x, w, bias, res, out, ws, B, H, W, Cin, N, th, tw, B * th * tw, relu,
                          p.ksplit < 0 ? -p.ksplit : p.ksplit, p.ksplit < 0 ? counters : nullptr, 0, 0};
-        e = conv_wino4_f32_launch(wp, s);
+        e = cfg >= 210 ? conv_wino4pc_f32_launch(wp, s) : conv_wino4_f32_launch(wp, s);
         break;
       }
       if (cfg >= 80) {

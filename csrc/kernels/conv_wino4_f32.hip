@@ -112,6 +112,15 @@ __device__ __forceinline__ void w4_row(f32x2 (&d)[30], int row) {
   }
 }
 
+// the same on one channel
+__device__ __forceinline__ void w4_row1(f32x2 (&d)[30], int row, int c) {
+  float v0 = d[row * 6 + 0][c], v1 = d[row * 6 + 1][c], v2 = d[row * 6 + 2][c];
+  float v3 = d[row * 6 + 3][c], v4 = d[row * 6 + 4][c], v5 = d[row * 6 + 5][c];
+  w4_bt(v0, v1, v2, v3, v4, v5);
+  d[row * 6 + 0][c] = v0; d[row * 6 + 1][c] = v1; d[row * 6 + 2][c] = v2;
+  d[row * 6 + 3][c] = v3; d[row * 6 + 4][c] = v4; d[row * 6 + 5][c] = v5;
+}
+
 // B^T column rows 3h .. 3h + 2 applied to column pb of the row-transformed patch (5 rows: patch rows
 // h .. h + 4) -> V[3h + a][pb], a = 0..2.  h = 0: [4 0 -5 0 1], [0 -4 -4 1 1], [0 4 -4 -1 1] on rows 0-4
 // (8 VALU); h = 1: [-2 -1 2 1 0], [2 -1 -2 1 0], [4 0 -5 0 1] on rows 1-5 (6 VALU)
@@ -147,7 +156,7 @@ __device__ __forceinline__ void w4_at(const float (&m)[6], float (&o)[4]) {
 // pixel offsets (in 16-B units) of patch column dx inside a 9-unit column group layout
 __device__ __forceinline__ constexpr int w4_dxu(int dx) { return dx < 4 ? 2 * dx : 2 * dx + 1; }
 
-template <int PIECES, int H>
+template <int PIECES, int H, int EXP>
 __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, int wave) {
   constexpr int NW = W4_NW, WPW = W4_WPW, SLOT = W4_SLOT, WCH = W4_WCH;
   constexpr int IMG = PIECES * 1024;                 // one image buffer of a tile group
@@ -319,17 +328,48 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
     for (int g = 0; g < 18; ++g) {
       if (g < 17) u[(g + 1) & 1] = *(const f32x4*)(sl + (g + 1) * 1024);
       if (g < HP) toff[g] = tab[g * 64 + lane];
-      if (g < WPW) issue_w(kw, slot ^ 1, g);
-      if (g >= 2 && g < 2 + HP && !(LAST_SHORT && g - 2 == HP - 1)) issue_x(kx, slot, g - 2, toff[g - 2]);
-      if (g < 8) {
+      if constexpr (EXP & 8) {
+        // one DMA per group: weight piece i in group 2 i, image piece ii in group 2 ii + 1 (the 9th / 10th
+        // image pieces double up in groups 16 / 14); patch reads 3 per group (groups 0-9); row r's
+        // transform in groups 2 r + 3 (channel 0) and 2 r + 4 (channel 1), column pb in group 12 + pb
+        if (!(EXP & 1) && (g & 1) == 0 && g / 2 < WPW) issue_w(kw, slot ^ 1, g / 2);
+        constexpr int ii_of[18] = {-1, 0, -1, 1, -1, 2, -1, 3, -1, 4, -1, 5, -1, 6, 9, 7, 8, -1};
+        const int ii = ii_of[g];
+        if (!(EXP & 2) && ii >= 0 && ii < HP && !(LAST_SHORT && ii == HP - 1)) issue_x(kx, slot, ii, toff[ii]);
+        if (g < 10) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (4 * g + e < 30) read_patch(d, slot ^ 1, 4 * g + e);
+          for (int e = 0; e < 3; ++e) read_patch(d, slot ^ 1, 3 * g + e);
+        }
+        if (!(EXP & 4) && g >= 3 && g < 13) {
+          const int row = (g - 3) >> 1, c = (g - 3) & 1;
+          w4_row1(d, row, c);
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            float t = d[row * 6 + k][c];
+            asm volatile("" : "+v"(t));
+            d[row * 6 + k][c] = t;
+          }
+        }
+      } else {
+        if (!(EXP & 1) && g < WPW) issue_w(kw, slot ^ 1, g);
+        if (!(EXP & 2) && g >= 2 && g < 2 + HP && !(LAST_SHORT && g - 2 == HP - 1))
+          issue_x(kx, slot, g - 2, toff[g - 2]);
+        if (g < 8) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * g + e < 30) read_patch(d, slot ^ 1, 4 * g + e);
+        }
+        if (!(EXP & 4) && g >= 3 && g < 8) w4_row(d, g - 3);
       }
-      if (g >= 3 && g < 8) w4_row(d, g - 3);
-      if (g >= 9 && g < 15) {
-        const int pb = g - 9;
-        w4_colh<H>(d, vn, pb);
+      constexpr int COL0 = (EXP & 8) ? 12 : 9;
+      if (g >= COL0 && g < COL0 + 6) {
+        const int pb = g - COL0;
+        if constexpr (EXP & 4) {
+#pragma unroll
+          for (int a = 0; a < 3; ++a) vn[a * 6 + pb] = d[a * 6 + pb] + d[(a + 2) * 6 + pb];
+        } else {
+          w4_colh<H>(d, vn, pb);
+        }
         // pin the finished column here: left alone, the compiler sinks the transform into the next
         // chunk (where vn is consumed), i.e. behind the barrier, in front of its MFMAs
 #pragma unroll
@@ -476,7 +516,9 @@ __device__ __forceinline__ void wino4_wave(const WinoF32Params& p, char* smem, i
   }
 }
 
-template <int PIECES>
+// EXP (measurement variants, tools/wino4_timeline.py --exp): bit 0 no weight DMA in the K loop, bit 1 no image
+// DMA, bit 2 no input transform (wrong results: timing attribution only); bit 3 the spread schedule
+template <int PIECES, int EXP>
 __global__ __launch_bounds__(256, 1) void conv_wino4_f32_kernel(WinoF32Params p) {
   constexpr int HP = (PIECES + 1) / 2;
   constexpr int LDS = 2 * W4_SLOT + 4 * PIECES * 1024 + W4_NW * HP * 256;
@@ -484,8 +526,8 @@ __global__ __launch_bounds__(256, 1) void conv_wino4_f32_kernel(WinoF32Params p)
   static_assert(LDS <= 163840, "LDS: at most 19 image pieces");
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave & 1) wino4_wave<PIECES, 1>(p, smem, wave);
-  else wino4_wave<PIECES, 0>(p, smem, wave);
+  if (wave & 1) wino4_wave<PIECES, 1, EXP>(p, smem, wave);
+  else wino4_wave<PIECES, 0, EXP>(p, smem, wave);
 }
 
 // 16-B units of a tile group's image for tiles tw0 .. tw0 + 15 (host mirror of the kernel's layout)
@@ -504,10 +546,10 @@ int w4_wave_units(int tw0, int T, int TW, bool align) {
   return units;
 }
 
-template <int PIECES>
+template <int PIECES, int EXP = 0>
 hipError_t launch_wino4(const WinoF32Params& p, int ns, hipStream_t s) {
   const dim3 grid((p.T + 31) / 32, p.N / (16 * W4_FN), ns), block(W4_NW * 64);   // 2 tile groups per block
-  hipLaunchKernelGGL((conv_wino4_f32_kernel<PIECES>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((conv_wino4_f32_kernel<PIECES, EXP>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
@@ -538,7 +580,29 @@ bool conv_wino4_f32_ok(int C, int N) { return C % 16 == 0 && N % 32 == 0; }
 
 // F(4x4, 3x3): p.TH / TW / T count 4x4 tiles; ksplit: |splits| (the fused fixup when p.counters is set)
 static unsigned long long* g_wino4_dbg = nullptr;
-void wino4_set_debug(unsigned long long* buf) { g_wino4_dbg = buf; }
+static int g_wino4_exp = 0;
+unsigned long long* wino4_debug_buffer() { return g_wino4_dbg; }
+int wino4_exp_flags() { return g_wino4_exp; }
+void wino4_set_debug(unsigned long long* buf, int exp) {
+  g_wino4_dbg = buf;
+  g_wino4_exp = exp;
+}
+
+template <int PIECES>
+hipError_t launch_wino4_exp(const WinoF32Params& p, int ns, hipStream_t s, int exp) {
+  switch (exp) {
+    case 1: return launch_wino4<PIECES, 1>(p, ns, s);
+    case 2: return launch_wino4<PIECES, 2>(p, ns, s);
+    case 3: return launch_wino4<PIECES, 3>(p, ns, s);
+    case 4: return launch_wino4<PIECES, 4>(p, ns, s);
+    case 7: return launch_wino4<PIECES, 7>(p, ns, s);
+    case 8: return launch_wino4<PIECES, 8>(p, ns, s);
+    case 9: return launch_wino4<PIECES, 9>(p, ns, s);
+    case 10: return launch_wino4<PIECES, 10>(p, ns, s);
+    case 12: return launch_wino4<PIECES, 12>(p, ns, s);
+  }
+  return hipErrorInvalidValue;
+}
 
 hipError_t conv_wino4_f32_launch(const WinoF32Params& p_in, hipStream_t s) {
   WinoF32Params p = p_in;
@@ -552,6 +616,11 @@ hipError_t conv_wino4_f32_launch(const WinoF32Params& p_in, hipStream_t s) {
   int align = 0;
   const int pieces = conv_wino4_pieces(p.B, p.H, p.W, &align);
   p.flags = align;
+  if (g_wino4_exp) {                                 // measurement variants: stages 1 / 2 geometries only
+    if (pieces == 15) return launch_wino4_exp<15>(p, ns, s, g_wino4_exp);
+    if (pieces == 16) return launch_wino4_exp<16>(p, ns, s, g_wino4_exp);
+    return hipErrorInvalidValue;
+  }
   switch (pieces) {
     case 15: return launch_wino4<15>(p, ns, s);
     case 16: return launch_wino4<16>(p, ns, s);

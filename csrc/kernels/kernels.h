@@ -177,8 +177,14 @@ hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
 int conv_wino4_pieces(int B, int H, int W, int* align = nullptr);
 bool conv_wino4_f32_ok(int C, int N);
 // tools/wino4_timeline.py: F(4x4) launches stamp 8 words per wave into buf while it is set
-void wino4_set_debug(unsigned long long* buf);
+void wino4_set_debug(unsigned long long* buf, int exp = 0);
 hipError_t conv_wino4_f32_launch(const WinoF32Params& p, hipStream_t s);
+unsigned long long* wino4_debug_buffer();
+int wino4_exp_flags();
+// producer / consumer F(4x4, 3x3) (conv_wino4pc_f32.hip, cfg 210): same weights and params; image pieces
+// (1 KiB) of the widest 32-tile block, 0 when the geometry is not supported
+int conv_wino4pc_pieces(int B, int H, int W);
+hipError_t conv_wino4pc_f32_launch(const WinoF32Params& p, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,

@@ -1,4 +1,5 @@
-"""fp32 Winograd F(4x4, 3x3) conv kernel (csrc/kernels/conv_wino4_f32.hip, cfg 200) against a float64
+"""fp32 Winograd F(4x4, 3x3) conv kernels (csrc/kernels/conv_wino4_f32.hip, cfg 200; the producer / consumer
+form csrc/kernels/conv_wino4pc_f32.hip, cfg 210) against a float64
 CPU oracle of the same 3x3 / stride-1 / pad-1 conv (bias, optional residual, ReLU / ReLU6), whole-K,
 slab split-K and fused split-K, on the ResNet stage shapes at small batch and on odd maps (partial
 tiles, tile groups straddling rows and images).  F(4x4) on fp32 must stay within 1e-4 of the fp64
@@ -34,9 +35,10 @@ def _case(shape, seed):
     return x, kern, bias, res
 
 
+@pytest.mark.parametrize("cfg", [200, 210])
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("ksplit", [1, 2, 4, -2, -4, -8])
-def test_wino4_f32_matches_fp64(shape, ksplit):
+def test_wino4_f32_matches_fp64(shape, ksplit, cfg):
     B, H, W, Cin, Cout, has_res, relu = shape
     if abs(ksplit) not in C.wino4_splits(Cin):
         pytest.skip("split-K needs an even chunk count per split")
@@ -51,16 +53,17 @@ def test_wino4_f32_matches_fp64(shape, ksplit):
     ctr = torch.zeros(C.wino4_blocks(B, H, W, Cout), dtype=torch.int32, device="cuda") if ksplit < 0 else None
     for rep in range(2 if ksplit < 0 else 1):        # the second launch checks the counters came back zero
         out.fill_(float("nan"))
-        C.conv_forward_f32(xd, pc, out, rd, relu=relu, cfg=200, ksplit=ksplit, counters=ctr)
+        C.conv_forward_f32(xd, pc, out, rd, relu=relu, cfg=cfg, ksplit=ksplit, counters=ctr)
         got = out.cpu().numpy()
         err = np.abs(got - want).max() / max(1.0, np.abs(want).max())
-        print(f"F(4x4) {shape} ksplit {ksplit}: rel err {err:.2e}")
+        print(f"F(4x4) cfg {cfg} {shape} ksplit {ksplit}: rel err {err:.2e}")
         assert np.isfinite(got).all() and err < 1e-4, f"ksplit {ksplit} rep {rep}: rel err {err}"
     if ctr is not None:
         assert int(ctr.abs().sum()) == 0, "fused split-K left arrival counters non-zero"
 
 
-def test_wino4_fused_split_matches_slab_split():
+@pytest.mark.parametrize("cfg", [200, 210])
+def test_wino4_fused_split_matches_slab_split(cfg):
     """The fused fixup adds the same slabs in the same (split) order as splitk_reduce_f32."""
     B, H, W, Cin, Cout = 4, 14, 14, 256, 256
     x, kern, bias, _ = _case((B, H, W, Cin, Cout, False, 1), 5)
@@ -69,8 +72,8 @@ def test_wino4_fused_split_matches_slab_split():
     a = torch.empty((B, H, W, Cout), device="cuda")
     b = torch.empty_like(a)
     ctr = torch.zeros(C.wino4_blocks(B, H, W, Cout), dtype=torch.int32, device="cuda")
-    C.conv_forward_f32(xd, pc, a, relu=1, cfg=200, ksplit=4)
-    C.conv_forward_f32(xd, pc, b, relu=1, cfg=200, ksplit=-4, counters=ctr)
+    C.conv_forward_f32(xd, pc, a, relu=1, cfg=cfg, ksplit=4)
+    C.conv_forward_f32(xd, pc, b, relu=1, cfg=cfg, ksplit=-4, counters=ctr)
     assert torch.equal(a, b)
 
 
@@ -83,11 +86,11 @@ def test_wino4_error_against_f2x2():
     xd = torch.from_numpy(x).cuda()
     out = torch.empty((B, H, W, Cout), device="cuda")
     errs = {}
-    for cfg, ks in ((200, 1), (118, 1)):
+    for cfg, ks in ((200, 1), (210, 1), (118, 1)):
         C.conv_forward_f32(xd, pc, out, cfg=cfg, ksplit=ks)
         errs[cfg] = np.abs(out.cpu().numpy() - want).max() / np.abs(want).max()
-    print(f"stage-5 3x3 rel err vs fp64: F(4x4) {errs[200]:.2e}, F(2x2) {errs[118]:.2e}")
-    assert errs[200] < 1e-4
+    print(f"stage-5 3x3 rel err vs fp64: F(4x4) {errs[200]:.2e} / pc {errs[210]:.2e}, F(2x2) {errs[118]:.2e}")
+    assert errs[200] < 1e-4 and errs[210] < 1e-4
 
 
 def test_wino4_rejects_bad_splits_and_maps():

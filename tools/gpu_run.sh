@@ -69,6 +69,11 @@ for p in "${P[@]}"; do
     w4)       steps+=("300|$out/pytest_wino4|python -u -m pytest tests/test_wino4_gpu.py -v -s -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/wino4_bench|python -u tools/wino4_bench.py") ;;
     w4t)      steps+=("200|$out/wino4_timeline|python -u tools/wino4_timeline.py --json gpurun_out/$out/wino4_timeline.json") ;;
+    w4pc)     steps+=("300|$out/pytest_wino4|python -u -m pytest tests/test_wino4_gpu.py -v -s -x --timeout 120 --timeout-method thread")
+              steps+=("120|$out/wino4pc_timeline|python -u tools/wino4_timeline.py --cfg 210 --json gpurun_out/$out/wino4pc_timeline.json")
+              steps+=("300|$out/wino4_bench|python -u tools/wino4_bench.py") ;;
+    w4pcx)    steps+=("200|$out/wino4pc_exp|python -u tools/wino4_timeline.py --cfg 210 --exp 0,1,4,5,12,13,14,17,21 --json gpurun_out/$out/wino4pc_exp.json") ;;
+    w4x)      steps+=("200|$out/wino4_exp|python -u tools/wino4_timeline.py --exp 0,8,4,1,2 --json gpurun_out/$out/wino4_exp.json") ;;
     loop)     steps+=("600|$out/pytest_loop|python -u -m pytest tests/test_rccl_loopback_gpu.py -v -s -x --timeout 300 --timeout-method thread") ;;
     qprobe)   for q in 4 8 16; do steps+=("90|$out/qprobe_$q|GPU_MAX_HW_QUEUES=$q python -u tools/queue_probe.py"); done ;;
     queues)   steps+=("180|$out/pytest_queues|python -u -m pytest tests/test_stream_queues_gpu.py -m gpu -v -s --timeout 120 --timeout-method thread") ;;

@@ -52,7 +52,7 @@ def main():
         f4_floor = 2.0 * tiles4 * 36 * Cin * Cout / 150e12 * 1e6
         print(f"shape {B}x{H}x{W}x{Cin}->{Cout}: pieces/align {tuple(C.kernels().conv_wino4_pieces(B, H, W))}, "
               f"F(4x4) MFMA floor {f4_floor:.1f} us at 150 TF", flush=True)
-        cands = [(200, ks) for ks in C.wino4_splits(Cin) for ks in ((ks,) if ks == 1 else (ks, -ks))]
+        cands = [(cfg, ks) for cfg in (200, 210) for ks in C.wino4_splits(Cin) for ks in ((ks,) if ks == 1 else (ks, -ks))]
         cands += F2[Cin]
         for cfg, ks in cands:
             nws = C.workspace_elems_f32(M, Cout, pc.Kpad, cfg, ks)
