@@ -102,7 +102,7 @@ def cmd_serve(argv):
     cfg = _cfg(a, transport=a.transport, codec=a.codec, replicas=a.replicas)
     from .dispatcher import DEFER
     m = _model(cfg)
-    cuts = cfg.cuts(m.graph)
+    cuts = cfg.cuts(m.graph, precision=a.dtype)
     d = DEFER(membership_port=cfg.membership_port, result_port=cfg.result_port, chunk_size=cfg.chunk_size,
               batch=cfg.batch, codec=cfg.codec, weight_codec=cfg.weight_codec, max_inflight=cfg.max_inflight,
               task_timeout=cfg.task_timeout, worker_wait=max(cfg.worker_wait, 60 if a.spawn else 0),
@@ -182,17 +182,22 @@ def cmd_plan(argv):
     ap = argparse.ArgumentParser(prog="plan")
     _common(ap)
     ap.add_argument("--stages", type=int, default=2)
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="activation precision of the job (frontier bytes, conv rate)")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     from .graph.planner import balance_ratio, plan_cuts
     from .graph.slicer import frontier_bytes, partition
     m = _model(cfg)
-    cuts = cfg.cuts(m.graph) if cfg.part_at else plan_cuts(m.graph, a.stages, batch=max(cfg.batch, 1))[0]
-    _, per = plan_cuts(m.graph, len(cuts) + 1, batch=max(cfg.batch, 1), candidates=cuts) if cuts else ([], [0])
+    b = max(cfg.batch, 1)
+    cuts = cfg.cuts(m.graph, precision=a.dtype) if cfg.part_at else \
+        plan_cuts(m.graph, a.stages, batch=b, precision=a.dtype)[0]
+    _, per = plan_cuts(m.graph, len(cuts) + 1, batch=b, candidates=cuts, precision=a.dtype) if cuts else ([], [0])
     print(f"part_at = {cuts}   (max stage / ideal = {balance_ratio(per):.3f})")
+    ab = 4 if a.dtype == "fp32" else 2
     for s, t in zip(partition(m.graph, cuts), per):
-        fb = frontier_bytes(m.graph, s.outputs) * max(cfg.batch, 1)
-        print(f"  {s.name}: {len(s.layers):3d} layers, est {t * 1e3:7.3f} ms, sends {s.outputs} ({fb / 1e6:.1f} MB bf16)")
+        fb = frontier_bytes(m.graph, s.outputs, ab) * b
+        print(f"  {s.name}: {len(s.layers):3d} layers, est {t * 1e3:7.3f} ms, sends {s.outputs} ({fb / 1e6:.1f} MB {a.dtype})")
 
 
 def cmd_summary(argv):

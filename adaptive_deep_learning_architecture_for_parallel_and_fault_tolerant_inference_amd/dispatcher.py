@@ -357,7 +357,7 @@ class DEFER:
         want = len(self._user_cuts) + 1
         if k == want:
             return list(self._user_cuts)
-        return plan_cuts(self._model.graph, k, batch=self.batch)[0]
+        return plan_cuts(self._model.graph, k, batch=self.batch, precision=self.precision)[0]
 
     # --------------------------------------------------------- membership
     def _worker_monitor(self) -> None:

@@ -16,7 +16,7 @@ ourselves, so this module provides:
 from __future__ import annotations
 
 import json
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -39,7 +39,22 @@ class HwModel:
     hbm_bw: float = 5.0e12                # measured 1x1-conv streaming rate (3.7-5.5 TB/s)
     link_bw: float = 150e9                # replaced by the measured RCCL p2p rate when present
     launch_s: float = 1.5e-6              # kernel boundary inside a hipGraph
-    act_bytes: int = 2                    # bf16 activations
+    act_bytes: int = 2                    # bf16 activations (for_precision: 4 for fp32 frontiers)
+
+
+# the fp32 path's sustained conv rate: the fp32 matrix cores peak at 1/16 of bf16 (157 TF); the tuned fp32
+# ResNet-50 forward sums 247 GFLOP in 2.26-2.30 ms at bs=32 (profiles/r4/roofline_r50_fp32_bs32.txt), ~0.11 PF
+FP32_MFMA_FLOPS = 0.11e15
+
+
+def for_precision(hw: "HwModel", precision: str) -> "HwModel":
+    """The model for a job's activation precision: fp32 frontiers cross a cut at 4 bytes per element (twice
+    the bf16 bytes the link terms were first written for) and fp32 convs run at the fp32 matrix rate."""
+    if precision == "fp32":
+        return replace(hw, act_bytes=4, mfma_flops=min(hw.mfma_flops, FP32_MFMA_FLOPS))
+    if precision == "bf16":
+        return replace(hw, act_bytes=2)
+    return hw
 
 
 def _calib_key(g: Graph, batch: int, precision: str) -> str:
@@ -220,7 +235,7 @@ def plan_cuts(g: Graph, stages: int, batch: int = 32, hw: Optional[HwModel] = No
     than the stages)."""
     if stages < 1:
         raise ValueError("stages must be >= 1")
-    hw = hw or default_hw()
+    hw = for_precision(hw or default_hw(), precision)
     if costs is None and calibrated:
         costs = load_calibration(g, batch, precision)
     costs = costs or layer_costs(g, batch, hw)

@@ -78,7 +78,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
     if model == "resnet_tiny":
         kw["classes"] = 10
     m = resnet(model, seed=0, **kw)
-    cuts, _ = plan_cuts(m.graph, workers, batch=batch)
+    cuts, _ = plan_cuts(m.graph, workers, batch=batch, precision=precision or "fp32")
     dkw = {}
     if hb_timeout is not None:
         dkw["hb_timeout"] = hb_timeout

@@ -92,7 +92,7 @@ class PipelineJob:
         self.replica = rank // stages
         self.stage = rank % stages
         if not part_at:
-            part_at, _ = plan_cuts(g, stages, batch=batch)
+            part_at, _ = plan_cuts(g, stages, batch=batch, precision=precision)
         if len(part_at) != stages - 1:
             raise ValueError(f"{stages} stages need {stages - 1} cuts, got {part_at}")
         self.part_at = list(part_at)

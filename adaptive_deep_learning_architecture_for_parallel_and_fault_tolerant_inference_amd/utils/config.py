@@ -85,8 +85,9 @@ class AdaptConfig:
             raise KeyError(f"unknown config keys {sorted(bad)}")
         return dataclasses.replace(self, **kw)
 
-    def cuts(self, graph=None) -> List[str]:
-        """Resolve `part_at` (list, 'a,b', or 'auto:K') to layer names."""
+    def cuts(self, graph=None, precision: str = "fp32") -> List[str]:
+        """Resolve `part_at` (list, 'a,b', or 'auto:K') to layer names ('auto:K': the planner's cuts for
+        the job's activation precision, DEFER's default fp32)."""
         p = self.part_at
         if isinstance(p, list) and len(p) == 1 and p[0].startswith("auto:"):
             p = p[0]
@@ -94,7 +95,7 @@ class AdaptConfig:
             if p.startswith("auto:"):
                 from ..graph.planner import plan_cuts
                 k = int(p.split(":", 1)[1])
-                return plan_cuts(graph, k, batch=max(self.batch, 1))[0]
+                return plan_cuts(graph, k, batch=max(self.batch, 1), precision=precision)[0]
             return [s for s in p.split(",") if s]
         return list(p)
 

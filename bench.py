@@ -268,6 +268,7 @@ def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, e
         ratio = getattr(link, "ratio", None)
         rec["codec"] = args.codec
         rec["wire_ratio"] = round(ratio, 4) if ratio else None
+        rec["codec_default"] = "none"          # DEFER(link_codec=...) default: xGMI links stay uncompressed
     if hasattr(job, "close"):
         rec["links_drained"] = bool(job.close())
     return rec
@@ -298,7 +299,10 @@ def plan_subruns(args, world: int, backend: str) -> list:
             pp += ["--codec", args.codec]
         elif world == 8:
             pp += ["--codec", "lz4"]
-            label = "BASELINE config 3: 8-stage pipeline, lz4 activation compression on a side stream"
+            label = ("BASELINE config 3: 8-stage pipeline, lz4 activation compression on a side stream -- a "
+                     "measured cost, not a gain: GPU LZ4 reaches ratio 1.07-1.09 on fp32 frontiers at 51-82 GB/s "
+                     "encode (profiles/r5/codec_fp32_r50_bs32.txt), below the xGMI link it would relieve, so "
+                     "DEFER's per-link default keeps xGMI uncompressed (link_codec='none')")
         subs.append(("pp", "bench", pp, world, SUB_LIMIT_S["pp"], label))
         if world == 4:
             r152 = ["--sub", "pp", "--model", "resnet152", "--pp-dtype", "bf16"] + common

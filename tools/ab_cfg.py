@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--env-a", default="", help="K=V;... set while building the A (tuned) executor")
     ap.add_argument("--env-b", default="", help="K=V;... set while building the B executor (plan switches)")
     ap.add_argument("--rounds", type=int, default=15)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     g = build_model(a.model)
@@ -48,7 +49,7 @@ def main():
         env = dict(kv.split("=", 1) for kv in (a.env_a if variant == "tuned" else a.env_b).split(";") if kv)
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        ex = SliceExecutor(g, w, a.batch, precision="bf16")
+        ex = SliceExecutor(g, w, a.batch, precision=a.precision)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
@@ -91,7 +92,7 @@ def main():
             e1.record()
             e1.synchronize()
             res[v].append(e0.elapsed_time(e1) / 50)
-    rec = {"model": a.model, "batch": a.batch, "sets": sets, "max_abs_diff": diff,
+    rec = {"model": a.model, "batch": a.batch, "precision": a.precision, "sets": sets, "max_abs_diff": diff,
            "ms_median": {v: statistics.median(t) for v, t in res.items()}}
     for v, t in res.items():
         m = statistics.median(t)

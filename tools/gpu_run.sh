@@ -46,6 +46,9 @@
 #   w4t       per-wave phase timelines of the F(4x4) kernel (tools/wino4_timeline.py)
 #   loop      the RCCL branch of the stage data plane over the test-only loopback communicator (steady,
 #             SIGKILL, hang; tests/test_rccl_loopback_gpu.py)
+#   ab4       whole-model fp32 A/B: the tuned 3x3s vs F(4x4) cfg 200 on stages 3-5 (tools/ab_cfg.py)
+#   codec     activation-codec table on the ResNet-50 bs=32 frontiers, fp32 (tools/codec_bench.py)
+#   w4x / w4pc / w4pcx  F(4x4) measurement variants / producer-consumer tests + timelines / its variants
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -72,6 +75,8 @@ for p in "${P[@]}"; do
     w4pc)     steps+=("300|$out/pytest_wino4|python -u -m pytest tests/test_wino4_gpu.py -v -s -x --timeout 120 --timeout-method thread")
               steps+=("120|$out/wino4pc_timeline|python -u tools/wino4_timeline.py --cfg 210 --json gpurun_out/$out/wino4pc_timeline.json")
               steps+=("300|$out/wino4_bench|python -u tools/wino4_bench.py") ;;
+    ab4)      steps+=("300|$out/ab_wino4|python -u tools/ab_cfg.py --precision fp32 --set 32x28x28x128,3x3s1p1111@200@1 --set 32x14x14x256,3x3s1p1111@200@2 --set 32x7x7x512,3x3s1p1111@200@4 --json gpurun_out/$out/ab_wino4.json") ;;
+    codec)    steps+=("300|$out/codec_fp32|python -u tools/codec_bench.py --precision fp32 --json gpurun_out/$out/codec_fp32.json") ;;
     w4pcx)    steps+=("200|$out/wino4pc_exp|python -u tools/wino4_timeline.py --cfg 210 --exp 0,1,4,5,12,13,14,17,21 --json gpurun_out/$out/wino4pc_exp.json") ;;
     w4x)      steps+=("200|$out/wino4_exp|python -u tools/wino4_timeline.py --exp 0,8,4,1,2 --json gpurun_out/$out/wino4_exp.json") ;;
     loop)     steps+=("600|$out/pytest_loop|python -u -m pytest tests/test_rccl_loopback_gpu.py -v -s -x --timeout 300 --timeout-method thread") ;;
