@@ -935,17 +935,23 @@ class Node:
                 pass
 
     def _start_epoch(self, cfg: Dict, m: SliceManifest, w: Dict[str, np.ndarray]) -> None:
+        t0 = time.perf_counter()
         with self._rt_lock:
             old = self.runtime
             if old is not None:
                 old.abort()
                 if not old.quiesced():            # a thread still inside the old compute: do not reuse it
                     self._evict_compute(old.cfg)
+            t1 = time.perf_counter()
             if cfg.get("transport", "tcp") == "tcp":
                 rt = StageRuntime(self, cfg, m, w)
             else:                                   # RCCL (xGMI) / gloo stage-to-stage links
                 from .parallel.stage_runtime import CollectiveStageRuntime
                 rt = CollectiveStageRuntime(self, cfg, m, w)
+            # epoch formation cost on this worker (old epoch's abort, new runtime incl. its compute: a cache
+            # hit when `prepare` built the slice); the collective runtime adds its link rendezvous on the data
+            # thread (stage_runtime.py setup_ms)
+            rt.form_ms = {"abort_old": round((t1 - t0) * 1e3, 1), "build": round((time.perf_counter() - t1) * 1e3, 1)}
             self.runtime = rt
             self.state.epoch = rt.epoch
             self.state.partition_index = m.part_index

@@ -20,7 +20,9 @@ tear the epoch down even while a peer is dead.
 """
 from __future__ import annotations
 
+import os
 import queue
+import sys
 import threading
 import time
 import traceback
@@ -256,14 +258,20 @@ class CollectiveStageRuntime:
 
     def _data_loop(self) -> None:
         cc = self.cfg["collective"]
+        t0 = time.perf_counter()
         try:
             self.group = EpochGroup(cc["backend"], cc["store_host"], int(cc["store_port"]), self.epoch, self.stage,
                                     self.stages, self.dev if self.gpu else None, float(cc.get("timeout", 30)),
                                     ctl=self.link_codec != "none", stall_s=float(cc.get("stall_s", 5.0)))
+            t1 = time.perf_counter()
             self._handshake(self.group)
         except Exception as e:  # noqa: BLE001 - rendezvous failed (a member died): epoch is dead
             self._fail("rendezvous", e)
             return
+        self.setup_ms = {"group": round((t1 - t0) * 1e3, 1), "handshake": round((time.perf_counter() - t1) * 1e3, 1)}
+        if os.environ.get("ADAPT_EPOCH_TIMING") == "1":
+            print(f"cstage{self.stage} epoch {self.epoch}: formed {getattr(self, 'form_ms', {})}, links "
+                  f"{self.setup_ms} ms", file=sys.stderr, flush=True)
         if self.stop.is_set():
             self.group.abort()
             return

@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _workers(port, n, tag):
-    env = dict(os.environ, ADAPT_TEST_LOOPBACK_COMM="1", ADAPT_LOOPBACK_SLOT_MB="16",
+    env = dict(os.environ, ADAPT_TEST_LOOPBACK_COMM="1", ADAPT_LOOPBACK_SLOT_MB="16", ADAPT_EPOCH_TIMING="1",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     return [subprocess.Popen([sys.executable, "-m", f"{PKG}.node", "--membership-port", str(port), "--data-port", "0",
                               "--config-port", "0", "--device", "cuda:0", "--id", f"{tag}{i}", "--ttl", "2.0",

@@ -20,6 +20,7 @@
 #   pmc32     two rocprofv3 PMC passes over the fp32 bench (tools/pmc_summary.py reads them)
 #   hang      4-stage wedged-stage (alive, no progress) recovery bench (device links)
 #   roof32    per-layer fp32 roofline table (two PMC passes over tools/roofline_r50.py --dtype fp32)
+#   roof16    the same for bf16
 #   cs3       channel-split 3x3 (stage 4/5) numerics, isolated timings vs the tile kernels, whole-model A/B
 #   wino      fp32 Winograd numerics + isolated timings of the v2 configs on the four ResNet-50 3x3 shapes
 #   pmcw      PMC passes over the fp32 Winograd kernel (tools/pmc_f32.sh), stage 2-5 shapes
@@ -97,6 +98,9 @@ for p in "${P[@]}"; do
     roof32)   steps+=("200|$out/roof32_meta|mkdir -p gpurun_out/$out/roof32 && python -u tools/roofline_r50.py --run --dtype fp32 --meta gpurun_out/$out/roof32/meta.json")
               steps+=("400|$out/roof32_pmc|bash tools/pmc_groups.sh gpurun_out/$out/roof32 'SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT' 'TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum' -- tools/roofline_r50.py --run --dtype fp32")
               steps+=("60|$out/roof32_table|python tools/roofline_r50.py --table gpurun_out/$out/roof32 --meta gpurun_out/$out/roof32/meta.json --json gpurun_out/$out/roof32/roofline_fp32.json") ;;
+    roof16)   steps+=("200|$out/roof16_meta|mkdir -p gpurun_out/$out/roof16 && python -u tools/roofline_r50.py --run --dtype bf16 --meta gpurun_out/$out/roof16/meta.json")
+              steps+=("400|$out/roof16_pmc|bash tools/pmc_groups.sh gpurun_out/$out/roof16 'SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT' 'TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum' -- tools/roofline_r50.py --run --dtype bf16")
+              steps+=("60|$out/roof16_table|python tools/roofline_r50.py --table gpurun_out/$out/roof16 --meta gpurun_out/$out/roof16/meta.json --json gpurun_out/$out/roof16/roofline_bf16.json") ;;
     wino)     steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py tests/test_wino.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/wino_bench|python -u tools/conv_bench_f32.py --shape 32,56,56,64,64,3,1,1,0 --shape 32,28,28,128,128,3,1,1,0 --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --only 103,104,105,106,107,108 --ks 1,2,4,-2,-4") ;;
     wino4)    steps+=("200|$out/pytest_wino|python -u -m pytest tests/test_wino_gpu.py tests/test_wino.py -v -x --timeout 120 --timeout-method thread")
