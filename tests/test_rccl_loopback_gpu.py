@@ -91,6 +91,16 @@ def test_rccl_branch_over_loopback_links(fault):
         feed.start()
         res = [outq.get(timeout=240) for _ in range(20)]
         assert len(d.pipeline.workers) == 3
+        if fault != "none":
+            # let DEFER's background work finish first: the whole-model push to every worker and the `prepare`
+            # hints (each survivor builds the slice it would take after a loss), as in a long-running job; the
+            # re-form then pays the per-epoch link rendezvous, not a slice build
+            t_end = time.time() + 120
+            while any(t.is_alive() for t in d._bg) and time.time() < t_end:
+                res.append(outq.get(timeout=240))
+            t_end = time.time() + 4.0
+            while time.time() < t_end:
+                res.append(outq.get(timeout=240))
         assert d.epoch_transport(d.pipeline.records) == "rccl"
         assert glob.glob("/dev/shm/adapt-lb-*"), "the stage links are not the loopback communicator"
         for y in res:

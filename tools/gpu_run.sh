@@ -48,6 +48,7 @@
 #   loop      the RCCL branch of the stage data plane over the test-only loopback communicator (steady,
 #             SIGKILL, hang; tests/test_rccl_loopback_gpu.py)
 #   ab4       whole-model fp32 A/B: the tuned 3x3s vs F(4x4) cfg 200 on stages 3-5 (tools/ab_cfg.py)
+#   li        the reference's local_infer protocol at fp32: ResNet-50 bs=1, 10 and 1000 requests
 #   codec     activation-codec table on the ResNet-50 bs=32 frontiers, fp32 (tools/codec_bench.py)
 #   w4x / w4pc / w4pcx  F(4x4) measurement variants / producer-consumer tests + timelines / its variants
 # Extra steps: GPU_EXTRA="secs|name|cmd" (one step; quoted as for gpu_steps.sh).
@@ -77,6 +78,10 @@ for p in "${P[@]}"; do
               steps+=("120|$out/wino4pc_timeline|python -u tools/wino4_timeline.py --cfg 210 --json gpurun_out/$out/wino4pc_timeline.json")
               steps+=("300|$out/wino4_bench|python -u tools/wino4_bench.py") ;;
     ab4)      steps+=("300|$out/ab_wino4|python -u tools/ab_cfg.py --precision fp32 --set 32x28x28x128,3x3s1p1111@200@1 --set 32x14x14x256,3x3s1p1111@200@2 --set 32x7x7x512,3x3s1p1111@200@4 --json gpurun_out/$out/ab_wino4.json") ;;
+    li)       steps+=("180|$out/local_infer_bs1_10|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd local-infer --model resnet50 --batch 1 --requests 10 --device cuda")
+              steps+=("180|$out/local_infer_bs1_1000|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd local-infer --model resnet50 --batch 1 --requests 1000 --device cuda") ;;
+    gemm1x1)  steps+=("300|$out/gemm1x1_bigtiles|python -u tools/conv_bench_f32.py --only 10,11,12,13,14,15,16,17,18,30,31,32,33,34,37,38 --ks 1,2,-1,-2 --top 8 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,28,28,512,128,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1") ;;
+    bf3x3)    steps+=("300|$out/bf16_3x3_s45|python -u tools/conv_bench.py --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --ks 1,2,3,4,-1,-2") ;;
     codec)    steps+=("300|$out/codec_fp32|python -u tools/codec_bench.py --precision fp32 --json gpurun_out/$out/codec_fp32.json") ;;
     w4pcx)    steps+=("200|$out/wino4pc_exp|python -u tools/wino4_timeline.py --cfg 210 --exp 0,1,4,5,12,13,14,17,21 --json gpurun_out/$out/wino4pc_exp.json") ;;
     w4x)      steps+=("200|$out/wino4_exp|python -u tools/wino4_timeline.py --exp 0,8,4,1,2 --json gpurun_out/$out/wino4_exp.json") ;;
