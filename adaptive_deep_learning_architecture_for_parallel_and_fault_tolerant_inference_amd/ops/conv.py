@@ -425,6 +425,8 @@ def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int
     if ksplit > 1:
         return ksplit * M * N
     if ksplit < 0:
+        if cfg in F32S_CFGS:
+            return f32s_ws_elems(cfg)
         if cfg in WINO4_F32_CFGS:
             return -ksplit * M * N
         if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
@@ -460,6 +462,8 @@ def f32_counter_elems(cfg: int, ksplit: int, B: int, H: int, W: int, OH: int, OW
     Winograd split-K blocks; 0 for plain launches."""
     if ksplit >= 0:
         return 0
+    if cfg in F32S_CFGS:
+        return f32s_tiles(cfg, B * OH * OW, N)
     if cfg in WINO4_F32_CFGS:
         return wino4_blocks(B, H, W, N)
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
@@ -607,6 +611,32 @@ PW_F32_BMS = {64: (1, 2, 4, 5, 16, 32), 128: (1, 2, 4, 5, 16, 32), 256: (1, 2, 3
               512: (1, 2, 3, 4, 5, 16, 32), 1024: (1, 2, 3, 4, 5, 16)}
 
 
+# fp32 big-tile 1x1 GEMM (csrc/kernels/gemm_f32s.hip, cfg ids 300+): id -> (BM, BN); 4 waves side by side
+# along N, BM chosen per layer so the tiles fill the CUs; 1x1 / pad 0 / stride 1-2, Cin % 32 == 0, N % 16 == 0;
+# ksplit 1 (one block per tile) or -1 (stream-K over 256 blocks, XCD-grouped, fused fixup)
+F32S_CFGS = {300: (112, 256), 301: (224, 256), 302: (112, 128), 303: (224, 128), 304: (64, 256), 305: (160, 256),
+             306: (192, 128)}
+# measured behind the pointwise / ring kernels on all 7 ResNet-50 bs=32 1x1 shapes (profiles/r5/
+# gemm_f32s_attribution.md: one tile per CU writes the whole output after the K loop, 5-14 us of HBM-bound
+# epilogue that nothing overlaps); runnable and tested, never tuned
+F32_UNTUNED = WINO4_UNTUNED | frozenset(F32S_CFGS)
+
+
+def f32s_supported(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 0, 0, 0, 0) and pc.stride in (1, 2)
+            and pc.cin % 32 == 0 and pc.cout % 16 == 0 and pc.Kpad == pc.cin)
+
+
+def f32s_tiles(cfg: int, M: int, N: int) -> int:
+    bm, bn = F32S_CFGS[cfg]
+    return math.ceil(M / bm) * math.ceil(N / bn)
+
+
+def f32s_ws_elems(cfg: int) -> int:
+    bm, bn = F32S_CFGS[cfg]
+    return 2 * 256 * bm * bn
+
+
 def pw_f32_slice(K: int) -> int:
     """Output channels per block of the pointwise kernel (FPW x 16 x waves per K group)."""
     return PW_F32_FPW[K] * 16 * (8 // PW_F32_KG.get(K, 1))
@@ -639,6 +669,8 @@ def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] 
                 and pw_f32_shape_ok(pc, PW_F32_CFGS[cfg]))
     if cfg in WINO4_F32_CFGS:
         return pc is not None and pc.wino4 is not None and wino4_supported(pc)
+    if cfg in F32S_CFGS:
+        return pc is not None and f32s_supported(pc)
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         fn = {**WINO_F32_CFGS, **WINO_F32_ABLATE}[cfg][1]
         return pc is not None and pc.wino is not None and wino_supported(pc) and cout % (16 * fn) == 0
@@ -746,6 +778,27 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         kernels().pw_f32_forward(ptr(x), ptr(pc.pwf), ptr(pc.bias), ptr(residual), ptr(out), M, C, N, int(relu),
                                  PW_F32_CFGS[cfg], stream_handle(stream), B, H, W, OH, OW, pc.stride, ptr(out2),
                                  int(ns), int(relu2))
+        return out
+    if cfg in F32S_CFGS:
+        # big-tile 1x1 GEMM: whole K per tile (ksplit 1) or stream-K over 256 blocks (ksplit -1)
+        ksplit = int(ksplit) or 1
+        if not f32_cfg_supported(cfg, C, N, pc) or x.dim() != 4 or ksplit not in (1, -1):
+            raise ValueError(f"fp32 1x1 GEMM config {cfg}: 1x1 / pad 0 / stride 1-2 conv, Cin % 32 == 0, "
+                             f"N % 16 == 0, ksplit 1 or -1")
+        ws_ptr = ctr_ptr = 0
+        if ksplit < 0:
+            need = f32s_ws_elems(cfg)
+            if workspace is None:
+                workspace = torch.empty(need, dtype=torch.float32, device=x.device)
+            if workspace.numel() < need or workspace.dtype != torch.float32:
+                raise ValueError(f"fp32 1x1 GEMM stream-K needs an fp32 workspace of {need} elements")
+            nt = f32s_tiles(cfg, M, N)
+            if counters is None or counters.numel() < nt or counters.dtype != torch.int32:
+                raise ValueError(f"fp32 1x1 GEMM stream-K needs {nt} int32 tile counters (zeroed)")
+            ws_ptr, ctr_ptr = ptr(workspace), ptr(counters)
+        kernels().conv_f32_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W,
+                                   C, OH, OW, N, 1, 1, pc.stride, 0, 0, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),
+                                   stream_handle(stream), ctr_ptr, ptr(out2), int(ns), int(relu2))
         return out
     if cfg in WINO4_F32_CFGS:
         # Winograd F(4x4, 3x3): ksplit > 1 slabs + splitk_reduce_f32, ksplit <= -2 fused fixup (counters)

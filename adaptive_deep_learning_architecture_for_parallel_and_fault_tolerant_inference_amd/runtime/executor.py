@@ -558,9 +558,9 @@ class SliceExecutor:
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
             for cfg in (list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.WINO4_F32_CFGS)
-                        + list(conv_ops.PW_F32_CFGS)):
+                        + list(conv_ops.PW_F32_CFGS) + list(conv_ops.F32S_CFGS)):
                 if (not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc) or cfg in conv_ops.WINO_MEASURE_CFGS
-                        or cfg in conv_ops.WINO4_UNTUNED):
+                        or cfg in conv_ops.F32_UNTUNED):
                     continue
                 if cfg in conv_ops.WINO4_F32_CFGS:           # Winograd F(4x4,3x3): splits with even chunk counts
                     if not conv_ops.wino4_map_ok(B, H, W, cfg):
@@ -569,6 +569,8 @@ class SliceExecutor:
                     tiles, kts, sks = conv_ops.wino4_blocks(B, H, W, N), C // 8, tuple(sp) + tuple(-k for k in sp)
                 elif cfg in conv_ops.PW_F32_CFGS:            # persistent pointwise: whole K, one launch
                     tiles, kts, sks = 0, 1, ()
+                elif cfg in conv_ops.F32S_CFGS:             # big-tile 1x1 GEMM: tiles, or stream-K over 256
+                    tiles, kts, sks = conv_ops.f32s_tiles(cfg, M, N), C // 32, (-1,)
                 elif cfg in conv_ops.WINO_F32_CFGS:         # Winograd F(2x2,3x3): split-K over 16-channel chunks
                     nwm, fn = conv_ops.WINO_F32_CFGS[cfg]
                     tiles = math.ceil(B * ((OH + 1) // 2) * ((OW + 1) // 2) / (16 * nwm)) * (N // (16 * fn))
@@ -582,7 +584,8 @@ class SliceExecutor:
                     tiles = math.ceil(M / bm) * math.ceil(N / bn)
                     kts = ktiles
                     sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
-                for ks in ((1,) if cfg in conv_ops.PW_F32_CFGS or cfg in conv_ops.WINO4_F32_CFGS else
+                for ks in ((1,) if cfg in conv_ops.PW_F32_CFGS or cfg in conv_ops.WINO4_F32_CFGS
+                           or cfg in conv_ops.F32S_CFGS else
                            (1, 2, 4, 8, 16) if cfg not in conv_ops.WINO_SK_CFGS else ()) + sks:
                     # split-K / stream-K only where the tiles alone leave CUs idle
                     if ks > 1 and (kts // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):

@@ -263,6 +263,14 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("wino_set_debug", [](u64 buf) { adapt::wino_set_debug(P<unsigned long long>(buf)); });
   m.def("conv_wino4pc_pieces", &adapt::conv_wino4pc_pieces);
+  m.def("gemm_f32s_cfg", [](int cfg) {
+    int bm = 0, bn = 0;
+    const bool ok = adapt::gemm_f32s_cfg(cfg, &bm, &bn);
+    return py::make_tuple(ok ? bm : 0, ok ? bn : 0);
+  });
+  m.def("gemm_f32s_ws_elems", &adapt::gemm_f32s_ws_elems);
+  m.def("gemm_f32s_set_debug", [](u64 buf, int exp) { adapt::gemm_f32s_set_debug(P<unsigned long long>(buf), exp); },
+        py::arg("buf"), py::arg("exp") = 0);
   m.def("wino4_set_debug", [](u64 buf, int exp) { adapt::wino4_set_debug(P<unsigned long long>(buf), exp); },
         py::arg("buf"), py::arg("exp") = 0);
   m.def("pw_set_debug", [](u64 buf) { adapt::pw_set_debug(P<unsigned long long>(buf)); });

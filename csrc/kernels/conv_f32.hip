@@ -270,7 +270,8 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
   ConvF32Params p{x, w, bias, res, out, ws, B, H, W, Cin, OH, OW, N, KH, KW, stride, pad_t, pad_l,
                   B * OH * OW, K, Kpad, relu, ksplit == 0 ? 1 : ksplit, counters, 0, out2, n_split, relu2};
   if (Kpad % FBK || (p.ksplit > 1 && ws == nullptr)) return hipErrorInvalidValue;
-  if (n_split && (n_split % 4 || n_split >= N || !out2 || res || cfg >= 80)) return hipErrorInvalidValue;
+  if (n_split && (n_split % 4 || n_split >= N || !out2 || res || (cfg >= 80 && cfg < 300))) return hipErrorInvalidValue;
+  if (cfg >= 300) return gemm_f32s_launch(p, cfg, s);   // big-tile 1x1 GEMM (gemm_f32s.hip)
   if (p.ksplit < 0 && cfg < 80) {
     // stream-K: v2 configs only
     int bm, bn, g;

@@ -185,6 +185,14 @@ int wino4_exp_flags();
 // (1 KiB) of the widest 32-tile block, 0 when the geometry is not supported
 int conv_wino4pc_pieces(int B, int H, int W);
 hipError_t conv_wino4pc_f32_launch(const WinoF32Params& p, hipStream_t s);
+// fp32 big-tile 1x1 GEMM (gemm_f32s.hip, cfg ids 300+): tile (BM, BN) per cfg; ksplit 1 (tiles) or -1 (stream-K
+// over 256 blocks: gemm_f32s_ws_elems floats of workspace, one zeroed int32 counter per tile)
+bool gemm_f32s_cfg(int cfg, int* bm, int* bn);
+size_t gemm_f32s_ws_elems(int cfg);
+// tools/gemm_f32s_timeline.py: launches stamp 8 words per wave into buf while it is set; exp selects a
+// measurement variant (1 no LDS-DMA in the loop, 2 no MFMAs)
+void gemm_f32s_set_debug(unsigned long long* buf, int exp);
+hipError_t gemm_f32s_launch(const ConvF32Params& p, int cfg, hipStream_t s);
 hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, const float* res, float* out,
                             float* ws, int B, int H, int W, int Cin, int OH, int OW, int N, int KH, int KW,
                             int stride, int pad_t, int pad_l, int K, int Kpad, int relu, int ksplit, int cfg,

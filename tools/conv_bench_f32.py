@@ -41,7 +41,7 @@ def bench(shape, only=None, ks_list=(1, 2, 4, -1, -2), reps=10, top=20):
                 continue                              # persistent Winograd: whole K
             if -100 < ks and abs(ks) > 1 and (wino or ks > 0) and (Cin // 16 if wino else pc.Kpad // C.F32_BK) // abs(ks) < 2:
                 continue
-            if ks < 0 and cfg not in C.F32G_CFGS and not (wino and ks <= -2):
+            if ks < 0 and cfg not in C.F32G_CFGS and not (wino and ks <= -2) and not (cfg in C.F32S_CFGS and ks == -1):
                 continue
             nws = C.workspace_elems_f32(M, N, pc.Kpad, cfg, ks)
             ws = torch.empty(nws, device=dev) if nws else None
@@ -73,8 +73,13 @@ def bench(shape, only=None, ks_list=(1, 2, 4, -1, -2), reps=10, top=20):
     print(f"\n== fp32 B{B} {H}x{W}x{Cin} -> {Cout} k{k} s{s} res{has_res}  M={M} N={N} K={pc.K}  "
           f"{flop / 1e9:.2f} GFLOP  (floor {flop / 150e12 * 1e6:.1f} us at 150 TF/s)", flush=True)
     for t, cfg, ks in rows[:top]:
-        print(f"  cfg {cfg:2d} {str(C.F32_TILES.get(cfg, (('pw', C.PW_F32_CFGS[cfg]) if cfg in C.PW_F32_CFGS else ('wino',) + {**C.WINO_F32_CFGS, **C.WINO_F32_ABLATE}.get(cfg, ())))):10s} ks {ks:2d}  {t:7.2f} us  {flop / t / 1e6:6.1f} TF/s",
-              flush=True)
+        if cfg in C.F32S_CFGS:
+            kind = ("gemm_s",) + C.F32S_CFGS[cfg]
+        elif cfg in C.PW_F32_CFGS:
+            kind = ("pw", C.PW_F32_CFGS[cfg])
+        else:
+            kind = C.F32_TILES.get(cfg, ("wino",) + {**C.WINO_F32_CFGS, **C.WINO_F32_ABLATE}.get(cfg, ()))
+        print(f"  cfg {cfg:2d} {str(kind):10s} ks {ks:2d}  {t:7.2f} us  {flop / t / 1e6:6.1f} TF/s", flush=True)
     return rows
 
 

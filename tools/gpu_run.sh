@@ -82,6 +82,9 @@ for p in "${P[@]}"; do
               steps+=("180|$out/local_infer_bs1_1000|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd local-infer --model resnet50 --batch 1 --requests 1000 --device cuda") ;;
     gemm1x1)  steps+=("300|$out/gemm1x1_bigtiles|python -u tools/conv_bench_f32.py --only 10,11,12,13,14,15,16,17,18,30,31,32,33,34,37,38 --ks 1,2,-1,-2 --top 8 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,28,28,512,128,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1") ;;
     bf3x3)    steps+=("300|$out/bf16_3x3_s45|python -u tools/conv_bench.py --shape 32,14,14,256,256,3,1,1,0 --shape 32,7,7,512,512,3,1,1,0 --ks 1,2,3,4,-1,-2") ;;
+    gs)       steps+=("300|$out/pytest_gemm_f32s|python -u -m pytest tests/test_gemm_f32s_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/gemm_f32s_bench|python -u tools/conv_bench_f32.py --only 300,301,302,303,304,305,306,18,38,122,123,125,126 --ks 1,-1,-2 --top 10 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,14,14,256,1024,1,1,0,1 --shape 32,7,7,2048,512,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1 --shape 32,28,28,512,128,1,1,0,0 --shape 32,28,28,128,512,1,1,0,1 --shape 32,56,56,256,64,1,1,0,0 --shape 32,56,56,64,256,1,1,0,1") ;;
+    gst)      steps+=("200|$out/gemm_f32s_timeline|python -u tools/gemm_f32s_timeline.py --json gpurun_out/$out/gemm_f32s_timeline.json") ;;
     codec)    steps+=("300|$out/codec_fp32|python -u tools/codec_bench.py --precision fp32 --json gpurun_out/$out/codec_fp32.json") ;;
     w4pcx)    steps+=("200|$out/wino4pc_exp|python -u tools/wino4_timeline.py --cfg 210 --exp 0,1,4,5,12,13,14,17,21 --json gpurun_out/$out/wino4pc_exp.json") ;;
     w4x)      steps+=("200|$out/wino4_exp|python -u tools/wino4_timeline.py --exp 0,8,4,1,2 --json gpurun_out/$out/wino4_exp.json") ;;
