@@ -211,6 +211,7 @@ constexpr int S2_ROWS0 = 11;                              // patch rows the firs
 constexpr int S2_ITEMS0 = (S2_ROWS0 * ST_PWC + S2_NT - 1) / S2_NT;
 constexpr int S2_ITEMS1 = (4 * ST_PWC + S2_NT - 1) / S2_NT;  // 4 new input rows per later step
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 union P8 {                                                 // 8 bf16 as 16 B or as 4 packed u16 pairs
   u32x4 u;
   u16x2 h[4];
@@ -218,13 +219,13 @@ union P8 {                                                 // 8 bf16 as 16 B or 
 }  // namespace
 
 // fp32 NHWC patch rows [row0, row0 + nrows) -> registers (loads only; `put_rows` converts + stores)
-template <int ITEMS>
+template <int ITEMS, int NT = S2_NT>
 __device__ __forceinline__ void get_rows(float (&pv)[ITEMS][4], const float* __restrict__ xi, int tid, int row0,
                                          int nrows, int row_end, int ih0, int H, int W, int C, int pwc, int pad_l) {
   const __amdgpu_buffer_rsrc_t xr = stem_rsrc(xi, H, W, C);
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
-    const int idx = tid + k * S2_NT;
+    const int idx = tid + k * NT;
     const int i = row0 + idx / ST_PWC, j = idx % ST_PWC;
     const int ih = ih0 + i, iw = j - pad_l;
     const bool ok = idx < nrows * ST_PWC && i < row_end && j < pwc && (unsigned)ih < (unsigned)H &&
@@ -250,11 +251,11 @@ __device__ __forceinline__ void put_rows(const float (&pv)[ITEMS][4], bf16* patc
 
 // patch items [k0, k0 + N) of a block's whole patch -> LDS, rows [rlo, rhi) only (k compile-time: no
 // register indexing; the compiler waits only for the loads of the items it stores)
-template <int K0, int N, int ITEMS>
+template <int K0, int N, int ITEMS, int NT = S2_NT>
 __device__ __forceinline__ void put_items(const float (&pv)[ITEMS][4], bf16* patch, int tid, int rlo, int rhi) {
 #pragma unroll
   for (int k = K0; k < K0 + N; ++k) {
-    const int idx = tid + k * S2_NT;
+    const int idx = tid + k * NT;
     if (idx >= rlo * ST_PWC && idx < rhi * ST_PWC) {
       bf16x4s v;
 #pragma unroll
@@ -392,6 +393,267 @@ __global__ __launch_bounds__(S2_NT, 1) void stem_pool_v2_kernel(const float* __r
   for (int t = t0 + 1; t < t1; ++t) step(t, std::integral_constant<bool, false>{});
 }
 
+// ---- v4 pooled stem: software-pipelined conv / pool, 8 waves -------------------------------------------
+//
+// v3 (26 us at bs=32, profiles/r4/stem_bf16) alternates "conv 2 rows | barrier | pool 1 row | barrier" with
+// 7 waves: MFMA busy 0.21, 37 % of LDS cycles lost to bank conflicts, 2 of the 4 SIMDs carrying 2 waves
+// and 2 carrying 1 or 2.  v4:
+// * one barrier per step: step k computes conv rows 2k+1, 2k+2 of the block into a 6-row ring while
+//   the same waves pool row k-1 from rows 2k-2..2k, finished the step before (the two row sets never
+//   share a ring slot);
+// * 8 waves = 2 per SIMD: one wave's pool reads / stores hide behind its SIMD partner's MFMAs;
+// * ring rows stored as pixel pairs (256 B = all 64 banks) with the 16-byte unit index XOR-swizzled by
+//   pair & 15: the MFMA epilogue's 16 lanes (8 aligned pairs x 2 pixels, one channel chunk) and the
+//   pool's 16 lanes (16 consecutive pool columns = 16 consecutive pairs, one chunk; the lane order is
+//   pool column fastest) both hit 16 distinct bank groups.
+namespace {
+constexpr int S4_SP = 7;                                   // pool rows per block
+constexpr int S4_WAVES = 8;
+constexpr int S4_NT = S4_WAVES * 64;
+constexpr int S4_RING = 6;
+constexpr int S4_PAIRS = ST_OWMAX / 2;
+constexpr int S4_PROWS = 4 * S4_SP + 7;
+constexpr int S4_ITEMS = (S4_PROWS * ST_PWC + S4_NT - 1) / S4_NT;     // 16
+constexpr int S4_ITEMS_A = (S2_ROWS0 * ST_PWC + S4_NT - 1) / S4_NT;   // items holding rows 0..10 (5)
+static_assert(S4_PROWS * ST_PWC * 8 + S4_RING * S4_PAIRS * 256 <= 160 * 1024, "v4 LDS");
+
+// barrier for LDS hand-offs only: __syncthreads() also waits for every outstanding global store (its
+// workgroup-scope release), which put the pool rows' HBM write latency (~1.8 us) into every v4 step
+__device__ __forceinline__ void s4_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct F3 {
+  float a, b, c;
+};
+// 3-channel images: one 12-byte load per patch item (consecutive lanes = consecutive pixels, fully
+// coalesced) instead of one 4-byte buffer load per channel; items outside the image read pixel 0 and
+// are zeroed after the load, so no load sits behind a branch
+template <int ITEMS, int NT>
+__device__ __forceinline__ void get_rows3(float (&pv)[ITEMS][4], const float* __restrict__ xi, int tid, int row_end,
+                                          int ih0, int H, int W, int pwc, int pad_l) {
+  F3 v[ITEMS];
+  bool ok[ITEMS];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int idx = tid + k * NT;
+    const int i = idx / ST_PWC, j = idx - i * ST_PWC;
+    const int ih = ih0 + i, iw = j - pad_l;
+    ok[k] = i < row_end && j < pwc && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    v[k] = *(const F3*)(xi + (ok[k] ? (ih * W + iw) * 3 : 0));
+  }
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    pv[k][0] = ok[k] ? v[k].a : 0.f;
+    pv[k][1] = ok[k] ? v[k].b : 0.f;
+    pv[k][2] = ok[k] ? v[k].c : 0.f;
+    pv[k][3] = 0.f;
+  }
+}
+
+// bf16 element offset of 16-byte channel chunk `chunk` of conv pixel `ow` in ring slot `slot`
+__device__ __forceinline__ int ring4_off(int slot, int ow, int chunk) {
+  const int pair = ow >> 1;
+  const int u = (((ow & 1) << 3) | chunk) ^ (pair & 15);
+  return ((slot * S4_PAIRS + pair) * 16 + u) * 8;
+}
+}  // namespace
+
+template <bool C3>
+__global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
+                                                                const float* __restrict__ bias, bf16* __restrict__ out,
+                                                                int H, int W, int C, int OH, int OW, int pad_t,
+                                                                int pad_l, int PH, int PW, int pool_pad, int groups,
+                                                                unsigned long long* dbg_all) {
+  __shared__ __attribute__((aligned(16))) bf16 patch[S4_PROWS * ST_PWC * 4];       // 63.4 KiB
+  __shared__ __attribute__((aligned(16))) bf16 ring[S4_RING * S4_PAIRS * 16 * 8];  // 84 KiB
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = logical / groups;
+  const int t0 = (logical - img * groups) * S4_SP;
+  const int t1 = min(PH, t0 + S4_SP);                      // pool rows [t0, t1)
+  const int r_first = 2 * t0 - pool_pad;                   // conv row of ring row 0 (may be -1)
+  const int ih0 = 2 * r_first - pad_t;                     // input row of patch row 0
+  const int row_end = 4 * (t1 - t0) + 7;
+  const int tpr = (OW + 15) >> 4;
+  const int pwc = 2 * tpr * 16 + 8;
+  const float* xi = x + (size_t)img * H * W * C;
+  // measurement only (tools/stem_timeline.py): per wave, shader clock at start / patch rows 0-10 in LDS /
+  // step 0 done / steps done / end, wall clock at start and end
+  unsigned long long* const dbg = dbg_all ? dbg_all + 8 * (wave + S4_WAVES * blockIdx.x) : nullptr;
+  auto stamp = [&](int i) {
+    if (dbg != nullptr && lane == 0) dbg[i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  if (dbg && lane == 0) dbg[6] = __builtin_amdgcn_s_memrealtime();
+
+  // weights and bias first: loads return in order, so step 0 then waits only for them and patch rows 0-10
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 bw[7][4];
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bw[s][n] = *(const bf16x8*)(w + (size_t)(n * 16 + fr) * ST_K + s * 32 + fq * 8);
+  float b4[4][4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b4[n][r] = bias[n * 16 + 4 * fq + r];
+  float pall[S4_ITEMS][4];
+  if constexpr (C3)
+    get_rows3<S4_ITEMS, S4_NT>(pall, xi, tid, row_end, ih0, H, W, pwc, pad_l);
+  else
+    get_rows<S4_ITEMS, S4_NT>(pall, xi, tid, 0, row_end, row_end, ih0, H, W, C, pwc, pad_l);
+  put_items<0, S4_ITEMS_A, S4_ITEMS, S4_NT>(pall, patch, tid, 0, S2_ROWS0);
+  s4_lds_barrier();
+  stamp(1);
+
+  // one 16-pixel x 64-channel conv tile: geometry / A-fragment reads / MFMAs / bias + ReLU into the ring.
+  // ReLU after the bf16 rounding as a packed signed max with 0: the same bits as rounding max(y, 0)
+  // (a value <= 0 rounds to a bf16 <= 0, including -0, which the integer max sends to +0)
+  struct Tile {
+    bool ok;
+    int slot;                                              // ring slot base (bf16 elements)
+    const bf16* pa;
+    int col[4];                                            // per 16-channel group: offset within the slot
+  };
+  auto tile_cols = [&](Tile& g, const int ow) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) g.col[n] = ring4_off(0, ow, 2 * n + (fq >> 1)) + 4 * (fq & 1);
+  };
+  auto tile_geo = [&](const int mt, const int rel0, const int ntiles) __attribute__((always_inline)) {
+    Tile g;
+    const int q = mt / tpr;
+    const int rel = rel0 + q, r = r_first + rel;
+    g.ok = mt < ntiles && r >= 0 && r < OH;               // wave-uniform; the pool never reads skipped rows
+    const int ow = (mt - q * tpr) * 16 + fr;
+    g.slot = (rel % S4_RING) * (S4_PAIRS * 128);
+    g.pa = patch + ((2 * rel) * ST_PWC + 2 * ow + 2 * fq) * 4;
+    tile_cols(g, ow);
+    return g;
+  };
+  auto tile_read = [&](const Tile& g, bf16x8 (&a)[7]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 7; ++s) a[s] = *(const bf16x8*)(g.pa + s * ST_PWC * 4);
+  };
+  auto tile_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][n], a[s], acc[n], 0, 0, 0);
+  };
+  auto tile_store = [&](const Tile& g, const f32x4 (&acc)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      union {
+        bf16x4s b;
+        s16x2 h[2];
+      } v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v.b.v[e] = f2bf(acc[n][e] + b4[n][e]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) v.h[i] = __builtin_elementwise_max(v.h[i], (s16x2){0, 0});
+      *(bf16x4s*)(ring + g.slot + g.col[n]) = v.b;
+    }
+  };
+  auto tile_run = [&](const Tile& g) __attribute__((always_inline)) {
+    bf16x8 a[7];
+    f32x4 acc[4];
+    tile_read(g, a);
+    tile_mfma(a, acc);
+    tile_store(g, acc);
+  };
+  // conv rows [rel0, rel0 + nr) of the block (ring row index rel = conv row - r_first) -> ring
+  auto conv_rows = [&](const int rel0, const int nr) __attribute__((always_inline)) {
+    const int ntiles = nr * tpr;
+    for (int mt = wave; mt < ntiles; mt += S4_WAVES) {
+      const Tile g = tile_geo(mt, rel0, ntiles);
+      if (g.ok) tile_run(g);
+    }
+  };
+  // pool row t from conv rows 2t-pp .. 2t-pp+2 (non-negative bf16: packed integer max; the zero padding
+  // is the 0 the max starts from).  A thread owns one item (chunk, pool column) for every row, pool
+  // column fastest across lanes (PW * 8 <= 512 threads: host check), its three ring column offsets
+  // hoisted.  Window positions outside the conv output are clamped to the nearest row / column, which is
+  // inside the same window: a duplicate cannot change a max, and all nine reads issue without a branch.
+  const bool pool_item = tid < PW * 8;
+  const int pch8 = tid / PW, ppw = tid - pch8 * PW;
+  int pcol[3];
+#pragma unroll
+  for (int dc = 0; dc < 3; ++dc) pcol[dc] = ring4_off(0, min(max(2 * ppw - pool_pad + dc, 0), OW - 1), pch8);
+  bf16* const pout = out + ((size_t)img * PH * PW + ppw) * 64 + pch8 * 8;
+  auto pool_read = [&](const int t, P8 (&v)[9]) __attribute__((always_inline)) {
+    int rb[3];
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+      const int oh = min(max(2 * t - pool_pad + dr, 0), OH - 1);
+      rb[dr] = ((oh - r_first) % S4_RING) * (S4_PAIRS * 128);
+    }
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+      for (int dc = 0; dc < 3; ++dc) v[3 * dr + dc].u = *(const u32x4*)(ring + rb[dr] + pcol[dc]);
+  };
+  auto pool_finish = [&](const int t, const P8 (&v)[9]) __attribute__((always_inline)) {
+    P8 m = v[0];
+#pragma unroll
+    for (int i = 1; i < 9; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m.h[e] = __builtin_elementwise_max(m.h[e], v[i].h[e]);
+    *(u32x4*)(pout + (size_t)t * PW * 64) = m.u;
+  };
+  auto pool_row = [&](const int t) __attribute__((always_inline)) {
+    if (!pool_item) return;
+    P8 v[9];
+    pool_read(t, v);
+    pool_finish(t, v);
+  };
+
+  // step 0: conv rows 0..2; the rest of the patch lands under its MFMAs (step 1 reads patch rows <= 14)
+  conv_rows(0, 3);
+  put_items<S4_ITEMS_A - 1, S4_ITEMS - S4_ITEMS_A + 1, S4_ITEMS, S4_NT>(pall, patch, tid, S2_ROWS0, row_end);
+  s4_lds_barrier();
+  stamp(2);
+  const int P = t1 - t0;
+  // step k: conv rows 2k+1, 2k+2 and pool row k-1 from rows 2k-2 .. 2k (ring slots disjoint).  A wave's
+  // (at most two) tiles sit at the same place of every step's row pair: their column geometry is computed
+  // once.  (Interleaving a wave's pool reads / second tile's reads under its first tile's MFMAs by hand
+  // measured slower: 22.4 vs 21.6 us.)
+  {
+    const int ntl = 2 * tpr;
+    Tile ga = tile_geo(wave, 0, ntl), gb = tile_geo(wave + S4_WAVES, 0, ntl);
+    const int qa = wave / tpr, qb = (wave + S4_WAVES) / tpr;
+    const bool has_a = wave < ntl, has_b = wave + S4_WAVES < ntl;
+    const bf16* const pa0 = ga.pa - (2 * qa) * ST_PWC * 4;   // tile_geo(., 0, .) put rel = q in pa
+    const bf16* const pb0 = gb.pa - (2 * qb) * ST_PWC * 4;
+    for (int k = 1; k < P; ++k) {
+      const int rel_a = 2 * k + 1 + qa, rel_b = 2 * k + 1 + qb;
+      ga.ok = has_a && r_first + rel_a < OH;               // rel >= 3: never above the image
+      ga.slot = (rel_a % S4_RING) * (S4_PAIRS * 128);
+      ga.pa = pa0 + (2 * rel_a) * ST_PWC * 4;
+      gb.ok = has_b && r_first + rel_b < OH;
+      gb.slot = (rel_b % S4_RING) * (S4_PAIRS * 128);
+      gb.pa = pb0 + (2 * rel_b) * ST_PWC * 4;
+      if (ga.ok) tile_run(ga);
+      if (gb.ok) tile_run(gb);
+      pool_row(t0 + k - 1);
+      s4_lds_barrier();
+    }
+  }
+  stamp(3);
+  pool_row(t1 - 1);
+  if (dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(4);
+    if (lane == 0) dbg[7] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+static unsigned long long* g_stem_dbg = nullptr;
+void stem_set_debug(unsigned long long* buf) { g_stem_dbg = buf; }
+
 hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
                         int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
                         hipStream_t s) {
@@ -403,9 +665,22 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
     // dozen blocks (8 at B=1): there the one-pool-row-per-block v1 grid fills more
     // CUs and wins.  ADAPT_STEM_V1=1 / =0 forces v1 / v2 (A/B switch).
     const int groups = (PH + S2_SP - 1) / S2_SP;
-    // ADAPT_STEM_V1=1 / =0 / =3: v1 / v2 / v3 (v3: the row-group kernel with the whole patch requested up front)
+    // ADAPT_STEM_V1=1 / =0 / =3 / =4: v1 / v2 / v3 (v3: the row-group kernel with the whole patch requested up
+    // front) / v4 (8 waves, pool of step k-1 beside the conv of step k)
     const char* v1 = getenv("ADAPT_STEM_V1");
-    const char ver = v1 && v1[0] ? v1[0] : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : '3');
+    // default: v1 for small batches, v4 (21.4 us vs v3's 26.1 at bs=32, profiles/r5/stem_bf16_v4.md) above
+    const char ver = v1 && v1[0] ? v1[0] : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : (PW * 8 <= S4_NT ? '4' : '3'));
+    if (ver == '4') {
+      if (PW * 8 > S4_NT) return hipErrorInvalidValue;
+      const int g4 = (PH + S4_SP - 1) / S4_SP;
+      if (C == 3)
+        hipLaunchKernelGGL(stem_pool_v4_kernel<true>, dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH,
+                           OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+      else
+        hipLaunchKernelGGL(stem_pool_v4_kernel<false>, dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH,
+                           OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+      return hipGetLastError();
+    }
     if (ver != '1') {
       if (ver == '3')
         hipLaunchKernelGGL(stem_pool_v2_kernel<true>, dim3(groups * B), dim3(S2_NT), 0, s, x, w, bias, out, H, W, C,

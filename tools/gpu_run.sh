@@ -28,6 +28,7 @@
 #             8-worker SIGKILL and a 4-worker hang, all workers on cuda:0 (parallel/fault_run.py)
 #   wino4     fp32 Winograd numerics + isolated timings incl. the v3 cfgs 116/117
 #   stem      fp32 stem numerics + isolated timing (tools/stem_bench.py)
+#   stem16    bf16 stem numerics (v1-v4) + isolated timing
 #   wino5     Winograd numerics + isolated timings of 118/119 vs the front-loaded DMA cfgs 150-153
 #   wino6     Winograd numerics + isolated timings of 118 vs the stagger / priority cfgs 154-156
 #   wtl       per-block phase timelines of the Winograd kernel on the four ResNet-50 3x3 shapes
@@ -122,6 +123,9 @@ for p in "${P[@]}"; do
               steps+=("300|$out/hang4_defaults|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel.fault_run --workers 4 --devices cuda:0 --model resnet50 --image 224 --batch 32 --duration 20 --kill-at 8 --fault hang --json gpurun_out/$out/hang_r50_4w_defaults.json") ;;
     pmcw)     steps+=("500|$out/pmcw|bash tools/pmc_f32.sh gpurun_out/$out/pmcw 32,56,56,64,64,3,1,1,0:106:1 32,56,56,64,64,3,1,1,0:103:1 32,28,28,128,128,3,1,1,0:106:1 32,28,28,128,128,3,1,1,0:103:1 32,14,14,256,256,3,1,1,0:108:1 32,14,14,256,256,3,1,1,0:105:1") ;;
     pmc1x1)   steps+=("500|$out/pmc1x1|bash tools/pmc_f32.sh gpurun_out/$out/pmc1x1 32,14,14,1024,256,1,1,0,0:18:-2 32,14,14,256,1024,1,1,0,1:38:1 32,56,56,64,256,1,1,0,1:3:1 32,28,28,512,1024,1,2,0,0:20:-1") ;;
+    stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
+    stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
+              steps+=("120|$out/stem_bench|python -u tools/stem_bench.py") ;;
     stem)     steps+=("200|$out/pytest_stem|python -u -m pytest tests/test_fp32_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
               steps+=("120|$out/stem_bench|python -u tools/stem_bench.py")
               steps+=("120|$out/stem_bench_b|python -u tools/stem_bench.py") ;;
