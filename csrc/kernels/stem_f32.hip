@@ -64,6 +64,10 @@ constexpr int SF_TPR = SF_OWMAX / 16;        // variant 2: pixel tiles of a 112-
 // V = 0: one unit (16 px x 16 ch) at a time; 1: units software-pipelined; 2: each wave of a pair
 // takes a whole conv row per step, its 7 tiles unrolled with every LDS address a per-row base plus
 // an immediate (OW = 112 only)
+// the step barriers hand off LDS only (patch rows, conv ring): __syncthreads() would also wait for the pool
+// rows' global stores still in flight (its workgroup-scope release), an HBM write round trip per step
+__device__ __forceinline__ void sf_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <int V>
 __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
       }
     }
     if (more) put_rows(pv, nxt_lo, 4);
-    __syncthreads();
+    sf_lds_barrier();
     // pool row t from conv rows 2t-pp .. 2t-pp+2; post-ReLU values are >= 0, so the
     // zero padding is the 0 the max starts from
     // (all 9 reads unconditional, out-of-image taps clamped and masked to 0, so they issue back to back)
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
       }
       *(f32x4*)(out + (((size_t)img * PH + t) * PW + pw) * 64 + ch * 4) = m;
     }
-    __syncthreads();                                            // ring slots of rows 2t-pp, 2t-pp+1 are free
+    sf_lds_barrier();                                           // ring slots of rows 2t-pp, 2t-pp+1 are free
   }
 }
 
