@@ -110,7 +110,8 @@ PYBIND11_MODULE(_C, m) {
     check(adapt::zvc_gpu_decompress_dev(P<const uint8_t>(stream), nseg, n, esz, P<void>(out), P<uint32_t>(offs), S(s)),
           "zvc_gpu_decompress_dev");
   });
-  m.def("stem_set_debug", [](u64 buf) { adapt::stem_set_debug(reinterpret_cast<unsigned long long*>(buf)); });
+  m.def("stem_set_debug", [](u64 buf, int exp) { adapt::stem_set_debug(reinterpret_cast<unsigned long long*>(buf), exp); },
+        py::arg("buf"), py::arg("exp") = 0);
   m.def("stem_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW, int pad_t,
                            int pad_l, int pool, int PH, int PW, int pool_pad, u64 s) {
     check(adapt::stem_forward(P<const float>(x), P<const bf16>(w), P<const float>(bias), P<bf16>(out), B, H, W, C,

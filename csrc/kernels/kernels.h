@@ -106,7 +106,7 @@ hipError_t pad(const bf16* x, bf16* y, int B, int H, int W, int C, int OH, int O
 hipError_t cast_f32_bf16(const float* x, bf16* y, size_t n, hipStream_t s);
 // stem: fp32 NHWC image -> 7x7/s2 conv (+BN folded, ReLU) [-> 3x3/s2 max-pool], weights [64][224] bf16
 // measurement only: per-wave phase stamps of the v4 pooled stem (8 words per wave), nullptr = off
-void stem_set_debug(unsigned long long* buf);
+void stem_set_debug(unsigned long long* buf, int exp = 0);
 hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
                         int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
                         hipStream_t s);

@@ -212,6 +212,9 @@ constexpr int S2_ITEMS0 = (S2_ROWS0 * ST_PWC + S2_NT - 1) / S2_NT;
 constexpr int S2_ITEMS1 = (4 * ST_PWC + S2_NT - 1) / S2_NT;  // 4 new input rows per later step
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 union P8 {                                                 // 8 bf16 as 16 B or as 4 packed u16 pairs
   u32x4 u;
   u16x2 h[4];
@@ -457,7 +460,9 @@ __device__ __forceinline__ int ring4_off(int slot, int ow, int chunk) {
 }
 }  // namespace
 
-template <bool C3>
+// EXP (tools/stem_timeline.py --exp, outputs wrong by design): 1 no MFMAs in the steps, 2 no pool in the
+// steps, 4 no ring stores in the steps, 8 no A-fragment reads in the steps
+template <bool C3, int EXP = 0>
 __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
                                                                 const float* __restrict__ bias, bf16* __restrict__ out,
                                                                 int H, int W, int C, int OH, int OW, int pad_t,
@@ -539,31 +544,59 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
   auto tile_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[4]) __attribute__((always_inline)) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // (pinning the 4-MFMA groups in order with sched_barrier: no change, 10.37 vs 10.2 us of steps)
 #pragma unroll
     for (int s = 0; s < 7; ++s)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][n], a[s], acc[n], 0, 0, 0);
   };
+  // packed: v_pk_add_f32 (bias) + v_cvt_pk_bf16_f32 + v_pk_max_i16 per channel pair (the scalar form
+  // compiled to one cvt per value plus a v_perm per pair)
   auto tile_store = [&](const Tile& g, const f32x4 (&acc)[4]) __attribute__((always_inline)) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      union {
-        bf16x4s b;
-        s16x2 h[2];
-      } v;
+      s16x2 h[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v.b.v[e] = f2bf(acc[n][e] + b4[n][e]);
+      for (int i = 0; i < 2; ++i) {
+        const f32x2 y = (f32x2){acc[n][2 * i], acc[n][2 * i + 1]} + (f32x2){b4[n][2 * i], b4[n][2 * i + 1]};
+        h[i] = __builtin_elementwise_max(__builtin_bit_cast(s16x2, __builtin_convertvector(y, bf16x2v)),
+                                         (s16x2){0, 0});
+      }
+      u32x2 w2 = {__builtin_bit_cast(unsigned, h[0]), __builtin_bit_cast(unsigned, h[1])};
+      *(u32x2*)(ring + g.slot + g.col[n]) = w2;
+    }
+  };
+  // the three phases of a tile with the measurement switches (EXP applies inside the step loop only)
+  auto t_read = [&](const Tile& g, bf16x8 (&a)[7], auto in_steps) __attribute__((always_inline)) {
+    if constexpr (decltype(in_steps)::value && (EXP & 8)) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) v.h[i] = __builtin_elementwise_max(v.h[i], (s16x2){0, 0});
-      *(bf16x4s*)(ring + g.slot + g.col[n]) = v.b;
+      for (int s = 0; s < 7; ++s) a[s] = bw[s][0];
+    } else {
+      tile_read(g, a);
+    }
+  };
+  auto t_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[4], auto in_steps) __attribute__((always_inline)) {
+    if constexpr (decltype(in_steps)::value && (EXP & 1)) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[n] = (f32x4){(float)a[0][0], (float)a[6][7], 0.f, 0.f};
+    } else {
+      tile_mfma(a, acc);
+    }
+  };
+  auto t_store = [&](const Tile& g, const f32x4 (&acc)[4], auto in_steps) __attribute__((always_inline)) {
+    if constexpr (decltype(in_steps)::value && (EXP & 4)) {
+      if (acc[0][0] == 12345.f && acc[3][1] == 1.f) ring[fr] = bf16(acc[0][0]);   // keep acc live
+    } else {
+      tile_store(g, acc);
     }
   };
   auto tile_run = [&](const Tile& g) __attribute__((always_inline)) {
+    constexpr std::integral_constant<bool, false> no{};
     bf16x8 a[7];
     f32x4 acc[4];
-    tile_read(g, a);
-    tile_mfma(a, acc);
-    tile_store(g, acc);
+    t_read(g, a, no);
+    t_mfma(a, acc, no);
+    t_store(g, acc, no);
   };
   // conv rows [rel0, rel0 + nr) of the block (ring row index rel = conv row - r_first) -> ring
   auto conv_rows = [&](const int rel0, const int nr) __attribute__((always_inline)) {
@@ -636,9 +669,24 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
       gb.ok = has_b && r_first + rel_b < OH;
       gb.slot = (rel_b % S4_RING) * (S4_PAIRS * 128);
       gb.pa = pb0 + (2 * rel_b) * ST_PWC * 4;
-      if (ga.ok) tile_run(ga);
-      if (gb.ok) tile_run(gb);
-      pool_row(t0 + k - 1);
+      // (both tiles' MFMAs before both epilogues measured slower: 11.5 vs 10.2 us of steps)
+      constexpr std::integral_constant<bool, true> yes{};
+      const int t = t0 + k - 1;
+      if (ga.ok) {
+        bf16x8 a[7];
+        f32x4 c[4];
+        t_read(ga, a, yes);
+        t_mfma(a, c, yes);
+        t_store(ga, c, yes);
+      }
+      if (gb.ok) {
+        bf16x8 a[7];
+        f32x4 c[4];
+        t_read(gb, a, yes);
+        t_mfma(a, c, yes);
+        t_store(gb, c, yes);
+      }
+      if (pool_item && !(EXP & 2)) pool_row(t);
       s4_lds_barrier();
     }
   }
@@ -652,7 +700,11 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
 }
 
 static unsigned long long* g_stem_dbg = nullptr;
-void stem_set_debug(unsigned long long* buf) { g_stem_dbg = buf; }
+static int g_stem_exp = 0;
+void stem_set_debug(unsigned long long* buf, int exp) {
+  g_stem_dbg = buf;
+  g_stem_exp = exp;
+}
 
 hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* out, int B, int H, int W, int C,
                         int OH, int OW, int pad_t, int pad_l, int pool, int PH, int PW, int pool_pad,
@@ -673,9 +725,23 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
     if (ver == '4') {
       if (PW * 8 > S4_NT) return hipErrorInvalidValue;
       const int g4 = (PH + S4_SP - 1) / S4_SP;
-      if (C == 3)
-        hipLaunchKernelGGL(stem_pool_v4_kernel<true>, dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH,
-                           OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+#define ADAPT_S4(E)                                                                                            \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, E>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH, \
+                     OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg)
+      if (C == 3 && g_stem_exp != 0) {
+        switch (g_stem_exp) {
+          case 1: ADAPT_S4(1); break;
+          case 2: ADAPT_S4(2); break;
+          case 4: ADAPT_S4(4); break;
+          case 8: ADAPT_S4(8); break;
+          case 3: ADAPT_S4(3); break;
+          case 13: ADAPT_S4(13); break;
+          case 15: ADAPT_S4(15); break;
+          default: return hipErrorInvalidValue;
+        }
+      } else if (C == 3)
+        ADAPT_S4(0);
+#undef ADAPT_S4
       else
         hipLaunchKernelGGL(stem_pool_v4_kernel<false>, dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH,
                            OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);

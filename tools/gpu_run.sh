@@ -124,6 +124,7 @@ for p in "${P[@]}"; do
     pmcw)     steps+=("500|$out/pmcw|bash tools/pmc_f32.sh gpurun_out/$out/pmcw 32,56,56,64,64,3,1,1,0:106:1 32,56,56,64,64,3,1,1,0:103:1 32,28,28,128,128,3,1,1,0:106:1 32,28,28,128,128,3,1,1,0:103:1 32,14,14,256,256,3,1,1,0:108:1 32,14,14,256,256,3,1,1,0:105:1") ;;
     pmc1x1)   steps+=("500|$out/pmc1x1|bash tools/pmc_f32.sh gpurun_out/$out/pmc1x1 32,14,14,1024,256,1,1,0,0:18:-2 32,14,14,256,1024,1,1,0,1:38:1 32,56,56,64,256,1,1,0,1:3:1 32,28,28,512,1024,1,2,0,0:20:-1") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
+    stemx)    steps+=("120|$out/stem_exp|python -u tools/stem_timeline.py --exp 0,1,2,4,8,3,13,15 --json gpurun_out/$out/stem_exp.json") ;;
     stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
               steps+=("120|$out/stem_bench|python -u tools/stem_bench.py") ;;
     stem)     steps+=("200|$out/pytest_stem|python -u -m pytest tests/test_fp32_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")

@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json", default="")
+    ap.add_argument("--exp", default="0", help="measurement variants: 1 no MFMA, 2 no pool, 4 no ring stores, "
+                    "8 no A reads in the steps (outputs wrong by design), comma list")
     a = ap.parse_args()
     K = C.kernels()
     B = a.batch
@@ -36,27 +38,32 @@ def main():
     out = torch.empty(B, 56, 56, 64, device="cuda", dtype=torch.bfloat16)
     os.environ["ADAPT_STEM_V1"] = "4"
     blocks = B * math.ceil(56 / SP)
-    dbg = torch.zeros(blocks * WAVES * 8, dtype=torch.int64, device="cuda")
-    for _ in range(3):
+    recs = []
+    for exp in [int(e) for e in a.exp.split(",")]:
+        dbg = torch.zeros(blocks * WAVES * 8, dtype=torch.int64, device="cuda")
+        for _ in range(3):
+            C.stem_forward(x, ps, out, pool=True)
+        torch.cuda.synchronize()
+        K.stem_set_debug(int(dbg.data_ptr()), exp)
         C.stem_forward(x, ps, out, pool=True)
-    torch.cuda.synchronize()
-    K.stem_set_debug(int(dbg.data_ptr()))
-    C.stem_forward(x, ps, out, pool=True)
-    torch.cuda.synchronize()
-    K.stem_set_debug(0)
-    d = dbg.view(blocks * WAVES, 8).cpu().numpy().astype(np.float64)
-    ghz = float(np.median((d[:, 4] - d[:, 0]) / np.maximum(d[:, 7] - d[:, 6], 1)) * 0.1)
-    ph = {}
-    for i, name in enumerate(("patch_rows_0_10", "step0", "steps", "last_pool_stores")):
-        v = (d[:, i + 1] - d[:, i]) / (ghz * 1e3)
-        ph[name] = {"median_us": round(float(np.median(v)), 2), "p90_us": round(float(np.percentile(v, 90)), 2),
-                    "max_us": round(float(v.max()), 2)}
-    start = (d[:, 6] - d[:, 6].min()) / 100.0
-    rec = {"kernel": "stem_pool_v4", "batch": B, "blocks": blocks, "clock_GHz": round(ghz, 3), "phases": ph,
-           "block_start_us": {"median": round(float(np.median(start)), 2), "max": round(float(start.max()), 2)},
-           "wave_total_us_median": round(float(np.median((d[:, 4] - d[:, 0]) / (ghz * 1e3))), 2),
-           "span_us": round(float((d[:, 7].max() - d[:, 6].min()) / 100.0), 2)}
-    print(json.dumps(rec), flush=True)
+        torch.cuda.synchronize()
+        K.stem_set_debug(0, 0)
+        d = dbg.view(blocks * WAVES, 8).cpu().numpy().astype(np.float64)
+        ghz = float(np.median((d[:, 4] - d[:, 0]) / np.maximum(d[:, 7] - d[:, 6], 1)) * 0.1)
+        ph = {}
+        for i, name in enumerate(("patch_rows_0_10", "step0", "steps", "last_pool_stores")):
+            v = (d[:, i + 1] - d[:, i]) / (ghz * 1e3)
+            ph[name] = {"median_us": round(float(np.median(v)), 2), "p90_us": round(float(np.percentile(v, 90)), 2),
+                        "max_us": round(float(v.max()), 2)}
+        start = (d[:, 6] - d[:, 6].min()) / 100.0
+        rec = {"kernel": "stem_pool_v4", "exp": exp, "batch": B, "blocks": blocks, "clock_GHz": round(ghz, 3),
+               "phases": ph,
+               "block_start_us": {"median": round(float(np.median(start)), 2), "max": round(float(start.max()), 2)},
+               "wave_total_us_median": round(float(np.median((d[:, 4] - d[:, 0]) / (ghz * 1e3))), 2),
+               "span_us": round(float((d[:, 7].max() - d[:, 6].min()) / 100.0), 2)}
+        print(json.dumps(rec), flush=True)
+        recs.append(rec)
+    rec = recs if len(recs) > 1 else recs[0]
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rec, f, indent=1)
