@@ -65,6 +65,8 @@ def cfg_supported(cfg: int, pc: "PackedConv", pure: bool) -> bool:
     pointwise configs (PW_CFGS) take 1x1 stride-1 convs of the shapes pw_wide.hip has."""
     if cfg in PW_CFGS:
         return pure and pw_supported(pc)
+    if cfg in PS_CFGS:
+        return pure and ps_supported(pc, cfg)
     if cfg in RR3_CFGS:
         return rr3_supported(pc)
     if cfg in CS3_CFGS:
@@ -179,7 +181,10 @@ def sk_plan(M: int, N: int, Kpad: int, cfg: int, mult: int = 1):
 
 
 def workspace_elems(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int:
-    """fp32 workspace a launch needs: split-K slabs or stream-K partial slots."""
+    """fp32 workspace a launch needs: split-K slabs or stream-K partial slots (none for the sliced pointwise
+    configs, whose `ksplit` is a grid size)."""
+    if cfg in PS_CFGS:
+        return 0
     if ksplit > 1:
         return ksplit * M * N
     if ksplit < 0:
@@ -237,6 +242,12 @@ def conv_forward(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residual: O
             raise ValueError(f"3x3 config {cfg}: stride-1 bf16 output, no residual / split-K")
         cs3_forward(x, pc, out.view(x.shape[0], OH, OW, N), relu=int(relu), stream=stream)
         return out
+    if cfg in PS_CFGS:                     # channel-sliced persistent pointwise kernel (pw_slice.hip)
+        # no split-K: `ksplit` 1 / 2 is the grid, one or two blocks per CU (PS_GRIDS)
+        if ksplit not in PS_GRIDS or ns or out_f32 or OH != H or OW != W:
+            raise ValueError(f"pointwise config {cfg}: single bf16 output, ksplit 1 / 2 = blocks per CU")
+        return ps_forward(x.reshape(M, C), pc, out.view(M, N), None if residual is None else residual.view(M, N),
+                          relu=int(relu), cfg=cfg, blocks=NUM_CUS * ksplit, stream=stream)
     if cfg in PW_CFGS:                     # persistent pointwise kernel (pw_wide.hip)
         if ksplit != 1 or ns or out_f32 or OH != H or OW != W:
             raise ValueError(f"pointwise config {cfg}: single bf16 output, no split-K")
@@ -925,6 +936,35 @@ def pw_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, residual: O
         raise ValueError(f"pw conv: x {tuple(x.shape)} / out {tuple(out.shape)} do not match {pc.cin} -> {pc.cout}")
     kernels().pw_res_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(residual), ptr(out), M, pc.cin,
                              pc.cout, int(relu), PW_CFGS[cfg], int(blocks), stream_handle(stream))
+    return out
+
+
+# channel-sliced persistent pointwise (csrc/kernels/pw_slice.hip): config id -> kernel code; a block keeps a
+# slice of NS = CF x WAVES x 16 output channels' weights in VGPRs and walks pixel tiles (code: (CF, WAVES, PT)
+# = 0: (4, 8, 16), 1: (2, 8, 16), 2: (1, 8, 16), 3: (2, 4, 32), 4: (1, 4, 32), 5: (4, 4, 16)); K in 256 / 512 /
+# 1024 with CF x K <= 1024, N a multiple of NS
+PS_CFGS = {74: 0, 75: 1, 76: 2, 77: 3, 78: 4, 79: 5}
+PS_GRIDS = (1, 2)          # the tuner's `ksplit` for these configs: blocks per CU (1 or 2 x NUM_CUS blocks)
+
+
+def ps_supported(pc: "PackedConv", cfg: int) -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (1, 1, 1, 0, 0, 0, 0)
+            and pc.cin == pc.Kpad and pc.cout <= pc.w.shape[0] and not pc.n_split     # padded rows never read
+            and bool(kernels().pw_slice_supported(int(pc.cin), int(pc.cout), PS_CFGS[cfg])))
+
+
+def ps_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, residual: Optional[torch.Tensor] = None,
+               relu: int = 0, cfg: int = 74, blocks: int = 256, stream=None) -> torch.Tensor:
+    if not ps_supported(pc, cfg):
+        raise ValueError(f"pw_slice conv: config {cfg} does not take {pc.cin} -> {pc.cout} (1x1 / stride 1)")
+    M = x.numel() // pc.cin
+    for t, n in ((x, "x"), (out, "out"), (residual, "residual")):
+        if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous()):
+            raise ValueError(f"pw_slice conv: {n} must be contiguous bf16")
+    if x.shape[-1] != pc.cin or out.numel() != M * pc.cout or (residual is not None and residual.numel() != M * pc.cout):
+        raise ValueError(f"pw_slice conv: x {tuple(x.shape)} / out {tuple(out.shape)} do not match {pc.cin} -> {pc.cout}")
+    kernels().pw_slice_forward(ptr(x), ptr(pw_fragments(pc)), ptr(pc.bias), ptr(residual), ptr(out), M, pc.cin,
+                               pc.cout, int(relu), PS_CFGS[cfg], int(blocks), stream_handle(stream))
     return out
 
 

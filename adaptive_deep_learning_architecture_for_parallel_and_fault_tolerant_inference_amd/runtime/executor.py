@@ -639,10 +639,14 @@ class SliceExecutor:
             extra = {"out2": torch.empty(M * (N - ns), dtype=torch.bfloat16, device=self.device)} if ns else {}
             best = None
             ktiles = pc.Kpad // conv_ops.BK
-            resident = list(conv_ops.PW_CFGS) + list(conv_ops.RR3_CFGS) + list(conv_ops.CS3_CFGS)
+            resident = (list(conv_ops.PW_CFGS) + list(conv_ops.PS_CFGS) + list(conv_ops.RR3_CFGS)
+                        + list(conv_ops.CS3_CFGS))
             for cfg in list(conv_ops.CFG_TILES) + resident:
                 for ks in (1, 2, 3, 4, 6, 8, -1, -2):
-                    if cfg in resident and ks != 1:
+                    if cfg in conv_ops.PS_CFGS:              # ks = blocks per CU for the sliced pointwise
+                        if ks not in conv_ops.PS_GRIDS:
+                            continue
+                    elif cfg in resident and ks != 1:
                         continue
                     if ks > 1 and ktiles // ks < 2:
                         continue

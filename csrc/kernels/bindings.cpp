@@ -352,6 +352,13 @@ PYBIND11_MODULE(_C, m) {
                       relu};
     check(adapt::pw_res_forward(p, K, N, pt, blocks, S(s)), "pw_res_forward");
   });
+  m.def("pw_slice_supported", [](int K, int N, int code) { return adapt::pw_slice_supported(K, N, code) != 0; });
+  m.def("pw_slice_forward", [](u64 x, u64 w, u64 bias, u64 res, u64 out, int M, int K, int N, int relu, int code,
+                               int blocks, u64 s) {
+    adapt::PwParams p{P<const bf16>(x), P<const bf16>(w), P<const float>(bias), P<const bf16>(res), P<bf16>(out), M,
+                      relu};
+    check(adapt::pw_slice_forward(p, K, N, code, blocks, S(s)), "pw_slice_forward");
+  });
   m.def("gap_large_f32", [](u64 x, u64 y, u64 part, int B, int HW, int C, u64 s) {
     check(adapt::gap_large_f32(P<const float>(x), P<float>(y), P<float>(part), B, HW, C, S(s)), "gap_large_f32");
   });

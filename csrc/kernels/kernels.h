@@ -313,6 +313,10 @@ struct PwParams {
 };
 int pw_res_supported(int K, int N);
 hipError_t pw_res_forward(const PwParams& p, int K, int N, int pt, int blocks, hipStream_t s);
+// channel-sliced persistent pointwise (pw_slice.hip): code -> (channel fragments per wave, waves, pixels per tile)
+bool pw_slice_cfg(int code, int* cf, int* waves, int* pt);
+int pw_slice_supported(int K, int N, int code);
+hipError_t pw_slice_forward(const PwParams& p, int K, int N, int code, int blocks, hipStream_t s);
 // serving ingest (ingest.hip): uint8 NHWC -> fp32, y = x[rev(c)] * scale[c] + shift[c] (host scale/shift, C <= 4)
 hipError_t ingest_u8(const uint8_t* x, float* y, size_t n, int C, int reverse, const float* scale,
                      const float* shift, hipStream_t s);

@@ -123,6 +123,10 @@ for p in "${P[@]}"; do
               steps+=("300|$out/hang4_defaults|python -u -m adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel.fault_run --workers 4 --devices cuda:0 --model resnet50 --image 224 --batch 32 --duration 20 --kill-at 8 --fault hang --json gpurun_out/$out/hang_r50_4w_defaults.json") ;;
     pmcw)     steps+=("500|$out/pmcw|bash tools/pmc_f32.sh gpurun_out/$out/pmcw 32,56,56,64,64,3,1,1,0:106:1 32,56,56,64,64,3,1,1,0:103:1 32,28,28,128,128,3,1,1,0:106:1 32,28,28,128,128,3,1,1,0:103:1 32,14,14,256,256,3,1,1,0:108:1 32,14,14,256,256,3,1,1,0:105:1") ;;
     pmc1x1)   steps+=("500|$out/pmc1x1|bash tools/pmc_f32.sh gpurun_out/$out/pmc1x1 32,14,14,1024,256,1,1,0,0:18:-2 32,14,14,256,1024,1,1,0,1:38:1 32,56,56,64,256,1,1,0,1:3:1 32,28,28,512,1024,1,2,0,0:20:-1") ;;
+    ps)       steps+=("300|$out/pytest_ps|python -u -m pytest tests/test_pw_slice_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/ps_bench|python -u tools/ps_bench.py --json gpurun_out/$out/ps_bench.json") ;;
+    psab)     steps+=("300|$out/ab_ps_s4out|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x256,1x1s1p0000,1024 --cfg 75 --ksplit 2 --json gpurun_out/$out/ab_ps_s4out.json")
+              steps+=("300|$out/ab_ps_s3one|python -u tools/ab_cfg.py --model resnet50 --key 32x28x28x512,1x1s1p0000,128 --cfg 76 --ksplit 1 --json gpurun_out/$out/ab_ps_s3one.json") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
     stemx)    steps+=("120|$out/stem_exp|python -u tools/stem_timeline.py --exp 0,1,2,4,8,3,13,15 --json gpurun_out/$out/stem_exp.json") ;;
     stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
