@@ -626,10 +626,14 @@ PW_F32_BMS = {64: (1, 2, 4, 5, 16, 32), 128: (1, 2, 4, 5, 16, 32), 256: (1, 2, 3
 # along N, BM chosen per layer so the tiles fill the CUs; 1x1 / pad 0 / stride 1-2, Cin % 32 == 0, N % 16 == 0;
 # ksplit 1 (one block per tile) or -1 (stream-K over 256 blocks, XCD-grouped, fused fixup)
 F32S_CFGS = {300: (112, 256), 301: (224, 256), 302: (112, 128), 303: (224, 128), 304: (64, 256), 305: (160, 256),
-             306: (192, 128)}
-# measured behind the pointwise / ring kernels on all 7 ResNet-50 bs=32 1x1 shapes (profiles/r5/
+             306: (192, 128),
+             # 112-row tiles placed 98 rows apart (the kernel's TM): 256 tiles on 6272 x 256 / 1568 x 2048; whole K
+             307: (98, 64), 308: (98, 128), 309: (49, 64)}
+F32S_TM = frozenset((307, 308, 309))     # owned-row tiles: ksplit 1 only
+# measured behind the pointwise / ring kernels on the ResNet-50 bs=32 1x1 shapes in isolation (profiles/r5/
 # gemm_f32s_attribution.md: one tile per CU writes the whole output after the K loop, 5-14 us of HBM-bound
-# epilogue that nothing overlaps); runnable and tested, never tuned
+# epilogue that nothing overlaps), so the isolated-timing tuner never picks them; cfg 307 on the stage-4 `_1`
+# convs wins in the whole-model A/B (tools/ab_cfg.py: 2.2738 -> 2.2648 ms) and is set in the table by hand
 F32_UNTUNED = WINO4_UNTUNED | frozenset(F32S_CFGS)
 
 
@@ -644,8 +648,8 @@ def f32s_tiles(cfg: int, M: int, N: int) -> int:
 
 
 def f32s_ws_elems(cfg: int) -> int:
-    bm, bn = F32S_CFGS[cfg]
-    return 2 * 256 * bm * bn
+    """Stream-K workspace floats (2 partial slots of a whole BM x BN tile per block, 256 blocks)."""
+    return int(kernels().gemm_f32s_ws_elems(cfg))
 
 
 def pw_f32_slice(K: int) -> int:

@@ -94,6 +94,7 @@ struct GsTile {
   char* smem;
   int wave, lane;
   u32x4 xdesc, wdesc;
+  int tm = S::BM;                                      // rows a tile owns (tile stride, <= BM): rows past it read zeros
   unsigned long long* dbg = nullptr;
 
   __device__ GsTile(const ConvF32Params& p_, char* smem_, int wave_, int lane_)
@@ -114,7 +115,7 @@ struct GsTile {
       const int r = min(wave * S::PA + j, S::BM / 8 - 1) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);                  // logical 4-float unit this lane fetches
       const int m = m0 + r;
-      voffA[j] = m < p.M ? (int)((gs_row_in(p, m) + c * 4) * 4) : (int)GS_OOB;
+      voffA[j] = (r < tm && m < p.M) ? (int)((gs_row_in(p, m) + c * 4) * 4) : (int)GS_OOB;
     }
 #pragma unroll
     for (int j = 0; j < S::PB; ++j) {
@@ -233,7 +234,7 @@ __device__ __forceinline__ void gs_epilogue(char* smem, int wave, int lane, int 
 // the staging writes, so their HBM latency hides under the LDS round trip instead of serialising per store
 template <int MF, int NF>
 __device__ __forceinline__ void gs_epilogue_direct(const ConvF32Params& p, char* smem, int wave, int lane, int m0,
-                                                   int n0w, const f32x4 (&acc)[MF][NF]) {
+                                                   int n0w, int mlim, const f32x4 (&acc)[MF][NF]) {
   constexpr int C4 = 4 * NF;
   constexpr int RPP = 64 / C4;
   constexpr int KS = 64 / RPP;
@@ -251,7 +252,7 @@ __device__ __forceinline__ void gs_epilogue_direct(const ConvF32Params& p, char*
     for (int k = 0; k < KS; ++k) {
       const int row = RPP * k + lane / C4, m = m0 + 64 * g + row;
       rv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (p.res && nok && row < rows && m < p.M) rv[k] = *(const f32x4*)(p.res + (size_t)m * p.N + n);
+      if (p.res && nok && row < rows && m < mlim) rv[k] = *(const f32x4*)(p.res + (size_t)m * p.N + n);
     }
 #pragma unroll
     for (int i = 4 * g; i < 4 * g + 4 && i < MF; ++i)
@@ -263,7 +264,7 @@ __device__ __forceinline__ void gs_epilogue_direct(const ConvF32Params& p, char*
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       const int row = RPP * k + lane / C4, m = m0 + 64 * g + row;
-      if (row < rows && m < p.M && nok) {
+      if (row < rows && m < mlim && nok) {
         f32x4 v = *(const f32x4*)(stg + row * GS_EPI_LD + 4 * c4) + bv + rv[k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], d.relu);
@@ -274,18 +275,23 @@ __device__ __forceinline__ void gs_epilogue_direct(const ConvF32Params& p, char*
   }
 }
 
-// EXP (measurement variants, outputs wrong by design): bit 0 no LDS-DMA in the K loop, bit 1 no MFMAs
-template <int MF, int NF, int EXP = 0>
+// EXP (measurement variants, outputs wrong by design): bit 0 no LDS-DMA in the K loop, bit 1 no MFMAs.
+// TM: rows a tile owns (0 = BM).  TM < BM places tiles TM rows apart, so the tile count can hit a multiple of
+// the 256 CUs (98-row tiles: 6272 rows x 256 / 64 columns = 256 tiles); the BM - TM rows past it read zeros.
+template <int MF, int NF, int EXP = 0, int TM = 0>
 __global__ __launch_bounds__(256, 1) void gemm_f32s_kernel(ConvF32Params p, unsigned long long* dbg_all) {
   static_assert(NF <= 4, "one 64-column staging pass per wave");
   using S = GsShape<MF, NF>;
+  constexpr int TMV = TM ? TM : S::BM;
+  static_assert(TMV <= S::BM, "owned rows within the tile");
   __shared__ __attribute__((aligned(16))) char smem[GS_LDS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tilesN = (p.N + S::BN - 1) / S::BN;
-  const int tilesM = (p.M + S::BM - 1) / S::BM;
+  const int tilesM = (p.M + TMV - 1) / TMV;
   const int KT = p.Kpad / GS_K;
   GsTile<MF, NF, EXP> T(p, smem, wave, lane);
+  T.tm = TMV;
   unsigned long long* const dbg = dbg_all ? dbg_all + 8 * (wave + 4 * blockIdx.x) : nullptr;
   T.dbg = dbg;
   gs_stamp(dbg, 0);
@@ -294,10 +300,10 @@ __global__ __launch_bounds__(256, 1) void gemm_f32s_kernel(ConvF32Params p, unsi
   if (p.ksplit == 1) {                               // one block per tile, whole K
     const int t = blockIdx.x;
     if (t >= tilesM * tilesN) return;
-    const int m0 = (t / tilesN) * S::BM, n0 = (t % tilesN) * S::BN;
+    const int m0 = (t / tilesN) * TMV, n0 = (t % tilesN) * S::BN;
     T.run(m0, n0, 0, KT, acc);
     gs_stamp(dbg, 2);
-    gs_epilogue_direct<MF, NF>(p, smem, wave, lane, m0, n0 + 16 * NF * wave, acc);
+    gs_epilogue_direct<MF, NF>(p, smem, wave, lane, m0, n0 + 16 * NF * wave, min(p.M, m0 + TMV), acc);
     if (dbg) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       gs_stamp(dbg, 3);
@@ -320,16 +326,17 @@ __global__ __launch_bounds__(256, 1) void gemm_f32s_kernel(ConvF32Params p, unsi
     const int t = (int)(u / KT);
     const int c0 = (int)(u - (long long)t * KT);
     const int c1 = (int)min((long long)KT, c0 + (u1 - u));
-    const int m0 = (t / tilesN) * S::BM, n0 = (t % tilesN) * S::BN;
+    const int m0 = (t / tilesN) * TMV, n0 = (t % tilesN) * S::BN;
+    const int mlim = min(p.M, m0 + TMV);
     T.run(m0, n0, c0, c1, acc);
     const int n0w = n0 + 16 * NF * wave;
     if (c0 == 0 && c1 == KT) {
-      gs_epilogue_direct<MF, NF>(p, smem, wave, lane, m0, n0w, acc);
+      gs_epilogue_direct<MF, NF>(p, smem, wave, lane, m0, n0w, mlim, acc);
       __syncthreads();                               // the staging is free before the next segment's DMA
     } else {
       // partial: this block's slot (2v for its first segment, 2v + 1 for a later one), written through L2
       const int slot = 2 * v + (u == u0 ? 0 : 1);
-      gs_epilogue<MF, NF>(smem, wave, lane, m0, n0w, p.M, p.N, acc, [&](int m, int n, f32x4 val) {
+      gs_epilogue<MF, NF>(smem, wave, lane, m0, n0w, mlim, p.N, acc, [&](int m, int n, f32x4 val) {
         const int off = (int)(((size_t)slot * tile_elems + (size_t)(m - m0) * S::BN + (n - n0)) * 4);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), wsr, off, 0, GS_CPOL_SC1);
       });
@@ -357,7 +364,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32s_kernel(ConvF32Params p, unsi
         for (int idx = threadIdx.x; idx < S::BM * (S::BN / 4); idx += 256) {
           const int row = idx / (S::BN / 4), c4 = idx - row * (S::BN / 4);
           const int m = m0 + row, n = n0 + 4 * c4;
-          if (m >= p.M || n >= p.N) continue;
+          if (m >= mlim || n >= p.N) continue;
           f32x4 acc4 = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int k = 0; k < GS_MAXSEG; ++k) {
@@ -377,12 +384,14 @@ __global__ __launch_bounds__(256, 1) void gemm_f32s_kernel(ConvF32Params p, unsi
 static unsigned long long* g_gs_dbg = nullptr;
 static int g_gs_exp = 0;
 
-template <int MF, int NF>
+template <int MF, int NF, int TM>
 hipError_t gs_launch(const ConvF32Params& p, hipStream_t s) {
   using S = GsShape<MF, NF>;
-  const int tiles = ((p.M + S::BM - 1) / S::BM) * ((p.N + S::BN - 1) / S::BN);
+  constexpr int TMV = TM ? TM : S::BM;
+  const int tiles = ((p.M + TMV - 1) / TMV) * ((p.N + S::BN - 1) / S::BN);
   int grid = tiles;
   if (p.ksplit < 0) {
+    if (TM) return hipErrorInvalidValue;             // stream-K only with whole BM-row tiles
     grid = 256;
     if ((long long)tiles * (p.Kpad / GS_K) < grid || !p.ws || !p.counters) return hipErrorInvalidValue;
     if ((size_t)2 * grid * S::BM * S::BN * 4 > 0x7fffffffu) return hipErrorInvalidValue;
@@ -392,9 +401,9 @@ hipError_t gs_launch(const ConvF32Params& p, hipStream_t s) {
     if (per < 1 || (p.Kpad / GS_K + per - 1) / per + 1 > GS_MAXSEG) return hipErrorInvalidValue;
   }
   switch (g_gs_exp) {
-    case 0: hipLaunchKernelGGL((gemm_f32s_kernel<MF, NF, 0>), dim3(grid), dim3(256), 0, s, p, g_gs_dbg); break;
-    case 1: hipLaunchKernelGGL((gemm_f32s_kernel<MF, NF, 1>), dim3(grid), dim3(256), 0, s, p, g_gs_dbg); break;
-    case 2: hipLaunchKernelGGL((gemm_f32s_kernel<MF, NF, 2>), dim3(grid), dim3(256), 0, s, p, g_gs_dbg); break;
+    case 0: hipLaunchKernelGGL((gemm_f32s_kernel<MF, NF, 0, TM>), dim3(grid), dim3(256), 0, s, p, g_gs_dbg); break;
+    case 1: hipLaunchKernelGGL((gemm_f32s_kernel<MF, NF, 1, TM>), dim3(grid), dim3(256), 0, s, p, g_gs_dbg); break;
+    case 2: hipLaunchKernelGGL((gemm_f32s_kernel<MF, NF, 2, TM>), dim3(grid), dim3(256), 0, s, p, g_gs_dbg); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -402,15 +411,20 @@ hipError_t gs_launch(const ConvF32Params& p, hipStream_t s) {
 
 }  // namespace
 
-// cfg -> (MF, NF): tile (16 MF) x (64 NF); ops/conv.py F32S_CFGS mirrors this
+// cfg -> (MF, NF, TM): tile (16 MF) x (64 NF), TM owned rows (0 = 16 MF); ops/conv.py F32S_CFGS mirrors this
+// (307 / 308 / 309: 98- / 98- / 49-row tiles on the ResNet-50 bs=32 K-heavy 1x1s, 256 tiles each: 6272 x 256,
+// 1568 x 2048 and 1568 x 512)
 #define ADAPT_F32S_CFGS(X) \
-  X(300, 7, 4)             \
-  X(301, 14, 4)            \
-  X(302, 7, 2)             \
-  X(303, 14, 2)            \
-  X(304, 4, 4)             \
-  X(305, 10, 4)            \
-  X(306, 12, 2)
+  X(300, 7, 4, 0)          \
+  X(301, 14, 4, 0)         \
+  X(302, 7, 2, 0)          \
+  X(303, 14, 2, 0)         \
+  X(304, 4, 4, 0)          \
+  X(305, 10, 4, 0)         \
+  X(306, 12, 2, 0)         \
+  X(307, 7, 1, 98)         \
+  X(308, 7, 2, 98)         \
+  X(309, 4, 1, 49)
 
 void gemm_f32s_set_debug(unsigned long long* buf, int exp) {
   g_gs_dbg = buf;
@@ -419,10 +433,10 @@ void gemm_f32s_set_debug(unsigned long long* buf, int exp) {
 
 bool gemm_f32s_cfg(int cfg, int* bm, int* bn) {
   switch (cfg) {
-#define X(id, MF_, NF_) \
-  case id:              \
-    *bm = 16 * MF_;     \
-    *bn = 64 * NF_;     \
+#define X(id, MF_, NF_, TM_)     \
+  case id:                       \
+    *bm = TM_ ? TM_ : 16 * MF_;  \
+    *bn = 64 * NF_;              \
     return true;
     ADAPT_F32S_CFGS(X)
 #undef X
@@ -432,9 +446,14 @@ bool gemm_f32s_cfg(int cfg, int* bm, int* bn) {
 
 // stream-K workspace (floats) and counters of a cfg-300+ launch with ksplit -1
 size_t gemm_f32s_ws_elems(int cfg) {
-  int bm = 0, bn = 0;
-  if (!gemm_f32s_cfg(cfg, &bm, &bn)) return 0;
-  return (size_t)2 * 256 * bm * bn;
+  switch (cfg) {
+#define X(id, MF_, NF_, TM_) \
+  case id:                   \
+    return (size_t)2 * 256 * (16 * MF_) * (64 * NF_);
+    ADAPT_F32S_CFGS(X)
+#undef X
+  }
+  return 0;
 }
 
 hipError_t gemm_f32s_launch(const ConvF32Params& p, int cfg, hipStream_t s) {
@@ -446,8 +465,8 @@ hipError_t gemm_f32s_launch(const ConvF32Params& p, int cfg, hipStream_t s) {
   if (!gemm_f32s_cfg(cfg, &bm, &bn)) return hipErrorInvalidValue;
   if ((long long)((p.N + bn - 1) / bn * bn) * p.Kpad * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
   switch (cfg) {
-#define X(id, MF_, NF_) \
-  case id: return gs_launch<MF_, NF_>(p, s);
+#define X(id, MF_, NF_, TM_) \
+  case id: return gs_launch<MF_, NF_, TM_>(p, s);
     ADAPT_F32S_CFGS(X)
 #undef X
   }

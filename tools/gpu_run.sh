@@ -127,6 +127,13 @@ for p in "${P[@]}"; do
               steps+=("300|$out/ps_bench|python -u tools/ps_bench.py --json gpurun_out/$out/ps_bench.json") ;;
     psab)     steps+=("300|$out/ab_ps_s4out|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x256,1x1s1p0000,1024 --cfg 75 --ksplit 2 --json gpurun_out/$out/ab_ps_s4out.json")
               steps+=("300|$out/ab_ps_s3one|python -u tools/ab_cfg.py --model resnet50 --key 32x28x28x512,1x1s1p0000,128 --cfg 76 --ksplit 1 --json gpurun_out/$out/ab_ps_s3one.json") ;;
+    gstm)     steps+=("300|$out/pytest_gemm_f32s|python -u -m pytest tests/test_gemm_f32s_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/gemm_f32s_tm_bench|python -u tools/conv_bench_f32.py --only 307,308,18,38,122,123,125,126 --ks 1,-1,-2 --top 8 --shape 32,14,14,1024,256,1,1,0,0 --shape 32,7,7,512,2048,1,1,0,1")
+              steps+=("300|$out/ab_f32s_307|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x14x14x1024,1x1s1p0000,256 --cfg 307 --ksplit 1 --json gpurun_out/$out/ab_f32s_307.json")
+              steps+=("300|$out/ab_f32s_308|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x7x7x512,1x1s1p0000,2048 --cfg 308 --ksplit 1 --json gpurun_out/$out/ab_f32s_308.json") ;;
+    gstm2)    steps+=("300|$out/pytest_gemm_f32s|python -u -m pytest tests/test_gemm_f32s_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/ab_f32s_307|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x14x14x1024,1x1s1p0000,256 --cfg 307 --ksplit 1 --rounds 25 --json gpurun_out/$out/ab_f32s_307.json")
+              steps+=("300|$out/ab_f32s_309|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x7x7x2048,1x1s1p0000,512 --cfg 309 --ksplit 1 --rounds 25 --json gpurun_out/$out/ab_f32s_309.json") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
     stemx)    steps+=("120|$out/stem_exp|python -u tools/stem_timeline.py --exp 0,1,2,4,8,3,13,15 --json gpurun_out/$out/stem_exp.json") ;;
     stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
