@@ -633,8 +633,9 @@ F32S_TM = frozenset((307, 308, 309))     # owned-row tiles: ksplit 1 only
 # measured behind the pointwise / ring kernels on the ResNet-50 bs=32 1x1 shapes in isolation (profiles/r5/
 # gemm_f32s_attribution.md: one tile per CU writes the whole output after the K loop, 5-14 us of HBM-bound
 # epilogue that nothing overlaps), so the isolated-timing tuner never picks them; cfg 307 on the stage-4 `_1`
-# convs wins in the whole-model A/B (tools/ab_cfg.py: 2.2738 -> 2.2648 ms) and is set in the table by hand
-F32_UNTUNED = WINO4_UNTUNED | frozenset(F32S_CFGS)
+# convs wins in the whole-model A/B (tools/ab_cfg.py: 2.2738 -> 2.2648 ms): the owned-row tiles (F32S_TM) are
+# tuner candidates, which the fp32 tuner's in-graph refinement can pick
+F32_UNTUNED = WINO4_UNTUNED | (frozenset(F32S_CFGS) - F32S_TM)
 
 
 def f32s_supported(pc: "PackedConv") -> bool:

@@ -537,11 +537,18 @@ class SliceExecutor:
         e.synchronize()
         return s.elapsed_time(e) / (3 * reps)
 
-    def autotune_f32(self, reps: int = 10, persist: bool = True) -> Dict[str, List]:
+    def autotune_f32(self, reps: int = 10, persist: bool = True, refine: int = 3,
+                     verbose: bool = False) -> Dict[str, List]:
         """fp32 path: time every (tile cfg, split-K) of conv_f32.hip per conv
-        problem in isolation and keep the fastest ("f32|" keys in the table)."""
+        problem in isolation and keep the fastest ("f32|" keys in the table);
+        then (refine > 1) re-decide each problem among its `refine` best isolated
+        candidates by replaying the whole captured slice, as the bf16 tuner does
+        (round 5: the 98-row GEMM tile cfg 307 is 5 % slower than the ring kernel
+        in isolation and 10 us per batch faster in the model)."""
         results: Dict[str, List] = {}
         done: Dict[str, Tuple[int, int]] = {}
+        ranked: Dict[str, List[Tuple[float, int, int]]] = {}
+        prev = dict(load_tuning())
         for i, st in enumerate(self.steps):
             if st.kind not in ("conv", "dense") or i in self._dense_part:
                 continue
@@ -604,13 +611,19 @@ class SliceExecutor:
                                                                                out2=out2), reps)
                     except (RuntimeError, ValueError):
                         continue
+                    ranked.setdefault(key, []).append((t, cfg, ks))
                     if best is None or t < best[0]:
                         best = (t, cfg, ks)
             if best:
                 results[key] = [best[1], best[2], round(best[0] * 1000, 2)]
                 done[key] = (best[1], best[2])
                 self.cfg[i] = (best[1], best[2])
+                if verbose:
+                    print(f"autotune {key}: cfg {best[1]} ksplit {best[2]} {best[0] * 1000:.2f} us", flush=True)
         self._ensure_ws()
+        refine = int(os.environ.get("ADAPT_TUNE_REFINE", refine))
+        if refine > 1 and ranked:
+            self._refine_in_graph(ranked, results, refine, prev, verbose, prefix="f32|")
         if persist:
             save_tuning(results)
         return results
@@ -722,12 +735,12 @@ class SliceExecutor:
         return sorted(times)[len(times) // 2]
 
     def _refine_in_graph(self, ranked, results, top: int, prev: Optional[Dict[str, List]] = None,
-                         verbose: bool = False) -> None:
+                         verbose: bool = False, prefix: str = "") -> None:
         steps_of: Dict[str, List[int]] = {}
         for i, st in enumerate(self.steps):
             if st.kind in ("conv", "dense") and i not in self._dense_part:
                 B, H, W, C, OH, OW, pc = self._conv_geom(i)
-                steps_of.setdefault(conv_key(B, H, W, C, pc), []).append(i)
+                steps_of.setdefault(prefix + conv_key(B, H, W, C, pc), []).append(i)
         # start from the previous table where it is still a valid candidate, so a
         # re-tune can only keep or improve the whole-slice time
         for key, idx in steps_of.items():

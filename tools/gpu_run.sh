@@ -97,6 +97,7 @@ for p in "${P[@]}"; do
     fp32t)    steps+=("400|$out/pytest_fp32|python -u -m pytest tests/test_fp32_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread") ;;
     models)   steps+=("600|$out/pytest_models|python -u -m pytest tests/test_model_gpu.py tests/test_multigpu_links.py tests/test_defer_gpu.py -m gpu -v --timeout 300 --timeout-method thread") ;;
     peak)     steps+=("60|$out/mfma_f32_peak|./tools/mfma_f32_peak.bin") ;;
+    tune16)   steps+=("900|$out/tune_bf16|python -u tools/tune_f32.py --precision bf16 --models resnet50 --batch 32 --out gpurun_out/$out/tune_bf16.json") ;;
     tune32)   steps+=("600|$out/tune_f32|python -u tools/tune_f32.py --models resnet50 --batch 32 --out gpurun_out/$out/tune_f32.json") ;;
     pmc32)    steps+=("500|$out/pmc32|bash tools/pmc_run.sh gpurun_out/$out/pmc32 bench.py --no-bf16 --steps 2 --warmup 1") ;;
     hang)     steps+=("300|$out/hang4_dev|python -u tools/fault_bench.py --workers 4 --device cuda:0 --model resnet50 --image 224 --batch 32 --duration 25 --kill-at 10 --links dev --inflight 8 --fault hang --json gpurun_out/$out/hang_r50_4w_dev.json") ;;

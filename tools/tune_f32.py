@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""fp32 conv autotune on the GPU box: every (tile config, split-K) of the v1
+"""fp32 (or --precision bf16) conv autotune on the GPU box: every (tile config, split-K) of the v1
 (conv_f32.hip) and v2 LDS-DMA (conv_f32g.hip) kernels per conv problem of the
 given models, isolated timings (SliceExecutor.autotune_f32).  Writes the chosen
 entries ("f32|" keys of tuning/gfx950_conv.json) to --out so they can be merged
@@ -40,21 +40,24 @@ def main():
     ap.add_argument("--models", default="resnet50")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: SliceExecutor.autotune (isolated timing + in-graph refinement of the best 3)")
     a = ap.parse_args()
     before = dict(E.load_tuning())
     allres = {}
     for name in a.models.split(","):
         g = build_model(name)
         w = init_weights(g, 0)
-        ex = E.SliceExecutor(g, w, a.batch, device="cuda:0", precision="fp32")
+        ex = E.SliceExecutor(g, w, a.batch, device="cuda:0", precision=a.precision)
         t_old = graph_ms(ex)
         t0 = time.time()
-        res = ex.autotune_f32(persist=True)
+        res = (ex.autotune_f32(persist=True, verbose=True) if a.precision == "fp32"
+               else ex.autotune(persist=True, verbose=True))
         for k, v in res.items():
             old = before.get(k)
             print(f"{name} {k}: {old} -> {v}", flush=True)
         allres.update(res)
-        ex2 = E.SliceExecutor(g, w, a.batch, device="cuda:0", precision="fp32")
+        ex2 = E.SliceExecutor(g, w, a.batch, device="cuda:0", precision=a.precision)
         t_new = graph_ms(ex2)
         print(json.dumps({"model": name, "batch": a.batch, "graph_ms_before": round(t_old, 4),
                           "graph_ms_after": round(t_new, 4), "img_s_after": round(a.batch / t_new * 1e3, 1),
