@@ -97,6 +97,10 @@ for p in "${P[@]}"; do
     fp32t)    steps+=("400|$out/pytest_fp32|python -u -m pytest tests/test_fp32_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread") ;;
     models)   steps+=("600|$out/pytest_models|python -u -m pytest tests/test_model_gpu.py tests/test_multigpu_links.py tests/test_defer_gpu.py -m gpu -v --timeout 300 --timeout-method thread") ;;
     peak)     steps+=("60|$out/mfma_f32_peak|./tools/mfma_f32_peak.bin") ;;
+    ab62)     steps+=("300|$out/ab_s5_3x3_62|python -u tools/ab_cfg.py --model resnet50 --key 32x7x7x512,3x3s1p1111,512 --cfg 62 --ksplit 2 --rounds 25 --json gpurun_out/$out/ab_s5_3x3_62.json")
+              steps+=("300|$out/ab_s5_3x3_64|python -u tools/ab_cfg.py --model resnet50 --key 32x7x7x512,3x3s1p1111,512 --cfg 64 --ksplit 4 --rounds 25 --json gpurun_out/$out/ab_s5_3x3_64.json") ;;
+    tune16w)  steps+=("900|$out/tune_bf16|env ADAPT_TUNE_REFINE=8 python -u tools/tune_f32.py --precision bf16 --models resnet50 --batch 32 --out gpurun_out/$out/tune_bf16.json")
+              steps+=("900|$out/tune_f32|env ADAPT_TUNE_REFINE=8 python -u tools/tune_f32.py --precision fp32 --models resnet50 --batch 32 --out gpurun_out/$out/tune_f32.json") ;;
     tune16)   steps+=("900|$out/tune_bf16|python -u tools/tune_f32.py --precision bf16 --models resnet50 --batch 32 --out gpurun_out/$out/tune_bf16.json") ;;
     tune32)   steps+=("600|$out/tune_f32|python -u tools/tune_f32.py --models resnet50 --batch 32 --out gpurun_out/$out/tune_f32.json") ;;
     pmc32)    steps+=("500|$out/pmc32|bash tools/pmc_run.sh gpurun_out/$out/pmc32 bench.py --no-bf16 --steps 2 --warmup 1") ;;
