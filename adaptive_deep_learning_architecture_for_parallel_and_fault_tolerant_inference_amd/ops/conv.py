@@ -946,8 +946,8 @@ def pw_forward(x: torch.Tensor, pc: "PackedConv", out: torch.Tensor, residual: O
 
 # channel-sliced persistent pointwise (csrc/kernels/pw_slice.hip): config id -> kernel code; a block keeps a
 # slice of NS = CF x WAVES x 16 output channels' weights in VGPRs and walks pixel tiles (code: (CF, WAVES, PT)
-# = 0: (4, 8, 16), 1: (2, 8, 16), 2: (1, 8, 16), 3: (2, 4, 32), 4: (1, 4, 32), 5: (4, 4, 16)); K in 256 / 512 /
-# 1024 with CF x K <= 1024, N a multiple of NS
+# = 0: (4, 8, 16), 1: (2, 8, 16), 2: (1, 8, 16), 3: (2, 4, 32), 4: (1, 4, 32), 5: (4, 4, 16)); K in 128 / 256 /
+# 512 / 1024 with CF x K <= 1024, N a multiple of NS
 PS_CFGS = {74: 0, 75: 1, 76: 2, 77: 3, 78: 4, 79: 5}
 PS_GRIDS = (1, 2)          # the tuner's `ksplit` for these configs: blocks per CU (1 or 2 x NUM_CUS blocks)
 

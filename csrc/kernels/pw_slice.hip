@@ -1,6 +1,7 @@
 // Channel-sliced persistent pointwise (1x1, stride 1) bf16 conv with the fused bias + residual + ReLU
 // epilogue:  out[m][n] = act(x[m] . W[n] + b[n] (+ res[m][n])), for the wide-K / wide-N 1x1s of ResNet
-// stages 4 and 5 (K = 256 -> N = 1024 + residual, K = 1024 -> N = 256, K = 512 -> N = 2048 + residual).
+// stages 3-5 (K = 128 -> N = 512 + residual, K = 256 -> N = 1024 + residual, K = 1024 -> N = 256,
+// K = 512 -> N = 2048 + residual).
 //
 // Those layers are memory-bound at bs=32 (stage-4 `_out`: 3.2 MB in, 12.8 MB residual, 12.8 MB out against
 // 3.3 GFLOP), yet the tuned LDS-DMA tile GEMM runs them at ~3 TB/s (9.7 us,
@@ -185,7 +186,7 @@ bool pw_slice_cfg(int code, int* cf, int* waves, int* pt) {
 int pw_slice_supported(int K, int N, int code) {
   int cf, waves, pt;
   if (!pw_slice_cfg(code, &cf, &waves, &pt)) return 0;
-  if (K != 256 && K != 512 && K != 1024) return 0;
+  if (K != 128 && K != 256 && K != 512 && K != 1024) return 0;
   if (cf * K > 1024) return 0;
   const int ns = cf * waves * 16;
   return N % ns == 0 && N / ns <= 256;
@@ -212,7 +213,9 @@ hipError_t pw_slice_forward(const PwParams& p, int K, int N, int code, int block
     case 4: PS_LAUNCH(KK, 1, 4, 32); break;  \
     case 5: PS_LAUNCH(KK, 4, 4, 16); break;  \
   }
-  if (K == 256) {
+  if (K == 128) {
+    PS_CODE(128)
+  } else if (K == 256) {
     PS_CODE(256)
   } else if (K == 512) {
     switch (code) {

@@ -10,6 +10,7 @@ from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inferen
 pytestmark = pytest.mark.gpu
 
 SHAPES = [  # (M, K, N, residual)
+    (25088, 128, 512, True),      # stage-3 _out
     (6272, 256, 1024, True),      # stage-4 _out
     (6272, 1024, 256, False),     # stage-4 _1
     (1568, 512, 2048, True),      # stage-5 _out

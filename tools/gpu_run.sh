@@ -139,6 +139,10 @@ for p in "${P[@]}"; do
     gstm2)    steps+=("300|$out/pytest_gemm_f32s|python -u -m pytest tests/test_gemm_f32s_gpu.py -v -x --timeout 120 --timeout-method thread")
               steps+=("300|$out/ab_f32s_307|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x14x14x1024,1x1s1p0000,256 --cfg 307 --ksplit 1 --rounds 25 --json gpurun_out/$out/ab_f32s_307.json")
               steps+=("300|$out/ab_f32s_309|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x7x7x2048,1x1s1p0000,512 --cfg 309 --ksplit 1 --rounds 25 --json gpurun_out/$out/ab_f32s_309.json") ;;
+    ps3)      steps+=("300|$out/pytest_ps|python -u -m pytest tests/test_pw_slice_gpu.py -v -x --timeout 120 --timeout-method thread")
+              steps+=("300|$out/ps_bench|python -u tools/ps_bench.py --shape 25088,128,512,1 --json gpurun_out/$out/ps_bench.json")
+              steps+=("300|$out/ab_ps_s3out_74|python -u tools/ab_cfg.py --model resnet50 --key 32x28x28x128,1x1s1p0000,512 --cfg 74 --ksplit 1 --rounds 25")
+              steps+=("300|$out/ab_ps_s3out_75|python -u tools/ab_cfg.py --model resnet50 --key 32x28x28x128,1x1s1p0000,512 --cfg 75 --ksplit 2 --rounds 25") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
     stemx)    steps+=("120|$out/stem_exp|python -u tools/stem_timeline.py --exp 0,1,2,4,8,3,13,15 --json gpurun_out/$out/stem_exp.json") ;;
     stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")

@@ -18,8 +18,8 @@ import torch  # noqa: E402
 
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C  # noqa: E402
 
-SHAPES = ["6272,256,1024,1", "6272,1024,256,0", "1568,512,2048,1", "25088,512,128,0", "1568,2048,512,0"]
-IGEMM = (20, 22, 23, 24, 54, 55, 56, 62, 63)
+SHAPES = ["25088,128,512,1", "6272,256,1024,1", "6272,1024,256,0", "1568,512,2048,1", "25088,512,128,0", "1568,2048,512,0"]
+IGEMM = (3, 20, 22, 23, 24, 54, 55, 56, 62, 63)
 
 
 def bench_shape(M, K, N, has_res, rounds):
