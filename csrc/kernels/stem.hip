@@ -462,7 +462,10 @@ __device__ __forceinline__ int ring4_off(int slot, int ow, int chunk) {
 
 // EXP (tools/stem_timeline.py --exp, outputs wrong by design): 1 no MFMAs in the steps, 2 no pool in the
 // steps, 4 no ring stores in the steps, 8 no A-fragment reads in the steps
-template <bool C3, int EXP = 0>
+// NH: 16-channel groups per wave.  4 = every wave computes all 64 channels of its tiles (v4).  2 (v5): waves
+// 0-3 take channels 0-31 and waves 4-7 channels 32-63 of every tile, so each wave loads half the weight
+// panel and the 28 half-tiles of a step split 7 / 7 / 7 / 7 over the SIMDs (v4: 4 / 4 / 3 / 3 tiles).
+template <bool C3, int EXP = 0, int NH = 4>
 __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
                                                                 const float* __restrict__ bias, bf16* __restrict__ out,
                                                                 int H, int W, int C, int OH, int OW, int pad_t,
@@ -494,16 +497,22 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
 
   // weights and bias first: loads return in order, so step 0 then waits only for them and patch rows 0-10
   const int fr = lane & 15, fq = lane >> 4;
-  bf16x8 bw[7][4];
+  static_assert(NH == 4 || NH == 2, "whole or half channel panel per wave");
+  constexpr int TSTRIDE = NH == 4 ? S4_WAVES : 4;          // tile index stride between a wave's tiles
+  const int hsel = NH == 4 ? 0 : (wave >> 2);              // channel half (NH = 2)
+  const int nb = hsel * NH;                                // first 16-channel group of this wave
+  const int tfirst = NH == 4 ? wave : (((wave & 3) + 2 * hsel) & 3);
+  bf16x8 bw[7][NH];
 #pragma unroll
   for (int s = 0; s < 7; ++s)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bw[s][n] = *(const bf16x8*)(w + (size_t)(n * 16 + fr) * ST_K + s * 32 + fq * 8);
-  float b4[4][4];
+    for (int n = 0; n < NH; ++n)
+      bw[s][n] = *(const bf16x8*)(w + (size_t)((nb + n) * 16 + fr) * ST_K + s * 32 + fq * 8);
+  float b4[NH][4];
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
+  for (int n = 0; n < NH; ++n)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) b4[n][r] = bias[n * 16 + 4 * fq + r];
+    for (int r = 0; r < 4; ++r) b4[n][r] = bias[(nb + n) * 16 + 4 * fq + r];
   float pall[S4_ITEMS][4];
   if constexpr (C3)
     get_rows3<S4_ITEMS, S4_NT>(pall, xi, tid, row_end, ih0, H, W, pwc, pad_l);
@@ -520,11 +529,11 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
     bool ok;
     int slot;                                              // ring slot base (bf16 elements)
     const bf16* pa;
-    int col[4];                                            // per 16-channel group: offset within the slot
+    int col[NH];                                           // per 16-channel group: offset within the slot
   };
   auto tile_cols = [&](Tile& g, const int ow) __attribute__((always_inline)) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) g.col[n] = ring4_off(0, ow, 2 * n + (fq >> 1)) + 4 * (fq & 1);
+    for (int n = 0; n < NH; ++n) g.col[n] = ring4_off(0, ow, 2 * (nb + n) + (fq >> 1)) + 4 * (fq & 1);
   };
   auto tile_geo = [&](const int mt, const int rel0, const int ntiles) __attribute__((always_inline)) {
     Tile g;
@@ -541,20 +550,20 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
 #pragma unroll
     for (int s = 0; s < 7; ++s) a[s] = *(const bf16x8*)(g.pa + s * ST_PWC * 4);
   };
-  auto tile_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[4]) __attribute__((always_inline)) {
+  auto tile_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[NH]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NH; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // (pinning the 4-MFMA groups in order with sched_barrier: no change, 10.37 vs 10.2 us of steps)
 #pragma unroll
     for (int s = 0; s < 7; ++s)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][n], a[s], acc[n], 0, 0, 0);
+      for (int n = 0; n < NH; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][n], a[s], acc[n], 0, 0, 0);
   };
   // packed: v_pk_add_f32 (bias) + v_cvt_pk_bf16_f32 + v_pk_max_i16 per channel pair (the scalar form
   // compiled to one cvt per value plus a v_perm per pair)
-  auto tile_store = [&](const Tile& g, const f32x4 (&acc)[4]) __attribute__((always_inline)) {
+  auto tile_store = [&](const Tile& g, const f32x4 (&acc)[NH]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NH; ++n) {
       s16x2 h[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -575,17 +584,17 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
       tile_read(g, a);
     }
   };
-  auto t_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[4], auto in_steps) __attribute__((always_inline)) {
+  auto t_mfma = [&](const bf16x8 (&a)[7], f32x4 (&acc)[NH], auto in_steps) __attribute__((always_inline)) {
     if constexpr (decltype(in_steps)::value && (EXP & 1)) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = (f32x4){(float)a[0][0], (float)a[6][7], 0.f, 0.f};
+      for (int n = 0; n < NH; ++n) acc[n] = (f32x4){(float)a[0][0], (float)a[6][7], 0.f, 0.f};
     } else {
       tile_mfma(a, acc);
     }
   };
-  auto t_store = [&](const Tile& g, const f32x4 (&acc)[4], auto in_steps) __attribute__((always_inline)) {
+  auto t_store = [&](const Tile& g, const f32x4 (&acc)[NH], auto in_steps) __attribute__((always_inline)) {
     if constexpr (decltype(in_steps)::value && (EXP & 4)) {
-      if (acc[0][0] == 12345.f && acc[3][1] == 1.f) ring[fr] = bf16(acc[0][0]);   // keep acc live
+      if (acc[0][0] == 12345.f && acc[NH - 1][1] == 1.f) ring[fr] = bf16(acc[0][0]);   // keep acc live
     } else {
       tile_store(g, acc);
     }
@@ -593,7 +602,7 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
   auto tile_run = [&](const Tile& g) __attribute__((always_inline)) {
     constexpr std::integral_constant<bool, false> no{};
     bf16x8 a[7];
-    f32x4 acc[4];
+    f32x4 acc[NH];
     t_read(g, a, no);
     t_mfma(a, acc, no);
     t_store(g, acc, no);
@@ -601,7 +610,7 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
   // conv rows [rel0, rel0 + nr) of the block (ring row index rel = conv row - r_first) -> ring
   auto conv_rows = [&](const int rel0, const int nr) __attribute__((always_inline)) {
     const int ntiles = nr * tpr;
-    for (int mt = wave; mt < ntiles; mt += S4_WAVES) {
+    for (int mt = tfirst; mt < ntiles; mt += TSTRIDE) {
       const Tile g = tile_geo(mt, rel0, ntiles);
       if (g.ok) tile_run(g);
     }
@@ -655,36 +664,37 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
   // once.  (Interleaving a wave's pool reads / second tile's reads under its first tile's MFMAs by hand
   // measured slower: 22.4 vs 21.6 us.)
   {
+    constexpr int TPW = NH == 4 ? 2 : 4;                   // most tiles a wave takes of a step's 14
     const int ntl = 2 * tpr;
-    Tile ga = tile_geo(wave, 0, ntl), gb = tile_geo(wave + S4_WAVES, 0, ntl);
-    const int qa = wave / tpr, qb = (wave + S4_WAVES) / tpr;
-    const bool has_a = wave < ntl, has_b = wave + S4_WAVES < ntl;
-    const bf16* const pa0 = ga.pa - (2 * qa) * ST_PWC * 4;   // tile_geo(., 0, .) put rel = q in pa
-    const bf16* const pb0 = gb.pa - (2 * qb) * ST_PWC * 4;
+    Tile g[TPW];
+    int q[TPW];
+    bool has[TPW];
+    const bf16* p0[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int mt = tfirst + TSTRIDE * i;
+      g[i] = tile_geo(mt, 0, ntl);
+      q[i] = mt / tpr;
+      has[i] = mt < ntl;
+      p0[i] = g[i].pa - (2 * q[i]) * ST_PWC * 4;           // tile_geo(., 0, .) put rel = q in pa
+    }
     for (int k = 1; k < P; ++k) {
-      const int rel_a = 2 * k + 1 + qa, rel_b = 2 * k + 1 + qb;
-      ga.ok = has_a && r_first + rel_a < OH;               // rel >= 3: never above the image
-      ga.slot = (rel_a % S4_RING) * (S4_PAIRS * 128);
-      ga.pa = pa0 + (2 * rel_a) * ST_PWC * 4;
-      gb.ok = has_b && r_first + rel_b < OH;
-      gb.slot = (rel_b % S4_RING) * (S4_PAIRS * 128);
-      gb.pa = pb0 + (2 * rel_b) * ST_PWC * 4;
       // (both tiles' MFMAs before both epilogues measured slower: 11.5 vs 10.2 us of steps)
       constexpr std::integral_constant<bool, true> yes{};
       const int t = t0 + k - 1;
-      if (ga.ok) {
-        bf16x8 a[7];
-        f32x4 c[4];
-        t_read(ga, a, yes);
-        t_mfma(a, c, yes);
-        t_store(ga, c, yes);
-      }
-      if (gb.ok) {
-        bf16x8 a[7];
-        f32x4 c[4];
-        t_read(gb, a, yes);
-        t_mfma(a, c, yes);
-        t_store(gb, c, yes);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int rel = 2 * k + 1 + q[i];
+        g[i].ok = has[i] && r_first + rel < OH;            // rel >= 3: never above the image
+        g[i].slot = (rel % S4_RING) * (S4_PAIRS * 128);
+        g[i].pa = p0[i] + (2 * rel) * ST_PWC * 4;
+        if (g[i].ok) {
+          bf16x8 a[7];
+          f32x4 c[NH];
+          t_read(g[i], a, yes);
+          t_mfma(a, c, yes);
+          t_store(g[i], c, yes);
+        }
       }
       if (pool_item && !(EXP & 2)) pool_row(t);
       s4_lds_barrier();
@@ -717,18 +727,24 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
     // dozen blocks (8 at B=1): there the one-pool-row-per-block v1 grid fills more
     // CUs and wins.  ADAPT_STEM_V1=1 / =0 forces v1 / v2 (A/B switch).
     const int groups = (PH + S2_SP - 1) / S2_SP;
-    // ADAPT_STEM_V1=1 / =0 / =3 / =4: v1 / v2 / v3 (v3: the row-group kernel with the whole patch requested up
-    // front) / v4 (8 waves, pool of step k-1 beside the conv of step k)
+    // ADAPT_STEM_V1=1 / =0 / =3 / =4 / =5: v1 / v2 / v3 (v3: the row-group kernel with the whole patch requested
+    // up front) / v4 (8 waves, pool of step k-1 beside the conv of step k) / v5 (v4 with each wave on half the
+    // channels: 3-channel images only)
     const char* v1 = getenv("ADAPT_STEM_V1");
-    // default: v1 for small batches, v4 (21.4 us vs v3's 26.1 at bs=32, profiles/r5/stem_bf16_v4.md) above
-    const char ver = v1 && v1[0] ? v1[0] : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : (PW * 8 <= S4_NT ? '4' : '3'));
-    if (ver == '4') {
+    // default: v1 for small batches, above it v5 for 3-channel images (20.3 us vs v4's 21.2 and v3's 26.1 at
+    // bs=32, profiles/r5/stem_bf16_v4.md), else v4
+    const char ver = v1 && v1[0] ? v1[0]
+                                 : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : (PW * 8 <= S4_NT ? (C == 3 ? '5' : '4') : '3'));
+    if (ver == '4' || ver == '5') {
       if (PW * 8 > S4_NT) return hipErrorInvalidValue;
       const int g4 = (PH + S4_SP - 1) / S4_SP;
 #define ADAPT_S4(E)                                                                                            \
   hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, E>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH, \
                      OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg)
-      if (C == 3 && g_stem_exp != 0) {
+      if (C == 3 && ver == '5') {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 2>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias,
+                           out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+      } else if (C == 3 && g_stem_exp != 0) {
         switch (g_stem_exp) {
           case 1: ADAPT_S4(1); break;
           case 2: ADAPT_S4(2); break;
