@@ -77,6 +77,19 @@ def _wino_flop(ex, i):
     return 2 * 16 * tiles * Cin * pc.cout
 
 
+def _wino4_flop(ex, i):
+    """F(4x4, 3x3) matrix work of any 3x3 / stride-1 conv step: 36 positions x (4x4 output tiles, edge tiles
+    included) x Cin x Cout MACs -- the floor an F(4,3) Winograd kernel would be measured against (round-4
+    verdict item 1), whatever kernel the step runs now.  None for every other step."""
+    if ex.steps[i].kind != "conv":
+        return None
+    B, H, W, Cin, OH, OW, pc = ex._conv_geom(i)
+    if (pc.kh, pc.kw, pc.stride) != (3, 3, 1):
+        return None
+    tiles = B * ((OH + 3) // 4) * ((OW + 3) // 4)
+    return 2 * 36 * tiles * Cin * pc.cout
+
+
 def run(a):
     import torch
     from profile_r50 import single_step, step_flop, time_fn
@@ -117,7 +130,8 @@ def run(a):
         act = sum(_bytes_of(ex, g, n, a.batch) for n in list(st.ins) + outs)
         meta.append({"i": i, "kind": st.kind, "out": st.out, "ms": t_ms, "flop": step_flop(g, st, a.batch),
                      "act_bytes": act, "weight_bytes": _weight_bytes(g, st, 4 if a.dtype == "fp32" else 2),
-                     "cfg": ex.cfg.get(i), "wino_flop": _wino_flop(ex, i)})
+                     "cfg": ex.cfg.get(i), "wino_flop": _wino_flop(ex, i),
+                     "wino4_flop": _wino4_flop(ex, i)})
     if a.meta:
         with open(a.meta, "w") as f:
             json.dump({"model": a.model, "batch": a.batch, "reps": REPS, "dtype": a.dtype, "steps": meta}, f,
@@ -184,6 +198,8 @@ def table(a):
         floor = max(st["flop"] / peak, comp / HBM_BW)           # compulsory traffic only
         wf = st.get("wino_flop")
         wfloor = max(wf / peak, comp / HBM_BW) if wf else None    # the Winograd kernel's own work floor
+        w4 = st.get("wino4_flop")
+        w4floor = max(w4 / peak, comp / HBM_BW) if w4 else None   # F(4x4, 3x3) work floor
         row = {"i": st["i"], "kind": st["kind"], "out": st["out"], "cfg": st["cfg"], "ms": st["ms"],
                "gflop": round(st["flop"] / 1e9, 3),
                "tflops": round(st["flop"] / t / 1e12, 1) if t and st["flop"] else None,
@@ -195,7 +211,8 @@ def table(a):
                "mfma_util": round(st["flop"] / t / peak, 3) if t and st["flop"] else None,
                "of_floor": round(t / floor, 2) if t and floor else None,
                "wino_floor_ms": round(wfloor * 1e3, 4) if wfloor else None,
-               "of_wino_floor": round(t / wfloor, 2) if t and wfloor else None}
+               "of_wino_floor": round(t / wfloor, 2) if t and wfloor else None,
+               "wino4_floor_ms": round(w4floor * 1e3, 4) if w4floor else None}
         gui = c.get("GRBM_GUI_ACTIVE")
         mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
         if gui and mfma is not None:
@@ -214,19 +231,24 @@ def table(a):
         tot["fabric"] += fabric or 0
         tot["compulsory"] += comp
     hdr = f"{'i':>3} {'kind':10} {'out':24} {'ms':>7} {'TF/s':>6} {'compMB':>7} {'fabMB':>7} {'TB/s':>5} " \
-          f"{'floor':>7} {'x':>5} {'wfloor':>7} {'xw':>5} {'mfma':>5} bound"
+          f"{'floor':>7} {'x':>5} {'wfloor':>7} {'xw':>5} {'w4floor':>7} {'mfma':>5} bound"
     print(hdr)
     for r in rows:
         wfl = f"{r['wino_floor_ms']:7.4f}" if r.get("wino_floor_ms") else f"{'-':>7}"
+        w4l = f"{r['wino4_floor_ms']:7.4f}" if r.get("wino4_floor_ms") else f"{'-':>7}"
         print(f"{r['i']:3d} {r['kind']:10} {r['out'][:24]:24} {r['ms'] or 0:7.4f} {str(r['tflops']):>6} "
               f"{r['compulsory_MB']:7.2f} {str(r['fabric_MB']):>7} {str(r['fabric_TBps']):>5} {r['floor_ms']:7.4f} "
-              f"{str(r['of_floor']):>5} {wfl} {str(r.get('of_wino_floor') or '-'):>5} "
+              f"{str(r['of_floor']):>5} {wfl} {str(r.get('of_wino_floor') or '-'):>5} {w4l} "
               f"{str(r.get('mfma_busy')):>5} {r['bound']}")
     floor_sum = sum(r["floor_ms"] for r in rows)
     wrows = [r for r in rows if r.get("wino_floor_ms")]
     if wrows:
         print(f"winograd 3x3: {len(wrows)} convs, {sum(r['ms'] or 0 for r in wrows):.4f} ms against a Winograd-work "
               f"floor of {sum(r['wino_floor_ms'] for r in wrows):.4f} ms")
+    w4rows = [r for r in rows if r.get("wino4_floor_ms")]
+    if w4rows:
+        print(f"3x3 stride-1: {len(w4rows)} convs, {sum(r['ms'] or 0 for r in w4rows):.4f} ms against an F(4x4, 3x3) "
+              f"floor of {sum(r['wino4_floor_ms'] for r in w4rows):.4f} ms")
     print(f"sum: {tot['ms']:.4f} ms, {tot['flop'] / 1e9:.1f} GFLOP, fabric {tot['fabric'] / 1e6:.1f} MB, "
           f"compulsory {tot['compulsory'] / 1e6:.1f} MB, floors {floor_sum:.4f} ms "
           f"(peak {peak / 1e12:.0f} TF/s, {HBM_BW / 1e12:.1f} TB/s)")
