@@ -107,6 +107,7 @@ MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": 
                "vgg19": "VGG19", "mobilenet_v2": "MobileNetV2", "densenet121": "DenseNet121",
                "efficientnetb0": "EfficientNetB0", "inception_v3": "InceptionV3"}
 # logits tolerance of a pipelined forward against the unsliced one: a cut changes
+BF16_MIN_WARMUP = 20      # untimed steps before the value_bf16 companion's K timed steps
 # where bf16 rounding happens (a fused epilogue becomes a stored bf16 frontier)
 PP_LOGIT_RTOL = {"bf16": 5e-2, "fp32": 1e-3}
 
@@ -139,6 +140,7 @@ def make_record(args, world: int, n_gpus: int, backend: str, value: float, elaps
     if bf16:
         rec["value_bf16"] = round(bf16["value"], 2)
         rec["ms_per_step_bf16"] = round(bf16["elapsed"] / args.steps * 1e3, 4)
+        rec["warmup_bf16"] = bf16.get("warmup", args.warmup)
     if pp is not None:
         rec["pp"] = pp
     for k, v in (subs or {}).items():
@@ -464,7 +466,7 @@ def main(argv=None):
     part_at = [s for s in args.part_at.split(",") if s]
     image = tuple(g.layers[g.input].out_shape)          # 224x224x3 (ResNet-50); the model's own size otherwise
 
-    def headline(precision: str):
+    def headline(precision: str, warmup: int):
         job = runner.build_job(g, weights, mode=args.mode, world=world, rank=rank, device=dev, batch=args.batch,
                                stages=args.stages, part_at=part_at, graph=not args.no_graph, tune=args.tune,
                                host_staged=(backend != "nccl"), streams=args.streams, codec=args.codec,
@@ -472,7 +474,7 @@ def main(argv=None):
         # synthetic input, resident on device (data="synthetic")
         gen = torch.Generator(device=dev).manual_seed(1234 + rank)
         job.set_synthetic_input(torch.randn((args.batch,) + image, generator=gen, device=dev))
-        elapsed = timed(job, args.steps, args.warmup, dev, world)
+        elapsed = timed(job, args.steps, warmup, dev, world)
         info = {"global_batch": job.global_batch, "parallelism": job.parallelism, "part_at": job.part_at}
         link = getattr(job, "link", None)
         if args.codec != "none" and link is not None:
@@ -485,11 +487,15 @@ def main(argv=None):
         torch.cuda.empty_cache()
         return value, elapsed, info
 
-    value, elapsed, info = headline(args.dtype)
+    value, elapsed, info = headline(args.dtype, args.warmup)
     bf16 = None
     if args.dtype == "fp32" and not args.no_bf16:
-        v16, e16, _ = headline("bf16")
-        bf16 = {"value": v16, "elapsed": e16}
+        # the companion runs after the headline's teardown, on a card whose clocks dropped while the bf16 job
+        # was built: at least 20 untimed steps (3 ms of work at W = 5 left 20-step timings 2-3 % low); still
+        # exactly K timed steps
+        w16 = max(args.warmup, BF16_MIN_WARMUP)
+        v16, e16, _ = headline("bf16", w16)
+        bf16 = {"value": v16, "elapsed": e16, "warmup": w16}
 
     n_gpus = 1
     if world > 1:
