@@ -146,6 +146,8 @@ for p in "${P[@]}"; do
     ab4s)     steps+=("300|$out/ab_w4_s5|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x7x7x512,3x3s1p1111 --cfg 200 --ksplit 4 --rounds 25")
               steps+=("300|$out/ab_w4_s4|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x14x14x256,3x3s1p1111 --cfg 200 --ksplit 2 --rounds 25")
               steps+=("300|$out/ab_w4_s3|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x28x28x128,3x3s1p1111 --cfg 200 --ksplit 1 --rounds 25") ;;
+    psab2)    steps+=("300|$out/ab_ps_s4one|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x1024,1x1s1p0000,256 --cfg 76 --ksplit 1 --rounds 25")
+              steps+=("300|$out/ab_ps_s5out|python -u tools/ab_cfg.py --model resnet50 --key 32x7x7x512,1x1s1p0000,2048 --cfg 75 --ksplit 1 --rounds 25") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
     stemx)    steps+=("120|$out/stem_exp|python -u tools/stem_timeline.py --exp 0,1,2,4,8,3,13,15 --json gpurun_out/$out/stem_exp.json") ;;
     stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
