@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json", default="")
+    ap.add_argument("--version", default="5", choices=["4", "5"], help="ADAPT_STEM_V1 (v5: channel halves)")
     ap.add_argument("--exp", default="0", help="measurement variants: 1 no MFMA, 2 no pool, 4 no ring stores, "
                     "8 no A reads in the steps (outputs wrong by design), comma list")
     a = ap.parse_args()
@@ -36,7 +37,9 @@ def main():
     ps = C.pack_stem(kern, np.zeros(64, np.float32), ((3, 3), (3, 3)), "cuda")
     x = torch.randn(B, 224, 224, 3, device="cuda")
     out = torch.empty(B, 56, 56, 64, device="cuda", dtype=torch.bfloat16)
-    os.environ["ADAPT_STEM_V1"] = "4"
+    os.environ["ADAPT_STEM_V1"] = a.version
+    if a.version == "5" and a.exp != "0":
+        ap.error("the --exp variants are built for v4 only")
     blocks = B * math.ceil(56 / SP)
     recs = []
     for exp in [int(e) for e in a.exp.split(",")]:
@@ -56,7 +59,7 @@ def main():
             ph[name] = {"median_us": round(float(np.median(v)), 2), "p90_us": round(float(np.percentile(v, 90)), 2),
                         "max_us": round(float(v.max()), 2)}
         start = (d[:, 6] - d[:, 6].min()) / 100.0
-        rec = {"kernel": "stem_pool_v4", "exp": exp, "batch": B, "blocks": blocks, "clock_GHz": round(ghz, 3),
+        rec = {"kernel": f"stem_pool v{a.version}", "exp": exp, "batch": B, "blocks": blocks, "clock_GHz": round(ghz, 3),
                "phases": ph,
                "block_start_us": {"median": round(float(np.median(start)), 2), "max": round(float(start.max()), 2)},
                "wave_total_us_median": round(float(np.median((d[:, 4] - d[:, 0]) / (ghz * 1e3))), 2),
