@@ -465,7 +465,10 @@ __device__ __forceinline__ int ring4_off(int slot, int ow, int chunk) {
 // NH: 16-channel groups per wave.  4 = every wave computes all 64 channels of its tiles (v4).  2 (v5): waves
 // 0-3 take channels 0-31 and waves 4-7 channels 32-63 of every tile, so each wave loads half the weight
 // panel and the 28 half-tiles of a step split 7 / 7 / 7 / 7 over the SIMDs (v4: 4 / 4 / 3 / 3 tiles).
-template <bool C3, int EXP = 0, int NH = 4>
+// WL (v6): the 28 KB weight panel is loaded once per block (3.5 16-byte loads a thread) and staged in the
+// not-yet-used ring area with a 232-element row pitch (conflict-free fragment reads), instead of every wave
+// loading the whole panel from L2 (229 KB per CU, >= 1.7 us at the 64 B/clk L1 path)
+template <bool C3, int EXP = 0, int NH = 4, bool WL = false>
 __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
                                                                 const float* __restrict__ bias, bf16* __restrict__ out,
                                                                 int H, int W, int C, int OH, int OW, int pad_t,
@@ -503,11 +506,23 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
   const int nb = hsel * NH;                                // first 16-channel group of this wave
   const int tfirst = NH == 4 ? wave : (((wave & 3) + 2 * hsel) & 3);
   bf16x8 bw[7][NH];
+  constexpr int WPITCH = ST_K + 8;                         // staged row pitch (bf16): 464 B, 16 rows on 16 bank groups
+  constexpr int WCH = 64 * ST_K / 8;                       // 16-byte chunks of the panel (1792)
+  constexpr int WIT = (WCH + S4_NT - 1) / S4_NT;
+  u32x4 wst[WL ? WIT : 1];
+  if constexpr (WL) {
 #pragma unroll
-  for (int s = 0; s < 7; ++s)
+    for (int k = 0; k < WIT; ++k) {
+      const int i = tid + k * S4_NT;
+      if (i < WCH) wst[k] = ((const u32x4*)w)[i];
+    }
+  } else {
 #pragma unroll
-    for (int n = 0; n < NH; ++n)
-      bw[s][n] = *(const bf16x8*)(w + (size_t)((nb + n) * 16 + fr) * ST_K + s * 32 + fq * 8);
+    for (int s = 0; s < 7; ++s)
+#pragma unroll
+      for (int n = 0; n < NH; ++n)
+        bw[s][n] = *(const bf16x8*)(w + (size_t)((nb + n) * 16 + fr) * ST_K + s * 32 + fq * 8);
+  }
   float b4[NH][4];
 #pragma unroll
   for (int n = 0; n < NH; ++n)
@@ -518,8 +533,22 @@ __global__ __launch_bounds__(S4_NT, 1) void stem_pool_v4_kernel(const float* __r
     get_rows3<S4_ITEMS, S4_NT>(pall, xi, tid, row_end, ih0, H, W, pwc, pad_l);
   else
     get_rows<S4_ITEMS, S4_NT>(pall, xi, tid, 0, row_end, row_end, ih0, H, W, C, pwc, pad_l);
+  if constexpr (WL) {
+    // the panel's loads were issued before the patch's: these stores wait for them only
+#pragma unroll
+    for (int k = 0; k < WIT; ++k) {
+      const int i = tid + k * S4_NT;
+      if (i < WCH) *(u32x4*)(ring + (i / (ST_K / 8)) * WPITCH + (i % (ST_K / 8)) * 8) = wst[k];
+    }
+    s4_lds_barrier();
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+#pragma unroll
+      for (int n = 0; n < NH; ++n)
+        bw[s][n] = *(const bf16x8*)(ring + ((nb + n) * 16 + fr) * WPITCH + s * 32 + fq * 8);
+  }
   put_items<0, S4_ITEMS_A, S4_ITEMS, S4_NT>(pall, patch, tid, 0, S2_ROWS0);
-  s4_lds_barrier();
+  s4_lds_barrier();                                        // (WL: every wave's panel reads are done: the ring is free)
   stamp(1);
 
   // one 16-pixel x 64-channel conv tile: geometry / A-fragment reads / MFMAs / bias + ReLU into the ring.
@@ -727,21 +756,28 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
     // dozen blocks (8 at B=1): there the one-pool-row-per-block v1 grid fills more
     // CUs and wins.  ADAPT_STEM_V1=1 / =0 forces v1 / v2 (A/B switch).
     const int groups = (PH + S2_SP - 1) / S2_SP;
-    // ADAPT_STEM_V1=1 / =0 / =3 / =4 / =5: v1 / v2 / v3 (v3: the row-group kernel with the whole patch requested
-    // up front) / v4 (8 waves, pool of step k-1 beside the conv of step k) / v5 (v4 with each wave on half the
-    // channels: 3-channel images only)
+    // ADAPT_STEM_V1=1 / =0 / =3 / =4 / =5 / =6 / =7: v1 / v2 / v3 (v3: the row-group kernel with the whole patch
+    // requested up front) / v4 (8 waves, pool of step k-1 beside the conv of step k) / v5 (v4 with each wave on
+    // half the channels) / v6 (v4 with the weight panel loaded once per block) / v7 (v5 + v6); v5-v7 take
+    // 3-channel images only
     const char* v1 = getenv("ADAPT_STEM_V1");
-    // default: v1 for small batches, above it v5 for 3-channel images (20.3 us vs v4's 21.2 and v3's 26.1 at
-    // bs=32, profiles/r5/stem_bf16_v4.md), else v4
+    // default: v1 for small batches, above it v6 for 3-channel images (18.4 us vs v5's 20.4, v4's 21.1 and v3's
+    // 26.1 at bs=32, profiles/r5/stem_bf16_v4.md), else v4
     const char ver = v1 && v1[0] ? v1[0]
-                                 : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : (PW * 8 <= S4_NT ? (C == 3 ? '5' : '4') : '3'));
-    if (ver == '4' || ver == '5') {
+                                 : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : (PW * 8 <= S4_NT ? (C == 3 ? '6' : '4') : '3'));
+    if (ver == '4' || ver == '5' || ver == '6' || ver == '7') {
       if (PW * 8 > S4_NT) return hipErrorInvalidValue;
       const int g4 = (PH + S4_SP - 1) / S4_SP;
 #define ADAPT_S4(E)                                                                                            \
   hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, E>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH, \
                      OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg)
-      if (C == 3 && ver == '5') {
+      if (C == 3 && ver == '6') {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 4, true>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w,
+                           bias, out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+      } else if (C == 3 && ver == '7') {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 2, true>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w,
+                           bias, out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+      } else if (C == 3 && ver == '5') {
         hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 2>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias,
                            out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
       } else if (C == 3 && g_stem_exp != 0) {

@@ -149,6 +149,8 @@ for p in "${P[@]}"; do
     psab2)    steps+=("300|$out/ab_ps_s4one|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x1024,1x1s1p0000,256 --cfg 76 --ksplit 1 --rounds 25")
               steps+=("300|$out/ab_ps_s5out|python -u tools/ab_cfg.py --model resnet50 --key 32x7x7x512,1x1s1p0000,2048 --cfg 75 --ksplit 1 --rounds 25") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
+    stemt67)  steps+=("120|$out/stem_timeline6|python -u tools/stem_timeline.py --version 6 --json gpurun_out/$out/stem_timeline6.json")
+              steps+=("120|$out/stem_timeline7|python -u tools/stem_timeline.py --version 7 --json gpurun_out/$out/stem_timeline7.json") ;;
     stemx)    steps+=("120|$out/stem_exp|python -u tools/stem_timeline.py --version 4 --exp 0,1,2,4,8,3,13,15 --json gpurun_out/$out/stem_exp.json") ;;
     stem16)   steps+=("200|$out/pytest_stem16|python -u -m pytest tests/test_kernels_gpu.py -k stem -v -x --timeout 120 --timeout-method thread")
               steps+=("120|$out/stem_bench|python -u tools/stem_bench.py") ;;

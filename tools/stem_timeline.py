@@ -26,7 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json", default="")
-    ap.add_argument("--version", default="5", choices=["4", "5"], help="ADAPT_STEM_V1 (v5: channel halves)")
+    ap.add_argument("--version", default="5", choices=["4", "5", "6", "7"],
+                    help="ADAPT_STEM_V1 (v5: channel halves, v6: v4 + block-staged weights, v7: v5 + block-staged weights)")
     ap.add_argument("--exp", default="0", help="measurement variants: 1 no MFMA, 2 no pool, 4 no ring stores, "
                     "8 no A reads in the steps (outputs wrong by design), comma list")
     a = ap.parse_args()
@@ -38,7 +39,7 @@ def main():
     x = torch.randn(B, 224, 224, 3, device="cuda")
     out = torch.empty(B, 56, 56, 64, device="cuda", dtype=torch.bfloat16)
     os.environ["ADAPT_STEM_V1"] = a.version
-    if a.version == "5" and a.exp != "0":
+    if a.version != "4" and a.exp != "0":
         ap.error("the --exp variants are built for v4 only")
     blocks = B * math.ceil(56 / SP)
     recs = []
