@@ -148,6 +148,11 @@ for p in "${P[@]}"; do
               steps+=("300|$out/ab_w4_s3|python -u tools/ab_cfg.py --precision fp32 --model resnet50 --key 32x28x28x128,3x3s1p1111 --cfg 200 --ksplit 1 --rounds 25") ;;
     psab2)    steps+=("300|$out/ab_ps_s4one|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x1024,1x1s1p0000,256 --cfg 76 --ksplit 1 --rounds 25")
               steps+=("300|$out/ab_ps_s5out|python -u tools/ab_cfg.py --model resnet50 --key 32x7x7x512,1x1s1p0000,2048 --cfg 75 --ksplit 1 --rounds 25") ;;
+    abs4)     steps+=("5|$out/abs4_start|true")
+              steps+=("300|$out/ab_s4_3x3_62_2|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x256,3x3s1p1111,256 --cfg 62 --ksplit 2 --rounds 25")
+              steps+=("300|$out/ab_s4_3x3_62_-2|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x256,3x3s1p1111,256 --cfg 62 --ksplit -2 --rounds 25")
+              steps+=("300|$out/ab_s4_3x3_63_2|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x256,3x3s1p1111,256 --cfg 63 --ksplit 2 --rounds 25")
+              steps+=("300|$out/ab_s4_3x3_64_2|python -u tools/ab_cfg.py --model resnet50 --key 32x14x14x256,3x3s1p1111,256 --cfg 64 --ksplit 2 --rounds 25") ;;
     stemt)    steps+=("120|$out/stem_timeline|python -u tools/stem_timeline.py --json gpurun_out/$out/stem_timeline.json") ;;
     stemt67)  steps+=("120|$out/stem_timeline6|python -u tools/stem_timeline.py --version 6 --json gpurun_out/$out/stem_timeline6.json")
               steps+=("120|$out/stem_timeline7|python -u tools/stem_timeline.py --version 7 --json gpurun_out/$out/stem_timeline7.json") ;;
