@@ -383,6 +383,11 @@ class DEFER:
             p = self._replica_of(wid)
             if ev.type == "DELETE" and p is not None:
                 self._mark_dirty(p.replica, f"worker {wid} left (lease expired or revoked)", wid=wid)
+            elif ev.type == "PUT" and rec.get("state") == "UNRECOVERABLE":
+                # the worker could not abort an RCCL communicator within its deadline and is
+                # exiting (node.py `give_up`): same as a dead process -- excluded until a fresh
+                # process (new pid) registers under this id
+                self._worker_dead(wid, rec.get("pid"), f"unrecoverable: {rec.get('error')}")
             elif ev.type == "PUT" and p is not None and rec.get("epoch") == p.epoch and \
                     rec.get("state") in ("LINK_ERROR", "STAGE_ERROR"):
                 if rec["state"] == "STAGE_ERROR":

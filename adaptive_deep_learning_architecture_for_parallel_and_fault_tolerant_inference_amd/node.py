@@ -65,6 +65,11 @@ def get_local_ip() -> str:
     return ip
 
 
+# exit status of a worker process that gave up after a stuck RCCL abort (EX_TEMPFAIL:
+# a supervisor may start a fresh process)
+EXIT_UNRECOVERABLE = 75
+
+
 class _Pending:
     """A pipelined GPU micro-batch in the send queue: `msg`'s host tensors are
     ready once `ev` has completed; `links` are its input's link slots."""
@@ -467,8 +472,12 @@ class Node:
     def __init__(self, dispatcher_ip: str = "127.0.0.1", membership_port: int = 2379, data_port: int = DATA_PORT,
                  config_port: int = CONFIG_PORT, device: Optional[str] = None, node_id: Optional[str] = None,
                  chunk_size: int = 512 * 1000, host: str = "0.0.0.0", advertise_host: Optional[str] = None,
-                 heartbeat_ttl: float = 1.0, register: bool = True) -> None:
+                 heartbeat_ttl: float = 1.0, register: bool = True, exit_on_unrecoverable: bool = False) -> None:
         self.weights_ready_event = threading.Event()        # reference attribute (src/node.py:27)
+        # process mode (main()): a stuck RCCL abort ends the process with EXIT_UNRECOVERABLE;
+        # library mode only publishes UNRECOVERABLE and stops the node
+        self.exit_on_unrecoverable = exit_on_unrecoverable
+        self.unrecoverable: Optional[str] = None
         if device is None:
             import torch
             device = "cuda:0" if torch.cuda.is_available() else "cpu"
@@ -684,6 +693,27 @@ class Node:
             if self.runtime is not rt or self.state.epoch != rt.epoch:
                 return
             self._publish(state=state, epoch=rt.epoch, error=rt.error)
+
+    def give_up(self, rt, reason: str) -> None:
+        """The epoch's communicator could not be aborted within its deadline
+        (`RcclComm.abort_stuck`): this process can no longer vouch for its RCCL
+        state, so it publishes UNRECOVERABLE (the dispatcher treats that as a
+        dead worker and re-plans without it), stops, and in process mode exits
+        with EXIT_UNRECOVERABLE so a supervisor can start a *fresh* process in
+        its place (never an exec: the GPU is initialised here).  The reference's
+        watchdog can only notice a worker that stops answering
+        (`/root/reference/src/dispatcher.py:186-194,302-304`)."""
+        if self.unrecoverable is not None:
+            return
+        self.unrecoverable = reason
+        print(f"node {self.node_id}: UNRECOVERABLE ({reason}); exiting {EXIT_UNRECOVERABLE}", file=sys.stderr,
+              flush=True)
+        self._publish(state="UNRECOVERABLE", epoch=getattr(rt, "epoch", self.state.epoch), error=reason)
+        if self.exit_on_unrecoverable:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(EXIT_UNRECOVERABLE)
+        threading.Thread(target=self.stop, daemon=True, name="node-give-up").start()
 
     # -------------------------------------------------- stage computes
     @staticmethod
@@ -1044,7 +1074,7 @@ def main(argv=None):
     if a.parent_pid:
         _follow_parent(a.parent_pid)
     node = Node(a.dispatcher, a.membership_port, a.data_port, a.config_port, a.device, a.id, a.chunk_size,
-                heartbeat_ttl=a.ttl)
+                heartbeat_ttl=a.ttl, exit_on_unrecoverable=True)
     print(f"node {node.node_id} device={node.device} data={node.data_port} config={node.config_port}", flush=True)
     node.run(block=True)
     # Communicator threads of aborted epochs may still sit in backend waits on

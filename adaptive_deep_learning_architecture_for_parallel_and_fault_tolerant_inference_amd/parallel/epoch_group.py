@@ -34,6 +34,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from .rccl import ABORT_DEADLINE_S
+
 
 class Aborted(RuntimeError):
     """The epoch was aborted (peer failure or reconfiguration)."""
@@ -56,6 +58,7 @@ class EpochGroup:
         self.rank, self.world, self.epoch = rank, world, epoch
         self.device = device
         self.abort_flag = threading.Event()
+        self._pg_stuck = False
         self.stall_s = stall_s
         self._sends: list = []                   # (work, posted_at) not yet seen complete
         self.links = None
@@ -214,7 +217,22 @@ class EpochGroup:
         for pg in (self.pg, self.ctl):
             if pg is None:
                 continue
-            try:
-                pg.abort()
-            except Exception:  # noqa: BLE001 - best effort; the group is discarded either way
-                pass
+            # bounded like the native links: ProcessGroupNCCL.abort() is an ncclCommAbort underneath
+            th = threading.Thread(target=_abort_quietly, args=(pg,), daemon=True, name=f"epoch{self.epoch}-pgabort")
+            th.start()
+            th.join(ABORT_DEADLINE_S)
+            if th.is_alive():
+                self._pg_stuck = True
+
+    def abort_stuck(self) -> bool:
+        """An abort of this epoch's communicators did not return within the deadline."""
+        if self._pg_stuck:
+            return True
+        return self.links is not None and hasattr(self.links, "abort_stuck") and self.links.abort_stuck()
+
+
+def _abort_quietly(pg) -> None:
+    try:
+        pg.abort()
+    except Exception:  # noqa: BLE001 - best effort; the group is discarded either way
+        pass

@@ -14,7 +14,12 @@ semantics beyond socket errors and a task watchdog keyed on start time
   the receive of t+1 and the compute of t run on three hardware queues;
 * `Work` is an event recorded on the link stream behind the grouped
   send/recv: ``wait()`` orders the caller's current stream after it (no host
-  block), ``wait_host()`` polls it abortably.
+  block), ``wait_host()`` polls it abortably;
+* ``abort()`` is bounded: ``ncclCommAbort`` runs on a native helper thread
+  and is waited for at most ``abort_deadline_s`` (3 s).  Past it the
+  communicator reports ``abort_stuck``; its owner then publishes
+  UNRECOVERABLE and exits non-zero (`StuckAbort`, node.py) so the
+  dispatcher re-plans without it and a supervisor may start a fresh process.
 
 Point-to-point matching is FIFO per communicator (RCCL has no tags): every
 caller posts its sends and receives in tick order, which the pipeline
@@ -35,6 +40,13 @@ _lock = threading.Lock()
 
 class LinkError(RuntimeError):
     """A communicator reported an asynchronous error or was aborted."""
+
+
+class StuckAbort(LinkError):
+    """ncclCommAbort did not return within the abort deadline: the process must be given up."""
+
+
+ABORT_DEADLINE_S = float(os.environ.get("ADAPT_ABORT_DEADLINE_S", "3.0"))
 
 
 def native():
@@ -106,7 +118,7 @@ class RcclComm:
 
     def __init__(self, store, key: str, nranks: int, rank: int, device, wait: bool = True,
                  timeout_s: float = 60.0, watch_us: int = 1000, abort_on_error: bool = True,
-                 stream: Optional[torch.cuda.Stream] = None):
+                 stream: Optional[torch.cuda.Stream] = None, abort_deadline_s: Optional[float] = None):
         self.device = torch.device(device)
         self.name = key
         self.nranks, self.rank = nranks, rank
@@ -121,6 +133,8 @@ class RcclComm:
             uid = _exchange_uid(store, f"{key}/uid", rank, timeout_s=timeout_s)
             self.t0 = time.perf_counter()
             self._c = native().Comm(uid, nranks, rank, self.device.index or 0, False, key[-63:])
+            if hasattr(self._c, "set_abort_deadline"):       # (test doubles of `_comm.Comm` may lack it)
+                self._c.set_abort_deadline(ABORT_DEADLINE_S if abort_deadline_s is None else abort_deadline_s)
         if watch_us > 0:
             self._c.start_watch(watch_us, abort_on_error)
         self.stream = stream if stream is not None else torch.cuda.Stream(device=self.device)
@@ -143,6 +157,12 @@ class RcclComm:
     @property
     def aborted(self) -> bool:
         return self._c.aborted
+
+    @property
+    def abort_stuck(self) -> bool:
+        """ncclCommAbort (or a caller inside RCCL) did not return within the
+        abort deadline: this process cannot vouch for its RCCL state any more."""
+        return bool(getattr(self._c, "abort_stuck", False))
 
     @property
     def error_text(self) -> str:
@@ -201,7 +221,8 @@ class RcclComm:
 
     # -- teardown
     def abort(self) -> float:
-        """ncclCommAbort (any thread); returns its latency in ms."""
+        """ncclCommAbort (any thread), bounded by the abort deadline; returns
+        its latency in ms (check `abort_stuck` afterwards)."""
         return self._c.abort()
 
     def destroy(self, timeout_s: float = 10.0) -> bool:
@@ -288,6 +309,9 @@ class PairLinks:
         self.abort_flag.set()
         for c in self.comms():
             c.abort()
+
+    def abort_stuck(self) -> bool:
+        return any(c.abort_stuck for c in self.comms())
 
     def destroy(self, timeout_s: float = 10.0) -> bool:
         """Bounded teardown of both links (see `RcclComm.destroy`); False when a

@@ -163,7 +163,12 @@ class PipelineJob:
         ok = True
         if self.links is not None:
             ok = self.links.destroy(timeout_s)
+            stuck = self.links.abort_stuck()
             self.links = None
+            if stuck:
+                # a device sync would wait on the transfer the abort could not end
+                from .rccl import StuckAbort
+                raise StuckAbort("pipeline links: ncclCommAbort exceeded its deadline; give the process up")
         torch.cuda.synchronize(self.ex.device)
         return ok
 

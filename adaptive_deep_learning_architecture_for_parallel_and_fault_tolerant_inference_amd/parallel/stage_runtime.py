@@ -132,6 +132,8 @@ class CollectiveStageRuntime:
         self.stop.set()
         if self.group is not None:
             self.group.abort()
+            if self.group.abort_stuck():
+                self.node.give_up(self, f"epoch {self.epoch}: communicator abort exceeded its deadline")
         for s in (self.upstream, self.downstream):
             if s is not None:
                 try:

@@ -11,8 +11,18 @@
 //    the GIL released and an abort flag checked between polls;
 //  * a watch thread polls ncclCommGetAsyncError and records (and optionally
 //    acts on) the first asynchronous error;
+//  * every ncclCommGetAsyncError of a communicator goes through one mutex: on a
+//    non-blocking communicator that call also completes (joins) a finished
+//    group job, and two threads (the watch thread and a waiter) joining the
+//    same job at once is undefined -- the round-5 driver box hung in exactly
+//    that pair of pollers;
 //  * abort() = ncclCommAbort from any thread, after every other user of the
-//    handle has left its poll loop (the handle is freed by the abort).
+//    handle has left its poll loop (the handle is freed by the abort), run on a
+//    helper thread with a deadline: an abort that does not return in time
+//    (a kernel that never drains, a proxy thread stuck on a dead peer) leaves
+//    the communicator marked `abort_stuck`, and the owner must give the
+//    process up (report UNRECOVERABLE, exit non-zero) -- a fresh process, never
+//    an exec, replaces it.
 //
 // The RCCL entry points are resolved with dlsym from the librccl that PyTorch
 // already mapped (libtorch_hip needs it), so the process holds exactly one RCCL
@@ -171,10 +181,8 @@ class Comm {
 
   ~Comm() {
     stop_watch();
-    if (comm_ && !aborted_.load()) {
-      // an unfinished object is abandoned, not finalized: finalize could wait on a dead peer
-      api().abort(comm_);
-    }
+    // an unfinished object is abandoned, not finalized: finalize could wait on a dead peer
+    if (comm_ && !aborted_.load()) abort();
     comm_ = nullptr;
   }
 
@@ -182,9 +190,7 @@ class Comm {
   int poll() {
     Use u(this);
     if (!u.ok) return -1;
-    ncclResult_t st = ncclSuccess;
-    ncclResult_t r = api().getAsyncError(comm_, &st);
-    if (r != ncclSuccess) st = r;
+    ncclResult_t st = async_error();
     const int forced = forced_err_.load();
     if (forced != ncclSuccess && st == ncclSuccess) st = (ncclResult_t)forced;
     note(st);
@@ -267,6 +273,9 @@ class Comm {
 
   // ncclCommAbort once every other user has left the handle; idempotent and
   // callable from any thread (the watch thread included).  Returns its latency.
+  // The RCCL call runs on a detached helper thread and is waited for at most
+  // `abort_deadline_s` (set_abort_deadline); past it the communicator is
+  // marked abort_stuck and the handle is abandoned to the helper.
   double abort() {
     auto t0 = Clock::now();
     bool expected = false;
@@ -274,14 +283,33 @@ class Comm {
     {
       NoGil ng;
       // users poll the flag between polls (<= ~50 us); bounded in case one is stuck
-      auto limit = Clock::now() + std::chrono::seconds(5);
+      auto limit = Clock::now() + std::chrono::duration<double>(abort_deadline_s_.load());
       while (users_.load() > 0 && Clock::now() < limit) std::this_thread::sleep_for(std::chrono::microseconds(20));
-      if (comm_) api().abort(comm_);
+      if (users_.load() > 0) abort_stuck_.store(true);     // a caller is stuck inside RCCL
+      ncclComm_t c = comm_;
       comm_ = nullptr;
+      if (c) {
+        auto done = std::make_shared<std::atomic<int>>(0);
+        const int stall_ms = abort_stall_ms_.load();
+        std::thread([c, done, stall_ms] {
+          if (stall_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(stall_ms));
+          api().abort(c);
+          done->store(1);
+        }).detach();
+        while (!done->load() && Clock::now() < limit) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (!done->load()) abort_stuck_.store(true);
+      }
     }
+    abort_ms_ = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
     if (std::this_thread::get_id() != watch_id_) stop_watch();
-    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    return abort_ms_;
   }
+
+  // deadline of abort() (users leaving + ncclCommAbort), seconds
+  void set_abort_deadline(double s) { abort_deadline_s_.store(s > 0.01 ? s : 0.01); }
+  // Fault injection for the deadline path: the helper thread sleeps `ms`
+  // before ncclCommAbort, standing in for an abort that RCCL never returns from.
+  void inject_abort_stall(int ms) { abort_stall_ms_.store(ms); }
 
   // orderly teardown of a healthy communicator (all peers call it)
   void destroy(double timeout_s) {
@@ -297,7 +325,7 @@ class Comm {
     auto end = Clock::now() + std::chrono::duration<double>(timeout_s);
     ncclResult_t st = r;
     while (r == ncclSuccess || r == ncclInProgress) {
-      a.getAsyncError(comm_, &st);
+      st = async_error();
       if (st != ncclInProgress) break;
       if (Clock::now() > end) break;
       std::this_thread::sleep_for(std::chrono::microseconds(50));
@@ -314,6 +342,7 @@ class Comm {
     if (watching_.exchange(true)) return;
     watch_stop_ = false;
     int period = period_us < 50 ? 50 : period_us;
+    watch_exited_ = false;
     watch_ = std::thread([this, period, abort_on_error] {
       watch_id_ = std::this_thread::get_id();
       while (!watch_stop_.load()) {
@@ -325,14 +354,25 @@ class Comm {
         }
         std::this_thread::sleep_for(std::chrono::microseconds(period));
       }
+      watch_exited_ = true;
     });
   }
 
+  // Joins the watch thread, bounded by the abort deadline: a watch thread
+  // still inside an RCCL call past it is detached and the communicator is
+  // marked abort_stuck (the process is to be given up).
   void stop_watch() {
     watch_stop_ = true;
     if (watch_.joinable() && std::this_thread::get_id() != watch_.get_id()) {
       NoGil ng;
-      watch_.join();
+      auto limit = Clock::now() + std::chrono::duration<double>(abort_deadline_s_.load());
+      while (!watch_exited_.load() && Clock::now() < limit) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      if (watch_exited_.load()) {
+        watch_.join();
+      } else {
+        abort_stuck_.store(true);
+        watch_.detach();
+      }
     }
     watching_ = false;
   }
@@ -342,6 +382,8 @@ class Comm {
     return e != ncclSuccess && e != ncclInProgress;
   }
   bool aborted() const { return aborted_.load(); }
+  bool abort_stuck() const { return abort_stuck_.load(); }
+  double abort_ms() const { return abort_ms_; }
   int error_code() const { return err_.load(); }
   std::string error_text() {
     std::lock_guard<std::mutex> lk(msg_mu_);
@@ -368,6 +410,15 @@ class Comm {
     }
   };
 
+  // ncclCommGetAsyncError, serialized per communicator (see the file comment);
+  // caller holds a Use (or is destroy(), after every user left)
+  ncclResult_t async_error() {
+    std::lock_guard<std::mutex> lk(poll_mu_);
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t r = api().getAsyncError(comm_, &st);
+    return r != ncclSuccess ? r : st;
+  }
+
   void note(ncclResult_t st) {
     if (st == ncclSuccess || st == ncclInProgress) return;
     int expected = ncclSuccess;
@@ -392,14 +443,11 @@ class Comm {
 
   // caller holds a Use
   void wait_ready_inner(double timeout_s) {
-    const Api& a = api();
     auto end = Clock::now() + std::chrono::duration<double>(timeout_s);
     int spins = 0;
     while (true) {
       if (aborted_.load()) throw CommAborted("rccl_p2p: communicator aborted");
-      ncclResult_t st = ncclSuccess;
-      ncclResult_t r = a.getAsyncError(comm_, &st);
-      if (r != ncclSuccess) st = r;
+      ncclResult_t st = async_error();
       if (st == ncclSuccess && forced_err_.load() != ncclSuccess) st = (ncclResult_t)forced_err_.load();
       if (st == ncclSuccess) break;
       if (st != ncclInProgress) {
@@ -419,6 +467,11 @@ class Comm {
   int nranks_, rank_, device_;
   std::string name_;
   std::atomic<bool> aborted_{false};
+  std::atomic<bool> abort_stuck_{false};
+  std::atomic<double> abort_deadline_s_{3.0};
+  std::atomic<int> abort_stall_ms_{0};
+  double abort_ms_ = 0.0;
+  std::mutex poll_mu_;
   std::atomic<int> users_{0};
   std::atomic<int> err_{ncclSuccess};
   std::atomic<int> forced_err_{ncclSuccess};
@@ -427,6 +480,7 @@ class Comm {
   std::thread watch_;
   std::thread::id watch_id_;
   std::atomic<bool> watch_stop_{false};
+  std::atomic<bool> watch_exited_{true};
   std::atomic<bool> watching_{false};
   std::atomic<uint64_t> bytes_sent_{0}, bytes_recv_{0}, ops_{0};
   Clock::time_point t_init_;
@@ -499,6 +553,10 @@ PYBIND11_MODULE(_comm, m) {
       .def("start_watch", &Comm::start_watch, py::arg("period_us") = 1000, py::arg("abort_on_error") = true)
       .def("inject_async_error", &Comm::inject_async_error, py::arg("code") = (int)ncclRemoteError)
       .def("stop_watch", &Comm::stop_watch)
+      .def("set_abort_deadline", &Comm::set_abort_deadline, py::arg("seconds"))
+      .def("inject_abort_stall", &Comm::inject_abort_stall, py::arg("ms"))
+      .def_property_readonly("abort_stuck", &Comm::abort_stuck)
+      .def_property_readonly("abort_ms", &Comm::abort_ms)
       .def_property_readonly("failed", &Comm::failed)
       .def_property_readonly("aborted", &Comm::aborted)
       .def_property_readonly("error_code", &Comm::error_code)

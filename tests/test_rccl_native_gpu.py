@@ -168,23 +168,63 @@ def test_pair_links_world1_rejects_wrong_peer():
     G.abort()
 
 
-def test_recv_without_matching_send_fails_loudly_then_rebuild():
-    """A receive with no matching send (world=1: a self-receive without its send)
-    surfaces as a LinkError from the grouped enqueue (RCCL: "Trying to recv to
-    self without a matching send") instead of a hang, and a fresh communicator
-    then works.  Runs in its own process (tools/rccl_selftest.py unmatched): RCCL's
-    process-wide state after an invalid-usage group error is not ours to vouch
-    for, and no later test should inherit it."""
+def _selftest(mode: str, limit_s: float = 45.0):
+    """Runs tools/rccl_selftest.py <mode> in its own process; the child arms
+    faulthandler at `limit_s` (every thread's stack on stderr, then exit), and
+    its per-phase stamps are printed here whatever happens."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_selftest.py"), "unmatched"], cwd=root,
-                       env=env, capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", RCCL_SELFTEST_LIMIT_S=str(limit_s))
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_selftest.py"), mode], cwd=root,
+                           env=env, capture_output=True, text=True, timeout=limit_s + 30)
+    except subprocess.TimeoutExpired as e:
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        pytest.fail(f"rccl_selftest {mode} still running after {limit_s + 30} s; stderr:\n{err[-4000:]}")
+    wall = time.perf_counter() - t0
+    print(r.stderr[-4000:])
     recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert r.returncode == 0 and recs, r.stdout[-2000:] + r.stderr[-2000:]
+    return r, recs, wall
+
+
+def test_recv_without_matching_send_fails_loudly_then_rebuild():
+    """A receive with no matching send (world=1: a self-receive without its send)
+    surfaces as a LinkError (RCCL: "Trying to recv to self without a matching
+    send") instead of a hang; the communicator is aborted within the abort
+    deadline and a fresh communicator then works.  Runs in its own process
+    (tools/rccl_selftest.py unmatched): RCCL's process-wide state after an
+    invalid-usage group error is not ours to vouch for.  Should the abort
+    exceed its deadline, the child gives up like a worker (exit 75, no rebuild
+    in that process) and a fresh process must then run p2p cleanly -- the
+    supervisor's path (node.py `give_up`)."""
+    r, recs, wall = _selftest("unmatched")
+    assert recs, r.stdout[-2000:] + r.stderr[-2000:]
     rec = recs[-1]
     print(rec)
     assert "LinkError" in rec["reported"] and "without a matching send" in rec["reported"]
-    assert rec["ms"] < 100.0 and rec["rebuilt_ok"]
+    assert rec["ms"] < 100.0
+    if rec["abort_stuck"]:
+        assert r.returncode == 75
+        r2, recs2, _ = _selftest("self")
+        assert r2.returncode == 0 and recs2 and recs2[-1]["bitexact"], r2.stdout[-2000:] + r2.stderr[-2000:]
+    else:
+        assert r.returncode == 0 and rec["rebuilt_ok"], r.stdout[-2000:] + r.stderr[-2000:]
+        assert rec["abort_ms"] < 1e3 * 3.0
+
+
+def test_stuck_abort_gives_up_within_deadline():
+    """The deadline path of the bounded abort (csrc/comm/rccl_p2p.cpp `abort`):
+    an injected stall keeps ncclCommAbort from returning; abort() returns at the
+    1 s deadline with abort_stuck set, and the worker's give-up ends the process
+    with exit 75 right after -- never a hang."""
+    r, recs, wall = _selftest("stuck")
+    assert recs, r.stdout[-2000:] + r.stderr[-2000:]
+    rec = recs[-1]
+    print(rec, f"child wall {wall:.1f} s")
+    assert rec["abort_stuck"] and rec["bitexact_before"]
+    assert 900.0 <= rec["abort_ms"] < 1500.0
+    assert r.returncode == 75, (r.returncode, r.stderr[-2000:])
+    assert wall < 40.0

@@ -233,3 +233,39 @@ def test_link_error_report_triggers_replan_without_a_death(tiny):
         d.shutdown(stop_workers=True)
         for n in nodes:
             n.stop()
+
+
+def test_unrecoverable_worker_is_dropped_and_replanned(tiny):
+    """A stage whose communicator abort exceeded its deadline gives up
+    (node.py `give_up`): it publishes UNRECOVERABLE and stops.  The dispatcher
+    treats that like a dead process -- the chain is re-formed on the other
+    workers at once and the worker is not offered again until a fresh process
+    (new pid) registers under its id."""
+    d = DEFER(membership_port=0, result_port=0, worker_wait=20, ordered=True, batch=1, weight_codec="lz4",
+              min_workers=2, replicas=1)
+    d.membership_server.start()
+    nodes = _nodes(d, 3, "u")
+    try:
+        inq, outq = queue.Queue(), queue.Queue()
+        threading.Thread(target=d.run_defer, args=(tiny, ["conv3_block1_out"], inq, outq), daemon=True).start()
+        assert _wait(lambda: d.pipeline is not None)
+        e0 = d.pipeline.epoch
+        x = np.random.default_rng(7).standard_normal((1, 32, 32, 3)).astype(np.float32)
+        inq.put(x)
+        outq.get(timeout=60)
+        victim = d.pipeline.workers[1]
+        nd = next(n for n in nodes if n.node_id == victim)
+        t0 = time.time()
+        nd.give_up(nd.runtime, "injected: ncclCommAbort exceeded its deadline")
+        assert nd.unrecoverable is not None
+        assert _wait(lambda: d.pipeline is not None and d.pipeline.epoch > e0 and victim not in d.pipeline.workers,
+                     timeout=10)
+        assert time.time() - t0 < 1.5
+        assert victim not in d._get_available_workers()
+        assert any("unrecoverable" in e for _, e in d.events)
+        inq.put(x)
+        np.testing.assert_allclose(outq.get(timeout=60), tiny.predict(x, device="cpu"), rtol=1e-4, atol=1e-5)
+    finally:
+        d.shutdown(stop_workers=True)
+        for n in nodes:
+            n.stop()
