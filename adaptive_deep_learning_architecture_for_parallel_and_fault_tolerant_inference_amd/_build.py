@@ -5,6 +5,10 @@
                 that torch already loaded (same SONAME libamdhip64.so.7).
 * ``_runtime``  host C++17 runtime (framing transport, LZ4 frame codec,
                 zfp-style reversible codec, membership store), built with g++.
+* ``_comm``     native RCCL p2p layer (csrc/comm).
+* ``_cpu``      OpenMP NHWC fp32 ops of the CPU execution path (csrc/cpu),
+                built with g++ -fopenmp; hot loops carry AVX-512 / AVX2 /
+                baseline clones picked at load time.
 
 Objects go to ``build/``; the two ``.so`` files are written next to this
 file so they travel to the GPU box with the repo snapshot.  Rebuilds are
@@ -144,9 +148,29 @@ def build_comm(verbose: bool = False) -> Path:
     return lib
 
 
+def cpu_lib_path() -> Path:
+    return PKG_DIR / f"_cpu{EXT}"
+
+
+def build_cpu(verbose: bool = False) -> Path:
+    """``_cpu``: the native CPU execution path (runtime/cpu_executor.py)."""
+    src_dir = CSRC / "cpu"
+    srcs = sorted(src_dir.glob("*.cpp"))
+    lib = cpu_lib_path()
+    if not _newer(lib, srcs + list(src_dir.glob("*.h"))):
+        return lib
+    cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-shared", "-Wall", "-fopenmp", "-ffp-contract=fast",
+           "-fno-math-errno", f"-I{src_dir}"] + _py_includes() + [str(s) for s in srcs] + ["-o", str(lib)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    _run(cmd)
+    return lib
+
+
 def build_all(verbose: bool = False) -> None:
     build_runtime(verbose)
     build_comm(verbose)
+    build_cpu(verbose)
     build_kernels(verbose)
 
 

@@ -85,17 +85,18 @@ class Model:
                 precision: str = "fp32") -> np.ndarray:
         """Single-device inference (`test/local_infer.py:22`): our HIP runtime on
         a GPU (precision "bf16" or "fp32", the reference's Keras float32), the
-        fp32 oracle on CPU.  Inputs are NHWC float32 images."""
+        native OpenMP fp32 path on CPU.  Inputs are NHWC float32 images."""
         import torch
         x = np.asarray(x, np.float32)
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         if device == "cpu":
-            from ..ops.reference import ReferenceExecutor
+            # the native OpenMP path (runtime/cpu_executor.py); PyTorch is only the test oracle
+            from ..runtime.cpu_executor import CpuExecutor
             ex = self._executors.get("cpu")
             if ex is None:
-                ex = self._executors["cpu"] = ReferenceExecutor(self.graph, self.weights)
-            return ex(torch.from_numpy(x)).numpy()
+                ex = self._executors["cpu"] = CpuExecutor(self.graph, self.weights)
+            return ex(x)
         from ..runtime.executor import SliceExecutor
         b = batch or x.shape[0]
         key = (device, b, precision)

@@ -69,6 +69,9 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
     from ..graph.planner import plan_cuts
     from ..models.model import resnet
 
+    from ..utils.telemetry import PhaseStamps
+    st = PhaseStamps("fault_run", stream=log if log is not None else open(os.devnull, "w"))
+
     def say(msg):
         if log is not None:
             print(f"fault_run: {msg}", file=log, flush=True)
@@ -88,6 +91,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
               max_inflight=inflight, task_timeout=30, min_workers=workers, transport=transport,
               replicas=replicas, links=links, **dkw)
     d.membership_server.start()
+    st.stamp("dispatcher_up", port=d.membership_port)
     devs = worker_devices(devices, workers)
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
     import tempfile
@@ -101,6 +105,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
             [sys.executable, "-m", f"{PKG}.node", "--membership-port", str(d.membership_port), "--data-port", "0",
              "--config-port", "0", "--device", devs[i], "--id", wid, "--ttl", str(ttl), "--parent-pid", str(os.getpid())],
             env=env, stdout=subprocess.DEVNULL, stderr=logs[wid], start_new_session=True)
+    st.stamp("workers_spawned", devices=",".join(devs))
 
     def worker_tails(n=300):
         out = {}
@@ -142,13 +147,16 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
             raise RuntimeError(f"no pipeline formed within {ready_timeout:.0f} s; events {d.events[-3:]}; "
                                f"worker stderr {worker_tails()}")
         epoch_transport = d.epoch_transport(d.pipeline.records)
+        st.stamp("pipeline_up", stages=len(d.pipeline.workers), transport=epoch_transport)
         say(f"pipeline up after {time.time() - t_start:.1f} s: {len(d.pipeline.workers)} stages, "
             f"transport {epoch_transport}")
         while time.time() < deadline and sum(1 for v in d._resident.values() if v) < workers:
             time.sleep(0.1)
+        st.stamp("models_resident")
         time.sleep(d.prepare_delay + 1.5)   # prepare hints: next plans' slices built in the background
         threading.Thread(target=feeder, daemon=True).start()
         t0 = time.time()
+        st.stamp("feeding")
         while time.time() - t0 < duration:
             if t_kill is None and time.time() - t0 >= kill_at:
                 victim = d.pipeline.workers[len(d.pipeline.workers) // 2]
@@ -157,6 +165,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
                 else:
                     d.inject_fault(victim, "hang")
                 t_kill = time.time()
+                st.stamp(fault, victim=victim)
                 say(f"{fault} {victim} at t={t_kill - t0:.2f} s")
             try:
                 outq.get(timeout=0.1)
@@ -164,6 +173,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
             except queue.Empty:
                 pass
         stop.set()
+        st.stamp("window_done", results=got, recoveries=len(d.recoveries))
         # drain: every request sent must come back exactly once
         deadline = time.time() + 60
         while got < sent[0] - inq.qsize() and time.time() < deadline:
@@ -172,6 +182,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
                 got += 1
             except queue.Empty:
                 pass
+        st.stamp("drained", results=got, sent=sent[0])
     finally:
         stop.set()
         d.shutdown(stop_workers=True)
@@ -187,6 +198,7 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
                 pass
         for f in logs.values():
             f.close()
+        st.stamp("teardown")
     ts = np.array(d.completion_times)
     pre = ts[(ts > t0 + 1.0) & (ts < t_kill)] if t_kill else ts
     rate_pre = len(pre) / max(1e-9, (t_kill - t0 - 1.0)) * batch if t_kill else None
@@ -216,8 +228,25 @@ def run(workers: int = 4, devices: str = "cpu", model: str = "resnet_tiny", imag
         "detected_by": next((e for t, e in d.events if t_kill and t > t_kill), None),
         "events": [(round(t - (t0 or t_start), 3), e) for t, e in d.events],
         "wall_s": round(time.time() - t_start, 1),
+        "phases": dict(st.phases),
     }
+    want = expected_transport(transport, devs)
+    if want is not None and epoch_transport is not None and epoch_transport != want:
+        # one worker per GPU at transport "auto" must run its hops over RCCL p2p, not a fallback
+        out["ok"] = False
+        out["error"] = f"epoch transport {epoch_transport!r}, expected {want!r} with devices {devs}"
     return out
+
+
+def expected_transport(transport: str, devs: List[str]) -> Optional[str]:
+    """The stage -> stage transport DEFER must pick for these workers: "rccl" when
+    transport is "auto" and every worker has a GPU of its own (one process per
+    MI355X); None when the run does not pin it."""
+    if transport != "auto" or len(devs) < 2:
+        return None
+    if all(d.startswith("cuda") for d in devs) and len(set(devs)) == len(devs):
+        return "rccl"
+    return None
 
 
 def parse(argv=None):
@@ -255,6 +284,9 @@ def _terminate(signum, frame):
 
 def main(argv=None) -> int:
     signal.signal(signal.SIGTERM, _terminate)
+    from ..utils.telemetry import PhaseStamps
+    # bench.py's sub-run limit: a hang dumps every thread's stack 10 s before it
+    PhaseStamps.arm_faulthandler(float(os.environ.get("ADAPT_SUB_LIMIT_S", "0") or 0))
     a = parse(argv)
     out = run(workers=a.workers, devices=a.devices, model=a.model, image=a.image, batch=a.batch,
               duration=a.duration, kill_at=a.kill_at, ttl=a.ttl, inflight=a.inflight, transport=a.transport,

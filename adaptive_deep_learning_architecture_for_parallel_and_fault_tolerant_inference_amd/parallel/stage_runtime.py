@@ -217,10 +217,11 @@ class CollectiveStageRuntime:
         if self.gpu:
             self.compute.ex.forward(j)
         else:
-            feed = dict(zip(self.compute.inputs, self.in_bufs[j]))
+            # the native CPU path (runtime/cpu_executor.py) works on numpy views of the host buffers
+            feed = {n: t.numpy() for n, t in zip(self.compute.inputs, self.in_bufs[j])}
             y = self.compute.ex.run(feed, outputs=self.compute.outputs)
             for t, n in zip(self.out_bufs[j], self.compute.outputs):
-                t.copy_(y[n])
+                t.copy_(torch.from_numpy(np.ascontiguousarray(y[n])))
         self.meta_out[j].copy_(self.meta_in[j])
 
     def _emit_result(self, j: int) -> None:

@@ -51,10 +51,14 @@ def _phys(name: str, packed: Set[str]) -> str:
     return name + "#packed" if name in packed else name
 
 
-def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = False) -> List[Step]:
+def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = False,
+                 device_fusions: bool = True) -> List[Step]:
     """fp32=True: the fp32 execution path (csrc/kernels/conv_f32.hip) keeps the
     image as it is (no bf16 pack, so no stem fusion) and runs sibling convs as
-    separate GEMMs."""
+    separate GEMMs.  device_fusions=False (with fp32): only the per-layer
+    fusions (BN folding, conv epilogues, folded pads) -- the plan of the native
+    CPU path (runtime/cpu_executor.py), which has no stem / pair / merged
+    sibling kernels."""
     outputs = list(outputs or g.output_names)
     outset = set(outputs)
     cons = g.consumers()
@@ -264,7 +268,7 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
             done.add(n)
         elif L.op == "reshape":
             src_shape = g.layers[L.inputs[0]].out_shape
-            if src_shape[-1] != L.out_shape[-1] and (src_shape[-1] % 8 or L.out_shape[-1] % 8):
+            if device_fusions and src_shape[-1] != L.out_shape[-1] and (src_shape[-1] % 8 or L.out_shape[-1] % 8):
                 raise NotImplementedError(f"Reshape {src_shape} -> {L.out_shape} ({n}): channels are padded to 8")
             if n in outset:
                 steps.append(Step("copy", n, [R(L.inputs[0])], [n]))
@@ -289,7 +293,7 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
                     continue
             else:
                 steps.append(Step("copy", n, [R(L.inputs[0])], [n]))
-            if L.op == "flatten" and len(src_shape) == 3 and src_shape[-1] % 8:
+            if device_fusions and L.op == "flatten" and len(src_shape) == 3 and src_shape[-1] % 8:
                 raise NotImplementedError(f"Flatten of a {src_shape[-1]}-channel tensor ({n}): channels are padded to 8")
             done.add(n)
         elif L.op == "gap":
@@ -315,6 +319,8 @@ def compile_plan(g: Graph, outputs: Optional[List[str]] = None, fp32: bool = Fal
     missing = [o for o in outputs if o not in produced]
     if missing:
         raise RuntimeError(f"plan does not produce outputs {missing}")
+    if fp32 and not device_fusions:
+        return steps
     if fp32:
         if os.environ.get("ADAPT_NO_STEM", "0") != "1":
             steps = _fuse_stem_f32(g, steps, outset)

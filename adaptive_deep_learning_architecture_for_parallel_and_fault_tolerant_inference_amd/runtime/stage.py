@@ -1,8 +1,9 @@
 """Stage compute wrapper used by `Node`: one slice, one device, fixed batch.
 
 GPU (``cuda:N``): `SliceExecutor` (our HIP kernels, hipGraph-captured).
-CPU: the fp32 oracle (`ops.reference`) — the "CPU plumbing path" of
-BASELINE.json config 1 and of the CPU-only integration tests.
+CPU: `CpuExecutor` (runtime/cpu_executor.py: the compiled fp32 plan on the
+native OpenMP ops of csrc/cpu) — the CPU path of BASELINE.json config 1 and
+of the CPU-only integration tests.  PyTorch's own ops are not on either path.
 
 Host-side arrays in/out are numpy; bfloat16 tensors travel as uint16 bit
 patterns with a flag (numpy has no bf16).  Device-resident paths (RCCL links)
@@ -103,8 +104,8 @@ class StageCompute:
             if graph_capture:
                 self.ex.capture(mode=capture_mode)
         else:
-            from ..ops.reference import ReferenceExecutor
-            self.ex = ReferenceExecutor(g, weights, device="cpu")
+            from .cpu_executor import CpuExecutor
+            self.ex = CpuExecutor(g, weights, outputs=self.outputs)
 
     def _pad(self, t: torch.Tensor, count: int) -> torch.Tensor:
         if t.shape[0] == self.batch:
@@ -269,10 +270,13 @@ class StageCompute:
             if a.dtype == np.uint8 and self.preprocess != "none":
                 from ..ops.eltwise import preprocess_ref
                 a = preprocess_ref(a, self.preprocess)
-            t = to_torch(a, b, "cpu").float()
+            a = np.asarray(a)
+            if b:                                   # bf16 bit patterns from a GPU stage -> fp32
+                a = (np.ascontiguousarray(a).view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+            a = np.asarray(a, np.float32)
             true_c = self.g.layers[name].out_shape[-1] if self.g.layers[name].out_shape else None
-            if true_c and t.dim() == 4 and t.shape[-1] != true_c:
-                t = t[..., :true_c]
-            feed[name] = t
+            if true_c and a.ndim == 4 and a.shape[-1] != true_c:
+                a = a[..., :true_c]
+            feed[name] = np.ascontiguousarray(a)
         outs = self.ex.run(feed, outputs=self.outputs)
-        return [outs[o][:count].float().numpy() for o in self.outputs], [False] * len(self.outputs)
+        return [np.asarray(outs[o][:count], np.float32) for o in self.outputs], [False] * len(self.outputs)

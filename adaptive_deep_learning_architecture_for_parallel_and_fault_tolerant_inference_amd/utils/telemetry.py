@@ -194,3 +194,37 @@ def gpu_telemetry(index: int = 0) -> Dict[str, float]:
         return out
     except Exception:  # noqa: BLE001 - no amdsmi / no GPU / not permitted
         return {}
+
+
+class PhaseStamps:
+    """Per-phase progress stamps of a multi-process job (bench.py sub-runs,
+    parallel/fault_run.py): every `stamp` prints ``[<tag> +<ms>] <phase> k=v``
+    to stderr at once and keeps ``{phase: ms}`` for the job's JSON record, so a
+    run that hangs on an 8-GPU node leaves the phase it reached in its log.
+    `arm_faulthandler(limit_s)` additionally dumps every thread's stack 10 s
+    before the caller's time limit (and exits), naming where it stopped."""
+
+    def __init__(self, tag: str, stream=None):
+        import sys
+        import time
+        self.tag = tag
+        self.stream = stream if stream is not None else sys.stderr
+        self.t0 = time.perf_counter()
+        self.phases: Dict[str, float] = {}
+
+    def stamp(self, phase: str, **kw) -> float:
+        import time
+        ms = (time.perf_counter() - self.t0) * 1e3
+        self.phases[phase] = round(ms, 1)
+        extra = " ".join(f"{k}={v}" for k, v in kw.items())
+        print(f"[{self.tag} +{ms:9.1f} ms] {phase}" + (f" {extra}" if extra else ""), file=self.stream, flush=True)
+        return ms
+
+    @staticmethod
+    def arm_faulthandler(limit_s: float, margin_s: float = 10.0) -> Optional[float]:
+        """Dump all stacks to stderr `margin_s` before `limit_s` (no-op for limit <= margin)."""
+        import faulthandler
+        if not limit_s or limit_s <= margin_s:
+            return None
+        faulthandler.dump_traceback_later(limit_s - margin_s, exit=True)
+        return limit_s - margin_s

@@ -167,14 +167,20 @@ def _max_over_ranks(x: float, world: int) -> float:
     return t.item()
 
 
-def timed(job, steps: int, warmup: int, dev, world: int) -> float:
+def timed(job, steps: int, warmup: int, dev, world: int, stamps=None) -> float:
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize;
-    returns the slowest rank's seconds."""
+    returns the slowest rank's seconds.  `stamps` (PhaseStamps): the first
+    step (a pipeline's first p2p), the end of warmup and of the timed steps."""
     if hasattr(job, "set_total_steps"):
         job.set_total_steps(warmup + steps)
-    for _ in range(warmup):
+    for i in range(warmup):
         job.step()
+        if i == 0 and stamps is not None:
+            torch.cuda.synchronize(dev)
+            stamps.stamp("first_step")
     torch.cuda.synchronize(dev)
+    if stamps is not None:
+        stamps.stamp("warmup_done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -186,55 +192,100 @@ def timed(job, steps: int, warmup: int, dev, world: int) -> float:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    if stamps is not None:
+        stamps.stamp("timed_done", steps=steps)
     if hasattr(job, "finish"):
         job.finish()
     return _max_over_ranks(elapsed, world)
 
 
-def _p2p_rate(job, dev, world: int, backend: str, mib: int = 64, reps: int = 10):
-    """Stage 0 -> stage 1 rate on the pipeline's own link (bytes/s), or None."""
+def _p2p_rates(job, dev, world: int, mib: int = 64, reps: int = 10) -> dict:
+    """Every adjacent stage pair's rate on the pipeline's own links, all pairs at
+    once (as a pipeline drives them): each stage sends `reps` x `mib` MiB to its
+    next stage while receiving as much from its previous one, and the receiver's
+    time gives the pair's rate.  Returns {"a-b": bytes/s} (global ranks), the
+    same dict on every rank; host-staged (gloo) pipelines time the same
+    exchange through host copies."""
     n = mib << 20
-    buf = torch.empty(n, dtype=torch.uint8, device=dev)
+    sbuf = torch.empty(n, dtype=torch.uint8, device=dev)
+    rbuf = torch.empty(n, dtype=torch.uint8, device=dev)
     links = getattr(job, "links", None)
-    role = job.stage if job.replica == 0 and job.stage < 2 else None
+    nxt, prv = job.next, job.prev
     dt = 0.0
     for it in range(2):                                 # warm-up round, then the timed round
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
-        if role is not None:
-            w = None
+        if links is not None:
+            ws, wr = None, None
             for _ in range(reps):
-                if links is not None:
-                    w = links.isend([buf]) if role == 0 else links.irecv([buf])
-                elif role == 0:
-                    dist.send(buf.cpu(), job.next)
-                else:
-                    tmp = buf.cpu()
-                    dist.recv(tmp, job.prev)
-                    buf.copy_(tmp)
-            if w is not None:
-                w.wait_host(timeout_s=60)
+                if nxt is not None:
+                    ws = links.isend([sbuf])
+                if prv is not None:
+                    wr = links.irecv([rbuf])
+            if wr is not None:
+                wr.wait_host(timeout_s=60)
+            dt = time.perf_counter() - t0
+            if ws is not None:
+                ws.wait_host(timeout_s=60)
+        else:
+            hs, hr = sbuf.cpu(), torch.empty(n, dtype=torch.uint8)
+            for _ in range(reps):
+                reqs = []
+                if nxt is not None:
+                    reqs.append(dist.isend(hs, nxt))
+                if prv is not None:
+                    reqs.append(dist.irecv(hr, prv))
+                for r in reqs:
+                    r.wait()
+                if prv is not None:
+                    rbuf.copy_(hr)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
         torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0 if role is not None else 0.0
-    dt = _max_over_ranks(dt, world)
-    return n * reps / dt if dt > 0 else None
+    mine = (prv, dist.get_rank(), dt) if prv is not None else None
+    allp = [None] * world
+    dist.all_gather_object(allp, mine)
+    return {f"{a}-{b}": n * reps / t for (a, b, t) in (x for x in allp if x) if t > 0}
 
 
-def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, executor, part_at) -> dict:
-    """The reference's layer-partitioned chain over RCCL, verified against an unsliced forward."""
+def _stamps(rank: int):
+    from importlib import import_module
+    return import_module(f"{PKG}.utils.telemetry").PhaseStamps(f"bench r{rank}")
+
+
+def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, executor, part_at,
+           stamps=None) -> dict:
+    """The reference's layer-partitioned chain over RCCL, verified against an unsliced forward.
+    Per-phase stamps go to stderr (and the record's ``phases``): link init per pair, first step
+    (first p2p), warmup, timed, p2p rates, verification, teardown (``links_drained``)."""
     dtype = args.pp_dtype or args.dtype
+    st = stamps or _stamps(rank)
     t_build = time.perf_counter()
     job = runner.build_job(g, weights, mode="pp", world=world, rank=rank, device=dev, batch=args.batch,
                            part_at=part_at, graph=not args.no_graph, host_staged=(backend != "nccl"),
                            codec=args.codec, precision=dtype)
     build_s = time.perf_counter() - t_build
+    links = getattr(job, "links", None)
+    mine = {}
+    if links is not None:
+        for c in links.comms():
+            mine[c.name.rsplit("/link", 1)[-1]] = round(c._c.init_ms, 1)
+    st.stamp("build_job", stage=job.stage, build_s=round(build_s, 2), link_init_ms=mine or None)
     image = tuple(g.layers[g.input].out_shape)
     x = torch.randn((args.batch,) + image, generator=torch.Generator().manual_seed(4321)).to(dev)
     job.set_synthetic_input(x)
-    elapsed = timed(job, args.steps, args.warmup, dev, world)
+    elapsed = timed(job, args.steps, args.warmup, dev, world, stamps=st)
     value = job.images_per_step * args.steps / elapsed
-    rate = _p2p_rate(job, dev, world, backend)
+    rates = _p2p_rates(job, dev, world)
+    st.stamp("p2p_rates", pairs={k: round(v / 1e9, 1) for k, v in rates.items()})
+    rate = rates.get("0-1")
+    inits = [None] * world
+    dist.all_gather_object(inits, mine)
+    link_init = {}
+    for d_ in inits:
+        for k, v in (d_ or {}).items():
+            link_init[k] = max(link_init.get(k, 0.0), v)
     ok, rel, top1 = 1, None, None
     if job.next is None:                       # last stage: logits vs the unsliced model on its own GPU
         full = executor.SliceExecutor(g, weights, args.batch, device=dev, precision=dtype)
@@ -263,8 +314,11 @@ def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, e
     rec = make_pp_record(value, elapsed, args.steps, job.stages, job.part_at, dtype, min(oks) == 1,
                          last[1].item(), last[2].item(), rate / 1e9 if rate else None,
                          world if native else 0, "rccl-native" if native else backend)
+    st.stamp("verified", ok=min(oks) == 1)
     rec["model"] = args.model
     rec["build_s"] = round(build_s, 2)
+    rec["p2p_GBps_pairs"] = {k: round(v / 1e9, 2) for k, v in rates.items()}
+    rec["link_init_ms"] = link_init or None
     link = getattr(job, "link", None)
     if args.codec != "none":
         ratio = getattr(link, "ratio", None)
@@ -273,6 +327,8 @@ def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, e
         rec["codec_default"] = "none"          # DEFER(link_codec=...) default: xGMI links stay uncompressed
     if hasattr(job, "close"):
         rec["links_drained"] = bool(job.close())
+    st.stamp("teardown", links_drained=rec.get("links_drained"))
+    rec["phases"] = dict(st.phases)
     return rec
 
 
@@ -343,6 +399,7 @@ def run_subrun(name: str, kind: str, argv: list, nprocs: int, limit_s: float, la
     t0 = time.monotonic()
     print(f"bench: sub-run {name} ({label}): {nprocs} process(es), limit {limit_s:.0f} s", file=sys.stderr,
           flush=True)
+    os.environ["ADAPT_SUB_LIMIT_S"] = f"{limit_s:.1f}"         # children arm faulthandler from it
     try:
         if kind == "bench":
             rc = launch.launch_local(argv + ["--out", out], nprocs, script=os.path.abspath(__file__),
@@ -391,6 +448,9 @@ def sub_main(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    st = _stamps(rank)
+    # a hang on the 8-GPU node dumps every thread's stack 10 s before the parent's limit
+    st.arm_faulthandler(float(os.environ.get("ADAPT_SUB_LIMIT_S", "0") or 0))
     try:
         ndev = torch.cuda.device_count()
         dev_idx = local % max(1, ndev)
@@ -398,6 +458,7 @@ def sub_main(args) -> int:
         dev = torch.device("cuda", dev_idx)
         backend = "gloo" if (args.backend == "nccl" and world > ndev) else args.backend
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=150))
+        st.stamp("init_process_group", world=world, backend=backend)
         zoo = import_module(f"{PKG}.models.zoo")
         resnet = import_module(f"{PKG}.models.resnet")
         runner = import_module(f"{PKG}.parallel.runner")
@@ -405,7 +466,7 @@ def sub_main(args) -> int:
         g = zoo.build_model(args.model)
         weights = resnet.init_weights(g, seed=args.seed)
         part_at = [c for c in args.part_at.split(",") if c]
-        rec = run_pp(args, g, weights, world, rank, dev, backend, runner, executor, part_at)
+        rec = run_pp(args, g, weights, world, rank, dev, backend, runner, executor, part_at, stamps=st)
         if rank == 0 and args.out:
             with open(args.out + ".tmp", "w") as f:
                 json.dump(rec, f)

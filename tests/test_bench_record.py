@@ -188,3 +188,46 @@ def test_fault_subrun_through_the_launcher_on_cpu():
     assert rec["ok"] is True and rec["exactly_once"] is True, rec
     assert rec["workers"] == 2 and rec["devices"] == ["cpu", "cpu"] and rec["precision"] == "fp32"
     assert rec["epoch_transport"] == "tcp" and rec["hb_timeout"] == 0.25 and rec["victim"] == "w1"
+    # per-phase stamps of the fault run travel in its record (the 8-GPU node's first run must say where it was)
+    for ph in ("dispatcher_up", "workers_spawned", "pipeline_up", "feeding", "kill", "drained", "teardown"):
+        assert ph in rec["phases"], (ph, rec["phases"])
+    assert rec["phases"]["kill"] >= rec["phases"]["feeding"] >= rec["phases"]["pipeline_up"]
+
+
+def test_fault_run_expects_rccl_with_one_gpu_per_worker():
+    """`--devices each` on enough GPUs at transport "auto" must run the hops over
+    RCCL p2p; a tcp fallback there is recorded as a failure, not a success."""
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.parallel import fault_run
+    assert fault_run.expected_transport("auto", ["cuda:0", "cuda:1", "cuda:2"]) == "rccl"
+    assert fault_run.expected_transport("auto", ["cuda:0", "cuda:0"]) is None        # shared GPU: tcp links
+    assert fault_run.expected_transport("auto", ["cpu", "cpu"]) is None
+    assert fault_run.expected_transport("tcp", ["cuda:0", "cuda:1"]) is None
+    assert fault_run.expected_transport("auto", ["cuda:0"]) is None
+
+
+def test_phase_stamps_print_and_record(capsys):
+    from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.utils.telemetry import (
+        PhaseStamps)
+    import sys
+    st = PhaseStamps("bench r3", stream=sys.stderr)
+    st.stamp("build_job", stage=3, link_init_ms={"2-3": 41.5})
+    st.stamp("first_step")
+    err = capsys.readouterr().err.splitlines()
+    assert err[0].startswith("[bench r3 +") and "] build_job stage=3 link_init_ms={'2-3': 41.5}" in err[0]
+    assert list(st.phases) == ["build_job", "first_step"] and st.phases["first_step"] >= st.phases["build_job"]
+    assert PhaseStamps.arm_faulthandler(5.0) is None           # a limit inside the margin arms nothing
+
+
+def test_pp_record_carries_pair_rates_and_phases():
+    """The N > 1 pipeline record: rccl_ranks, the stage0 -> 1 rate, every pair's
+    rate, each pair's link init and the per-phase stamps (bench.py run_pp)."""
+    b = _bench()
+    pp = b.make_pp_record(1000.0, 1.0, 20, 4, ["a", "b", "c"], "fp32", True, 1e-6, 1.0, 120.0, 4, "rccl-native")
+    pp["p2p_GBps_pairs"] = {"0-1": 120.0, "1-2": 118.2, "2-3": 121.4}
+    pp["link_init_ms"] = {"0-1": 40.0, "1-2": 38.0, "2-3": 44.0}
+    pp["phases"] = {"init_process_group": 10.0, "build_job": 900.0, "first_step": 950.0, "teardown": 2000.0}
+    line = json.loads(json.dumps(pp))
+    assert line["rccl_ranks"] == 4 and line["p2p_GBps"] == 120.0 and len(line["p2p_GBps_pairs"]) == 3
+    src = open(b.__file__).read()
+    for key in ("p2p_GBps_pairs", "link_init_ms", '"phases"', "first_step", "arm_faulthandler", "ADAPT_SUB_LIMIT_S"):
+        assert key in src
