@@ -333,7 +333,7 @@ def run_pp(args, g, weights, world: int, rank: int, dev, backend: str, runner, e
 
 
 # ---------------------------------------------------------------- sub-runs
-SUB_LIMIT_S = {"pp": 180.0, "pp_r152": 200.0, "fault": 240.0}
+SUB_LIMIT_S = {"pp": 90.0, "pp_r152": 90.0, "fault": 240.0}   # N = 4 worst case: 420 s
 
 
 def plan_subruns(args, world: int, backend: str) -> list:

@@ -231,3 +231,19 @@ def test_pp_record_carries_pair_rates_and_phases():
     src = open(b.__file__).read()
     for key in ("p2p_GBps_pairs", "link_init_ms", '"phases"', "first_step", "arm_faulthandler", "ADAPT_SUB_LIMIT_S"):
         assert key in src
+
+
+def test_every_planned_subrun_gets_time_at_n4():
+    """Round 6's N=4 rehearsal skipped the plain pipeline sub-run ("budget spent"):
+    the later sub-runs' reserved limits exceeded the budget.  Every planned
+    sub-run now starts with at least 60 s even when the ones before it used
+    their whole limits."""
+    b = _bench()
+    a = b.parse([])
+    for world in (2, 4, 8):
+        plan = b.plan_subruns(a, world, "nccl")
+        left = a.sub_budget
+        for i in range(len(plan)):
+            lim = b.subrun_limit(plan, i, left)
+            assert lim >= 60.0, (world, plan[i][0], lim)
+            left -= lim
