@@ -109,6 +109,7 @@ class PackedConv:
     wino: Optional[torch.Tensor] = None   # fp32 3x3/s1/p1: Winograd-transformed weights (pack_wino_f32)
     pwf: Optional[torch.Tensor] = None    # fp32 1x1/s1: fragment-packed weights of pw_f32.hip (pack_pw_f32)
     wino4: Optional[torch.Tensor] = None  # fp32 3x3/s1/p1: Winograd F(4x4, 3x3) weights (wino4_pack_np)
+    wino4s: Optional[torch.Tensor] = None  # the same for the transform + GEMM pipeline (wino4s_pack_np)
 
     @property
     def K(self) -> int:
@@ -477,6 +478,8 @@ def f32_counter_elems(cfg: int, ksplit: int, B: int, H: int, W: int, OH: int, OW
         return f32s_tiles(cfg, B * OH * OW, N)
     if cfg in WINO4_F32_CFGS:
         return wino4_blocks(B, H, W, N)
+    if cfg in WINO4S_F32_CFGS:
+        return int(kernels().wino4s_blocks(cfg, B, H, W, N))
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         return wino_blocks(cfg, B, H, W, N)
     return f32_sk_plan(B * OH * OW, N, Kpad, cfg, -ksplit)[0]
@@ -587,6 +590,42 @@ def wino4_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
                                 .astype(np.float32))
 
 
+# fp32 Winograd F(4x4, 3x3) as transform + pure-MFMA GEMM (csrc/kernels/wino4s_f32.hip): id -> (WT, WN, PG, R,
+# order): a block of WT x WN waves (16 tiles x 16 output channels x 36 positions each), PG positions per LDS
+# ring stage, R ring slots, block order 0 = channel blocks fastest / 1 = tile blocks fastest.  ksplit >= 1
+# (C / 16 divisible by it; > 1 adds the split-K reduce launch).  Workspace: V (36 x 16-tile groups x C) then
+# the split-K partial outputs (wino4s_ws_elems).
+WINO4S_F32_CFGS = {220: (2, 2, 6, 4, 0), 221: (2, 2, 6, 3, 0), 222: (1, 2, 6, 4, 0), 223: (2, 4, 4, 4, 0),
+                   224: (2, 2, 6, 4, 1), 225: (2, 1, 6, 4, 0), 226: (1, 1, 9, 4, 0), 227: (2, 2, 4, 4, 0),
+                   228: (4, 2, 4, 4, 0), 229: (4, 2, 4, 4, 1)}
+
+
+def wino4s_supported(pc: "PackedConv") -> bool:
+    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (3, 3, 1, 1, 1, 1, 1)
+            and pc.cin % 16 == 0 and pc.cout % 16 == 0)
+
+
+def wino4s_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
+    """U_p = (G g G^T)_p in fp64, rounded once to fp32, in the fragment order of wino4s_f32.hip:
+    [N/16][C/16][36 positions][64 lanes][4], lane 16 g + n holding U_p[16 kc + 4 g + j][16 ng + n] at j."""
+    kh, kw, C, N = kernel_hwio.shape
+    if (kh, kw) != (3, 3) or C % 16 or N % 16:
+        raise ValueError(f"Winograd F(4x4) split packs 3x3 filters with C, N % 16 == 0 (got {kernel_hwio.shape})")
+    U = np.einsum("ai,ijcn,bj->abcn", WINO4_G, np.asarray(kernel_hwio, np.float64), WINO4_G)   # [6][6][C][N]
+    U = U.reshape(36, C // 16, 4, 4, N // 16, 16)                  # p, kc, g, j, ng, n
+    return np.ascontiguousarray(U.transpose(4, 1, 0, 2, 5, 3).reshape(N // 16, C // 16, 36, 64, 4)
+                                .astype(np.float32))
+
+
+def wino4s_ws_elems(B: int, H: int, W: int, C: int, N: int, ksplit: int) -> int:
+    return int(kernels().wino4s_ws_floats(B, H, W, C, N, ksplit))
+
+
+def wino4s_splits(C: int) -> list:
+    kc = C // 16
+    return [k for k in (1, 2, 4, 8) if kc % k == 0]
+
+
 def wino4_map_ok(B: int, H: int, W: int, cfg: int = 200) -> bool:
     """cfg 200 stages a tile group's 16 4x4 tiles as <= 8 tile-row segments in <= 19 KiB; cfg 210 a block's
     32 tiles in <= 43 KiB (tile rows of <= 70 tiles)."""
@@ -685,6 +724,9 @@ def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] 
                 and pw_f32_shape_ok(pc, PW_F32_CFGS[cfg]))
     if cfg in WINO4_F32_CFGS:
         return pc is not None and pc.wino4 is not None and wino4_supported(pc)
+    if cfg in WINO4S_F32_CFGS:
+        return (pc is not None and pc.wino4s is not None and wino4s_supported(pc)
+                and bool(kernels().wino4s_ok(cfg, cin, cout, 1)))
     if cfg in F32S_CFGS:
         return pc is not None and f32s_supported(pc)
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
@@ -712,6 +754,8 @@ def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, 
         pc.wino = torch.from_numpy(wino_pack_np(kernel_hwio)).to(device=device).contiguous()
     if wino4_supported(pc):
         pc.wino4 = torch.from_numpy(wino4_pack_np(kernel_hwio)).to(device=device).contiguous()
+    if wino4s_supported(pc):
+        pc.wino4s = torch.from_numpy(wino4s_pack_np(kernel_hwio)).to(device=device).contiguous()
     if pw_f32_packable(pc) and cout % 16 == 0:
         pc.pwf = torch.from_numpy(pack_pw_f32(kernel_hwio)).to(device=device).contiguous()
     return pc
@@ -843,6 +887,28 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         kernels().conv_f32_forward(ptr(x), ptr(pc.wino4), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W,
                                    C, OH, OW, N, 3, 3, 1, 1, 1, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),
                                    stream_handle(stream), ctr_ptr)
+        return out
+    if cfg in WINO4S_F32_CFGS:
+        # Winograd F(4x4, 3x3): input transform -> V (workspace), pure-MFMA GEMM with the output transform in
+        # its epilogue, and for ksplit > 1 the split-K reduce (bias / ReLU there)
+        ksplit = int(ksplit) or 1
+        if (not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 or residual is not None
+                or not kernels().wino4s_ok(cfg, C, N, ksplit)):
+            raise ValueError(f"Winograd F(4x4) split config {cfg}: 3x3/s1/p1 conv with wino4s weights, C % 16 == 0, "
+                             f"N % (16 x WN) == 0, no residual, |ksplit| in {wino4s_splits(C)} (fused: <= -2)")
+        need = wino4s_ws_elems(B, H, W, C, N, ksplit)
+        if workspace is None:
+            workspace = torch.empty(need, dtype=torch.float32, device=x.device)
+        if workspace.numel() < need or workspace.dtype != torch.float32:
+            raise ValueError(f"Winograd F(4x4) split needs an fp32 workspace of {need} elements")
+        ctr_ptr = 0
+        if ksplit < 0:                       # fused split-K fixup: one arrival counter per (tile, channel) block
+            nb = int(kernels().wino4s_blocks(cfg, B, H, W, N))
+            if counters is None or counters.numel() < nb or counters.dtype != torch.int32:
+                raise ValueError(f"Winograd F(4x4) fused split-K needs {nb} int32 arrival counters (zeroed)")
+            ctr_ptr = ptr(counters)
+        kernels().wino4s_forward(ptr(x), ptr(pc.wino4s), ptr(pc.bias), ptr(out), ptr(workspace), B, H, W, C, N,
+                                 int(relu), ksplit, int(cfg), stream_handle(stream), ctr_ptr)
         return out
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
         # ksplit > 1: slabs + splitk_reduce_f32; ksplit <= -2: -ksplit slabs, the last split of

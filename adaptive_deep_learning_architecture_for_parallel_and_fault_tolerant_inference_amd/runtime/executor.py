@@ -474,6 +474,11 @@ class SliceExecutor:
         need = ctr = 0
         for i, (cfg, ks) in self.cfg.items():
             if self.fp32:
+                if cfg in conv_ops.WINO4S_F32_CFGS:        # V and the split-K partials, whatever the split
+                    B, H, W, C, OH, OW, pc = self._conv_geom(i)
+                    need = max(need, conv_ops.wino4s_ws_elems(B, H, W, C, pc.cout, ks))
+                    ctr = max(ctr, conv_ops.f32_counter_elems(cfg, ks, B, H, W, OH, OW, pc.cout, pc.Kpad))
+                    continue
                 if ks != 1:
                     B, H, W, C, OH, OW, pc = self._conv_geom(i)
                     need = max(need, conv_ops.workspace_elems_f32(B * OH * OW, pc.cout, pc.Kpad, cfg, ks))

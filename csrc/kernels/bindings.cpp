@@ -203,6 +203,23 @@ PYBIND11_MODULE(_C, m) {
      py::arg("OH"), py::arg("OW"), py::arg("stride"), py::arg("out2") = 0, py::arg("n_split") = 0,
      py::arg("relu2") = 0);
   m.def("pw_f32_fpw", &adapt::pw_f32_fpw);
+  m.def("wino4s_forward", [](u64 x, u64 u, u64 bias, u64 out, u64 ws, int B, int H, int W, int C, int N, int relu,
+                             int ksplit, int cfg, u64 s, u64 counters) {
+    adapt::Wino4sParams p{};
+    p.x = P<const float>(x);
+    p.u = P<const float>(u);
+    p.bias = P<const float>(bias);
+    p.out = P<float>(out);
+    p.ws = P<float>(ws);
+    p.B = B; p.H = H; p.W = W; p.C = C; p.N = N; p.relu = relu; p.ksplit = ksplit;
+    p.counters = P<int>(counters);
+    check(adapt::wino4s_forward(p, cfg, S(s)), "wino4s_forward");
+  }, py::arg("x"), py::arg("u"), py::arg("bias"), py::arg("out"), py::arg("ws"), py::arg("B"), py::arg("H"),
+     py::arg("W"), py::arg("C"), py::arg("N"), py::arg("relu"), py::arg("ksplit"), py::arg("cfg"), py::arg("s"),
+     py::arg("counters") = 0);
+  m.def("wino4s_blocks", &adapt::wino4s_blocks);
+  m.def("wino4s_ok", &adapt::wino4s_ok);
+  m.def("wino4s_ws_floats", &adapt::wino4s_ws_floats);
   m.def("pw_f32_tail_plan", [](int M, int K, int N, int n_split, int bm) {
     int tail = 0, parts = 0;
     adapt::pw_f32_tail_plan(M, K, N, n_split, bm, &tail, &parts);

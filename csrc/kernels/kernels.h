@@ -181,6 +181,26 @@ bool conv_wino4_f32_ok(int C, int N);
 // tools/wino4_timeline.py: F(4x4) launches stamp 8 words per wave into buf while it is set
 void wino4_set_debug(unsigned long long* buf, int exp = 0);
 hipError_t conv_wino4_f32_launch(const WinoF32Params& p, hipStream_t s);
+
+// fp32 Winograd F(4x4, 3x3) as transform + pure-MFMA GEMM (wino4s_f32.hip, cfg ids 220-227): u = weights in
+// fragment order [N/16][C/16][36 positions][64 lanes][4] (ops/conv.py wino4s_pack_np); ws holds V (then the
+// split-K slabs), wino4s_ws_floats of it
+struct Wino4sParams {
+  const float* x;
+  float* v;           // set by wino4s_forward (= ws)
+  const float* u;
+  const float* bias;
+  float* out;
+  float* ws;
+  int B, H, W, C, N;
+  int relu, ksplit;   // ksplit <= -2: fused split-K fixup (counters)
+  int* counters;
+  int TH, TW, T, TG, KC, order;   // derived by wino4s_forward
+};
+bool wino4s_ok(int cfg, int C, int N, int ksplit);
+int wino4s_blocks(int cfg, int B, int H, int W, int N);
+size_t wino4s_ws_floats(int B, int H, int W, int C, int N, int ksplit);
+hipError_t wino4s_forward(const Wino4sParams& p, int cfg, hipStream_t s);
 unsigned long long* wino4_debug_buffer();
 int wino4_exp_flags();
 // producer / consumer F(4x4, 3x3) (conv_wino4pc_f32.hip, cfg 210): same weights and params; image pieces
