@@ -597,7 +597,9 @@ def wino4_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
 # the split-K partial outputs (wino4s_ws_elems).
 WINO4S_F32_CFGS = {220: (2, 2, 6, 4, 0), 221: (2, 2, 6, 3, 0), 222: (1, 2, 6, 4, 0), 223: (2, 4, 4, 4, 0),
                    224: (2, 2, 6, 4, 1), 225: (2, 1, 6, 4, 0), 226: (1, 1, 9, 4, 0), 227: (2, 2, 4, 4, 0),
-                   228: (4, 2, 4, 4, 0), 229: (4, 2, 4, 4, 1)}
+                   228: (4, 2, 4, 4, 0), 229: (4, 2, 4, 4, 1), 230: (2, 2, 12, 3, 0), 231: (2, 2, 12, 3, 1),
+                   # fragments of the next stage read under the current stage's MFMAs
+                   232: (2, 2, 4, 4, 0), 233: (2, 2, 6, 3, 0), 234: (2, 2, 6, 4, 0), 235: (2, 4, 4, 4, 0)}
 
 
 def wino4s_supported(pc: "PackedConv") -> bool:

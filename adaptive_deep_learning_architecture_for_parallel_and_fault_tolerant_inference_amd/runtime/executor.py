@@ -570,7 +570,7 @@ class SliceExecutor:
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
             for cfg in (list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.WINO4_F32_CFGS)
-                        + list(conv_ops.PW_F32_CFGS) + list(conv_ops.F32S_CFGS)):
+                        + list(conv_ops.WINO4S_F32_CFGS) + list(conv_ops.PW_F32_CFGS) + list(conv_ops.F32S_CFGS)):
                 if (not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc) or cfg in conv_ops.WINO_MEASURE_CFGS
                         or cfg in conv_ops.F32_UNTUNED):
                     continue
@@ -579,6 +579,10 @@ class SliceExecutor:
                         continue
                     sp = [k for k in conv_ops.wino4_splits(C) if k > 1]
                     tiles, kts, sks = conv_ops.wino4_blocks(B, H, W, N), C // 8, tuple(sp) + tuple(-k for k in sp)
+                elif cfg in conv_ops.WINO4S_F32_CFGS:       # F(4x4) transform + GEMM: split-K, fused fixup
+                    sp = [k for k in conv_ops.wino4s_splits(C) if k > 1]
+                    tiles, kts, sks = int(conv_ops.kernels().wino4s_blocks(cfg, B, H, W, N)), C // 16, \
+                        tuple(-k for k in sp)
                 elif cfg in conv_ops.PW_F32_CFGS:            # persistent pointwise: whole K, one launch
                     tiles, kts, sks = 0, 1, ()
                 elif cfg in conv_ops.F32S_CFGS:             # big-tile 1x1 GEMM: tiles, or stream-K over 256
@@ -606,7 +610,8 @@ class SliceExecutor:
                         continue
                     if -100 < ks < 0 and cfg in conv_ops.WINO_F32_CFGS and (kts // -ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):
                         continue
-                    nws = conv_ops.workspace_elems_f32(M, N, pc.Kpad, cfg, ks)
+                    nws = (conv_ops.wino4s_ws_elems(B, H, W, C, N, ks) if cfg in conv_ops.WINO4S_F32_CFGS
+                           else conv_ops.workspace_elems_f32(M, N, pc.Kpad, cfg, ks))
                     ws = torch.empty(nws, dtype=torch.float32, device=self.device) if nws else None
                     nctr = conv_ops.f32_counter_elems(cfg, ks, B, H, W, OH, OW, N, pc.Kpad)
                     ctr = torch.zeros(nctr, dtype=torch.int32, device=self.device) if nctr else None

@@ -28,6 +28,8 @@
 // equal share of the stage's LDS-DMA pieces R - 1 stages ahead.  One s_barrier per stage: after it, every
 // wave's pieces of this stage have landed (each waited for its own with a partial vmcnt first) and every
 // wave is done reading the previous stage, whose slot is then refilled.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace adapt {
@@ -59,15 +61,16 @@ __device__ __forceinline__ void w4s_vmcnt() {
 }
 
 // B^T of F(4x4, 3x3) on 6 values: rows [4 0 -5 0 1 0], [0 -4 -4 1 1 0], [0 4 -4 -1 1 0], [0 -2 -1 2 1 0],
-// [0 2 -1 -2 1 0], [0 4 0 -5 0 1]
-__device__ __forceinline__ void w4s_bt(float& d0, float& d1, float& d2, float& d3, float& d4, float& d5) {
-  const float s12 = d1 + d2, s34 = d3 + d4, m12 = d1 - d2, m43 = d4 - d3, m13 = d1 - d3, m42 = d4 - d2;
-  const float t0 = fmaf(4.f, d0, fmaf(-5.f, d2, d4));
-  const float t5 = fmaf(4.f, d1, fmaf(-5.f, d3, d5));
-  d1 = fmaf(-4.f, s12, s34);
-  d2 = fmaf(4.f, m12, m43);
-  d3 = fmaf(-2.f, m13, m42);
-  d4 = fmaf(2.f, m13, m42);
+// [0 2 -1 -2 1 0], [0 4 0 -5 0 1] (elementwise on T = float or a float vector)
+template <typename T>
+__device__ __forceinline__ void w4s_bt(T& d0, T& d1, T& d2, T& d3, T& d4, T& d5) {
+  const T s12 = d1 + d2, s34 = d3 + d4, m12 = d1 - d2, m43 = d4 - d3, m13 = d1 - d3, m42 = d4 - d2;
+  const T t0 = 4.f * d0 - 5.f * d2 + d4;
+  const T t5 = 4.f * d1 - 5.f * d3 + d5;
+  d1 = s34 - 4.f * s12;
+  d2 = 4.f * m12 + m43;
+  d3 = m42 - 2.f * m13;
+  d4 = 2.f * m13 + m42;
   d0 = t0;
   d5 = t5;
 }
@@ -83,50 +86,61 @@ __device__ __forceinline__ void w4s_at(float m0, float m1, float m2, float m3, f
 }
 
 // ---------------------------------------------------------------- 1. input transform
-// one block per (tile group, chunk) unit; thread 4 l + j: fragment lane l = 16 g + r (tile 16 tg + r) and
-// element j (channel 16 kc + 4 g + j), so the 36 stores of a block each write one contiguous KiB and every
-// pixel read is a 4-byte load whose 16 neighbours (g, j) fill a 64-B segment
+// One block of 256 threads per (tile group, chunk) unit and CPT channels per thread (CPT = 1, 2, 4; 4 / CPT
+// units per block): thread (l, jj) owns fragment lane l = 16 g + r (tile 16 tg + r) and elements
+// CPT jj .. CPT jj + CPT - 1 (channels 16 kc + 4 g + CPT jj + e).  Each of the 36 position stores of a unit is
+// one contiguous KiB; each pixel read is a CPT x 4-byte load whose lane neighbours fill a 64-B segment.
+// CPT trades load width (4: 16-B loads, 1/4 of the threads) against parallelism (1: 4x the waves, for the
+// small late-stage maps whose unit count alone would not fill the chip).
+template <int CPT>
 __global__ __launch_bounds__(256) void wino4s_in_kernel(Wino4sParams p) {
-  const int unit = blockIdx.x;
+  typedef float vec __attribute__((ext_vector_type(CPT)));
+  constexpr int TPU = 64 * 4 / CPT;                // threads per unit
+  const int unit = blockIdx.x * (256 / TPU) + threadIdx.x / TPU;
+  if (unit >= p.TG * p.KC) return;
+  const int tid = threadIdx.x % TPU;
   const int tg = unit / p.KC, kc = unit - tg * p.KC;
-  const int l = threadIdx.x >> 2, j = threadIdx.x & 3;
+  const int l = tid / (4 / CPT), jj = tid % (4 / CPT);
   const int r = l & 15, g = l >> 4;
   const int t = tg * 16 + r;
-  float d[6][6];
+  vec d[6][6];
+  const vec z = (vec)(0.f);
   if (t < p.T) {
     const int per = p.TH * p.TW;
     const int b = t / per, rem = t - b * per;
     const int th = rem / p.TW, tw = rem - th * p.TW;
     const int h0 = 4 * th - 1, w0 = 4 * tw - 1;
-    const float* xb = p.x + (size_t)b * p.H * p.W * p.C + kc * 16 + 4 * g + j;
+    const float* xb = p.x + (size_t)b * p.H * p.W * p.C + kc * 16 + 4 * g + CPT * jj;
 #pragma unroll
     for (int dy = 0; dy < 6; ++dy) {
       const int h = h0 + dy;
 #pragma unroll
       for (int dx = 0; dx < 6; ++dx) {
         const int w = w0 + dx;
-        d[dy][dx] = (h >= 0 && h < p.H && w >= 0 && w < p.W) ? xb[((size_t)h * p.W + w) * p.C] : 0.f;
+        d[dy][dx] = (h >= 0 && h < p.H && w >= 0 && w < p.W) ? *(const vec*)(xb + ((size_t)h * p.W + w) * p.C) : z;
       }
     }
   } else {
 #pragma unroll
     for (int dy = 0; dy < 6; ++dy)
 #pragma unroll
-      for (int dx = 0; dx < 6; ++dx) d[dy][dx] = 0.f;
+      for (int dx = 0; dx < 6; ++dx) d[dy][dx] = z;
   }
 #pragma unroll
   for (int dx = 0; dx < 6; ++dx) w4s_bt(d[0][dx], d[1][dx], d[2][dx], d[3][dx], d[4][dx], d[5][dx]);
 #pragma unroll
   for (int a = 0; a < 6; ++a) w4s_bt(d[a][0], d[a][1], d[a][2], d[a][3], d[a][4], d[a][5]);
-  float* vo = p.v + (size_t)unit * 36 * 256 + threadIdx.x;
+  vec* vo = (vec*)(p.v + (size_t)unit * 36 * 256) + tid;
 #pragma unroll
   for (int a = 0; a < 6; ++a)
 #pragma unroll
-    for (int b = 0; b < 6; ++b) vo[(a * 6 + b) * 256] = d[a][b];
+    for (int b = 0; b < 6; ++b) vo[(a * 6 + b) * TPU] = d[a][b];
 }
 
 // ---------------------------------------------------------------- 2. GEMM + output transform
-template <int WT, int WN, int PG, int R>
+// PIPE: the fragments of stage st + 1 are read (after its barrier) before the MFMAs of stage st are issued,
+// so the LDS read latency runs under the MFMA burst instead of in front of it (two fragment register sets)
+template <int WT, int WN, int PG, int R, bool PIPE>
 __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sParams p) {
   constexpr int NW = WT * WN;
   constexpr int NST = 36 / PG;                   // stages per 16-channel chunk
@@ -205,22 +219,61 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
 
   const char* const ra = smem + (wt * PG) * 1024 + lane * 16;
   const char* const rb = smem + (WT * PG + wn * PG) * 1024 + lane * 16;
-  for (int kcl = 0; kcl < KCs; ++kcl) {
+  auto wait_land = [&](int st) {        // this wave's pieces of stage st have landed, then every wave's
+    if (NS - 1 - st >= R - 2) w4s_vmcnt<(R - 2) * PPW>();
+    else w4s_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();       // every wave's pieces of st landed; st - 1 fully read
+    asm volatile("" ::: "memory");
+    if (st + R - 1 < NS) issue(st + R - 1);
+  };
+  auto read = [&](int st, f32x4v (&a)[PG], f32x4v (&b)[PG]) {
+    const int so = (st % R) * SLOT;
 #pragma unroll
-    for (int sg = 0; sg < NST; ++sg) {
-      const int st = kcl * NST + sg;
-      if (NS - 1 - st >= R - 2) w4s_vmcnt<(R - 2) * PPW>();
-      else w4s_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();               // every wave's pieces of st landed; st - 1 fully read
-      asm volatile("" ::: "memory");
-      if (st + R - 1 < NS) issue(st + R - 1);
-      const int so = (st % R) * SLOT;
+    for (int pp = 0; pp < PG; ++pp) {
+      a[pp] = *(const f32x4v*)(ra + so + pp * 1024);
+      b[pp] = *(const f32x4v*)(rb + so + pp * 1024);
+    }
+  };
+  // MFMAs step-major: consecutive MFMAs accumulate into different positions (a dependent 16x16x4 f32 MFMA
+  // waits 40 cycles, an independent one issues at 32)
+  auto mfmas = [&](int sg, const f32x4v (&a)[PG], const f32x4v (&b)[PG]) {
 #pragma unroll
-      for (int pp = 0; pp < PG; ++pp) {
-        const f32x4v a = *(const f32x4v*)(ra + so + pp * 1024);
-        const f32x4v b = *(const f32x4v*)(rb + so + pp * 1024);
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[sg * PG + pp] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc[sg * PG + pp], 0, 0, 0);
+      for (int pp = 0; pp < PG; ++pp)
+        acc[sg * PG + pp] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[pp][j], b[pp][j], acc[sg * PG + pp], 0, 0, 0);
+  };
+  if constexpr (!PIPE) {
+    for (int kcl = 0; kcl < KCs; ++kcl) {
+#pragma unroll
+      for (int sg = 0; sg < NST; ++sg) {
+        const int st = kcl * NST + sg;
+        wait_land(st);
+        f32x4v a[PG], b[PG];
+        read(st, a, b);
+        mfmas(sg, a, b);
+      }
+    }
+  } else {
+    f32x4v ca[PG], cb[PG];
+    wait_land(0);
+    read(0, ca, cb);
+    for (int kcl = 0; kcl < KCs; ++kcl) {
+#pragma unroll
+      for (int sg = 0; sg < NST; ++sg) {
+        const int st = kcl * NST + sg;
+        f32x4v na[PG], nb_[PG];
+        if (st + 1 < NS) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own reads of st done: its slot is refilled
+          wait_land(st + 1);                                      // after this barrier
+          read(st + 1, na, nb_);
+        }
+        mfmas(sg, ca, cb);
+#pragma unroll
+        for (int pp = 0; pp < PG; ++pp) {
+          ca[pp] = na[pp];
+          cb[pp] = nb_[pp];
+        }
       }
     }
   }
@@ -281,20 +334,40 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
     }
     __syncthreads();
     if (!*flag) return;
+    // the other splits' slabs, 2 float4 per split per round with every load of a round in flight at once
+    // (their latency is a cross-XCD round trip), then the sums in split order
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      f32x4v v = {0.f, 0.f, 0.f, 0.f};
-      for (int z = 0; z < S; ++z) {
-        if (z == s) {
-          v += (f32x4v){y[q >> 2][(q & 3) * 4], y[q >> 2][(q & 3) * 4 + 1], y[q >> 2][(q & 3) * 4 + 2],
-                        y[q >> 2][(q & 3) * 4 + 3]};
-        } else {
-          v += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                              wsr, lane_base + z * split_stride + q * 1024u, 0, 16));
+    for (int q0 = 0; q0 < 16; q0 += 2) {
+      f32x4v sl[7][2];
+#pragma unroll
+      for (int zz = 0; zz < 7; ++zz) {
+        const int z = zz < s ? zz : zz + 1;            // the splits other than this one, in order
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          sl[zz][k] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+          if (z < S)
+            sl[zz][k] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     wsr, lane_base + z * split_stride + (q0 + k) * 1024u, 0, 16));
         }
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[q >> 2][(q & 3) * 4 + e] = v[e];
+      for (int k = 0; k < 2; ++k) {
+        const int q = q0 + k;
+        const f32x4v mine = {y[q >> 2][(q & 3) * 4], y[q >> 2][(q & 3) * 4 + 1], y[q >> 2][(q & 3) * 4 + 2],
+                             y[q >> 2][(q & 3) * 4 + 3]};
+        // split order with this split's own partial at position s; every array index is a constant (a
+        // runtime index would put sl in scratch)
+        f32x4v v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int z = 0; z < 8; ++z) {
+          if (z >= S) break;
+          const f32x4v other = z < 7 ? sl[z < 7 ? z : 6][k] : (f32x4v){0.f, 0.f, 0.f, 0.f};
+          const f32x4v prev = z > 0 ? sl[z > 0 ? z - 1 : 0][k] : (f32x4v){0.f, 0.f, 0.f, 0.f};
+          v += z < s ? other : (z == s ? mine : prev);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[q >> 2][(q & 3) * 4 + e] = v[e];
+      }
     }
   }
   const float bv = p.bias[n];
@@ -363,14 +436,21 @@ bool w4s_cfg(int cfg, W4sCfg* c) {
     case 227: *c = {2, 2, 4, 4, 0}; return true;
     case 228: *c = {4, 2, 4, 4, 0}; return true;
     case 229: *c = {4, 2, 4, 4, 1}; return true;
+    case 230: *c = {2, 2, 12, 3, 0}; return true;
+    case 231: *c = {2, 2, 12, 3, 1}; return true;
+    case 232: *c = {2, 2, 4, 4, 0}; return true;     // 232-235: pipelined fragment reads (PIPE)
+    case 233: *c = {2, 2, 6, 3, 0}; return true;
+    case 234: *c = {2, 2, 6, 4, 0}; return true;
+    case 235: *c = {2, 4, 4, 4, 0}; return true;
   }
   return false;
 }
 
-template <int WT, int WN, int PG, int R>
+template <int WT, int WN, int PG, int R, bool PIPE = false>
 hipError_t launch_gemm(const Wino4sParams& p, hipStream_t s) {
   const int TBn = (p.TG + WT - 1) / WT, NBn = p.N / (16 * WN);
-  hipLaunchKernelGGL((wino4s_gemm_kernel<WT, WN, PG, R>), dim3(TBn * NBn * p.ksplit), dim3(WT * WN * 64), 0, s, p);
+  hipLaunchKernelGGL((wino4s_gemm_kernel<WT, WN, PG, R, PIPE>), dim3(TBn * NBn * p.ksplit), dim3(WT * WN * 64), 0,
+                     s, p);
   return hipGetLastError();
 }
 
@@ -381,7 +461,7 @@ hipError_t launch_gemm(const Wino4sParams& p, hipStream_t s) {
 bool wino4s_ok(int cfg, int C, int N, int ksplit) {
   W4sCfg c;
   const int ks = ksplit < 0 ? -ksplit : ksplit;
-  if (!w4s_cfg(cfg, &c) || C % 16 || N % (16 * c.wn) || ks < 1 || ksplit == -1) return false;
+  if (!w4s_cfg(cfg, &c) || C % 16 || N % (16 * c.wn) || ks < 1 || ks > 8 || ksplit == -1) return false;
   return (C / 16) % ks == 0;
 }
 
@@ -423,7 +503,13 @@ hipError_t wino4s_forward(const Wino4sParams& p_in, int cfg, hipStream_t s) {
   if (!p.ws) return hipErrorInvalidValue;
   p.v = p.ws;
   float* slabs = p.ws + vfl;
-  hipLaunchKernelGGL(wino4s_in_kernel, dim3(p.TG * p.KC), dim3(256), 0, s, p);
+  // channels per thread of the input transform: the widest loads that still give ~8 waves per CU
+  const long units = (long)p.TG * p.KC;
+  int cpt = units * 64 >= 2048L * 64 ? 4 : (units * 128 >= 2048L * 64 ? 2 : 1);
+  if (const char* e = getenv("ADAPT_W4S_CPT")) cpt = atoi(e);
+  if (cpt == 4) hipLaunchKernelGGL(wino4s_in_kernel<4>, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, s, p);
+  else if (cpt == 2) hipLaunchKernelGGL(wino4s_in_kernel<2>, dim3((unsigned)((units + 1) / 2)), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(wino4s_in_kernel<1>, dim3((unsigned)units), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   Wino4sParams q = p;
@@ -433,6 +519,11 @@ hipError_t wino4s_forward(const Wino4sParams& p_in, int cfg, hipStream_t s) {
     case 221: e = launch_gemm<2, 2, 6, 3>(q, s); break;
     case 227: e = launch_gemm<2, 2, 4, 4>(q, s); break;
     case 228: case 229: e = launch_gemm<4, 2, 4, 4>(q, s); break;
+    case 230: case 231: e = launch_gemm<2, 2, 12, 3>(q, s); break;
+    case 232: e = launch_gemm<2, 2, 4, 4, true>(q, s); break;
+    case 233: e = launch_gemm<2, 2, 6, 3, true>(q, s); break;
+    case 234: e = launch_gemm<2, 2, 6, 4, true>(q, s); break;
+    case 235: e = launch_gemm<2, 4, 4, 4, true>(q, s); break;
     case 222: e = launch_gemm<1, 2, 6, 4>(q, s); break;
     case 223: e = launch_gemm<2, 4, 4, 4>(q, s); break;
     case 225: e = launch_gemm<2, 1, 6, 4>(q, s); break;

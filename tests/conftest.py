@@ -29,7 +29,7 @@ def pytest_unconfigure(config):
     The test verdict is already decided; skipping interpreter teardown keeps the
     exit code equal to it."""
     status = _EXIT["status"]
-    if status is None:
+    if status is None or os.environ.get("ADAPT_TEST_NORMAL_EXIT") == "1":
         return
     try:
         import torch

@@ -139,6 +139,15 @@ def test_rccl_branch_over_loopback_links(fault):
             if wins:
                 print(f"rccl-branch {fault}: recovery-to-steady {wins[0]['end_ms']:.0f} ms "
                       f"(first 0.5 s window at >= 95 % of the new steady state)")
+            # where the time between ready and steady goes: completions per 100 ms from the fault on,
+            # and the events after ready (re-captures, prepare builds, late reports)
+            ts = np.array(d.completion_times)
+            bins = [int(np.count_nonzero((ts > t_fault + k * 0.1) & (ts <= t_fault + (k + 1) * 0.1)))
+                    for k in range(int((r["t_ready"] + 3.0 - t_fault) / 0.1))]
+            print(f"rccl-branch {fault}: completions per 100 ms from the fault: {bins}")
+            for t_ev, ev in d.events:
+                if r["t_ready"] + 0.05 < t_ev <= r["t_ready"] + 3.0:
+                    print(f"  +{(t_ev - t_fault) * 1e3:7.1f} ms  {ev}")
         stop.set()
         feed.join()
         if fault == "hang":
