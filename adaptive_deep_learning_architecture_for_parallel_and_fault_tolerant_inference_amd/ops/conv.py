@@ -108,8 +108,7 @@ class PackedConv:
     n_split: int = 0         # > 0: two sibling convs packed along N (outputs [0, n_split) and [n_split, cout))
     wino: Optional[torch.Tensor] = None   # fp32 3x3/s1/p1: Winograd-transformed weights (pack_wino_f32)
     pwf: Optional[torch.Tensor] = None    # fp32 1x1/s1: fragment-packed weights of pw_f32.hip (pack_pw_f32)
-    wino4: Optional[torch.Tensor] = None  # fp32 3x3/s1/p1: Winograd F(4x4, 3x3) weights (wino4_pack_np)
-    wino4s: Optional[torch.Tensor] = None  # the same for the transform + GEMM pipeline (wino4s_pack_np)
+    wino4s: Optional[torch.Tensor] = None  # fp32 3x3/s1/p1: Winograd F(4x4, 3x3) weights (wino4s_pack_np)
 
     @property
     def K(self) -> int:
@@ -439,8 +438,6 @@ def workspace_elems_f32(M: int, N: int, Kpad: int, cfg: int, ksplit: int) -> int
     if ksplit < 0:
         if cfg in F32S_CFGS:
             return f32s_ws_elems(cfg)
-        if cfg in WINO4_F32_CFGS:
-            return -ksplit * M * N
         if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
             return (4 if ksplit <= WINO_SK_BASE else -ksplit) * M * N    # stream-K: <= 4 partials per unit
         return f32_sk_plan(M, N, Kpad, cfg, -ksplit)[3]
@@ -476,8 +473,6 @@ def f32_counter_elems(cfg: int, ksplit: int, B: int, H: int, W: int, OH: int, OW
         return 0
     if cfg in F32S_CFGS:
         return f32s_tiles(cfg, B * OH * OW, N)
-    if cfg in WINO4_F32_CFGS:
-        return wino4_blocks(B, H, W, N)
     if cfg in WINO4S_F32_CFGS:
         return int(kernels().wino4s_blocks(cfg, B, H, W, N))
     if cfg in WINO_F32_CFGS or cfg in WINO_F32_ABLATE:
@@ -552,16 +547,6 @@ def wino_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(U.transpose(1, 4, 0, 2, 5, 3).reshape(C // 16, N // 16, 16, 64, 4).astype(np.float32))
 
 
-# fp32 Winograd F(4x4, 3x3) (csrc/kernels/conv_wino4_f32.hip, cfg ids >= 200): id -> description.  A block
-# is 32 tiles (two tile groups of 16 4x4 tiles) x 32 output channels; K walks 8-channel chunks; split-K
-# ksplit > 1 (slabs + splitk_reduce_f32) or <= -2 (fixup fused in the kernel), |ksplit| dividing the
-# chunks into an even number per split
-WINO4_F32_CFGS = {200: "F(4x4,3x3) wave pairs split by transform row, 1 wave per SIMD",
-                  210: "F(4x4,3x3) producer / consumer: waves 0-3 MFMA only (weights from L2), waves 4-7 "
-                       "image DMA + input transform (conv_wino4pc_f32.hip)"}
-# measured slower than 200 on every ResNet-50 shape (profiles/r5/wino4_attribution.md: the producers' fp32
-# VALU takes MFMA issue time from the consumers on the same SIMD); kept runnable and tested, never tuned
-WINO4_UNTUNED = frozenset((210,))
 # B^T (input), G (weights) and A^T (output) of F(4x4, 3x3), interpolation points 0, +-1, +-2 (Lavin & Gray 2016)
 WINO4_BT = np.array([[4, 0, -5, 0, 1, 0], [0, -4, -4, 1, 1, 0], [0, 4, -4, -1, 1, 0],
                      [0, -2, -1, 2, 1, 0], [0, 2, -1, -2, 1, 0], [0, 4, 0, -5, 0, 1]], np.float64)
@@ -569,25 +554,6 @@ WINO4_G = np.array([[1 / 4, 0, 0], [-1 / 6, -1 / 6, -1 / 6], [-1 / 6, 1 / 6, -1 
                     [1 / 24, 1 / 12, 1 / 6], [1 / 24, -1 / 12, 1 / 6], [0, 0, 1]], np.float64)
 WINO4_AT = np.array([[1, 1, 1, 1, 1, 0], [0, 1, -1, 2, -2, 0], [0, 1, 1, 4, 4, 0], [0, 1, -1, 8, -8, 1]],
                     np.float64)
-
-
-def wino4_supported(pc: "PackedConv") -> bool:
-    return ((pc.kh, pc.kw, pc.stride, pc.pad_t, pc.pad_l, pc.pad_b, pc.pad_r) == (3, 3, 1, 1, 1, 1, 1)
-            and pc.cin % 16 == 0 and pc.cout % 32 == 0)
-
-
-def wino4_pack_np(kernel_hwio: np.ndarray) -> np.ndarray:
-    """U_p = (G g G^T)_p of every (cin, cout) filter in fp64, rounded to fp32, in the fragment order
-    conv_wino4_f32.hip streams: [N/32][C/8][36 positions][64 lanes][2 fragments][2 steps], lane
-    l = 16 q + n' holding U_p[8 kc + 2 q + s][32 cg + 16 j + n'] at (j, s); p = 6 pa + pb."""
-    kh, kw, C, N = kernel_hwio.shape
-    if (kh, kw) != (3, 3) or C % 16 or N % 32:
-        raise ValueError(f"Winograd F(4x4,3x3) packs 3x3 filters with C % 16 == 0, N % 32 == 0 "
-                         f"(got {kernel_hwio.shape})")
-    U = np.einsum("ai,ijcn,bj->abcn", WINO4_G, np.asarray(kernel_hwio, np.float64), WINO4_G)   # [6][6][C][N]
-    U = U.reshape(36, C // 8, 4, 2, N // 32, 2, 16)          # p, kc, q, s, cg, j, n'
-    return np.ascontiguousarray(U.transpose(4, 1, 0, 2, 6, 5, 3).reshape(N // 32, C // 8, 36, 64, 2, 2)
-                                .astype(np.float32))
 
 
 # fp32 Winograd F(4x4, 3x3) as transform + pure-MFMA GEMM (csrc/kernels/wino4s_f32.hip): id -> (WT, WN, PG, R,
@@ -628,26 +594,6 @@ def wino4s_splits(C: int) -> list:
     return [k for k in (1, 2, 4, 8) if kc % k == 0]
 
 
-def wino4_map_ok(B: int, H: int, W: int, cfg: int = 200) -> bool:
-    """cfg 200 stages a tile group's 16 4x4 tiles as <= 8 tile-row segments in <= 19 KiB; cfg 210 a block's
-    32 tiles in <= 43 KiB (tile rows of <= 70 tiles)."""
-    if cfg == 210:
-        return kernels().conv_wino4pc_pieces(B, H, W) > 0
-    return kernels().conv_wino4_pieces(B, H, W)[0] > 0
-
-
-def wino4_blocks(B: int, H: int, W: int, N: int) -> int:
-    """Blocks per split of a Winograd F(4x4) launch: the fused split-K arrival counters it needs."""
-    T = B * ((H + 3) // 4) * ((W + 3) // 4)
-    return math.ceil(T / 32) * (N // 32)
-
-
-def wino4_splits(C: int) -> list:
-    """The split-K factors an F(4x4) launch of C input channels accepts (even chunk count per split)."""
-    kc = C // 8
-    return [k for k in (1, 2, 4, 8) if kc % k == 0 and (kc // k) % 2 == 0]
-
-
 # fp32 persistent pointwise configs (csrc/kernels/pw_f32.hip): id -> pixels per tile; 1x1 / s1 / p0 convs
 # with K in {64, 128, 256, 512} and N a multiple of the slice (FPW x 128 channels), ksplit 1
 # 122 / 123: the streaming variant (no LDS, no block barrier; bm codes 1 / 2: two waves per SIMD / the
@@ -676,7 +622,7 @@ F32S_TM = frozenset((307, 308, 309))     # owned-row tiles: ksplit 1 only
 # epilogue that nothing overlaps), so the isolated-timing tuner never picks them; cfg 307 on the stage-4 `_1`
 # convs wins in the whole-model A/B (tools/ab_cfg.py: 2.2738 -> 2.2648 ms): the owned-row tiles (F32S_TM) are
 # tuner candidates, which the fp32 tuner's in-graph refinement can pick
-F32_UNTUNED = WINO4_UNTUNED | (frozenset(F32S_CFGS) - F32S_TM)
+F32_UNTUNED = frozenset(F32S_CFGS) - F32S_TM
 
 
 def f32s_supported(pc: "PackedConv") -> bool:
@@ -724,8 +670,6 @@ def f32_cfg_supported(cfg: int, cin: int, cout: int, pc: Optional["PackedConv"] 
     if cfg in PW_F32_CFGS:
         return (pc is not None and pc.pwf is not None and PW_F32_CFGS[cfg] in PW_F32_BMS[pc.cin]
                 and pw_f32_shape_ok(pc, PW_F32_CFGS[cfg]))
-    if cfg in WINO4_F32_CFGS:
-        return pc is not None and pc.wino4 is not None and wino4_supported(pc)
     if cfg in WINO4S_F32_CFGS:
         return (pc is not None and pc.wino4s is not None and wino4s_supported(pc)
                 and bool(kernels().wino4s_ok(cfg, cin, cout, 1)))
@@ -754,8 +698,6 @@ def pack_conv_f32(kernel_hwio: np.ndarray, bias: np.ndarray, stride: int, pads, 
                     kh=kh, kw=kw, cin=cin, cout=cout, stride=stride, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
     if wino_supported(pc):
         pc.wino = torch.from_numpy(wino_pack_np(kernel_hwio)).to(device=device).contiguous()
-    if wino4_supported(pc):
-        pc.wino4 = torch.from_numpy(wino4_pack_np(kernel_hwio)).to(device=device).contiguous()
     if wino4s_supported(pc):
         pc.wino4s = torch.from_numpy(wino4s_pack_np(kernel_hwio)).to(device=device).contiguous()
     if pw_f32_packable(pc) and cout % 16 == 0:
@@ -861,34 +803,6 @@ def conv_forward_f32(x: torch.Tensor, pc: PackedConv, out: torch.Tensor, residua
         kernels().conv_f32_forward(ptr(x), ptr(pc.w), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W,
                                    C, OH, OW, N, 1, 1, pc.stride, 0, 0, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),
                                    stream_handle(stream), ctr_ptr, ptr(out2), int(ns), int(relu2))
-        return out
-    if cfg in WINO4_F32_CFGS:
-        # Winograd F(4x4, 3x3): ksplit > 1 slabs + splitk_reduce_f32, ksplit <= -2 fused fixup (counters)
-        ksplit = int(ksplit) or 1
-        if not f32_cfg_supported(cfg, C, N, pc) or (OH, OW) != (H, W) or x.dim() != 4 \
-                or not wino4_map_ok(B, H, W, cfg):
-            raise ValueError(f"Winograd F(4x4) config {cfg}: 3x3/s1/p1 conv with transformed weights, C % 16 == 0, "
-                             f"N % 32 == 0, map tiles at least 2 wide")
-        if abs(ksplit) not in wino4_splits(C) or ksplit == -1:
-            raise ValueError(f"Winograd F(4x4) split-K {ksplit}: |ksplit| in {wino4_splits(C)} (fused: <= -2)")
-        ws_ptr = ctr_ptr = 0
-        if ksplit != 1:
-            need = workspace_elems_f32(M, N, pc.Kpad, cfg, ksplit)
-            if need * 4 > 0x7fffffff:
-                raise ValueError("Winograd split-K slabs beyond 2 GiB")
-            if workspace is None:
-                workspace = torch.empty(need, dtype=torch.float32, device=x.device)
-            if workspace.numel() < need or workspace.dtype != torch.float32:
-                raise ValueError(f"Winograd split-K {ksplit} needs an fp32 workspace of {need} elements")
-            ws_ptr = ptr(workspace)
-        if ksplit < 0:
-            nb = wino4_blocks(B, H, W, N)
-            if counters is None or counters.numel() < nb or counters.dtype != torch.int32:
-                raise ValueError(f"Winograd fused split-K needs {nb} int32 arrival counters (zeroed)")
-            ctr_ptr = ptr(counters)
-        kernels().conv_f32_forward(ptr(x), ptr(pc.wino4), ptr(pc.bias), ptr(residual), ptr(out), ws_ptr, B, H, W,
-                                   C, OH, OW, N, 3, 3, 1, 1, 1, pc.K, pc.Kpad, int(relu), ksplit, int(cfg),
-                                   stream_handle(stream), ctr_ptr)
         return out
     if cfg in WINO4S_F32_CFGS:
         # Winograd F(4x4, 3x3): input transform -> V (workspace), pure-MFMA GEMM with the output transform in

@@ -569,17 +569,12 @@ class SliceExecutor:
             out2 = torch.empty(M * (N - ns), dtype=torch.float32, device=self.device) if ns else None
             ktiles = pc.Kpad // conv_ops.F32_BK
             best = None
-            for cfg in (list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.WINO4_F32_CFGS)
-                        + list(conv_ops.WINO4S_F32_CFGS) + list(conv_ops.PW_F32_CFGS) + list(conv_ops.F32S_CFGS)):
+            for cfg in (list(conv_ops.F32_TILES) + list(conv_ops.WINO_F32_CFGS) + list(conv_ops.WINO4S_F32_CFGS)
+                        + list(conv_ops.PW_F32_CFGS) + list(conv_ops.F32S_CFGS)):
                 if (not conv_ops.f32_cfg_supported(cfg, C, pc.cout, pc) or cfg in conv_ops.WINO_MEASURE_CFGS
                         or cfg in conv_ops.F32_UNTUNED):
                     continue
-                if cfg in conv_ops.WINO4_F32_CFGS:           # Winograd F(4x4,3x3): splits with even chunk counts
-                    if not conv_ops.wino4_map_ok(B, H, W, cfg):
-                        continue
-                    sp = [k for k in conv_ops.wino4_splits(C) if k > 1]
-                    tiles, kts, sks = conv_ops.wino4_blocks(B, H, W, N), C // 8, tuple(sp) + tuple(-k for k in sp)
-                elif cfg in conv_ops.WINO4S_F32_CFGS:       # F(4x4) transform + GEMM: split-K, fused fixup
+                if cfg in conv_ops.WINO4S_F32_CFGS:       # F(4x4) transform + GEMM: split-K, fused fixup
                     sp = [k for k in conv_ops.wino4s_splits(C) if k > 1]
                     tiles, kts, sks = int(conv_ops.kernels().wino4s_blocks(cfg, B, H, W, N)), C // 16, \
                         tuple(-k for k in sp)
@@ -600,8 +595,7 @@ class SliceExecutor:
                     tiles = math.ceil(M / bm) * math.ceil(N / bn)
                     kts = ktiles
                     sks = (-1, -2) if cfg in conv_ops.F32G_CFGS else ()
-                for ks in ((1,) if cfg in conv_ops.PW_F32_CFGS or cfg in conv_ops.WINO4_F32_CFGS
-                           or cfg in conv_ops.F32S_CFGS else
+                for ks in ((1,) if cfg in conv_ops.PW_F32_CFGS or cfg in conv_ops.F32S_CFGS else
                            (1, 2, 4, 8, 16) if cfg not in conv_ops.WINO_SK_CFGS else ()) + sks:
                     # split-K / stream-K only where the tiles alone leave CUs idle
                     if ks > 1 and (kts // ks < 2 or tiles >= 2 * conv_ops.NUM_CUS):

@@ -270,18 +270,12 @@ PYBIND11_MODULE(_C, m) {
     adapt::conv_wino_sk_plan(units, kc, mult, &g, &it, &smax);
     return py::make_tuple(g, it, smax);
   });
-  m.def("conv_wino4_pieces", [](int B, int H, int W) {
-    int align = 0;
-    const int pieces = adapt::conv_wino4_pieces(B, H, W, &align);
-    return py::make_tuple(pieces, align);
-  });
   m.def("conv_f32g_sk_plan", [](int tiles, int kt, int mult) {
     int g = 0, it = 0;
     adapt::conv_f32g_sk_plan(tiles, kt, mult, &g, &it);
     return std::make_pair(g, it);
   });
   m.def("wino_set_debug", [](u64 buf) { adapt::wino_set_debug(P<unsigned long long>(buf)); });
-  m.def("conv_wino4pc_pieces", &adapt::conv_wino4pc_pieces);
   m.def("gemm_f32s_cfg", [](int cfg) {
     int bm = 0, bn = 0;
     const bool ok = adapt::gemm_f32s_cfg(cfg, &bm, &bn);
@@ -289,8 +283,6 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_f32s_ws_elems", &adapt::gemm_f32s_ws_elems);
   m.def("gemm_f32s_set_debug", [](u64 buf, int exp) { adapt::gemm_f32s_set_debug(P<unsigned long long>(buf), exp); },
-        py::arg("buf"), py::arg("exp") = 0);
-  m.def("wino4_set_debug", [](u64 buf, int exp) { adapt::wino4_set_debug(P<unsigned long long>(buf), exp); },
         py::arg("buf"), py::arg("exp") = 0);
   m.def("pw_set_debug", [](u64 buf) { adapt::pw_set_debug(P<unsigned long long>(buf)); });
   m.def("stem_f32_forward", [](u64 x, u64 w, u64 bias, u64 out, int B, int H, int W, int C, int OH, int OW,

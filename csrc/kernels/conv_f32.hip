@@ -289,19 +289,7 @@ hipError_t conv_f32_forward(const float* x, const float* w, const float* bias, c
     ADAPT_F32_CFGS(X)
 #undef X
     default:
-      if (cfg >= 200) {
-        // Winograd F(4x4, 3x3) (conv_wino4_f32.hip): ksplit > 1 slabs + splitk_reduce_f32, ksplit <= -2 the
-        // fused fixup (needs ws + counters)
-        if (KH != 3 || KW != 3 || stride != 1 || pad_t != 1 || pad_l != 1 || OH != H || OW != W ||
-            p.ksplit == 0 || p.ksplit == -1 || p.ksplit < -64 || !conv_wino4_f32_ok(Cin, N) ||
-            (p.ksplit < 0 && (!ws || !counters)))
-          return hipErrorInvalidValue;
-        const int th = (H + 3) / 4, tw = (W + 3) / 4;
-        WinoF32Params wp{x, w, bias, res, out, ws, B, H, W, Cin, N, th, tw, B * th * tw, relu,
-                         p.ksplit < 0 ? -p.ksplit : p.ksplit, p.ksplit < 0 ? counters : nullptr, 0, 0};
-        e = cfg >= 210 ? conv_wino4pc_f32_launch(wp, s) : conv_wino4_f32_launch(wp, s);
-        break;
-      }
+      if (cfg >= 200) return hipErrorInvalidValue;   // F(4x4): wino4s_forward (its own entry point)
       if (cfg >= 80) {
         // Winograd F(2x2, 3x3) (conv_wino_f32.hip): w is the transformed, fragment-packed weight tensor
         // ksplit <= -100: stream-K over (-ksplit - 100) x 256 blocks; -100 < ksplit < 0: split -ksplit

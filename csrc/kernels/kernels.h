@@ -174,15 +174,9 @@ void conv_wino_sk_plan(int units, int kc, int mult, int* grid, int* iters, int* 
 bool conv_wino_f32_ok(int cfg, int C, int N);
 bool conv_wino_f32_cfg(int cfg, int* nw, int* fn);
 hipError_t conv_wino_f32_launch(const WinoF32Params& p, int cfg, hipStream_t s);
-// fp32 Winograd F(4x4, 3x3) (conv_wino4_f32.hip, cfg ids >= 200): u = transformed weights in fragment order
-// [N/32][C/8][36 positions][2 fragments][64 lanes][2] (ops/conv.py wino4_pack_np); TH / TW / T count 4x4 tiles
-int conv_wino4_pieces(int B, int H, int W, int* align = nullptr);
-bool conv_wino4_f32_ok(int C, int N);
-// tools/wino4_timeline.py: F(4x4) launches stamp 8 words per wave into buf while it is set
-void wino4_set_debug(unsigned long long* buf, int exp = 0);
-hipError_t conv_wino4_f32_launch(const WinoF32Params& p, hipStream_t s);
 
-// fp32 Winograd F(4x4, 3x3) as transform + pure-MFMA GEMM (wino4s_f32.hip, cfg ids 220-227): u = weights in
+// fp32 Winograd F(4x4, 3x3) as transform + pure-MFMA GEMM (wino4s_f32.hip, cfg ids 220-235; the fused
+// F(4x4) kernels of round 5, cfg 200 / 210, are retired to tools/experiments/): u = weights in
 // fragment order [N/16][C/16][36 positions][64 lanes][4] (ops/conv.py wino4s_pack_np); ws holds V (then the
 // split-K slabs), wino4s_ws_floats of it
 struct Wino4sParams {
@@ -201,12 +195,6 @@ bool wino4s_ok(int cfg, int C, int N, int ksplit);
 int wino4s_blocks(int cfg, int B, int H, int W, int N);
 size_t wino4s_ws_floats(int B, int H, int W, int C, int N, int ksplit);
 hipError_t wino4s_forward(const Wino4sParams& p, int cfg, hipStream_t s);
-unsigned long long* wino4_debug_buffer();
-int wino4_exp_flags();
-// producer / consumer F(4x4, 3x3) (conv_wino4pc_f32.hip, cfg 210): same weights and params; image pieces
-// (1 KiB) of the widest 32-tile block, 0 when the geometry is not supported
-int conv_wino4pc_pieces(int B, int H, int W);
-hipError_t conv_wino4pc_f32_launch(const WinoF32Params& p, hipStream_t s);
 // fp32 big-tile 1x1 GEMM (gemm_f32s.hip, cfg ids 300+): tile (BM, BN) per cfg; ksplit 1 (tiles) or -1 (stream-K
 // over 256 blocks: gemm_f32s_ws_elems floats of workspace, one zeroed int32 counter per tile)
 bool gemm_f32s_cfg(int cfg, int* bm, int* bn);

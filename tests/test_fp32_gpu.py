@@ -295,5 +295,9 @@ def test_resnet50_fp32_plan_uses_fused_stem_and_v2_convs():
     cfgs = {c for c, _ in ex.cfg.values()}
     assert cfgs & set(C.WINO_F32_CFGS), "no Winograd config on the fp32 3x3 convs"
     assert cfgs & set(C.PW_F32_CFGS), "no persistent pointwise config on the fp32 1x1 convs"
+    # every 3x3 runs a Winograd kernel: F(2x2) fused (stages 2-3) or the F(4x4) transform + GEMM pipeline
+    # (stages 4-5, wino4s_f32.hip, the whole-model A/B winner of round 6)
     wino3x3 = [i for i, st in enumerate(ex.steps) if st.kind == "conv" and st.p.get("kernel") == (3, 3)]
-    assert wino3x3 and all(ex.cfg[i][0] in C.WINO_F32_CFGS for i in wino3x3)
+    wino = set(C.WINO_F32_CFGS) | set(C.WINO4S_F32_CFGS)
+    assert wino3x3 and all(ex.cfg[i][0] in wino for i in wino3x3)
+    assert sum(1 for i in wino3x3 if ex.cfg[i][0] in C.WINO4S_F32_CFGS) == 9      # 6 stage-4 + 3 stage-5
