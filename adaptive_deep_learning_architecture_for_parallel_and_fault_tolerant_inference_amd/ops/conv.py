@@ -565,7 +565,8 @@ WINO4S_F32_CFGS = {220: (2, 2, 6, 4, 0), 221: (2, 2, 6, 3, 0), 222: (1, 2, 6, 4,
                    224: (2, 2, 6, 4, 1), 225: (2, 1, 6, 4, 0), 226: (1, 1, 9, 4, 0), 227: (2, 2, 4, 4, 0),
                    228: (4, 2, 4, 4, 0), 229: (4, 2, 4, 4, 1), 230: (2, 2, 12, 3, 0), 231: (2, 2, 12, 3, 1),
                    # fragments of the next stage read under the current stage's MFMAs
-                   232: (2, 2, 4, 4, 0), 233: (2, 2, 6, 3, 0), 234: (2, 2, 6, 4, 0), 235: (2, 4, 4, 4, 0)}
+                   232: (2, 2, 4, 4, 0), 233: (2, 2, 6, 3, 0), 234: (2, 2, 6, 4, 0), 235: (2, 4, 4, 4, 0),
+                   299: (2, 2, 6, 3, 0)}     # 299: 221 with per-wave stamps (tools/wino4s_timeline.py), never tuned
 
 
 def wino4s_supported(pc: "PackedConv") -> bool:
@@ -622,7 +623,7 @@ F32S_TM = frozenset((307, 308, 309))     # owned-row tiles: ksplit 1 only
 # epilogue that nothing overlaps), so the isolated-timing tuner never picks them; cfg 307 on the stage-4 `_1`
 # convs wins in the whole-model A/B (tools/ab_cfg.py: 2.2738 -> 2.2648 ms): the owned-row tiles (F32S_TM) are
 # tuner candidates, which the fp32 tuner's in-graph refinement can pick
-F32_UNTUNED = frozenset(F32S_CFGS) - F32S_TM
+F32_UNTUNED = (frozenset(F32S_CFGS) - F32S_TM) | {299}
 
 
 def f32s_supported(pc: "PackedConv") -> bool:

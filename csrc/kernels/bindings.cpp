@@ -218,6 +218,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("W"), py::arg("C"), py::arg("N"), py::arg("relu"), py::arg("ksplit"), py::arg("cfg"), py::arg("s"),
      py::arg("counters") = 0);
   m.def("wino4s_blocks", &adapt::wino4s_blocks);
+  m.def("wino4s_set_debug", [](u64 buf) { adapt::wino4s_set_debug(P<unsigned long long>(buf)); });
   m.def("wino4s_ok", &adapt::wino4s_ok);
   m.def("wino4s_ws_floats", &adapt::wino4s_ws_floats);
   m.def("pw_f32_tail_plan", [](int M, int K, int N, int n_split, int bm) {

@@ -190,7 +190,9 @@ struct Wino4sParams {
   int relu, ksplit;   // ksplit <= -2: fused split-K fixup (counters)
   int* counters;
   int TH, TW, T, TG, KC, order;   // derived by wino4s_forward
+  unsigned long long* dbg;        // cfg 299 (measurement): 8 words per wave
 };
+void wino4s_set_debug(unsigned long long* buf);
 bool wino4s_ok(int cfg, int C, int N, int ksplit);
 int wino4s_blocks(int cfg, int B, int H, int W, int N);
 size_t wino4s_ws_floats(int B, int H, int W, int C, int N, int ksplit);

@@ -140,7 +140,11 @@ __global__ __launch_bounds__(256) void wino4s_in_kernel(Wino4sParams p) {
 // ---------------------------------------------------------------- 2. GEMM + output transform
 // PIPE: the fragments of stage st + 1 are read (after its barrier) before the MFMAs of stage st are issued,
 // so the LDS read latency runs under the MFMA burst instead of in front of it (two fragment register sets)
-template <int WT, int WN, int PG, int R, bool PIPE>
+// STAMP (measurement only, tools/wino4s_timeline.py): lane 0 of every wave writes 8 words to p.dbg --
+// shader clock at start / first stage landed / K loop done / epilogue done, the summed clocks spent in the
+// per-stage land wait (vmcnt + barrier), the summed clocks from each barrier to the stage's last MFMA issue,
+// the stage count and HW_ID
+template <int WT, int WN, int PG, int R, bool PIPE, bool STAMP = false>
 __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sParams p) {
   constexpr int NW = WT * WN;
   constexpr int NST = 36 / PG;                   // stages per 16-channel chunk
@@ -219,11 +223,20 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
 
   const char* const ra = smem + (wt * PG) * 1024 + lane * 16;
   const char* const rb = smem + (WT * PG + wn * PG) * 1024 + lane * 16;
+  unsigned long long t_start = 0, t_first = 0, t_wait = 0, t_mfma = 0, t_mark = 0;
+  if constexpr (STAMP) t_start = __builtin_amdgcn_s_memtime();
   auto wait_land = [&](int st) {        // this wave's pieces of stage st have landed, then every wave's
+    unsigned long long t0 = 0;
+    if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
     if (NS - 1 - st >= R - 2) w4s_vmcnt<(R - 2) * PPW>();
     else w4s_vmcnt<0>();
     __builtin_amdgcn_s_barrier();       // every wave's pieces of st landed; st - 1 fully read
     asm volatile("" ::: "memory");
+    if constexpr (STAMP) {
+      t_mark = __builtin_amdgcn_s_memtime();
+      t_wait += t_mark - t0;
+      if (st == 0) t_first = t_mark;
+    }
     if (st + R - 1 < NS) issue(st + R - 1);
   };
   auto read = [&](int st, f32x4v (&a)[PG], f32x4v (&b)[PG]) {
@@ -252,6 +265,7 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
         f32x4v a[PG], b[PG];
         read(st, a, b);
         mfmas(sg, a, b);
+        if constexpr (STAMP) t_mfma += __builtin_amdgcn_s_memtime() - t_mark;
       }
     }
   } else {
@@ -278,6 +292,8 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
     }
   }
 
+  unsigned long long t_loop = 0;
+  if constexpr (STAMP) t_loop = __builtin_amdgcn_s_memtime();
   // ---- output transform on the accumulators: lane l holds M_p[tile 16 tg + 4 (l >> 4) + i][cout] at acc[p][i]
   const int tg = tb * WT + wt;
   const int n = (nb * WN + wn) * 16 + (lane & 15);
@@ -389,6 +405,21 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
       }
     }
   }
+  if constexpr (STAMP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && p.dbg) {
+      unsigned long long* d = p.dbg + (size_t)(blockIdx.x * NW + wave) * 8;
+      d[0] = t_start;
+      d[1] = t_first;
+      d[2] = t_loop;
+      d[3] = t_end;
+      d[4] = t_wait;
+      d[5] = t_mfma;
+      d[6] = (unsigned long long)NS;
+      d[7] = ((unsigned long long)__builtin_amdgcn_s_getreg(0x7814) << 32) | (unsigned)__builtin_amdgcn_s_getreg(0xF804);   // XCC_ID : HW_ID
+    }
+  }
 }
 
 // ---------------------------------------------------------------- 3. split-K reduce
@@ -442,15 +473,16 @@ bool w4s_cfg(int cfg, W4sCfg* c) {
     case 233: *c = {2, 2, 6, 3, 0}; return true;
     case 234: *c = {2, 2, 6, 4, 0}; return true;
     case 235: *c = {2, 4, 4, 4, 0}; return true;
+    case 299: *c = {2, 2, 6, 3, 0}; return true;     // 221 + per-wave stamps (measurement, wino4s_set_debug)
   }
   return false;
 }
 
-template <int WT, int WN, int PG, int R, bool PIPE = false>
+template <int WT, int WN, int PG, int R, bool PIPE = false, bool STAMP = false>
 hipError_t launch_gemm(const Wino4sParams& p, hipStream_t s) {
   const int TBn = (p.TG + WT - 1) / WT, NBn = p.N / (16 * WN);
-  hipLaunchKernelGGL((wino4s_gemm_kernel<WT, WN, PG, R, PIPE>), dim3(TBn * NBn * p.ksplit), dim3(WT * WN * 64), 0,
-                     s, p);
+  hipLaunchKernelGGL((wino4s_gemm_kernel<WT, WN, PG, R, PIPE, STAMP>), dim3(TBn * NBn * p.ksplit),
+                     dim3(WT * WN * 64), 0, s, p);
   return hipGetLastError();
 }
 
@@ -484,8 +516,12 @@ size_t wino4s_ws_floats(int B, int H, int W, int C, int N, int ksplit) {
   return v;
 }
 
+static unsigned long long* g_w4s_dbg = nullptr;
+void wino4s_set_debug(unsigned long long* buf) { g_w4s_dbg = buf; }
+
 hipError_t wino4s_forward(const Wino4sParams& p_in, int cfg, hipStream_t s) {
   Wino4sParams p = p_in;
+  p.dbg = g_w4s_dbg;
   W4sCfg c;
   if (!wino4s_ok(cfg, p.C, p.N, p.ksplit) || !w4s_cfg(cfg, &c)) return hipErrorInvalidValue;
   const bool fused = p.ksplit < 0;
@@ -524,6 +560,7 @@ hipError_t wino4s_forward(const Wino4sParams& p_in, int cfg, hipStream_t s) {
     case 233: e = launch_gemm<2, 2, 6, 3, true>(q, s); break;
     case 234: e = launch_gemm<2, 2, 6, 4, true>(q, s); break;
     case 235: e = launch_gemm<2, 4, 4, 4, true>(q, s); break;
+    case 299: e = launch_gemm<2, 2, 6, 3, false, true>(q, s); break;
     case 222: e = launch_gemm<1, 2, 6, 4>(q, s); break;
     case 223: e = launch_gemm<2, 4, 4, 4>(q, s); break;
     case 225: e = launch_gemm<2, 1, 6, 4>(q, s); break;
