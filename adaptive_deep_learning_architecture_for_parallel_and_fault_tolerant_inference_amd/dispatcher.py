@@ -208,6 +208,11 @@ class DEFER:
         self.max_replays = max_replays
         self.precision = precision                  # worker compute: "bf16" or "fp32" (reference float32)
         self.prepare_delay = 1.0                    # s after an epoch forms before `prepare` hints go out
+        # ... and after an epoch that REPLACES a replica (failure / join): building the next plans' slices
+        # (weight packing under the GIL, graph capture on the GPU) halved a just-recovered pipeline's
+        # throughput for ~1 s on the loopback run (profiles/r6/pytest_loopback_hang_r6k.log), and that dip,
+        # not the recovery, set its recovery-to-steady; the hints are for the NEXT failure, so they wait
+        self.recovery_prepare_delay = 4.0
         self.preprocess = preprocess
         self.links = links
         from .transport import shm as _shm
@@ -837,7 +842,8 @@ class DEFER:
             except OSError:
                 pass
         if self.resident or self.prepare:
-            t = threading.Thread(target=self._after_epoch, args=(p,), daemon=True, name="defer-after-epoch")
+            t = threading.Thread(target=self._after_epoch, args=(p, old is not None), daemon=True,
+                                 name="defer-after-epoch")
             t.start()
             self._bg.append(t)
 
@@ -933,7 +939,7 @@ class DEFER:
                     self._send_ctrl(w, {"cmd": "stop_epoch"})
             return p
 
-    def _after_epoch(self, p: Pipeline) -> None:
+    def _after_epoch(self, p: Pipeline, reformed: bool = False) -> None:
         """Background work after an epoch forms: push the whole model once to
         every worker that lacks it (so later re-plans are local slicing), then
         tell each member which slices the likely next plans need (`prepare`)."""
@@ -962,8 +968,12 @@ class DEFER:
             return
         # building the next plans' slices competes with the serving threads for CPU
         # and the GPU: let a freshly formed epoch reach its steady state first
-        if self._shutdown_event.wait(self.prepare_delay):
+        if self._shutdown_event.wait(self.recovery_prepare_delay if reformed else self.prepare_delay):
             return
+        with self._rep_lock:
+            current = self.replicas.get(p.replica)
+        if current is not p:
+            return                                  # replaced meanwhile: its hints would be stale
         k = len(p.workers)
         spares = [w for w in live if w not in self._assigned()]
         want = len(self._user_cuts) + 1

@@ -566,6 +566,7 @@ WINO4S_F32_CFGS = {220: (2, 2, 6, 4, 0), 221: (2, 2, 6, 3, 0), 222: (1, 2, 6, 4,
                    228: (4, 2, 4, 4, 0), 229: (4, 2, 4, 4, 1), 230: (2, 2, 12, 3, 0), 231: (2, 2, 12, 3, 1),
                    # fragments of the next stage read under the current stage's MFMAs
                    232: (2, 2, 4, 4, 0), 233: (2, 2, 6, 3, 0), 234: (2, 2, 6, 4, 0), 235: (2, 4, 4, 4, 0),
+                   236: (2, 2, 4, 5, 0), 237: (2, 2, 2, 8, 0),      # deeper rings, 2 blocks per CU
                    299: (2, 2, 6, 3, 0)}     # 299: 221 with per-wave stamps (tools/wino4s_timeline.py), never tuned
 
 

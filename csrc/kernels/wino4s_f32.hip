@@ -310,16 +310,62 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
       w4s_at(tr[0][j], tr[1][j], tr[2][j], tr[3][j], tr[4][j], tr[5][j], y[i][j], y[i][4 + j], y[i][8 + j],
              y[i][12 + j]);
   }
+  // Output rows leave through LDS: the block's (tile, pixel) rows of WN x 16 channels are staged, then stored
+  // as 16-B chunks, 8 lanes per 128-B row segment (direct from the fragments every store instruction would
+  // write 4 x 64 B with 4-B lanes: 12 us of the stage-2 epilogue, tools/wino4s_timeline.py)
+  constexpr bool STAGE = NW * 16 * 16 * 16 * 4 <= R * SLOT;
+  constexpr int CB = WN * 16, RP = CB + 4;
+  const int per = p.TH * p.TW;
+  auto store_rows = [&](auto&& rowp) {
+    if constexpr (STAGE) {
+      __syncthreads();                               // every wave is done with the ring
+      float* stg = (float*)smem;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          stg[((wt * 16 + 4 * (lane >> 4) + i) * 16 + u) * RP + wn * 16 + (lane & 15)] = y[i][u];
+      __syncthreads();
+      constexpr int C4 = CB / 4, TOTAL = WT * 16 * 16 * C4;
+      for (int e = threadIdx.x; e < TOTAL; e += NW * 64) {
+        const int c4 = e % C4, row = e / C4;
+        const int t = tb * WT * 16 + row / 16;
+        float* dst = rowp(t, row & 15);
+        if (dst) *(f32x4v*)(dst + nb * CB + c4 * 4) = *(const f32x4v*)(stg + row * RP + c4 * 4);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          float* dst = rowp(tg * 16 + 4 * (lane >> 4) + i, u);
+          if (dst) dst[n] = y[i][u];
+        }
+    }
+  };
+  auto write_stamps = [&]() {
+    if constexpr (STAMP) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+      if (lane == 0 && p.dbg) {
+        unsigned long long* d = p.dbg + (size_t)(blockIdx.x * NW + wave) * 8;
+        d[0] = t_start;
+        d[1] = t_first;
+        d[2] = t_loop;
+        d[3] = t_end;
+        d[4] = t_wait;
+        d[5] = t_mfma;
+        d[6] = (unsigned long long)NS;
+        d[7] = ((unsigned long long)__builtin_amdgcn_s_getreg(0x7814) << 32) | (unsigned)__builtin_amdgcn_s_getreg(0xF804);
+      }
+    }
+  };
   if (S > 1 && p.counters == nullptr) {
     // split-K through wino4s_reduce_kernel: partial outputs [split][tile][16 pixels][N]
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = tg * 16 + 4 * (lane >> 4) + i;
-      if (t >= p.T) continue;
-      float* o = p.ws + (((size_t)s * p.TG * 16 + t) * 16) * p.N + n;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) o[(size_t)u * p.N] = y[i][u];
-    }
+    store_rows([&](int t, int u) -> float* {
+      return t < p.T ? p.ws + (((size_t)s * p.TG * 16 + t) * 16 + u) * p.N : nullptr;
+    });
+    write_stamps();
     return;
   }
   if (S > 1) {
@@ -387,39 +433,18 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
     }
   }
   const float bv = p.bias[n];
-  const int per = p.TH * p.TW;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int t = tg * 16 + 4 * (lane >> 4) + i;
-    if (t >= p.T) continue;
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int u = 0; u < 16; ++u) y[i][u] = act_relu(y[i][u] + bv, p.relu);
+  store_rows([&](int t, int u) -> float* {
+    if (t >= p.T) return nullptr;
     const int b = t / per, rem = t - b * per;
     const int th = rem / p.TW, tw = rem - th * p.TW;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int h = 4 * th + u;
-      if (h >= p.H) continue;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int w = 4 * tw + v;
-        if (w < p.W) p.out[(((size_t)b * p.H + h) * p.W + w) * p.N + n] = act_relu(y[i][u * 4 + v] + bv, p.relu);
-      }
-    }
-  }
-  if constexpr (STAMP) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
-    if (lane == 0 && p.dbg) {
-      unsigned long long* d = p.dbg + (size_t)(blockIdx.x * NW + wave) * 8;
-      d[0] = t_start;
-      d[1] = t_first;
-      d[2] = t_loop;
-      d[3] = t_end;
-      d[4] = t_wait;
-      d[5] = t_mfma;
-      d[6] = (unsigned long long)NS;
-      d[7] = ((unsigned long long)__builtin_amdgcn_s_getreg(0x7814) << 32) | (unsigned)__builtin_amdgcn_s_getreg(0xF804);   // XCC_ID : HW_ID
-    }
-  }
+    const int h = 4 * th + (u >> 2), w = 4 * tw + (u & 3);
+    return h < p.H && w < p.W ? p.out + (((size_t)b * p.H + h) * p.W + w) * p.N : nullptr;
+  });
+  write_stamps();
 }
 
 // ---------------------------------------------------------------- 3. split-K reduce
@@ -473,6 +498,8 @@ bool w4s_cfg(int cfg, W4sCfg* c) {
     case 233: *c = {2, 2, 6, 3, 0}; return true;
     case 234: *c = {2, 2, 6, 4, 0}; return true;
     case 235: *c = {2, 4, 4, 4, 0}; return true;
+    case 236: *c = {2, 2, 4, 5, 0}; return true;     // 236-237: deeper rings at 2 blocks per CU
+    case 237: *c = {2, 2, 2, 8, 0}; return true;
     case 299: *c = {2, 2, 6, 3, 0}; return true;     // 221 + per-wave stamps (measurement, wino4s_set_debug)
   }
   return false;
@@ -560,6 +587,8 @@ hipError_t wino4s_forward(const Wino4sParams& p_in, int cfg, hipStream_t s) {
     case 233: e = launch_gemm<2, 2, 6, 3, true>(q, s); break;
     case 234: e = launch_gemm<2, 2, 6, 4, true>(q, s); break;
     case 235: e = launch_gemm<2, 4, 4, 4, true>(q, s); break;
+    case 236: e = launch_gemm<2, 2, 4, 5>(q, s); break;
+    case 237: e = launch_gemm<2, 2, 2, 8>(q, s); break;
     case 299: e = launch_gemm<2, 2, 6, 3, false, true>(q, s); break;
     case 222: e = launch_gemm<1, 2, 6, 4>(q, s); break;
     case 223: e = launch_gemm<2, 4, 4, 4>(q, s); break;

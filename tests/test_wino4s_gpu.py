@@ -51,7 +51,7 @@ def test_resnet_stage_shapes_whole_k(cfg):
         assert rel < 3e-5, (cfg, H, C, rel)
 
 
-@pytest.mark.parametrize("cfg", [220, 221, 223, 227, 228, 234])
+@pytest.mark.parametrize("cfg", [220, 221, 223, 227, 228, 234, 236, 237])
 @pytest.mark.parametrize("H,C,ks", [(56, 64, 1), (56, 64, 2), (56, 64, -2), (28, 128, 2), (28, 128, -2),
                                     (14, 256, 2), (14, 256, -4), (7, 512, 4), (7, 512, -8), (7, 512, -4)])
 def test_resnet_bs32_splits(cfg, H, C, ks):
