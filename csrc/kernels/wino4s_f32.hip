@@ -313,8 +313,8 @@ __global__ __launch_bounds__(WT * WN * 64, 2) void wino4s_gemm_kernel(Wino4sPara
   // Output rows leave through LDS: the block's (tile, pixel) rows of WN x 16 channels are staged, then stored
   // as 16-B chunks, 8 lanes per 128-B row segment (direct from the fragments every store instruction would
   // write 4 x 64 B with 4-B lanes: 12 us of the stage-2 epilogue, tools/wino4s_timeline.py)
-  constexpr bool STAGE = NW * 16 * 16 * 16 * 4 <= R * SLOT;
   constexpr int CB = WN * 16, RP = CB + 4;
+  constexpr bool STAGE = WT * 16 * 16 * RP * 4 <= R * SLOT;      // the padded rows fit in the ring
   const int per = p.TH * p.TW;
   auto store_rows = [&](auto&& rowp) {
     if constexpr (STAGE) {
