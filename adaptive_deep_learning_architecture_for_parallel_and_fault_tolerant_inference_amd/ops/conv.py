@@ -385,7 +385,8 @@ def pack_stem_f32(kernel_hwio: np.ndarray, bias: np.ndarray, pads, device) -> Pa
                       cin=3, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
 
 
-STEM_F32_VARIANT = 2  # stem_f32.hip: 0 = one unit at a time, 1 = software-pipelined units, 2 = whole rows (OW 112)
+STEM_F32_VARIANT = 2  # stem_f32.hip: 0 = one unit at a time, 1 = software-pipelined units, 2 = whole rows (OW 112),
+#                       5 = whole rows, horizontal pool in the conv epilogue, vertical pool beside the next step
 
 
 def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pad: int = 1,

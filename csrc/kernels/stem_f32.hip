@@ -153,15 +153,7 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   asm volatile("" : "+v"(b4));
   __syncthreads();
 
-  // V = 3: waves 4-7 (each SIMD's younger partner) at priority 1; V = 4: they start every step
-  // ~128 cycles late (MI355X_MICROARCH.md "two waves per SIMD", items 4 and 9)
-  if constexpr (V == 3) {
-    if (wave >= SF_WAVES / 2) __builtin_amdgcn_s_setprio(1);
-  }
   for (int t = t0; t < t1; ++t) {
-    if constexpr (V == 4) {
-      if (wave >= SF_WAVES / 2) __builtin_amdgcn_s_sleep(2);
-    }
     const bool first = t == t0;
     const int ra = first ? r_first : 2 * t - pool_pad + 1;     // first conv row this step computes
     const int nr = first ? 3 : 2;
@@ -340,6 +332,207 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_pool_f32_kernel(const float* __
   }
 }
 
+// ---------------------------------------------------------------- variant 5
+// Variant 2's whole-row conv with the max-pool split in two and taken off the step's critical path
+// (variant 2 spends a pool phase between two barriers every step, with no MFMA in flight on the CU):
+// * horizontal, in the conv epilogue: a tile's C^T fragment holds 16 consecutive pixels in the 16 lanes
+//   of a DPP row, so the 3-wide / stride-2 max at the even pixels is two row shifts (lane 0's left
+//   neighbour is lane 15 of the row's previous tile: a row rotate of that tile's result); the half-width
+//   row (56 x 64) goes to a 5-row LDS ring;
+// * vertical: pool row t - 1 (3 ring reads per output instead of 9) runs in step t next to step t's conv
+//   rows, so a step has one barrier and the MFMA bursts of consecutive steps are back to back.
+// The first step's extra conv row is split at tile 3 / 4 between the wave sets, the second set recomputing
+// tile 3 for its carry (4 tiles each).
+constexpr int SF_HP = SF_OWMAX / 2;          // half-width (horizontally pooled) row
+constexpr int SF_HR = 5;                     // ring rows: pool t - 1 reads 2t-3 .. 2t-1 while step t writes 2t, 2t+1
+
+namespace {
+__device__ __forceinline__ int hring_off(int slot, int pc, int chunk) {
+  return ((slot * SF_HP + pc) * 16 + (chunk ^ (pc & 15))) * 4;
+}
+
+// row shifts of the 16-lane DPP rows, per component.  Inline asm: through __builtin_amdgcn_update_dpp /
+// mov_dpp the compiler (ROCm 7.2) folded the four components' moves into the first one's and fed that to
+// all four maxes.  The s_nop 1 covers the VALU-write -> DPP-read hazard inside the statement.  Source lanes
+// outside the row leave the destination undefined; those lanes' results are never used.
+#define ADAPT_SF_DPP(NAME, CTRL)                                                                          \
+  __device__ __forceinline__ f32x4 NAME(f32x4 v) {                                                        \
+    f32x4 r;                                                                                              \
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %4 " CTRL " row_mask:0xf bank_mask:0xf\n\t"              \
+                 "v_mov_b32_dpp %1, %5 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                            \
+                 "v_mov_b32_dpp %2, %6 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                            \
+                 "v_mov_b32_dpp %3, %7 " CTRL " row_mask:0xf bank_mask:0xf"                                 \
+                 : "=&v"(r.x), "=&v"(r.y), "=&v"(r.z), "=&v"(r.w)                                        \
+                 : "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));                                               \
+    return r;                                                                                             \
+  }
+ADAPT_SF_DPP(sf_shl1, "row_shl:1")           // lane i <- lane i + 1 of its row of 16
+ADAPT_SF_DPP(sf_shr1, "row_shr:1")           // lane i <- lane i - 1
+ADAPT_SF_DPP(sf_ror1, "row_ror:1")           // lane i <- lane (i - 1) mod 16
+#undef ADAPT_SF_DPP
+
+__device__ __forceinline__ f32x4 max4(f32x4 a, f32x4 b) {
+  return (f32x4){fmaxf(a[0], b[0]), fmaxf(a[1], b[1]), fmaxf(a[2], b[2]), fmaxf(a[3], b[3])};
+}
+}  // namespace
+
+__global__ __launch_bounds__(SF_NT, 1) void stem_hpool_f32_kernel(const float* __restrict__ x,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ bias,
+                                                                  float* __restrict__ out, int H, int W, int OH,
+                                                                  int pad_t, int pad_l, int PH, int groups) {
+  __shared__ __attribute__((aligned(16))) float patch[SF_RING * SF_ROWLEN];     // 44 KiB
+  __shared__ __attribute__((aligned(16))) float hring[SF_HR * SF_HP * 64];      // 70 KiB
+  constexpr int PW = SF_HP;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = logical / groups;
+  const int t0 = (logical - img * groups) * SF_SP;
+  const int t1 = min(PH, t0 + SF_SP);
+  const float* xi = x + (size_t)img * H * W * 3;
+  const int c4row = W * 3 / 4;
+
+  for (int i = tid; i < SF_RING * SF_ROWLEN / 4; i += SF_NT) *(f32x4*)(patch + i * 4) = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  constexpr int MAXC = (11 * (SF_OWMAX * 2 * 3 / 4) + SF_NT - 1) / SF_NT;
+  auto get_rows = [&](f32x4 (&v)[MAXC], int ih_lo, int n) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int idx = tid + k * SF_NT;
+      const int r = idx / c4row, c = idx - r * c4row;
+      const int ih = ih_lo + r;
+      v[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (r < n && (unsigned)ih < (unsigned)H) v[k] = *(const f32x4*)(xi + (size_t)ih * W * 3 + c * 4);
+    }
+  };
+  auto put_rows = [&](const f32x4 (&v)[MAXC], int ih_lo, int n) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int idx = tid + k * SF_NT;
+      const int r = idx / c4row, c = idx - r * c4row;
+      if (r >= n) continue;
+      float* row = patch + ((ih_lo + r + 4 * SF_RING) % SF_RING) * SF_ROWLEN + SF_OFF + pad_l * 3 + c * 4;
+      row[0] = v[k][0]; row[1] = v[k][1]; row[2] = v[k][2]; row[3] = v[k][3];
+    }
+  };
+
+  const int r_first = 2 * t0 - 1;            // pool_pad 1: the first step's conv rows r_first .. r_first + 2
+  __syncthreads();
+  {
+    f32x4 v0[MAXC];
+    get_rows(v0, 2 * r_first - pad_t, 11);
+    put_rows(v0, 2 * r_first - pad_t, 11);
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ct = wave & 3;
+  f32x4 wa[SF_KH];
+#pragma unroll
+  for (int h = 0; h < SF_KH; ++h) wa[h] = *(const f32x4*)(w + (size_t)(ct * 16 + fr) * SF_K + h * 16 + fq * 4);
+  float wa9 = w[(size_t)(ct * 16 + fr) * SF_K + SF_KH * 16 + fq * 4];
+  f32x4 b4 = *(const f32x4*)(bias + ct * 16 + fq * 4);
+  int koff[SF_KH - 1];
+#pragma unroll
+  for (int h = 0; h < SF_KH - 1; ++h) {
+    const int p = 4 * h + fq;
+    koff[h] = (p / 5) * 0x10000 + 4 * (p % 5);
+  }
+  const bool g8 = fq == 3;
+  const int j8 = g8 ? 20 : 4 * (fq + 2);
+  const int r9 = fq < 3 ? 4 + fq : 4;
+#pragma unroll
+  for (int h = 0; h < SF_KH; ++h) asm volatile("" : "+v"(wa[h]));
+  asm volatile("" : "+v"(wa9));
+  asm volatile("" : "+v"(b4));
+  __syncthreads();
+
+  // conv row r, tiles cb .. ce - 1 (wave-uniform), for this wave's 16 channels; the half-width pooled
+  // values of tiles >= st go to the ring
+  auto conv_row = [&](int r, int cb, int ce, int st) {
+    if (r < 0 || r >= OH) return;
+    const int rb = 2 * r - pad_t + 4 * SF_RING;
+    const int pbase = SF_OFF + 6 * fr;
+    int ah[SF_KH - 1], ag[4];
+#pragma unroll
+    for (int h = 0; h < SF_KH - 1; ++h)
+      ah[h] = pbase + ((rb + (koff[h] >> 16)) & (SF_RING - 1)) * SF_ROWLEN + (koff[h] & 0xffff);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ag[e] = pbase + ((rb + (g8 ? e : 6)) & (SF_RING - 1)) * SF_ROWLEN + j8 + (g8 ? 0 : e);
+    const int a9 = pbase + ((rb + r9) & (SF_RING - 1)) * SF_ROWLEN + 20;
+    const int slot = r % SF_HR;
+    const bool even = (fr & 1) == 0;
+    f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < SF_TPR; ++c) {
+      if (c < cb || c >= ce) continue;
+      const int po = c * 96;
+      f32x4 acc0 = b4, acc1 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 bh[SF_KH - 1];
+#pragma unroll
+      for (int h = 0; h < SF_KH - 1; ++h) {
+        const f32x2 lo = *(const f32x2*)(patch + ah[h] + po), hi = *(const f32x2*)(patch + ah[h] + po + 2);
+        bh[h] = (f32x4){lo[0], lo[1], hi[0], hi[1]};
+      }
+      f32x4 b8;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b8[e] = patch[ag[e] + po];
+      const float b9 = patch[a9 + po];
+#pragma unroll
+      for (int h = 0; h < SF_KH - 1; h += 2)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], bh[h][e], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], bh[h + 1][e], acc1, 0, 0, 0);
+        }
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][0], b8[0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][1], b8[1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][2], b8[2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][3], b8[3], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa9, b9, acc0, 0, 0, 0);
+      f32x4 y = acc0 + acc1;
+      y = max4(y, (f32x4){0.f, 0.f, 0.f, 0.f});
+      // post-ReLU values are >= 0, so the pad column left of the image is the 0 the carry starts from
+      const f32x4 rgt = sf_shl1(y), lsh = sf_shr1(y), lro = sf_ror1(prev);
+      const f32x4 lft = fr == 0 ? lro : lsh;
+      if (c >= st && even) *(f32x4*)(hring + hring_off(slot, 8 * c + (fr >> 1), ct * 4 + fq)) = max4(max4(lft, y), rgt);
+      prev = y;
+    }
+  };
+  // pool row tp from the half-width rows 2tp - 1 .. 2tp + 1 (rows outside the map are skipped: the max of
+  // post-ReLU values starts from 0)
+  auto pool_row = [&](int tp) {
+    for (int idx = tid; idx < PW * 16; idx += SF_NT) {
+      const int ch = idx & 15, pc = idx >> 4;
+      f32x4 m = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const int oh = 2 * tp - 1 + dr;
+        if ((unsigned)oh < (unsigned)OH) m = max4(m, *(const f32x4*)(hring + hring_off(oh % SF_HR, pc, ch)));
+      }
+      *(f32x4*)(out + (((size_t)img * PH + tp) * PW + pc) * 64 + ch * 4) = m;
+    }
+  };
+
+  const int set = wave >> 2;                 // wave sets: 4 waves (one per channel tile) each
+  for (int t = t0; t < t1; ++t) {
+    const bool first = t == t0, more = t + 1 < t1;
+    const int nxt_lo = 2 * (2 * (t + 1)) - pad_t + 5;
+    f32x4 pv[MAXC];
+    if (more) get_rows(pv, nxt_lo, 4);
+    if (!first) pool_row(t - 1);
+    if (first) {
+      conv_row(r_first, set ? 3 : 0, set ? SF_TPR : 4, set ? 4 : 0);
+      conv_row(r_first + 1 + set, 0, SF_TPR, 0);
+    } else {
+      conv_row(2 * t + set, 0, SF_TPR, 0);
+    }
+    if (more) put_rows(pv, nxt_lo, 4);
+    sf_lds_barrier();
+  }
+  pool_row(t1 - 1);
+}
+
 // weights [64][160] fp32 in the slot order above (ops/conv.py pack_stem_f32); image NHWC, C = 3
 bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
   return C == 3 && W % 4 == 0 && OW >= 1 && OW <= SF_OWMAX && 2 * OW + 8 <= SF_COLS && pool_pad == 1;
@@ -348,11 +541,12 @@ bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                             int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s,
                             int variant) {
-  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 4 || B < 1 || PH < 1 || PW < 1 ||
-      PH > (OH + 2 * pool_pad - 3) / 2 + 1 || PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
+  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 5 || variant == 3 ||
+      variant == 4 || B < 1 || PH < 1 || PW < 1 || PH > (OH + 2 * pool_pad - 3) / 2 + 1 ||
+      PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
     return hipErrorInvalidValue;
   const int groups = (PH + SF_SP - 1) / SF_SP;
-  if (variant >= 2 && OW != 16 * SF_TPR) variant = 1;          // the row kernels take 112-wide rows only
+  if (variant >= 2 && (OW != 16 * SF_TPR || (variant == 5 && PW != SF_HP))) variant = 1;   // 112-wide rows only
   if (variant == 0)
     hipLaunchKernelGGL(stem_pool_f32_kernel<0>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
@@ -362,12 +556,9 @@ hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, f
   else if (variant == 2)
     hipLaunchKernelGGL(stem_pool_f32_kernel<2>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
-  else if (variant == 3)
-    hipLaunchKernelGGL(stem_pool_f32_kernel<3>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
-                       pad_t, pad_l, PH, PW, pool_pad, groups);
   else
-    hipLaunchKernelGGL(stem_pool_f32_kernel<4>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
-                       pad_t, pad_l, PH, PW, pool_pad, groups);
+    hipLaunchKernelGGL(stem_hpool_f32_kernel, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, pad_t,
+                       pad_l, PH, groups);
   return hipGetLastError();
 }
 

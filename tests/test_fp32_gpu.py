@@ -258,7 +258,7 @@ def test_other_families_fp32_logits_match_oracle(name):
     assert torch.isfinite(probs).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 5])
 @pytest.mark.parametrize("B,H", [(2, 224), (1, 64), (3, 112)])
 def test_stem_f32_fused_matches_fp64(B, H, variant):
     """csrc/kernels/stem_f32.hip: 7x7/s2 conv (+bias, ReLU) + 3x3/s2 max-pool in one launch vs a float64 oracle."""
@@ -300,4 +300,4 @@ def test_resnet50_fp32_plan_uses_fused_stem_and_v2_convs():
     wino3x3 = [i for i, st in enumerate(ex.steps) if st.kind == "conv" and st.p.get("kernel") == (3, 3)]
     wino = set(C.WINO_F32_CFGS) | set(C.WINO4S_F32_CFGS)
     assert wino3x3 and all(ex.cfg[i][0] in wino for i in wino3x3)
-    assert sum(1 for i in wino3x3 if ex.cfg[i][0] in C.WINO4S_F32_CFGS) == 9      # 6 stage-4 + 3 stage-5
+    assert sum(1 for i in wino3x3 if ex.cfg[i][0] in C.WINO4S_F32_CFGS) == 12     # 3 stage-2 + 6 stage-4 + 3 stage-5
