@@ -50,11 +50,6 @@ def main():
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         ex = SliceExecutor(g, w, a.batch, precision=a.precision)
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
         if env:
             print(f"{variant}: built with {env}, {len(ex.steps)} steps")
         if variant != "tuned":
@@ -72,7 +67,12 @@ def main():
                                     if ex.input_buf(g.input).shape[-1] == x.shape[-1] else
                                     torch.nn.functional.pad(x, (0, ex.input_buf(g.input).shape[-1] - x.shape[-1]))
                                     .to(ex.input_buf(g.input).dtype))
-        ex.capture()
+        ex.capture()                     # launch-time switches (env read by the host launchers) land in the graph
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         exs[variant] = ex
     outs = {}
     for v, ex in exs.items():
