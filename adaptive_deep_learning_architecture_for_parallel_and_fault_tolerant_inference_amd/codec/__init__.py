@@ -39,6 +39,37 @@ BF16 = 9          # flag value: payload is bfloat16 (numpy has no bf16; carried 
 _DT_CODE = {np.dtype(v): k for k, v in DTYPES.items()}
 
 
+def zfp_shape(shape) -> Tuple[int, ...]:
+    """The 1-4 dimensional array zfp codes for a tensor of `shape`: adjacent axes
+    folded so that the 4^d blocks need the least edge padding (ties: the most
+    axes, then the innermost split).  Padded blocks are coded as real data, so
+    NHWC maps of 7x7 or 14x14 kept as 4-D grew by (8/7)^2 or (16/14)^2 and the
+    codec expanded them (x0.75, profiles/r5/codec_fp32_r50_bs32.txt); (B*H*W, C)
+    or (B, H*W, C) have no padding there.  The container records this shape, and
+    both ends of a wire derive it from the message shape."""
+    shape = tuple(int(v) for v in shape)
+    if len(shape) == 0:
+        return (1,)
+    n = len(shape)
+    best = None
+    for mask in range(1 << (n - 1)):                  # bit i set: a split after axis i
+        if bin(mask).count("1") > 3:
+            continue
+        dims, cur = [], 1
+        for i, v in enumerate(shape):
+            cur *= v
+            if i == n - 1 or mask >> i & 1:
+                dims.append(cur)
+                cur = 1
+        padded = 1
+        for v in dims:
+            padded *= (v + 3) // 4 * 4
+        key = (padded, -len(dims), -mask)
+        if best is None or key < best[0]:
+            best = (key, tuple(dims))
+    return best[1]
+
+
 def _header(codec: int, dtype_code: int, shape: Tuple[int, ...]) -> bytes:
     return struct.pack(f"<BBBB{len(shape)}Q", codec, dtype_code, len(shape), 0, *shape)
 
@@ -71,10 +102,7 @@ def encode_parts(arr: np.ndarray, codec: str = "zfp+lz4", bf16: bool = False, th
         c = 1                               # zfp is float32/float64 only
     if c == 4 and arr.dtype.itemsize not in (2, 4):
         c = 1                               # zvc works on 2- or 4-byte elements
-    if c in (2, 3) and (arr.ndim > 4 or arr.ndim == 0):
-        arr_z = arr.reshape(-1) if arr.ndim == 0 else arr.reshape((-1,) + arr.shape[-3:])
-    else:
-        arr_z = arr
+    arr_z = arr.reshape(zfp_shape(arr.shape)) if c in (2, 3) else arr
     raw = arr.reshape(-1).view(np.uint8) if arr.size else np.zeros(0, np.uint8)
     if c == 0:
         payload = memoryview(raw)

@@ -20,15 +20,7 @@ import torch
 from ..ops._lib import kernels
 
 
-def zfp_shape(shape: Sequence[int]) -> tuple:
-    """zfp codes 1-4 dimensions: higher-rank tensors fold their leading axes
-    (the host codec does the same, codec/__init__.py)."""
-    shape = tuple(int(v) for v in shape)
-    if len(shape) == 0:
-        return (1,)
-    if len(shape) > 4:
-        return (int(np.prod(shape[:-3])),) + shape[-3:]
-    return shape
+from . import zfp_shape  # noqa: E402  (shared with the host codec: the same folding at both ends)
 
 
 def header(shape: Sequence[int]) -> bytes:
