@@ -615,8 +615,7 @@ PW_F32_BMS = {64: (1, 2, 4, 5, 16, 32), 128: (1, 2, 4, 5, 16, 32), 256: (1, 2, 3
 # fp32 big-tile 1x1 GEMM (csrc/kernels/gemm_f32s.hip, cfg ids 300+): id -> (BM, BN); 4 waves side by side
 # along N, BM chosen per layer so the tiles fill the CUs; 1x1 / pad 0 / stride 1-2, Cin % 32 == 0, N % 16 == 0;
 # ksplit 1 (one block per tile) or -1 (stream-K over 256 blocks, XCD-grouped, fused fixup)
-F32S_CFGS = {300: (112, 256), 301: (224, 256), 302: (112, 128), 303: (224, 128), 304: (64, 256), 305: (160, 256),
-             306: (192, 128),
+F32S_CFGS = {300: (112, 256), 302: (112, 128),          # (301, 303-306 retired: never picked in-graph)
              # 112-row tiles placed 98 rows apart (the kernel's TM): 256 tiles on 6272 x 256 / 1568 x 2048; whole K
              307: (98, 64), 308: (98, 128), 309: (49, 64)}
 F32S_TM = frozenset((307, 308, 309))     # owned-row tiles: ksplit 1 only

@@ -414,14 +414,11 @@ hipError_t gs_launch(const ConvF32Params& p, hipStream_t s) {
 // cfg -> (MF, NF, TM): tile (16 MF) x (64 NF), TM owned rows (0 = 16 MF); ops/conv.py F32S_CFGS mirrors this
 // (307 / 308 / 309: 98- / 98- / 49-row tiles on the ResNet-50 bs=32 K-heavy 1x1s, 256 tiles each: 6272 x 256,
 // 1568 x 2048 and 1568 x 512)
+// (301 / 303-306, the other whole-row tiles, were never picked in-graph and are no longer built; 300 / 302 keep
+// the whole-row and stream-K paths tested)
 #define ADAPT_F32S_CFGS(X) \
   X(300, 7, 4, 0)          \
-  X(301, 14, 4, 0)         \
   X(302, 7, 2, 0)          \
-  X(303, 14, 2, 0)         \
-  X(304, 4, 4, 0)          \
-  X(305, 10, 4, 0)         \
-  X(306, 12, 2, 0)         \
   X(307, 7, 1, 98)         \
   X(308, 7, 2, 98)         \
   X(309, 4, 1, 49)

@@ -756,47 +756,29 @@ hipError_t stem_forward(const float* x, const bf16* w, const float* bias, bf16* 
     // dozen blocks (8 at B=1): there the one-pool-row-per-block v1 grid fills more
     // CUs and wins.  ADAPT_STEM_V1=1 / =0 forces v1 / v2 (A/B switch).
     const int groups = (PH + S2_SP - 1) / S2_SP;
-    // ADAPT_STEM_V1=1 / =0 / =3 / =4 / =5 / =6 / =7: v1 / v2 / v3 (v3: the row-group kernel with the whole patch
-    // requested up front) / v4 (8 waves, pool of step k-1 beside the conv of step k) / v5 (v4 with each wave on
-    // half the channels) / v6 (v4 with the weight panel loaded once per block) / v7 (v5 + v6); v5-v7 take
-    // 3-channel images only
+    // ADAPT_STEM_V1=1 / =0 / =3 / =4 / =6: v1 / v2 / v3 (v3: the row-group kernel with the whole patch
+    // requested up front) / v4 (8 waves, pool of step k-1 beside the conv of step k) / v6 (v4 with the weight
+    // panel loaded once per block, 3-channel images).  v5 / v7 (each wave on half the channels) and the v4
+    // ablation builds were measurement variants (profiles/r5/stem_bf16_v4.md) and are no longer built.
     const char* v1 = getenv("ADAPT_STEM_V1");
     // default: v1 for small batches, above it v6 for 3-channel images (18.4 us vs v5's 20.4, v4's 21.1 and v3's
     // 26.1 at bs=32, profiles/r5/stem_bf16_v4.md), else v4
     const char ver = v1 && v1[0] ? v1[0]
                                  : (PH * B <= ST_V1_MAX_BLOCKS ? '1' : (PW * 8 <= S4_NT ? (C == 3 ? '6' : '4') : '3'));
-    if (ver == '4' || ver == '5' || ver == '6' || ver == '7') {
+    if (ver == '5' || ver == '7') return hipErrorInvalidValue;
+    if (ver == '4' || ver == '6') {
       if (PW * 8 > S4_NT) return hipErrorInvalidValue;
       const int g4 = (PH + S4_SP - 1) / S4_SP;
-#define ADAPT_S4(E)                                                                                            \
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, E>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH, \
-                     OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg)
       if (C == 3 && ver == '6') {
         hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 4, true>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w,
                            bias, out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
-      } else if (C == 3 && ver == '7') {
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 2, true>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w,
-                           bias, out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
-      } else if (C == 3 && ver == '5') {
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0, 2>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias,
+      } else if (C == 3) {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_pool_v4_kernel<true, 0>), dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias,
                            out, H, W, C, OH, OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
-      } else if (C == 3 && g_stem_exp != 0) {
-        switch (g_stem_exp) {
-          case 1: ADAPT_S4(1); break;
-          case 2: ADAPT_S4(2); break;
-          case 4: ADAPT_S4(4); break;
-          case 8: ADAPT_S4(8); break;
-          case 3: ADAPT_S4(3); break;
-          case 13: ADAPT_S4(13); break;
-          case 15: ADAPT_S4(15); break;
-          default: return hipErrorInvalidValue;
-        }
-      } else if (C == 3)
-        ADAPT_S4(0);
-#undef ADAPT_S4
-      else
+      } else {
         hipLaunchKernelGGL(stem_pool_v4_kernel<false>, dim3(g4 * B), dim3(S4_NT), 0, s, x, w, bias, out, H, W, C, OH,
                            OW, pad_t, pad_l, PH, PW, pool_pad, g4, g_stem_dbg);
+      }
       return hipGetLastError();
     }
     if (ver != '1') {

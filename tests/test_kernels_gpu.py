@@ -92,12 +92,12 @@ def test_conv_vs_torch(ops, case, cfg):
 
 @pytest.mark.parametrize("B,H,W,pool", [(4, 224, 224, True), (3, 224, 224, False), (2, 64, 48, True),
                                          (2, 37, 29, True), (1, 21, 30, False), (3, 230, 218, True)])
-@pytest.mark.parametrize("version", ["v7", "v6", "v5", "v4", "v3", "v2", "v1"])
+@pytest.mark.parametrize("version", ["v6", "v4", "v3", "v2", "v1"])
 def test_stem_vs_torch(ops, B, H, W, pool, version, monkeypatch):
     """Fused fp32-image -> conv1(7x7/s2)+BN+ReLU [-> 3x3/s2 max-pool] vs F.conv2d/F.max_pool2d
     (v2 = row-group kernel with the conv-row ring; v3 = v2 with the whole patch requested up front;
     v1 = one pool row per block; v4 = 8 waves, pool of step k-1 beside the conv of step k)."""
-    monkeypatch.setenv("ADAPT_STEM_V1", {"v1": "1", "v2": "0", "v3": "3", "v4": "4", "v5": "5", "v6": "6", "v7": "7"}[version])
+    monkeypatch.setenv("ADAPT_STEM_V1", {"v1": "1", "v2": "0", "v3": "3", "v4": "4", "v6": "6"}[version])
     conv, _ = ops
     dev = "cuda"
     torch.manual_seed(1)
@@ -127,7 +127,7 @@ def test_stem_vs_torch(ops, B, H, W, pool, version, monkeypatch):
 
 @pytest.mark.parametrize("B,H,W", [(32, 224, 224), (3, 230, 218)])
 def test_stem_versions_bitwise_equal(ops, B, H, W, monkeypatch):
-    """v1 - v7 of the pooled bf16 stem do the same sums in the same order: bit-identical outputs."""
+    """v1 - v4 and v6 of the pooled bf16 stem do the same sums in the same order: bit-identical outputs."""
     conv, _ = ops
     torch.manual_seed(2)
     x = torch.randn(B, H, W, 3, device="cuda") * 40.0
@@ -135,7 +135,7 @@ def test_stem_versions_bitwise_equal(ops, B, H, W, monkeypatch):
     ps = conv.pack_stem(kern, (torch.randn(64) * 0.1).numpy(), ((3, 3), (3, 3)), "cuda")
     OH, OW = ps.out_hw(H, W)
     outs = []
-    for ver in ("1", "0", "3", "4", "5", "6", "7"):
+    for ver in ("1", "0", "3", "4", "6"):
         monkeypatch.setenv("ADAPT_STEM_V1", ver)
         out = torch.full((B, (OH - 1) // 2 + 1, (OW - 1) // 2 + 1, 64), float("nan"), device="cuda",
                          dtype=torch.bfloat16)

@@ -19,7 +19,7 @@ import torch  # noqa: E402
 from adaptive_deep_learning_architecture_for_parallel_and_fault_tolerant_inference_amd.ops import conv as C  # noqa: E402
 
 CASES = [(32, 28, 28, 512, 128, 302), (32, 7, 7, 512, 2048, 302), (32, 14, 14, 256, 1024, 300),
-         (32, 28, 28, 128, 512, 301)]
+         (32, 28, 28, 128, 512, 300)]
 
 
 def main():

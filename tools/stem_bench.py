@@ -55,7 +55,7 @@ def main():
     ps16 = C.pack_stem(kern, np.zeros(64, np.float32), ((3, 3), (3, 3)), "cuda")
     o16 = torch.empty(B, 56, 56, 64, device="cuda", dtype=torch.bfloat16)
     r16 = {}
-    for ver in ("1", "0", "3", "4", "5", "6", "7"):
+    for ver in ("1", "0", "3", "4", "6"):
         os.environ["ADAPT_STEM_V1"] = ver
         for _ in range(10):
             C.stem_forward(x, ps16, o16, pool=True)
@@ -66,7 +66,7 @@ def main():
             C.stem_forward(x, ps16, o16, pool=True)
         e.record()
         torch.cuda.synchronize()
-        r16[{"1": "v1", "0": "v2", "3": "v3", "4": "v4", "5": "v5", "6": "v6", "7": "v7"}[ver]] = (s.elapsed_time(e) * 1e3 / a.iters, o16.clone())
+        r16[{"1": "v1", "0": "v2", "3": "v3", "4": "v4", "6": "v6"}[ver]] = (s.elapsed_time(e) * 1e3 / a.iters, o16.clone())
     os.environ.pop("ADAPT_STEM_V1")
     print(json.dumps({"kernel": "stem_bf16", "batch": B, "us_by_version": {k: round(t, 2) for k, (t, _) in r16.items()},
                       "versions_bitwise_equal": all(torch.equal(r16["v1"][1], o[1]) for o in r16.values())}))

@@ -26,10 +26,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--json", default="")
-    ap.add_argument("--version", default="5", choices=["4", "5", "6", "7"],
-                    help="ADAPT_STEM_V1 (v5: channel halves, v6: v4 + block-staged weights, v7: v5 + block-staged weights)")
-    ap.add_argument("--exp", default="0", help="measurement variants: 1 no MFMA, 2 no pool, 4 no ring stores, "
-                    "8 no A reads in the steps (outputs wrong by design), comma list")
+    ap.add_argument("--version", default="6", choices=["4", "6"],
+                    help="ADAPT_STEM_V1 (v6: v4 + block-staged weights; the v5 / v7 channel-half variants and the "
+                    "ablation builds are retired, profiles/r5/stem_bf16_v4.md holds their timelines)")
+    ap.add_argument("--exp", default="0", help="0 only (the ablation builds are no longer compiled)")
     a = ap.parse_args()
     K = C.kernels()
     B = a.batch
