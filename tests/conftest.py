@@ -21,15 +21,16 @@ def pytest_sessionfinish(session, exitstatus):
 
 
 def pytest_unconfigure(config):
-    """GPU sessions end with `os._exit` once pytest has reported: the DEFER tests
-    leave aborted per-epoch gloo groups (host-staged links between GPU stages)
-    whose backend threads are still parked in a cancelled recv, and the C++
-    static teardown of the HIP runtime under them aborts the process
-    ("terminate called without an active exception") after every test passed.
-    The test verdict is already decided; skipping interpreter teardown keeps the
-    exit code equal to it."""
+    """GPU sessions exit through normal interpreter teardown.  Until round 6 they
+    ended with `os._exit`: aborted per-epoch groups from the DEFER tests left
+    backend threads parked in native receives, and HIP's static teardown under
+    them aborted the process after every test had passed.  With the RCCL
+    async-error poll serialised and every communicator abort bounded
+    (csrc/comm/rccl_p2p.cpp), the whole GPU suite exits cleanly
+    (profiles/r6/pytest_gpu_normal_exit.log, rc 0).  ADAPT_TEST_FAST_EXIT=1
+    restores the old exit for a box where teardown misbehaves."""
     status = _EXIT["status"]
-    if status is None or os.environ.get("ADAPT_TEST_NORMAL_EXIT") == "1":
+    if status is None or os.environ.get("ADAPT_TEST_FAST_EXIT") != "1":
         return
     try:
         import torch
