@@ -385,8 +385,10 @@ def pack_stem_f32(kernel_hwio: np.ndarray, bias: np.ndarray, pads, device) -> Pa
                       cin=3, pad_t=pt, pad_l=pl, pad_b=pb, pad_r=pr)
 
 
-STEM_F32_VARIANT = 2  # stem_f32.hip: 0 = one unit at a time, 1 = software-pipelined units, 2 = whole rows (OW 112),
-#                       5 = whole rows, horizontal pool in the conv epilogue, vertical pool beside the next step
+STEM_F32_VARIANT = 6  # stem_f32.hip: 0 = one unit at a time, 1 = software-pipelined units, 2 = whole rows (OW 112),
+#                       5 = whole rows, horizontal pool in the conv epilogue, vertical pool beside the next step,
+#                       6 = 5 with the next tile's operand reads issued ahead of the MFMAs (ADAPT_STEM_F32_VARIANT
+#                       overrides the default at launch / capture time)
 
 
 def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pad: int = 1,
@@ -404,7 +406,8 @@ def stem_f32_forward(x: torch.Tensor, ps: PackedStem, out: torch.Tensor, pool_pa
         raise ValueError(f"fp32 stem output buffer must be contiguous fp32 with {need} elements")
     kernels().stem_f32_forward(ptr(x), ptr(ps.w), ptr(ps.bias), ptr(out), B, H, W, 3, OH, OW, ps.pad_t, ps.pad_l,
                                PH, PW, pool_pad, stream_handle(stream),
-                               STEM_F32_VARIANT if variant is None else int(variant))
+                               int(os.environ.get("ADAPT_STEM_F32_VARIANT", STEM_F32_VARIANT)) if variant is None
+                               else int(variant))
     return out
 
 

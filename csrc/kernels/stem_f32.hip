@@ -376,6 +376,10 @@ __device__ __forceinline__ f32x4 max4(f32x4 a, f32x4 b) {
 }
 }  // namespace
 
+// PIPE (variant 6): a whole row's tiles with the next tile's 21 LDS operand reads issued ahead of this tile's
+// 37 MFMAs (two operand sets, alternating over the unrolled tiles), so the read latency hides under the MFMA
+// burst instead of sitting in front of it (the two waves of a SIMD reach each tile start together)
+template <bool PIPE>
 __global__ __launch_bounds__(SF_NT, 1) void stem_hpool_f32_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ bias,
@@ -463,6 +467,55 @@ __global__ __launch_bounds__(SF_NT, 1) void stem_hpool_f32_kernel(const float* _
     const int slot = r % SF_HR;
     const bool even = (fr & 1) == 0;
     f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (PIPE) {
+      if (cb == 0 && ce == SF_TPR && st == 0) {           // a whole row (wave-uniform)
+        // the 8 float4 halves are read a tile ahead; the gathered half and the last element (5 reads, used by
+        // the tile's last 5 MFMAs) are read at the tile's start
+        struct Ops {
+          f32x4 h[SF_KH - 1];
+        };
+        auto load = [&](int c, Ops& o) __attribute__((always_inline)) {
+          const int po = c * 96;
+#pragma unroll
+          for (int h = 0; h < SF_KH - 1; ++h) {
+            const f32x2 lo = *(const f32x2*)(patch + ah[h] + po), hi = *(const f32x2*)(patch + ah[h] + po + 2);
+            o.h[h] = (f32x4){lo[0], lo[1], hi[0], hi[1]};
+          }
+        };
+        Ops oa, ob;
+        load(0, oa);
+#pragma unroll
+        for (int c = 0; c < SF_TPR; ++c) {
+          Ops& cur = (c & 1) ? ob : oa;
+          Ops& nxt = (c & 1) ? oa : ob;
+          f32x4 g8;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) g8[e] = patch[ag[e] + c * 96];
+          const float g9 = patch[a9 + c * 96];
+          if (c + 1 < SF_TPR) load(c + 1, nxt);
+          __builtin_amdgcn_sched_barrier(0);
+          f32x4 acc0 = b4, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int h = 0; h < SF_KH - 1; h += 2)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h][e], cur.h[h][e], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[h + 1][e], cur.h[h + 1][e], acc1, 0, 0, 0);
+            }
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][0], g8[0], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][1], g8[1], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][2], g8[2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[8][3], g8[3], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa9, g9, acc0, 0, 0, 0);
+          f32x4 y = max4(acc0 + acc1, (f32x4){0.f, 0.f, 0.f, 0.f});
+          const f32x4 rgt = sf_shl1(y), lsh = sf_shr1(y), lro = sf_ror1(prev);
+          const f32x4 lft = fr == 0 ? lro : lsh;
+          if (even) *(f32x4*)(hring + hring_off(slot, 8 * c + (fr >> 1), ct * 4 + fq)) = max4(max4(lft, y), rgt);
+          prev = y;
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int c = 0; c < SF_TPR; ++c) {
       if (c < cb || c >= ce) continue;
@@ -541,12 +594,12 @@ bool stem_f32_supported(int C, int W, int OW, int pool_pad) {
 hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, float* out, int B, int H, int W, int C,
                             int OH, int OW, int pad_t, int pad_l, int PH, int PW, int pool_pad, hipStream_t s,
                             int variant) {
-  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 5 || variant == 3 ||
+  if (!stem_f32_supported(C, W, OW, pool_pad) || pad_l != 3 || variant < 0 || variant > 6 || variant == 3 ||
       variant == 4 || B < 1 || PH < 1 || PW < 1 || PH > (OH + 2 * pool_pad - 3) / 2 + 1 ||
       PW > (OW + 2 * pool_pad - 3) / 2 + 1 || W + pad_l > SF_COLS)
     return hipErrorInvalidValue;
   const int groups = (PH + SF_SP - 1) / SF_SP;
-  if (variant >= 2 && (OW != 16 * SF_TPR || (variant == 5 && PW != SF_HP))) variant = 1;   // 112-wide rows only
+  if (variant >= 2 && (OW != 16 * SF_TPR || (variant >= 5 && PW != SF_HP))) variant = 1;   // 112-wide rows only
   if (variant == 0)
     hipLaunchKernelGGL(stem_pool_f32_kernel<0>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
@@ -556,9 +609,12 @@ hipError_t stem_f32_forward(const float* x, const float* w, const float* bias, f
   else if (variant == 2)
     hipLaunchKernelGGL(stem_pool_f32_kernel<2>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, OW,
                        pad_t, pad_l, PH, PW, pool_pad, groups);
+  else if (variant == 6)
+    hipLaunchKernelGGL(stem_hpool_f32_kernel<true>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH,
+                       pad_t, pad_l, PH, groups);
   else
-    hipLaunchKernelGGL(stem_hpool_f32_kernel, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH, pad_t,
-                       pad_l, PH, groups);
+    hipLaunchKernelGGL(stem_hpool_f32_kernel<false>, dim3(groups * B), dim3(SF_NT), 0, s, x, w, bias, out, H, W, OH,
+                       pad_t, pad_l, PH, groups);
   return hipGetLastError();
 }
 

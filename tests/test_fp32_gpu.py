@@ -258,7 +258,7 @@ def test_other_families_fp32_logits_match_oracle(name):
     assert torch.isfinite(probs).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 5, 6])
 @pytest.mark.parametrize("B,H", [(2, 224), (1, 64), (3, 112)])
 def test_stem_f32_fused_matches_fp64(B, H, variant):
     """csrc/kernels/stem_f32.hip: 7x7/s2 conv (+bias, ReLU) + 3x3/s2 max-pool in one launch vs a float64 oracle."""
