@@ -269,3 +269,35 @@ def test_unrecoverable_worker_is_dropped_and_replanned(tiny):
         d.shutdown(stop_workers=True)
         for n in nodes:
             n.stop()
+
+
+def test_prepare_hints_wait_longer_after_a_reformed_epoch():
+    """Background `prepare` (building the likely next plans' slices) competes with the serving threads: after a
+    re-formed epoch it waits `recovery_prepare_delay` (the loopback hang run's dip ~1 s after recovery came from
+    it), after a first epoch only `prepare_delay`."""
+    d = DEFER(membership_port=0, result_port=0, resident=False, prepare=True)
+
+    class _G:
+        graph = object()
+
+    waits = []
+
+    class _Ev:
+        def wait(self, t):
+            waits.append(t)
+            return True                               # behave as shut down: stop right after the wait
+
+        def is_set(self):
+            return False
+
+    real_model, real_ev = d._model, d._shutdown_event
+    d._model, d._model_key, d._resident = _G(), "m", {"a": {"m"}}
+    d._shutdown_event = _Ev()
+    try:
+        d._after_epoch(None, reformed=False)
+        d._after_epoch(None, reformed=True)
+    finally:
+        d._model, d._shutdown_event = real_model, real_ev
+        d.shutdown()
+    assert waits == [d.prepare_delay, d.recovery_prepare_delay]
+    assert d.recovery_prepare_delay > d.prepare_delay
