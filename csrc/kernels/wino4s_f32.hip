@@ -474,6 +474,37 @@ __global__ __launch_bounds__(256) void wino4s_reduce_kernel(Wino4sParams p) {
   *((f32x4v*)(p.out + (((size_t)b * p.H + h) * p.W + w) * p.N) + n4) = o;
 }
 
+// the same with the split count a template parameter (every split's load in flight at once) and 32-bit index
+// math (the generic kernel's 64-bit divisions are software sequences)
+template <int KS>
+__global__ __launch_bounds__(256) void wino4s_reduce_ks_kernel(Wino4sParams p) {
+  const int N4 = p.N >> 2;
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  const unsigned total = (unsigned)p.T * 16u * (unsigned)N4;
+  if (idx >= total) return;
+  const unsigned tp = idx / (unsigned)N4;
+  const int n4 = (int)(idx - tp * (unsigned)N4);
+  const int u = (int)(tp & 15u), t = (int)(tp >> 4);
+  const int per = p.TH * p.TW;
+  const int b = t / per, rem = t - b * per;
+  const int th = rem / p.TW, tw = rem - th * p.TW;
+  const int h = 4 * th + (u >> 2), w = 4 * tw + (u & 3);
+  if (h >= p.H || w >= p.W) return;
+  const unsigned slab4 = (unsigned)p.TG * 16u * 16u * (unsigned)N4;        // f32x4 per split slab
+  const f32x4v* src = (const f32x4v*)p.ws + tp * (unsigned)N4 + n4;
+  f32x4v part[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) part[s] = src[s * slab4];
+  f32x4v acc = part[0];
+#pragma unroll
+  for (int s = 1; s < KS; ++s) acc += part[s];
+  const f32x4v bv = *((const f32x4v*)p.bias + n4);
+  f32x4v o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = act_relu(acc[j] + bv[j], p.relu);
+  *((f32x4v*)(p.out + (((size_t)b * p.H + h) * p.W + w) * p.N) + n4) = o;
+}
+
 struct W4sCfg {
   int wt, wn, pg, r, order;
 };
@@ -598,7 +629,13 @@ hipError_t wino4s_forward(const Wino4sParams& p_in, int cfg, hipStream_t s) {
   }
   if (e != hipSuccess || p.ksplit == 1 || fused) return e;
   const long total = (long)p.T * 16 * (p.N / 4);
-  hipLaunchKernelGGL(wino4s_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, q);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  const char* rk = getenv("ADAPT_W4S_REDUCE");
+  const bool generic = (rk && rk[0] == '0') || (size_t)p.TG * 256 * (p.N / 4) * p.ksplit >= 0xffffffffu;
+  if (!generic && p.ksplit == 2) hipLaunchKernelGGL(wino4s_reduce_ks_kernel<2>, grid, dim3(256), 0, s, q);
+  else if (!generic && p.ksplit == 4) hipLaunchKernelGGL(wino4s_reduce_ks_kernel<4>, grid, dim3(256), 0, s, q);
+  else if (!generic && p.ksplit == 8) hipLaunchKernelGGL(wino4s_reduce_ks_kernel<8>, grid, dim3(256), 0, s, q);
+  else hipLaunchKernelGGL(wino4s_reduce_kernel, grid, dim3(256), 0, s, q);
   return hipGetLastError();
 }
 

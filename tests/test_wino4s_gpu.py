@@ -53,7 +53,8 @@ def test_resnet_stage_shapes_whole_k(cfg):
 
 @pytest.mark.parametrize("cfg", [220, 221, 223, 227, 228, 234, 236, 237])
 @pytest.mark.parametrize("H,C,ks", [(56, 64, 1), (56, 64, 2), (56, 64, -2), (28, 128, 2), (28, 128, -2),
-                                    (14, 256, 2), (14, 256, -4), (7, 512, 4), (7, 512, -8), (7, 512, -4)])
+                                    (14, 256, 2), (14, 256, 4), (14, 256, -4), (7, 512, 4), (7, 512, 8),
+                                    (7, 512, -8), (7, 512, -4)])
 def test_resnet_bs32_splits(cfg, H, C, ks):
     if not C_.kernels().wino4s_ok(cfg, C, C, ks):
         pytest.skip("config / split not built for this shape")
@@ -70,6 +71,23 @@ def test_odd_maps_and_partial_tile_groups(B, H, W, C, N):
             continue
         rel = _run(B, H, W, C, N, cfg, 1, relu=0, seed=B * H + W)
         assert rel < 3e-5, (cfg, rel)
+
+
+@pytest.mark.parametrize("ks", [2, 4, 8])
+def test_split_reduce_kernels_agree(ks, monkeypatch):
+    """The split-count-templated reduce (default) and the generic one (ADAPT_W4S_REDUCE=0) give the same bits."""
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("ADAPT_W4S_REDUCE", mode)
+        g = torch.Generator().manual_seed(ks)
+        x = torch.randn((4, 7, 7, 512), generator=g).cuda()
+        k = torch.randn((3, 3, 512, 512), generator=g) / 60.0
+        pc = C_.pack_conv_f32(k.numpy(), np.zeros(512, np.float32), 1, ((1, 1), (1, 1)), "cuda")
+        out = torch.full((4, 7, 7, 512), float("nan"), device="cuda")
+        C_.conv_forward_f32(x, pc, out, relu=1, cfg=221, ksplit=ks)
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_rejects_residual_and_bad_split():
