@@ -183,8 +183,22 @@ __global__ __launch_bounds__(256) void dense_finish_reg_kernel(const float* __re
     v[j] = (ok[j] && bias) ? bias[i] : 0.f;
   }
   // four slices' loads in flight per round (the fp32 head has 16 slices; a loop of dependent
-  // rounds left the finish latency-bound at 8 us)
+  // rounds left the finish latency-bound at 8 us); 16 slices: all of them in one round
   int sl = 0;
+  if (KS == 16) {
+    float t[16][4];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float* pr = part + ((size_t)u * M + row) * N;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[u][j] = ok[j] ? pr[tid + 256 * j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += t[u][j];
+    sl = 16;
+  }
   for (; sl + 4 <= KS; sl += 4) {
     float t[4][4];
 #pragma unroll
@@ -250,6 +264,28 @@ __global__ __launch_bounds__(256) void dense_partial_f32_kernel(const float* __r
   const int k0 = blockIdx.y * DHF_KSL, k1 = min(Kpad, k0 + DHF_KSL);
   const float* wr = w + (size_t)n * Kpad + 4 * q;
   f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  if (k1 - k0 == DHF_KSL && k1 <= K) {
+    // a whole slice (the ImageNet head: every slice): all 8 weight and 16 activation loads issued before the
+    // first MFMA -- one memory latency per block instead of one per unrolled group of K steps
+    constexpr int ST = DHF_KSL / 16;
+    f32x4 b[ST], a[ST][2];
+#pragma unroll
+    for (int i = 0; i < ST; ++i) {
+      b[i] = *(const f32x4*)(wr + k0 + 16 * i);
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) {
+        const int row = mf * 16 + r;
+        a[i][mf] = row < M ? *(const f32x4*)(x + (size_t)row * K + k0 + 16 * i + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ST; ++i)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf)
+          acc[mf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][mf][s4], b[i][s4], acc[mf], 0, 0, 0);
+  } else {
 #pragma unroll 4
   for (int k = k0; k < k1; k += 16) {
     const f32x4 b = *(const f32x4*)(wr + k);
@@ -264,6 +300,7 @@ __global__ __launch_bounds__(256) void dense_partial_f32_kernel(const float* __r
     for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf) acc[mf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mf][s4], b[s4], acc[mf], 0, 0, 0);
+  }
   }
   // acc[mf][e] = C[row mf*16 + 4q + e][column n]
   if (n >= N) return;
