@@ -17,6 +17,8 @@
 //
 // Split-K (ksplit > 1): each K-slice writes an fp32 partial slab
 // ws[slice][M][N]; conv_splitk_reduce applies the epilogue.
+#include <cstdlib>
+
 #include "kernels.h"
 #include "epilogue.h"
 
@@ -204,18 +206,43 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_igemm_kernel(ConvParams p) {
 }
 
 // split-K reduction + epilogue: out = act(sum_s ws[s] + bias (+res))
-template <bool OUT_F32>
+// KS > 0: the split count at compile time (every split's loads in flight at once) and 32-bit chunk math
+// (host: chunks < 2^31); KS = 0: any split count
+template <bool OUT_F32, int KS = 0>
 __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvParams p) {
   const size_t chunks = (size_t)p.M * (p.N / 8);
   for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < chunks; c += (size_t)gridDim.x * blockDim.x) {
-    const int m = (int)(c / (p.N / 8));
-    const int n = (int)(c % (p.N / 8)) * 8;
+    int m, n;
+    if constexpr (KS > 0) {
+      const unsigned n8 = (unsigned)(p.N / 8), cc = (unsigned)c;
+      const unsigned mm = cc / n8;
+      m = (int)mm;
+      n = (int)(cc - mm * n8) * 8;
+    } else {
+      m = (int)(c / (p.N / 8));
+      n = (int)(c % (p.N / 8)) * 8;
+    }
     float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int s = 0; s < p.ksplit; ++s) {
-      const float* src = p.ws + (size_t)s * p.M * p.N + (size_t)m * p.N + n;
-      f32x4 a = *(const f32x4*)src, b = *(const f32x4*)(src + 4);
-      v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
-      v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+    if constexpr (KS > 0) {
+      f32x4 a[KS], b[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float* src = p.ws + (size_t)s * p.M * p.N + (size_t)m * p.N + n;
+        a[s] = *(const f32x4*)src;
+        b[s] = *(const f32x4*)(src + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        v[0] += a[s][0]; v[1] += a[s][1]; v[2] += a[s][2]; v[3] += a[s][3];
+        v[4] += b[s][0]; v[5] += b[s][1]; v[6] += b[s][2]; v[7] += b[s][3];
+      }
+    } else {
+      for (int s = 0; s < p.ksplit; ++s) {
+        const float* src = p.ws + (size_t)s * p.M * p.N + (size_t)m * p.N + n;
+        f32x4 a = *(const f32x4*)src, b = *(const f32x4*)(src + 4);
+        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+        v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+      }
     }
     if (p.bias) {
 #pragma unroll
@@ -301,8 +328,19 @@ hipError_t conv_forward(const ConvParams& p, int cfg, hipStream_t s, bool out_f3
   const size_t chunks = (size_t)p.M * (p.N / 8);
   int blocks = (int)((chunks + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  if (out_f32) hipLaunchKernelGGL((conv_splitk_reduce<true>), dim3(blocks), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((conv_splitk_reduce<false>), dim3(blocks), dim3(256), 0, s, p);
+  const char* gk = getenv("ADAPT_SPLITK_GENERIC");            // A/B switch: the runtime-split kernel
+  const bool small = chunks < 0x7fffffffu && !(gk && gk[0] == '1');
+  if (small && p.ksplit == 2) {
+    if (out_f32) hipLaunchKernelGGL((conv_splitk_reduce<true, 2>), dim3(blocks), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv_splitk_reduce<false, 2>), dim3(blocks), dim3(256), 0, s, p);
+  } else if (small && p.ksplit == 4) {
+    if (out_f32) hipLaunchKernelGGL((conv_splitk_reduce<true, 4>), dim3(blocks), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv_splitk_reduce<false, 4>), dim3(blocks), dim3(256), 0, s, p);
+  } else if (out_f32) {
+    hipLaunchKernelGGL((conv_splitk_reduce<true>), dim3(blocks), dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((conv_splitk_reduce<false>), dim3(blocks), dim3(256), 0, s, p);
+  }
   return hipGetLastError();
 }
 
