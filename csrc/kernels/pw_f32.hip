@@ -19,6 +19,8 @@
 // Transposed MFMA as in pw_pair_f32.hip: A = weight fragment, B = activation fragment
 // (ds_read_b128 of a pixel row, lane group q supplying k = 16h + 4q + s to step s), D =
 // [channel][pixel], so a lane's accumulator is 4 consecutive channels of one pixel.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace adapt {
@@ -238,7 +240,9 @@ __device__ __forceinline__ void pw_tail_pick(int jj, const f32x4 (&wr)[FPW][KH],
   }
 }
 
-template <int K, int FPW, int D, int OCC, bool TAIL = false>
+// ACT >= 0: the activation mode at compile time (single-output launches; the runtime mode costs a max, a
+// min and two selects per output element, ~25 % of the VALU work of a tile); -1: p.relu / p.relu2 at run time
+template <int K, int FPW, int D, int OCC, bool TAIL = false, int ACT = -1>
 __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, int ncg, int nslots, int full,
                                                                  int tail) {
   constexpr int KH = K / 16;
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
         for (int a = 1; a < NA; ++a) v += acc[a][j];
         if (has_res) v += res[j];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
+        for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], ACT >= 0 ? ACT : relu);
         *(f32x4*)(dst + (size_t)m * ldo + (cg * FPW + j) * 16 + fq * 4 - cof) = v;
       }
     }
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(256, OCC) void pw_stream_f32_kernel(PwF32Params p, 
     v += acc[3];
     if (has_res) v += *(const f32x4*)(p.res + (size_t)min(m, p.M - 1) * p.N + col);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], relu);
+    for (int e = 0; e < 4; ++e) v[e] = act_relu(v[e], ACT >= 0 ? ACT : relu);
     if (m < p.M) *(f32x4*)(dst + (size_t)m * ldo + col - cof) = v;
     if (dbg) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -475,6 +479,22 @@ static hipError_t pw_stream_launch(const PwF32Params& p_, int ncg, int ntiles, h
   if (nslots < 1) nslots = 1;
   if (nslots > ntiles) nslots = ntiles;
   const int blocks = (ncg * nslots + 3) / 4;
+  const char* ag = getenv("ADAPT_PW_ACT_GENERIC");             // A/B switch: the run-time activation mode
+  if (p.n_split == 0 && p.relu == 1 && !(ag && ag[0] == '1')) {
+    if constexpr (!TAIL) {
+      hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O, false, 1>), dim3(blocks), dim3(256), 0, s, p, ncg,
+                         nslots, 0, 0);
+      return hipGetLastError();
+    } else if constexpr (F > 1) {
+      const int full = ntiles / nslots, tail = ntiles - full * nslots;
+      if (pw_tail_fits(F, ntiles, nslots)) {
+        hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O, true, 1>), dim3(blocks), dim3(256), 0, s, p, ncg,
+                           nslots, full, tail);
+        return hipGetLastError();
+      }
+      return hipErrorInvalidValue;
+    }
+  }
   if constexpr (!TAIL) {
     hipLaunchKernelGGL((pw_stream_f32_kernel<K, F, D, O>), dim3(blocks), dim3(256), 0, s, p, ncg, nslots, 0, 0);
     return hipGetLastError();
